@@ -1,0 +1,147 @@
+"""bench.py — distinct states/sec of the Raft BFS model checker on MI355X.
+
+Workload (BASELINE.json configs[1], `C2`): thirdparty/raft_original.tla with
+configs/c2.cfg (3 servers, 2 values, term <= 3, log <= 2, |DOMAIN messages|
+<= 5 with counts 0..1), checking ElectionSafety and LogMatching.  One *step*
+is one complete breadth-first model-checking run of that model on the GPU
+(seen-set re-zeroed, every level expanded; the state store stays allocated
+between steps, the inputs are the spec/cfg only).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N > 1 (torchrun, one process per GPU): every rank checks its own replica of
+the model (no data-path collective yet), value = all
+ranks' distinct states / max-over-ranks time, "scaling": "weak".
+
+The JSON line adds:
+  roofline      expand kernel (orig_expand): algorithmic bytes F*S + G_in*8 +
+                D*(16+S) / summed HIP-event kernel time,
+                against the 8 TB/s HBM peak; traffic from rocprofv3 PMC passes
+                when --traffic-json points at their summary (else null)
+  cpu_baseline  the CPU oracle (oracle/, test infrastructure: "port") on a
+                bounded sample of the same model (first --cpu-states distinct
+                states of its BFS), single thread
+"""
+import argparse
+import importlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+TLA = os.path.join(ROOT, "configs", "raft_original_mc.tla")
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def cpu_baseline(cfg, max_states):
+    exe = os.path.join(ROOT, "oracle", "_build", "raft_oracle")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    t0 = time.time()
+    out = subprocess.run([exe, "bfs", "--tla", TLA, "--cfg", cfg, "--max-states", str(max_states)],
+                         capture_output=True, text=True, check=True, timeout=600)
+    wall = time.time() - t0
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    secs = r["seconds"] or wall
+    return {"value": r["distinct"] / secs, "unit": "distinct states/s", "cores": 1, "kind": "port",
+            "sample": "oracle BFS of the same model stopped after %d distinct states (%d generated, %.1f s, 1 thread)"
+                      % (r["distinct"], r["generated"], secs)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default=os.path.join(ROOT, "configs", "c2.cfg"))
+    ap.add_argument("--cpu-states", type=int, default=150000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    mod = importlib.import_module("raft-tla_amd")
+    mc = mod.ModelChecker(TLA, args.config, device=local, seed=0x5EED)
+
+    def barrier_sync():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        mc.run()
+    barrier_sync()
+    t0 = time.perf_counter()
+    res = None
+    for _ in range(args.steps):
+        res = mc.run()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    mc.close()
+    assert res.verdict == "OK", (res.verdict, res.error)
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed, float(res.distinct)], dtype=torch.float64, device="cuda")
+        mx = t.clone()
+        dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, total_distinct = float(mx[0]), float(t[1])
+    else:
+        total_distinct = float(res.distinct)
+
+    if rank == 0:
+        per_step = elapsed / args.steps
+        achieved = res.algo_bytes / res.kernel_seconds / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "distinct states/sec (node) on Raft BFS",
+            "value": total_distinct / per_step,
+            "unit": "distinct states/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": per_step * 1000.0,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic: the model's own reachable state space (no external data)",
+            "config": {"workload": "C2: raft_original.tla + configs/c2.cfg (3 servers, 2 values, term<=3, log<=2, msgs<=5)",
+                       "distinct_per_run": res.distinct, "generated_per_run": res.generated, "depth": res.depth,
+                       "kernel_ms_per_run": res.kernel_seconds * 1000.0, "launches_per_run": res.n_launches,
+                       "state_bytes": res.state_bytes,
+                       "parallelism": "single" if world == 1 else "replicas%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "orig_expand", "algo_bytes_per_launch": res.algo_bytes / max(1, res.n_launches),
+                         "avg_launch_ms": res.kernel_seconds * 1000.0 / max(1, res.n_launches)},
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_states)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,140 @@
+/*
+ * raftmc — C ABI of the MI355X-native explicit-state model checker for the
+ * dranov/raft-tla specs.  This is the drop-in boundary for the hot path.
+ *
+ * The reference has no FFI: the path sits behind TLC's command-line contract
+ * (SURVEY.md §8b), i.e.
+ *     java -cp tla2tools.jar tlc2.TLC [-workers N] [-config F.cfg] [-deadlock] F.tla
+ * driven by tlc_membership/raft.cfg:1-87 (README.md:5 "passed to TLC").
+ * Each entry point below replaces one part of that contract:
+ *   mc_open      <- TLC argument parsing + SANY/cfg loading
+ *                   (the .tla given as F.tla, the .cfg given by -config; the
+ *                   cfg keywords of tlc_membership/raft.cfg:1-87)
+ *   mc_run       <- tlc2.TLC model checking (ModelChecker BFS: Init, Next,
+ *                   CONSTRAINTS raft.cfg:37-55, INVARIANTS raft.cfg:60-87,
+ *                   SYMMETRY raft.cfg:29, VIEW raft.cfg:30)
+ *   mc_summary   <- TLC's final lines "N states generated, M distinct states
+ *                   found, K states left on queue", "The depth of the complete
+ *                   state graph search is D", the fingerprint collision
+ *                   probability lines, and the process exit code
+ *   mc_trace     <- TLC's "Error: Invariant X is violated." + "State k:" blocks
+ *   mc_report    <- the whole TLC-style stdout text
+ *
+ * Conventions: every function returns 0 or a negative MC_E_* code and never
+ * throws.  The library owns all buffers; text returned through an out
+ * parameter is freed by the caller with mc_free().  A handle is used by one
+ * host thread at a time; distinct handles are independent.  All GPU work runs
+ * on the HIP device selected in mc_opts; there is no CPU fallback: on a host
+ * without a usable gfx950 device mc_run fails with MC_E_NO_DEVICE.
+ */
+#ifndef RAFTMC_H
+#define RAFTMC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RAFTMC_ABI_VERSION 1
+
+/* error codes */
+#define MC_OK 0
+#define MC_E_INVALID (-1)      /* bad argument / unusable handle                   */
+#define MC_E_IO (-2)           /* cannot read the .tla / .cfg                      */
+#define MC_E_PARSE (-3)        /* cfg syntax error                                 */
+#define MC_E_UNSUPPORTED (-4)  /* spec / cfg feature or shape not compiled in       */
+#define MC_E_NO_DEVICE (-5)    /* no HIP device / HIP runtime failure              */
+#define MC_E_OOM (-6)          /* device allocation failed                         */
+#define MC_E_STATE (-7)        /* call out of order (e.g. mc_trace before mc_run)  */
+
+/* verdicts (mc_summary_t.verdict) and the TLC-like exit codes mc_exit_code() maps them to */
+#define MC_VERDICT_OK 0
+#define MC_VERDICT_INVARIANT_VIOLATION 1
+#define MC_VERDICT_EVAL_ERROR 2
+#define MC_VERDICT_CAPACITY_OVERFLOW 3
+#define MC_VERDICT_DEADLOCK 4
+#define MC_VERDICT_DEPTH_LIMIT 5
+
+/* tlc_compat_flags: the [ext] TLC-semantics switches */
+#define MC_COMPAT_INV_OUT_OF_MODEL 0x1u /* check invariants on !seen successors that fail a constraint (TLC default) */
+
+typedef struct mc_ctx mc_ctx;
+
+typedef struct mc_opts {
+  int32_t abi_version;        /* RAFTMC_ABI_VERSION                                       */
+  int32_t device;             /* HIP device ordinal (one process per GPU)                  */
+  int32_t n_gpus;             /* 1 (multi-GPU runs use one process per GPU) */
+  int32_t workers;            /* TLC -workers (recorded only; the GPU backend is data-parallel) */
+  uint64_t fp_table_bytes;    /* seen-set bytes (power of two used; 0 = auto)             */
+  uint64_t state_store_bytes; /* bytes for the per-state store (packed states + parents); 0 = auto */
+  int64_t max_depth;          /* 0 = unbounded (TLC -dfid/-depth analogue for BFS)        */
+  uint64_t seed;              /* fingerprint seed (0 = default)                           */
+  uint32_t tlc_compat_flags;  /* MC_COMPAT_* (default MC_COMPAT_INV_OUT_OF_MODEL)         */
+  int32_t check_deadlock;     /* 1 = report states without successors (TLC default; -deadlock disables) */
+  int32_t block_size;         /* expand kernel workgroup size (0 = 256)                   */
+  int32_t reserved[7];
+} mc_opts;
+
+typedef struct mc_summary_t {
+  int64_t generated;          /* "states generated" (initial states included)             */
+  int64_t distinct;           /* "distinct states found"                                  */
+  int64_t left_on_queue;      /* "states left on queue"                                   */
+  int64_t depth;              /* "depth of the complete state graph search" (Init = 1)    */
+  int32_t verdict;            /* MC_VERDICT_*                                              */
+  int32_t n_actions;          /* per-action statistics available via mc_action_stats      */
+  double collision_prob_optimistic;   /* TLC's "calculated (optimistic)" estimate          */
+  double collision_prob_observed;     /* from the minimum gap between fingerprints (or -1) */
+  double seconds_total;       /* mc_run wall time                                         */
+  double seconds_kernels;     /* sum of expand-kernel times (HIP events)                   */
+  uint64_t fp_seed;
+  double algo_bytes;           /* expand-kernel algorithmic bytes, SURVEY.md §8d: F*S + G_in*8 + D*(16+S) */
+  int64_t generated_in_model;  /* successors that passed every state constraint (G_in)  */
+  int32_t state_bytes;         /* S: stored bytes per packed state                      */
+  int32_t n_launches;          /* expand-kernel launches (BFS levels expanded)          */
+  char violated[64];          /* property name for INVARIANT_VIOLATION                     */
+  char spec[32];              /* "raft_original" | "tlc_membership"                        */
+} mc_summary_t;
+
+/* Fill opts with defaults. */
+void mc_default_opts(mc_opts* o);
+
+/* Load a spec module (.tla) and a TLC model config (.cfg); no GPU work yet. */
+int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx** out);
+
+/* Breadth-first model checking on the GPU until completion, violation or error. */
+int mc_run(mc_ctx* ctx);
+
+/* Summary of the last mc_run. */
+int mc_summary(const mc_ctx* ctx, mc_summary_t* out);
+
+/* Per-action statistics: name and (generated, distinct) counts, 0 <= k < n_actions. */
+int mc_action_stats(const mc_ctx* ctx, int32_t k, const char** name, int64_t* generated, int64_t* distinct);
+
+/* Per-BFS-level statistics of the last run, 0 <= level < depth. */
+int mc_level_stats(const mc_ctx* ctx, int32_t level, int64_t* states, int64_t* generated, double* kernel_ms);
+
+/* Counterexample (TLC "State k:" blocks) as text; caller frees with mc_free. */
+int mc_trace(const mc_ctx* ctx, char** text, size_t* len);
+
+/* Full TLC-style report (summary + trace) as text; caller frees with mc_free. */
+int mc_report(const mc_ctx* ctx, char** text, size_t* len);
+
+/* Write every distinct state, one canonical TLA+ line each, to path (parity tests). */
+int mc_dump_states(const mc_ctx* ctx, const char* path);
+
+/* Resolved model (spec family, constants, shape, compiled predicates) as JSON text; no GPU needed. */
+int mc_describe(const mc_ctx* ctx, char** text, size_t* len);
+
+/* TLC-like process exit code for the verdict (0 ok, 12 safety, 11 deadlock, 75 error). */
+int mc_exit_code(const mc_ctx* ctx);
+
+void mc_free(void* p);
+void mc_close(mc_ctx* ctx);
+const char* mc_last_error(const mc_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAFTMC_H */

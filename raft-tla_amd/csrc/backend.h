@@ -1,0 +1,53 @@
+// raftmc host: the interface between the C ABI (mc_api.cpp) and a compiled
+// spec backend (one per spec family; each owns its GPU buffers and kernels).
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "model.h"
+
+namespace rmc {
+
+struct RunOpts {
+  int device = 0;
+  uint64_t fp_table_bytes = 0, state_store_bytes = 0;
+  int64_t max_depth = 0;
+  uint64_t seed = 0;
+  bool inv_out_of_model = true;
+  bool check_deadlock = false;
+  int block_size = 256;
+};
+
+struct LevelStat { int64_t states = 0, generated = 0; double kernel_ms = 0; };
+
+struct RunResult {
+  int64_t generated = 0, distinct = 0, left_on_queue = 0, depth = 0;
+  int verdict = 0;                       // MC_VERDICT_*
+  std::string violated, error;
+  std::vector<std::string> action_names;
+  std::vector<int64_t> act_generated, act_distinct;
+  std::vector<LevelStat> levels;
+  std::vector<std::pair<std::string, std::string>> trace;   // (action label, multi-line state text)
+  double seconds_total = 0, seconds_kernels = 0;
+  double collision_optimistic = 0, collision_observed = -1;
+  uint64_t seed = 0;
+  // algorithmic byte accounting of the expand kernel
+  double algo_bytes = 0;                 // F*S + G_in*8 + D*(8+8+S) summed over levels
+  int64_t generated_in_model = 0;
+  int state_bytes = 0;
+  int n_launches = 0;
+};
+
+struct Backend {
+  virtual ~Backend() {}
+  virtual std::string family() const = 0;
+  virtual std::string describe_json() const = 0;
+  virtual int run(const RunOpts& o, RunResult& r, std::string& err) = 0;
+  virtual int dump_states(const std::string& path, std::string& err) = 0;
+};
+
+Backend* make_orig_backend(const CfgFile& cfg);   // throws CfgError
+
+}  // namespace rmc

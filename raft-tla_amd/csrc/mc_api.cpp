@@ -1,0 +1,210 @@
+// raftmc — C ABI implementation (include/raftmc.h).  Parses the .tla/.cfg,
+// picks the compiled spec backend, drives mc_run and renders TLC-style text.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <sstream>
+#include <string>
+
+#include "../../include/raftmc.h"
+#include "backend.h"
+#include "model.h"
+
+struct mc_ctx {
+  std::unique_ptr<rmc::Backend> be;
+  rmc::RunOpts ro;
+  rmc::RunResult res;
+  bool ran = false;
+  std::string last_error, tla_path, cfg_path;
+};
+
+namespace {
+char* dup_text(const std::string& s, size_t* len) {
+  char* p = (char*)std::malloc(s.size() + 1);
+  if (!p) return nullptr;
+  std::memcpy(p, s.c_str(), s.size() + 1);
+  if (len) *len = s.size();
+  return p;
+}
+const char* verdict_name(int v) {
+  switch (v) {
+    case MC_VERDICT_OK: return "OK";
+    case MC_VERDICT_INVARIANT_VIOLATION: return "INVARIANT_VIOLATION";
+    case MC_VERDICT_EVAL_ERROR: return "EVAL_ERROR";
+    case MC_VERDICT_CAPACITY_OVERFLOW: return "CAPACITY_OVERFLOW";
+    case MC_VERDICT_DEADLOCK: return "DEADLOCK";
+    case MC_VERDICT_DEPTH_LIMIT: return "DEPTH_LIMIT";
+  }
+  return "?";
+}
+std::string trace_text(const rmc::RunResult& r) {
+  std::ostringstream o;
+  for (size_t k = 0; k < r.trace.size(); ++k) {
+    o << "State " << (k + 1) << ": " << (k == 0 ? "<Initial predicate>" : "<" + r.trace[k].first + ">") << "\n";
+    o << r.trace[k].second << "\n\n";
+  }
+  return o.str();
+}
+}  // namespace
+
+extern "C" {
+
+void mc_default_opts(mc_opts* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof *o);
+  o->abi_version = RAFTMC_ABI_VERSION;
+  o->n_gpus = 1;
+  o->workers = 1;
+  o->tlc_compat_flags = MC_COMPAT_INV_OUT_OF_MODEL;
+  o->check_deadlock = 1;
+  o->block_size = 256;
+}
+
+int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx** out) {
+  if (!tla_path || !cfg_path || !out) return MC_E_INVALID;
+  *out = nullptr;
+  auto* c = new mc_ctx();
+  c->tla_path = tla_path; c->cfg_path = cfg_path;
+  mc_opts d; mc_default_opts(&d);
+  if (!o) o = &d;
+  if (o->abi_version != RAFTMC_ABI_VERSION) { delete c; return MC_E_INVALID; }
+  if (o->n_gpus != 1) { delete c; return MC_E_UNSUPPORTED; }
+  c->ro.device = o->device;
+  c->ro.fp_table_bytes = o->fp_table_bytes;
+  c->ro.state_store_bytes = o->state_store_bytes;
+  c->ro.max_depth = o->max_depth;
+  c->ro.seed = o->seed;
+  c->ro.inv_out_of_model = (o->tlc_compat_flags & MC_COMPAT_INV_OUT_OF_MODEL) != 0;
+  c->ro.check_deadlock = o->check_deadlock != 0;
+  c->ro.block_size = o->block_size ? o->block_size : 256;
+  try {
+    std::string fam = rmc::detect_spec_family(rmc::read_text_file(tla_path));
+    rmc::CfgFile cfg = rmc::parse_cfg_text(rmc::read_text_file(cfg_path));
+    if (fam == "raft_original") c->be.reset(rmc::make_orig_backend(cfg));
+    else throw rmc::CfgError(MC_E_UNSUPPORTED, "spec family '" + fam + "' has no GPU backend in this build (raft_original only)");
+  } catch (const rmc::CfgError& e) {
+    c->last_error = e.what();
+    int code = e.code;
+    *out = c;   // handle kept so mc_last_error can explain; caller must mc_close
+    return code;
+  } catch (const std::exception& e) {
+    c->last_error = e.what();
+    *out = c;
+    return MC_E_PARSE;
+  }
+  *out = c;
+  return MC_OK;
+}
+
+int mc_run(mc_ctx* c) {
+  if (!c) return MC_E_INVALID;
+  if (!c->be) return MC_E_STATE;
+  std::string err;
+  int rc = c->be->run(c->ro, c->res, err);
+  c->last_error = err.empty() ? c->res.error : err;
+  c->ran = rc == 0;
+  return rc;
+}
+
+int mc_summary(const mc_ctx* c, mc_summary_t* s) {
+  if (!c || !s) return MC_E_INVALID;
+  if (!c->ran) return MC_E_STATE;
+  std::memset(s, 0, sizeof *s);
+  const auto& r = c->res;
+  s->generated = r.generated; s->distinct = r.distinct; s->left_on_queue = r.left_on_queue; s->depth = r.depth;
+  s->verdict = r.verdict; s->n_actions = (int32_t)r.action_names.size();
+  s->collision_prob_optimistic = r.collision_optimistic; s->collision_prob_observed = r.collision_observed;
+  s->seconds_total = r.seconds_total; s->seconds_kernels = r.seconds_kernels; s->fp_seed = r.seed;
+  s->algo_bytes = r.algo_bytes; s->generated_in_model = r.generated_in_model; s->state_bytes = r.state_bytes;
+  s->n_launches = r.n_launches;
+  std::snprintf(s->violated, sizeof s->violated, "%s", r.violated.c_str());
+  std::snprintf(s->spec, sizeof s->spec, "%s", c->be->family().c_str());
+  return MC_OK;
+}
+
+int mc_action_stats(const mc_ctx* c, int32_t k, const char** name, int64_t* gen, int64_t* dist) {
+  if (!c) return MC_E_INVALID;
+  if (!c->ran) return MC_E_STATE;
+  if (k < 0 || k >= (int32_t)c->res.action_names.size()) return MC_E_INVALID;
+  if (name) *name = c->res.action_names[k].c_str();
+  if (gen) *gen = c->res.act_generated[k];
+  if (dist) *dist = c->res.act_distinct[k];
+  return MC_OK;
+}
+
+int mc_level_stats(const mc_ctx* c, int32_t level, int64_t* states, int64_t* gen, double* ms) {
+  if (!c) return MC_E_INVALID;
+  if (!c->ran) return MC_E_STATE;
+  if (level < 0 || level >= (int32_t)c->res.levels.size()) return MC_E_INVALID;
+  const auto& l = c->res.levels[level];
+  if (states) *states = l.states;
+  if (gen) *gen = l.generated;
+  if (ms) *ms = l.kernel_ms;
+  return MC_OK;
+}
+
+int mc_trace(const mc_ctx* c, char** text, size_t* len) {
+  if (!c || !text) return MC_E_INVALID;
+  if (!c->ran) return MC_E_STATE;
+  *text = dup_text(trace_text(c->res), len);
+  return *text ? MC_OK : MC_E_OOM;
+}
+
+int mc_report(const mc_ctx* c, char** text, size_t* len) {
+  if (!c || !text) return MC_E_INVALID;
+  if (!c->ran) return MC_E_STATE;
+  const auto& r = c->res;
+  std::ostringstream o;
+  o << "raftmc (MI355X/gfx950) checking " << c->tla_path << " with " << c->cfg_path << "\n";
+  if (r.verdict == MC_VERDICT_INVARIANT_VIOLATION) {
+    o << "Error: Invariant " << r.violated << " is violated.\n";
+    o << "Error: The behavior up to this point is:\n" << trace_text(r);
+  } else if (r.verdict == MC_VERDICT_DEADLOCK) {
+    o << "Error: Deadlock reached.\nError: The behavior up to this point is:\n" << trace_text(r);
+  } else if (r.verdict == MC_VERDICT_EVAL_ERROR || r.verdict == MC_VERDICT_CAPACITY_OVERFLOW) {
+    o << "Error: " << r.error << "\n";
+  } else if (r.verdict == MC_VERDICT_OK) {
+    o << "Model checking completed. No error has been found.\n";
+    char buf[160];
+    std::snprintf(buf, sizeof buf, "  The probability of a fingerprint collision is calculated (optimistic): val = %.1E\n", r.collision_optimistic);
+    o << buf;
+  }
+  o << r.generated << " states generated, " << r.distinct << " distinct states found, " << r.left_on_queue << " states left on queue.\n";
+  o << "The depth of the complete state graph search is " << r.depth << ".\n";
+  o << "Verdict: " << verdict_name(r.verdict) << "\n";
+  *text = dup_text(o.str(), len);
+  return *text ? MC_OK : MC_E_OOM;
+}
+
+int mc_dump_states(const mc_ctx* c, const char* path) {
+  if (!c || !path) return MC_E_INVALID;
+  if (!c->ran) return MC_E_STATE;
+  std::string err;
+  int rc = c->be->dump_states(path, err);
+  if (rc) const_cast<mc_ctx*>(c)->last_error = err;
+  return rc;
+}
+
+int mc_describe(const mc_ctx* c, char** text, size_t* len) {
+  if (!c || !text) return MC_E_INVALID;
+  if (!c->be) return MC_E_STATE;
+  *text = dup_text(c->be->describe_json(), len);
+  return *text ? MC_OK : MC_E_OOM;
+}
+
+int mc_exit_code(const mc_ctx* c) {
+  if (!c || !c->ran) return 75;
+  switch (c->res.verdict) {
+    case MC_VERDICT_OK: case MC_VERDICT_DEPTH_LIMIT: return 0;
+    case MC_VERDICT_INVARIANT_VIOLATION: return 12;
+    case MC_VERDICT_DEADLOCK: return 11;
+    default: return 75;
+  }
+}
+
+void mc_free(void* p) { std::free(p); }
+void mc_close(mc_ctx* c) { delete c; }
+const char* mc_last_error(const mc_ctx* c) { return c ? c->last_error.c_str() : "null handle"; }
+
+}  // extern "C"

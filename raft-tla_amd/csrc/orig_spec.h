@@ -1,0 +1,559 @@
+// raftmc — thirdparty/raft_original.tla (Ongaro 2014) hand-compiled to a
+// fixed-width packed state, shared by the gfx950 kernels and the host decoder.
+//
+// Shape parameters (compile time): N servers, NV values, MT = MaxTerm,
+// ML = MaxLogLen, MK = MaxMsgDomain.  They come from the cfg (configs/*.cfg,
+// the MC wrapper configs/raft_original_mc.tla) and size every field; the
+// message-count range [MinMsgCount, MaxMsgCount] is a runtime parameter.
+//
+// Working state ("Work", registers): one scalar word per per-server array
+// (currentTerm, state, votedFor, commitIndex, votesResponded, votesGranted),
+// small per-row arrays for nextIndex/matchIndex/log/voterLog (read through
+// select chains, never scratch), the allLogs bitmap over the log universe,
+// and the elections / messages sets as sorted code arrays (~0 = empty slot).
+// Out-of-model successors may hold one transient extra log entry / message /
+// term, so working widths are one step wider than the packed (stored) ones.
+//
+// Canonical packed state: the concatenation of the fields below in a fixed
+// bit order; equal TLA+ states <=> equal packed words (sets/bags sorted,
+// unused slots zero).  Semantics cite raft_original.tla line numbers.
+#pragma once
+#include "common.h"
+
+namespace rmc {
+
+enum OrigAct {
+  OA_Restart, OA_Timeout, OA_RequestVote, OA_BecomeLeader, OA_ClientRequest, OA_AdvanceCommitIndex,
+  OA_AppendEntries, OA_UpdateTerm, OA_HandleRequestVoteRequest, OA_DropStaleResponse,
+  OA_HandleRequestVoteResponse, OA_HandleAppendEntriesRequest, OA_HandleAppendEntriesResponse,
+  OA_DuplicateMessage, OA_DropMessage, OA_NACT
+};
+static const char* const kOrigActNames[OA_NACT] = {
+    "Restart", "Timeout", "RequestVote", "BecomeLeader", "ClientRequest", "AdvanceCommitIndex",
+    "AppendEntries", "UpdateTerm", "HandleRequestVoteRequest", "DropStaleResponse",
+    "HandleRequestVoteResponse", "HandleAppendEntriesRequest", "HandleAppendEntriesResponse",
+    "DuplicateMessage", "DropMessage"};
+
+// constraint / invariant selection bits (resolved from cfg names on the host)
+enum { OC_BoundedTerms = 1, OC_BoundedLogs = 2, OC_BoundedMessages = 4 };
+enum { OI_ElectionSafety = 1, OI_LogMatching = 2, OI_NoLeader = 4 };
+static const char* const kOrigInvNames[3] = {"ElectionSafety", "LogMatching", "NoLeader"};
+
+// error flags raised by the successor function (TLC evaluation errors / capacity)
+enum { OE_EVAL_LOG_INDEX = 1, OE_CAP_ELECTIONS = 2, OE_CAP_COUNT = 4 };
+
+struct OrigRuntime {
+  int min_count, max_count;   // MinMsgCount..MaxMsgCount
+  u32 constraints;            // OC_* mask
+  u32 invariants;             // OI_* mask (cfg order kept on host)
+};
+
+template <int N_, int NV_, int MT_, int ML_, int MK_>
+struct Orig {
+  static constexpr int N = N_, NV = NV_, MT = MT_, ML = ML_, MK = MK_;
+  // ---- widths
+  static constexpr int SB = bits_for(N - 1);        // server id 0..N-1
+  static constexpr int VB = bits_for(N);            // votedFor 0..N (N = Nil)
+  static constexpr int TB = bits_for(MT + 1);       // terms 0..MT+1 (transient MT+1)
+  static constexpr int E = MT * NV;                 // entry kinds: (term, value)
+  static constexpr int EB = bits_for(E);            // entry code 0 (none) / 1..E
+  static constexpr int LLB = bits_for(ML + 1);      // working log length 0..ML+1
+  static constexpr int SLLB = bits_for(ML);         // stored log length 0..ML
+  static constexpr int CIB = bits_for(ML);          // commitIndex / matchIndex / indices 0..ML
+  static constexpr int NIB = bits_for(ML + 1);      // nextIndex 1..ML+1
+  static constexpr long long U = log_universe(E, ML);   // number of logs of length <= ML
+  static constexpr int LIB = bits_for(U - 1);       // log universe index 0..U-1
+  static constexpr int AW = (int)((U + 63) / 64);   // allLogs bitmap words
+  static constexpr int EMAX = MT;                   // elections capacity (one per (term, leader))
+  static constexpr int VLB = 1 + LIB;               // voterLog cell: present bit + log index
+  static constexpr int CNTB = 4;                    // message count field (count + 8)
+  // message code: type(2) term(TB) src(SB) dst(SB) payload
+  static constexpr int MP0 = 2 + TB + 2 * SB;
+  static constexpr int PAY_RVQ = TB + CIB, PAY_RVP = 1 + LIB, PAY_AEQ = CIB + TB + EB + LIB + CIB, PAY_AEP = 1 + CIB;
+  static constexpr int PAYB = PAY_AEQ > PAY_RVP ? (PAY_AEQ > PAY_RVQ ? PAY_AEQ : PAY_RVQ) : (PAY_RVP > PAY_RVQ ? PAY_RVP : PAY_RVQ);
+  static constexpr int MSGB = MP0 + (PAYB > PAY_AEP ? PAYB : PAY_AEP);
+  static constexpr int ENTB = MSGB + CNTB;          // bag entry width
+  static constexpr int ELB = TB + SB + LIB + N + N * VLB;   // election record width
+  // ---- packed (stored) layout
+  static constexpr int PBITS = N * TB + N * 2 + N * VB + N * CIB + N * N + N * N + N * N * NIB + N * N * CIB +
+                               N * (SLLB + ML * EB) + N * N * VLB + (int)U + EMAX * ELB + MK * ENTB;
+  static constexpr int NW = (PBITS + 31) / 32;      // u32 words per stored state
+  static constexpr int NI = 3 * N + 2 * N * N + N * NV + N + 3 * MK;   // action instances per state
+
+  static_assert(N >= 1 && N <= 7, "N");
+  static_assert(N * TB <= 32 && N * VB <= 32 && N * CIB <= 32 && N * N <= 32, "scalar field words");
+  static_assert(N * NIB <= 32 && N * CIB <= 32, "index rows");
+  static_assert(LLB + (ML + 1) * EB <= 32, "working log word");
+  static_assert(N * VLB <= 64, "voterLog row");
+  static_assert(MSGB + CNTB <= 64 && ELB <= 64, "message / election codes");
+
+  struct Work {
+    u32 term, st, voted, commit, vresp, vgrant;
+    Arr<u32, N> nexti, matchi, log;
+    Arr<u64, N> vl;
+    u64 allLogs[AW];
+    u64 el[EMAX];
+    Arr<u64, MK + 1> bag;
+  };
+  static constexpr u32 F = 0, C = 1, L = 2;   // Follower, Candidate, Leader
+
+  // ---------------------------------------------------------------- logs
+  RMC_HD static int llen(u32 lw) { return (int)(lw & lomask(LLB)); }
+  RMC_HD static int lent(u32 lw, int p) { return (int)((lw >> (LLB + p * EB)) & lomask(EB)); }   // 0-based p
+  RMC_HD static int eterm(int e) { return e == 0 ? 0 : (e - 1) / NV + 1; }
+  RMC_HD static int evalue(int e) { return (e - 1) % NV; }
+  RMC_HD static int ecode(int term, int v) { return (term - 1) * NV + v + 1; }
+  RMC_HD static int last_term(u32 lw) { int n = llen(lw); return n == 0 ? 0 : eterm(lent(lw, n - 1)); }
+  RMC_HD static u32 lappend(u32 lw, int e) {
+    int n = llen(lw);
+    lw |= (u32)e << (LLB + n * EB);
+    return (lw & ~(u32)lomask(LLB)) | (u32)(n + 1);
+  }
+  RMC_HD static u32 ldrop_last(u32 lw) {
+    int n = llen(lw);
+    lw &= ~((u32)lomask(EB) << (LLB + (n - 1) * EB));
+    return (lw & ~(u32)lomask(LLB)) | (u32)(n - 1);
+  }
+  // universe index of a log of length <= ML (mixed radix over entry codes)
+  RMC_HD static u32 lidx(u32 lw) {
+    int n = llen(lw);
+    u32 off = 0, pw = 1, d = 0;
+#pragma unroll
+    for (int k = 0; k < ML + 1; ++k) { if (k < n) { off += pw; pw *= (u32)E; } }
+#pragma unroll
+    for (int p = 0; p < ML + 1; ++p) if (p < n) d = d * (u32)E + (u32)(lent(lw, p) - 1);
+    return off + d;
+  }
+  // host: index -> working log
+  static u32 lfrom_idx(u32 idx) {
+    u32 off = 0, pw = 1; int n = 0;
+    while (n <= ML && idx >= off + pw) { off += pw; pw *= (u32)E; ++n; }
+    u32 d = idx - off, lw = 0;
+    int ent[ML + 2];
+    for (int p = n - 1; p >= 0; --p) { ent[p] = (int)(d % (u32)E) + 1; d /= (u32)E; }
+    for (int p = 0; p < n; ++p) lw = lappend(lw, ent[p]);
+    return lw;
+  }
+
+  // ---------------------------------------------------------------- messages
+  enum { RVQ = 0, RVP = 1, AEQ = 2, AEP = 3 };
+  RMC_HD static u64 mhdr(int type, int term, int src, int dst) {
+    return (u64)type | ((u64)term << 2) | ((u64)src << (2 + TB)) | ((u64)dst << (2 + TB + SB));
+  }
+  RMC_HD static int mtype(u64 c) { return (int)(c & 3); }
+  RMC_HD static int mterm(u64 c) { return (int)((c >> 2) & lomask(TB)); }
+  RMC_HD static int msrc(u64 c) { return (int)((c >> (2 + TB)) & lomask(SB)); }
+  RMC_HD static int mdst(u64 c) { return (int)((c >> (2 + TB + SB)) & lomask(SB)); }
+  RMC_HD static u64 mpay(u64 c, int off, int w) { return (c >> (MP0 + off)) & lomask(w); }
+  RMC_HD static u64 m_rvq(int term, int llt, int lli, int src, int dst) {
+    return mhdr(RVQ, term, src, dst) | ((u64)llt << MP0) | ((u64)lli << (MP0 + TB));
+  }
+  RMC_HD static u64 m_rvp(int term, bool granted, u32 logidx, int src, int dst) {
+    return mhdr(RVP, term, src, dst) | ((u64)granted << MP0) | ((u64)logidx << (MP0 + 1));
+  }
+  RMC_HD static u64 m_aeq(int term, int pli, int plt, int entry, u32 logidx, int commit, int src, int dst) {
+    return mhdr(AEQ, term, src, dst) | ((u64)pli << MP0) | ((u64)plt << (MP0 + CIB)) | ((u64)entry << (MP0 + CIB + TB)) |
+           ((u64)logidx << (MP0 + CIB + TB + EB)) | ((u64)commit << (MP0 + CIB + TB + EB + LIB));
+  }
+  RMC_HD static u64 m_aep(int term, bool success, int mmi, int src, int dst) {
+    return mhdr(AEP, term, src, dst) | ((u64)success << MP0) | ((u64)mmi << (MP0 + 1));
+  }
+  // bag entries: code << CNTB | (count + 8); ~0 = empty; kept sorted ascending
+  static constexpr u64 EMPTY = ~0ull;
+  RMC_HD static u64 ecode_of(u64 ent) { return ent >> CNTB; }
+  RMC_HD static int ecount(u64 ent) { return (int)(ent & lomask(CNTB)) - 8; }
+  // WithMessage (raft_original.tla:106-110)
+  RMC_HD static void with_msg(Arr<u64, MK + 1>& bag, u64 code, u32& err) {
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < MK + 1; ++k) {
+      if (bag.v[k] != EMPTY && ecode_of(bag.v[k]) == code) {
+        found = true;
+        int c = ecount(bag.v[k]) + 1;
+        if (c > 7) err |= OE_CAP_COUNT;
+        bag.v[k] = (code << CNTB) | (u64)(c + 8);
+      }
+    }
+    if (!found) {
+      const u64 x = (code << CNTB) | (u64)(1 + 8);
+      if (bag.v[MK] != EMPTY) err |= OE_CAP_COUNT;   // cannot happen from an in-model pre-state
+      u64 prev = 0; bool prev_lt = true;
+#pragma unroll
+      for (int k = 0; k < MK + 1; ++k) {
+        const u64 cur = bag.v[k];
+        const bool cur_lt = cur < x;
+        bag.v[k] = cur_lt ? cur : (prev_lt ? x : prev);
+        prev = cur; prev_lt = cur_lt;
+      }
+    }
+  }
+  // WithoutMessage (raft_original.tla:114-118): decrement, entry stays (G1)
+  RMC_HD static void without_msg(Arr<u64, MK + 1>& bag, u64 code, u32& err) {
+#pragma unroll
+    for (int k = 0; k < MK + 1; ++k) {
+      if (bag.v[k] != EMPTY && ecode_of(bag.v[k]) == code) {
+        int c = ecount(bag.v[k]) - 1;
+        if (c < -8) err |= OE_CAP_COUNT;
+        bag.v[k] = (code << CNTB) | (u64)(c + 8);
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- per-server fields
+  RMC_HD static int g_term(const Work& s, int i) { return (int)fget<TB>(s.term, i); }
+  RMC_HD static int g_st(const Work& s, int i) { return (int)fget<2>(s.st, i); }
+  RMC_HD static int g_voted(const Work& s, int i) { return (int)fget<VB>(s.voted, i); }
+  RMC_HD static int g_commit(const Work& s, int i) { return (int)fget<CIB>(s.commit, i); }
+  RMC_HD static u32 row_bits(u32 x, int i) { return (x >> (i * N)) & (u32)lomask(N); }
+  RMC_HD static void set_row_bits(u32& x, int i, u32 v) { fset<N>(x, i, v); }
+  RMC_HD static int g_ni(const Work& s, int i, int j) { return (int)fget<NIB>(sel(s.nexti, i), j); }
+  RMC_HD static int g_mi(const Work& s, int i, int j) { return (int)fget<CIB>(sel(s.matchi, i), j); }
+  RMC_HD static void s_ni(Work& t, int i, int j, int v) { u32 r = sel(t.nexti, i); fset<NIB>(r, j, (u32)v); put(t.nexti, i, r); }
+  RMC_HD static void s_mi(Work& t, int i, int j, int v) { u32 r = sel(t.matchi, i); fset<CIB>(r, j, (u32)v); put(t.matchi, i, r); }
+
+  // ---------------------------------------------------------------- Init (raft_original.tla:139-159)
+  RMC_HD static void init(Work& s) {
+    s.term = fsplat<TB, u32>(1, N); s.st = 0; s.voted = fsplat<VB, u32>((u32)N, N); s.commit = 0;
+    s.vresp = 0; s.vgrant = 0;
+    for (int i = 0; i < N; ++i) { s.nexti.v[i] = fsplat<NIB, u32>(1, N); s.matchi.v[i] = 0; s.log.v[i] = 0; s.vl.v[i] = 0; }
+    for (int k = 0; k < AW; ++k) s.allLogs[k] = 0;
+    for (int k = 0; k < EMAX; ++k) s.el[k] = EMPTY;
+    for (int k = 0; k < MK + 1; ++k) s.bag.v[k] = EMPTY;
+  }
+
+  // allLogs' = allLogs \cup {log[i] : i \in Server} (raft_original.tla:464, G3): same for every successor
+  RMC_HD static void all_logs_next(const Work& s, u64 (&al)[AW]) {
+#pragma unroll
+    for (int k = 0; k < AW; ++k) al[k] = s.allLogs[k];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const u32 ix = lidx(s.log.v[i]);
+#pragma unroll
+      for (int k = 0; k < AW; ++k) if ((int)(ix >> 6) == k) al[k] |= 1ull << (ix & 63);
+    }
+  }
+
+  // ---------------------------------------------------------------- instance -> successor
+  // Returns the OrigAct id of the successor written to t, or -1 when instance
+  // k is disabled in s.  Instances (uniform across a wave): Restart(i) N,
+  // Timeout(i) N, RequestVote(i,j) N^2, BecomeLeader(i) N, ClientRequest(i,v)
+  // N*NV, AdvanceCommitIndex(i) N, AppendEntries(i,j) N^2, Receive(slot) MK,
+  // DuplicateMessage(slot) MK, DropMessage(slot) MK (Next, :453-462).
+  RMC_HD static int apply(const Work& s, int k, Work& t, u32& err) {
+    t = s;
+    if (k < N) {                                                   // Restart(i) :166-174
+      const int i = k;
+      fset<2>(t.st, i, F);
+      set_row_bits(t.vresp, i, 0); set_row_bits(t.vgrant, i, 0);
+      put(t.vl, i, (u64)0);
+      put(t.nexti, i, fsplat<NIB, u32>(1, N));
+      put(t.matchi, i, (u32)0);
+      fset<CIB>(t.commit, i, 0u);
+      return OA_Restart;
+    }
+    k -= N;
+    if (k < N) {                                                   // Timeout(i) :177-186
+      const int i = k, st = g_st(s, i);
+      if (!(st == F || st == C)) return -1;
+      fset<2>(t.st, i, C);
+      fset<TB>(t.term, i, (u32)(g_term(s, i) + 1));
+      fset<VB>(t.voted, i, (u32)N);
+      set_row_bits(t.vresp, i, 0); set_row_bits(t.vgrant, i, 0);
+      put(t.vl, i, (u64)0);
+      return OA_Timeout;
+    }
+    k -= N;
+    if (k < N * N) {                                               // RequestVote(i, j) :189-198
+      const int i = k / N, j = k % N;
+      if (g_st(s, i) != C) return -1;
+      if ((row_bits(s.vresp, i) >> j) & 1u) return -1;
+      const u32 li = sel(s.log, i);
+      with_msg(t.bag, m_rvq(g_term(s, i), last_term(li), llen(li), i, j), err);
+      return OA_RequestVote;
+    }
+    k -= N * N;
+    if (k < N) {                                                   // BecomeLeader(i) :228-242
+      const int i = k;
+      if (g_st(s, i) != C) return -1;
+      const u32 vg = row_bits(s.vgrant, i);
+      if (!(popc32(vg) * 2 > N)) return -1;
+      fset<2>(t.st, i, L);
+      const u32 li = sel(s.log, i);
+      put(t.nexti, i, fsplat<NIB, u32>((u32)(llen(li) + 1), N));
+      put(t.matchi, i, (u32)0);
+      const u64 rec = (u64)g_term(s, i) | ((u64)i << TB) | ((u64)lidx(li) << (TB + SB)) | ((u64)vg << (TB + SB + LIB)) |
+                      (sel(s.vl, i) << (TB + SB + LIB + N));
+      set_insert(t.el, rec, err);
+      return OA_BecomeLeader;
+    }
+    k -= N;
+    if (k < N * NV) {                                              // ClientRequest(i, v) :245-252
+      const int i = k / NV, v = k % NV;
+      if (g_st(s, i) != L) return -1;
+      put(t.log, i, lappend(sel(s.log, i), ecode(g_term(s, i), v)));
+      return OA_ClientRequest;
+    }
+    k -= N * NV;
+    if (k < N) {                                                   // AdvanceCommitIndex(i) :258-275
+      const int i = k;
+      if (g_st(s, i) != L) return -1;
+      const u32 li = sel(s.log, i), mrow = sel(s.matchi, i);
+      const int n = llen(li);
+      int best = 0;
+#pragma unroll
+      for (int index = 1; index <= ML + 1; ++index) {
+        if (index > n) continue;
+        u32 agree = 1u << i;                                       // Agree(index) == {i} \cup {k : matchIndex[i][k] >= index}
+#pragma unroll
+        for (int q = 0; q < N; ++q) if ((int)fget<CIB>(mrow, q) >= index) agree |= 1u << q;
+        if (popc32(agree) * 2 > N) best = index;                   // Max(agreeIndexes)
+      }
+      int nci = g_commit(s, i);
+      if (best > 0 && eterm(lent(li, best - 1)) == g_term(s, i)) nci = best;
+      fset<CIB>(t.commit, i, (u32)nci);
+      return OA_AdvanceCommitIndex;
+    }
+    k -= N;
+    if (k < N * N) {                                               // AppendEntries(i, j) :203-225
+      const int i = k / N, j = k % N;
+      if (i == j || g_st(s, i) != L) return -1;
+      const u32 li = sel(s.log, i);
+      const int n = llen(li), ni = g_ni(s, i, j), pli = ni - 1;
+      int plt = 0;
+      if (pli > 0) {
+        if (pli > n) { err |= OE_EVAL_LOG_INDEX; return -1; }     // log[i][prevLogIndex] out of domain (unguarded :207-210)
+        plt = eterm(lent(li, pli - 1));
+      }
+      const int lastEntry = n < ni ? n : ni;
+      const int entry = (ni <= lastEntry) ? lent(li, ni - 1) : 0;  // SubSeq(log[i], nextIndex, lastEntry): <= 1 entry
+      const int ci = g_commit(s, i);
+      with_msg(t.bag, m_aeq(g_term(s, i), pli, plt, entry, lidx(li), ci < lastEntry ? ci : lastEntry, i, j), err);
+      return OA_AppendEntries;
+    }
+    k -= N * N;
+    if (k < MK) {                                                  // Receive(m) :420-435
+      const u64 ent = sel(s.bag, k);
+      if (ent == EMPTY) return -1;
+      return receive(s, ecode_of(ent), t, err);
+    }
+    k -= MK;
+    if (k < MK) {                                                  // DuplicateMessage(m) :442-444
+      const u64 ent = sel(s.bag, k);
+      if (ent == EMPTY) return -1;
+      with_msg(t.bag, ecode_of(ent), err);
+      return OA_DuplicateMessage;
+    }
+    k -= MK;
+    {                                                              // DropMessage(m) :447-449
+      const u64 ent = sel(s.bag, k);
+      if (ent == EMPTY) return -1;
+      without_msg(t.bag, ecode_of(ent), err);
+      return OA_DropMessage;
+    }
+  }
+
+  RMC_HD static void set_insert(u64 (&el)[EMAX], u64 x, u32& err) {   // elections' = elections \cup {x}
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) found |= el[k] == x;
+    if (found) return;
+    if (el[EMAX - 1] != EMPTY) { err |= OE_CAP_ELECTIONS; return; }
+    u64 prev = 0; bool prev_lt = true;
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) {
+      const u64 cur = el[k]; const bool cur_lt = cur < x;
+      el[k] = cur_lt ? cur : (prev_lt ? x : prev);
+      prev = cur; prev_lt = cur_lt;
+    }
+  }
+
+  // Receive(m): UpdateTerm excludes every handler (they need mterm <= currentTerm), so <= 1 successor.
+  RMC_HD static int receive(const Work& s, u64 m, Work& t, u32& err) {
+    const int i = mdst(m), j = msrc(m), mt = mterm(m), ct = g_term(s, i), ty = mtype(m);
+    if (mt > ct) {                                                 // UpdateTerm :405-411
+      fset<TB>(t.term, i, (u32)mt);
+      fset<2>(t.st, i, F);
+      fset<VB>(t.voted, i, (u32)N);
+      return OA_UpdateTerm;
+    }
+    const u32 li = sel(s.log, i);
+    const int n = llen(li);
+    if (ty == RVQ) {                                               // HandleRequestVoteRequest :283-302
+      const int llt = (int)mpay(m, 0, TB), lli = (int)mpay(m, TB, CIB), lt = last_term(li);
+      const bool logOk = llt > lt || (llt == lt && lli >= n);
+      const int vf = g_voted(s, i);
+      const bool grant = mt == ct && logOk && (vf == N || vf == j);
+      if (grant) fset<VB>(t.voted, i, (u32)j);
+      with_msg(t.bag, m_rvp(ct, grant, lidx(li), i, j), err);      // Reply (:128-129)
+      without_msg(t.bag, m, err);
+      return OA_HandleRequestVoteRequest;
+    }
+    if (ty == RVP) {
+      if (mt < ct) { without_msg(t.bag, m, err); return OA_DropStaleResponse; }   // :414-417
+      set_row_bits(t.vresp, i, row_bits(s.vresp, i) | (1u << j));                 // HandleRequestVoteResponse :306-320
+      if (mpay(m, 0, 1)) {
+        set_row_bits(t.vgrant, i, row_bits(s.vgrant, i) | (1u << j));
+        u64 row = sel(s.vl, i);
+        if (!((row >> (j * VLB)) & 1ull))                                         // voterLog[i] @@ (j :> m.mlog): left-biased
+          row |= ((mpay(m, 1, LIB) << 1) | 1ull) << (j * VLB);
+        put(t.vl, i, row);
+      }
+      without_msg(t.bag, m, err);
+      return OA_HandleRequestVoteResponse;
+    }
+    if (ty == AEQ) {                                               // HandleAppendEntriesRequest :326-388
+      const int pli = (int)mpay(m, 0, CIB), plt = (int)mpay(m, CIB, TB), ment = (int)mpay(m, CIB + TB, EB);
+      const int mci = (int)mpay(m, CIB + TB + EB + LIB, CIB);
+      const int st = g_st(s, i);
+      const bool logOk = pli == 0 || (pli > 0 && pli <= n && plt == eterm(lent(li, pli - 1)));
+      if (mt < ct || (st == F && !logOk)) {                        // reject request
+        with_msg(t.bag, m_aep(ct, false, 0, i, j), err);
+        without_msg(t.bag, m, err);
+        return OA_HandleAppendEntriesRequest;
+      }
+      if (st == C) { fset<2>(t.st, i, F); return OA_HandleAppendEntriesRequest; }   // return to follower state
+      if (st == F) {                                               // accept request (logOk)
+        const int index = pli + 1;
+        if (ment == 0 || (n >= index && eterm(lent(li, index - 1)) == eterm(ment))) {   // already done
+          fset<CIB>(t.commit, i, (u32)mci);
+          with_msg(t.bag, m_aep(ct, true, pli + (ment ? 1 : 0), i, j), err);
+          without_msg(t.bag, m, err);
+          return OA_HandleAppendEntriesRequest;
+        }
+        if (n >= index) { put(t.log, i, ldrop_last(li)); return OA_HandleAppendEntriesRequest; }   // conflict: remove 1 entry
+        if (n == pli) { put(t.log, i, lappend(li, ment)); return OA_HandleAppendEntriesRequest; }  // no conflict: append
+      }
+      return -1;                                                   // Leader in the same term: nothing enabled
+    }
+    // AppendEntriesResponse
+    if (mt < ct) { without_msg(t.bag, m, err); return OA_DropStaleResponse; }
+    {                                                              // HandleAppendEntriesResponse :392-402
+      const int mmi = (int)mpay(m, 1, CIB);
+      if (mpay(m, 0, 1)) { s_ni(t, i, j, mmi + 1); s_mi(t, i, j, mmi); }
+      else { const int ni = g_ni(s, i, j); s_ni(t, i, j, ni - 1 > 1 ? ni - 1 : 1); }
+      without_msg(t.bag, m, err);
+      return OA_HandleAppendEntriesResponse;
+    }
+  }
+
+  // ---------------------------------------------------------------- constraints (configs/raft_original_mc.tla)
+  RMC_HD static bool in_model(const Work& t, const OrigRuntime& rt) {
+    bool ok = true;
+    if (rt.constraints & OC_BoundedTerms) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) ok &= g_term(t, i) <= MT;
+    }
+    if (rt.constraints & OC_BoundedLogs) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) ok &= llen(t.log.v[i]) <= ML;
+    }
+    if (rt.constraints & OC_BoundedMessages) {
+      ok &= t.bag.v[MK] == EMPTY;
+#pragma unroll
+      for (int k = 0; k < MK; ++k) {
+        const int c = ecount(t.bag.v[k]);
+        ok &= t.bag.v[k] == EMPTY || (c >= rt.min_count && c <= rt.max_count);
+      }
+    }
+    return ok;
+  }
+
+  // ---------------------------------------------------------------- invariants; returns OI_* bit of the first violated (cfg order
+  // is applied on the host by the order mask), 0 if all hold
+  RMC_HD static u32 violated(const Work& t, u32 invs) {
+    u32 bad = 0;
+    if (invs & OI_ElectionSafety) {   // \A e, f \in elections : e.eterm = f.eterm => e.eleader = f.eleader
+      bool ok = true;
+#pragma unroll
+      for (int a = 0; a < EMAX; ++a)
+#pragma unroll
+        for (int b = a + 1; b < EMAX; ++b)
+          if (t.el[a] != EMPTY && t.el[b] != EMPTY && (t.el[a] & lomask(TB)) == (t.el[b] & lomask(TB)) &&
+              ((t.el[a] >> TB) & lomask(SB)) != ((t.el[b] >> TB) & lomask(SB)))
+            ok = false;
+      if (!ok) bad |= OI_ElectionSafety;
+    }
+    if (invs & OI_LogMatching) {      // \A i,j, n <= min: log[i][n].term = log[j][n].term => prefixes equal
+      bool ok = true;
+#pragma unroll
+      for (int a = 0; a < N; ++a)
+#pragma unroll
+        for (int b = a + 1; b < N; ++b) {
+          const u32 x = t.log.v[a], y = t.log.v[b];
+          const int nx = llen(x), ny = llen(y), mn = nx < ny ? nx : ny;
+          bool pref = true;   // entries 1..n-1 equal so far
+#pragma unroll
+          for (int p = 0; p < ML + 1; ++p) {
+            if (p < mn) {
+              const int ex = lent(x, p), ey = lent(y, p);
+              if (eterm(ex) == eterm(ey) && !(pref && ex == ey)) ok = false;
+              pref = pref && ex == ey;
+            }
+          }
+        }
+      if (!ok) bad |= OI_LogMatching;
+    }
+    if (invs & OI_NoLeader) {
+      bool ok = true;
+#pragma unroll
+      for (int i = 0; i < N; ++i) ok &= g_st(t, i) != L;
+      if (!ok) bad |= OI_NoLeader;
+    }
+    return bad;
+  }
+
+  // ---------------------------------------------------------------- pack / unpack (canonical stored form)
+  RMC_HD static void pack(const Work& t, u32 (&w)[NW]) {
+    BitOut<NW> o;
+    o.put(t.term, N * TB); o.put(t.st, N * 2); o.put(t.voted, N * VB); o.put(t.commit, N * CIB);
+    o.put(t.vresp, N * N); o.put(t.vgrant, N * N);
+#pragma unroll
+    for (int i = 0; i < N; ++i) o.put(t.nexti.v[i], N * NIB);
+#pragma unroll
+    for (int i = 0; i < N; ++i) o.put(t.matchi.v[i], N * CIB);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {     // stored log: len (SLLB) + ML entries
+      const u32 lw = t.log.v[i];
+      o.put((u64)(lw & lomask(LLB)), SLLB);
+      o.put((u64)(lw >> LLB) & lomask(ML * EB), ML * EB);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) o.put(t.vl.v[i], N * VLB);
+#pragma unroll
+    for (int k = 0; k < AW; ++k) o.put(t.allLogs[k], (k == AW - 1) ? (int)(U - 64 * (AW - 1)) : 64);
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) o.put(t.el[k] == EMPTY ? 0ull : t.el[k], ELB);
+#pragma unroll
+    for (int k = 0; k < MK; ++k) o.put(t.bag.v[k] == EMPTY ? 0ull : t.bag.v[k], ENTB);
+#pragma unroll
+    for (int k = 0; k < NW; ++k) w[k] = o.w[k];
+  }
+  template <int M>
+  RMC_HD static void unpack(const u32 (&w)[M], Work& t) {
+    static_assert(M >= NW, "packed array too small");
+    BitIn<M> in(w);
+    t.term = (u32)in.get(N * TB); t.st = (u32)in.get(N * 2); t.voted = (u32)in.get(N * VB); t.commit = (u32)in.get(N * CIB);
+    t.vresp = (u32)in.get(N * N); t.vgrant = (u32)in.get(N * N);
+#pragma unroll
+    for (int i = 0; i < N; ++i) t.nexti.v[i] = (u32)in.get(N * NIB);
+#pragma unroll
+    for (int i = 0; i < N; ++i) t.matchi.v[i] = (u32)in.get(N * CIB);
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const u32 len = (u32)in.get(SLLB);
+      const u32 ents = (u32)in.get(ML * EB);
+      t.log.v[i] = len | (ents << LLB);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) t.vl.v[i] = in.get(N * VLB);
+#pragma unroll
+    for (int k = 0; k < AW; ++k) t.allLogs[k] = in.get((k == AW - 1) ? (int)(U - 64 * (AW - 1)) : 64);
+#pragma unroll
+    for (int k = 0; k < EMAX; ++k) { const u64 x = in.get(ELB); t.el[k] = x ? x : EMPTY; }
+#pragma unroll
+    for (int k = 0; k < MK; ++k) { const u64 x = in.get(ENTB); t.bag.v[k] = x ? x : EMPTY; }
+    t.bag.v[MK] = EMPTY;
+  }
+};
+
+}  // namespace rmc

@@ -1,0 +1,58 @@
+// raftmc — command-line front end mirroring TLC's flags:
+//   raftmc [-config F.cfg] [-workers N] [-deadlock] [-depth D] [-device K]
+//          [-fptable BYTES] [-store BYTES] [-seed S] [-no-inv-oom] [-dump FILE] [-json] F.tla
+// Prints TLC-style lines and exits with TLC-like codes (0 ok, 12 safety
+// violation, 11 deadlock, 75 error).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "../../include/raftmc.h"
+
+int main(int argc, char** argv) {
+  mc_opts o;
+  mc_default_opts(&o);
+  std::string tla, cfg, dump;
+  bool json = false;
+  for (int a = 1; a < argc; ++a) {
+    std::string k = argv[a];
+    auto val = [&]() -> const char* {
+      if (a + 1 >= argc) { std::fprintf(stderr, "missing value for %s\n", k.c_str()); std::exit(2); }
+      return argv[++a];
+    };
+    if (k == "-config") cfg = val();
+    else if (k == "-workers") o.workers = std::atoi(val());
+    else if (k == "-deadlock") o.check_deadlock = 0;   // TLC: -deadlock turns deadlock checking OFF
+    else if (k == "-depth") o.max_depth = std::atoll(val());
+    else if (k == "-device") o.device = std::atoi(val());
+    else if (k == "-fptable") o.fp_table_bytes = std::strtoull(val(), nullptr, 10);
+    else if (k == "-store") o.state_store_bytes = std::strtoull(val(), nullptr, 10);
+    else if (k == "-seed") o.seed = std::strtoull(val(), nullptr, 0);
+    else if (k == "-no-inv-oom") o.tlc_compat_flags &= ~MC_COMPAT_INV_OUT_OF_MODEL;
+    else if (k == "-dump") dump = val();
+    else if (k == "-json") json = true;
+    else if (!k.empty() && k[0] == '-') { std::fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
+    else tla = k;
+  }
+  if (tla.empty()) { std::fprintf(stderr, "usage: raftmc [-config F.cfg] [options] F.tla\n"); return 2; }
+  if (cfg.empty()) { cfg = tla.substr(0, tla.size() > 4 ? tla.size() - 4 : tla.size()) + ".cfg"; }
+  mc_ctx* c = nullptr;
+  int rc = mc_open(tla.c_str(), cfg.c_str(), &o, &c);
+  if (rc) { std::fprintf(stderr, "raftmc: %s (code %d)\n", c ? mc_last_error(c) : "open failed", rc); mc_close(c); return 75; }
+  rc = mc_run(c);
+  if (rc) { std::fprintf(stderr, "raftmc: %s (code %d)\n", mc_last_error(c), rc); mc_close(c); return 75; }
+  char* text = nullptr; size_t len = 0;
+  mc_report(c, &text, &len);
+  std::fwrite(text, 1, len, stdout);
+  mc_free(text);
+  if (json) {
+    mc_summary_t s; mc_summary(c, &s);
+    std::printf("{\"verdict\": %d, \"generated\": %lld, \"distinct\": %lld, \"depth\": %lld, \"seconds\": %.6f, \"kernel_seconds\": %.6f}\n",
+                s.verdict, (long long)s.generated, (long long)s.distinct, (long long)s.depth, s.seconds_total, s.seconds_kernels);
+  }
+  if (!dump.empty() && mc_dump_states(c, dump.c_str())) std::fprintf(stderr, "raftmc: dump failed: %s\n", mc_last_error(c));
+  int ec = mc_exit_code(c);
+  mc_close(c);
+  return ec;
+}

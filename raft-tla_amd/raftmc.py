@@ -1,0 +1,198 @@
+"""Host-side mirror of TLC's model-checking contract over the raftmc C ABI.
+
+The reference path is TLC's command line:
+    java -cp tla2tools.jar tlc2.TLC [-workers N] [-config F.cfg] [-deadlock] F.tla
+This module exposes the same arguments with the same meaning:
+
+    res = check("configs/raft_original_mc.tla", config="configs/c2.cfg")
+    res.distinct, res.generated, res.depth, res.verdict, res.trace_text
+    tlc_main(["-config", "c2.cfg", "raft_original_mc.tla"])   # TLC-style stdout + exit code
+
+Every call goes to libraftmc.so (HIP kernels for gfx950).  There is no CPU
+fallback: without the built library or a usable GPU the calls raise.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libraftmc.so")
+ABI_VERSION = 1
+
+VERDICTS = {0: "OK", 1: "INVARIANT_VIOLATION", 2: "EVAL_ERROR", 3: "CAPACITY_OVERFLOW", 4: "DEADLOCK", 5: "DEPTH_LIMIT"}
+MC_COMPAT_INV_OUT_OF_MODEL = 0x1
+
+# every symbol include/raftmc.h declares
+EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stats", "mc_level_stats",
+           "mc_trace", "mc_report", "mc_dump_states", "mc_describe", "mc_exit_code", "mc_free",
+           "mc_close", "mc_last_error"]
+
+
+class McOpts(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("device", ctypes.c_int32), ("n_gpus", ctypes.c_int32),
+                ("workers", ctypes.c_int32), ("fp_table_bytes", ctypes.c_uint64),
+                ("state_store_bytes", ctypes.c_uint64), ("max_depth", ctypes.c_int64), ("seed", ctypes.c_uint64),
+                ("tlc_compat_flags", ctypes.c_uint32), ("check_deadlock", ctypes.c_int32),
+                ("block_size", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7)]
+
+
+class McSummary(ctypes.Structure):
+    _fields_ = [("generated", ctypes.c_int64), ("distinct", ctypes.c_int64), ("left_on_queue", ctypes.c_int64),
+                ("depth", ctypes.c_int64), ("verdict", ctypes.c_int32), ("n_actions", ctypes.c_int32),
+                ("collision_prob_optimistic", ctypes.c_double), ("collision_prob_observed", ctypes.c_double),
+                ("seconds_total", ctypes.c_double), ("seconds_kernels", ctypes.c_double),
+                ("fp_seed", ctypes.c_uint64), ("algo_bytes", ctypes.c_double),
+                ("generated_in_model", ctypes.c_int64), ("state_bytes", ctypes.c_int32), ("n_launches", ctypes.c_int32),
+                ("violated", ctypes.c_char * 64), ("spec", ctypes.c_char * 32)]
+
+
+class RaftMCError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("raftmc error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libraftmc.so (raises if it has not been built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RaftMCError(-5, "libraftmc.so not built at %s (run __graft_entry__.build())" % path)
+    lib = ctypes.CDLL(path)
+    P = ctypes.c_void_p
+    lib.mc_default_opts.argtypes = [ctypes.POINTER(McOpts)]
+    lib.mc_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(McOpts), ctypes.POINTER(P)]
+    lib.mc_run.argtypes = [P]
+    lib.mc_summary.argtypes = [P, ctypes.POINTER(McSummary)]
+    lib.mc_action_stats.argtypes = [P, ctypes.c_int32, ctypes.POINTER(ctypes.c_char_p),
+                                    ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
+    lib.mc_level_stats.argtypes = [P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64),
+                                   ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]
+    for f in ("mc_trace", "mc_report", "mc_describe"):
+        getattr(lib, f).argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
+    lib.mc_dump_states.argtypes = [P, ctypes.c_char_p]
+    lib.mc_exit_code.argtypes = [P]
+    lib.mc_free.argtypes = [P]
+    lib.mc_close.argtypes = [P]
+    lib.mc_last_error.argtypes = [P]
+    lib.mc_last_error.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+class Result:
+    """Outcome of one model-checking run (TLC's summary lines + trace)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    def __repr__(self):
+        return "Result(verdict=%s, generated=%d, distinct=%d, depth=%d)" % (
+            self.verdict, self.generated, self.distinct, self.depth)
+
+
+class ModelChecker:
+    """One raftmc handle: mc_open on construction, mc_run in run()."""
+
+    def __init__(self, spec, config=None, workers=1, deadlock=True, device=0, max_depth=0,
+                 fp_table_bytes=0, state_store_bytes=0, seed=0, inv_out_of_model=True):
+        self.lib = load_library()
+        if config is None:
+            config = spec[:-4] + ".cfg" if spec.endswith(".tla") else spec + ".cfg"
+        o = McOpts()
+        self.lib.mc_default_opts(ctypes.byref(o))
+        o.device, o.workers, o.max_depth = device, workers, max_depth
+        o.fp_table_bytes, o.state_store_bytes, o.seed = fp_table_bytes, state_store_bytes, seed
+        o.check_deadlock = 1 if deadlock else 0
+        o.tlc_compat_flags = MC_COMPAT_INV_OUT_OF_MODEL if inv_out_of_model else 0
+        self.h = ctypes.c_void_p()
+        rc = self.lib.mc_open(spec.encode(), config.encode(), ctypes.byref(o), ctypes.byref(self.h))
+        if rc:
+            msg = self.lib.mc_last_error(self.h).decode() if self.h else "open failed"
+            self.close()
+            raise RaftMCError(rc, msg)
+
+    def _text(self, fn):
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        rc = fn(self.h, ctypes.byref(p), ctypes.byref(n))
+        if rc:
+            raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
+        s = ctypes.string_at(p, n.value).decode()
+        self.lib.mc_free(p)
+        return s
+
+    def describe(self):
+        import json
+        return json.loads(self._text(self.lib.mc_describe))
+
+    def run(self):
+        rc = self.lib.mc_run(self.h)
+        if rc:
+            raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
+        s = McSummary()
+        self.lib.mc_summary(self.h, ctypes.byref(s))
+        actions = {}
+        for k in range(s.n_actions):
+            name, g, d = ctypes.c_char_p(), ctypes.c_int64(), ctypes.c_int64()
+            self.lib.mc_action_stats(self.h, k, ctypes.byref(name), ctypes.byref(g), ctypes.byref(d))
+            actions[name.value.decode()] = [g.value, d.value]
+        levels = []
+        for k in range(s.depth):
+            st, g, ms = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
+            if self.lib.mc_level_stats(self.h, k, ctypes.byref(st), ctypes.byref(g), ctypes.byref(ms)) == 0:
+                levels.append((st.value, g.value, ms.value))
+        return Result(verdict=VERDICTS.get(s.verdict, str(s.verdict)), generated=s.generated, distinct=s.distinct,
+                      left_on_queue=s.left_on_queue, depth=s.depth, violated=s.violated.decode(),
+                      spec=s.spec.decode(), actions=actions, levels=levels,
+                      collision_prob_optimistic=s.collision_prob_optimistic,
+                      seconds=s.seconds_total, kernel_seconds=s.seconds_kernels, fp_seed=s.fp_seed,
+                      algo_bytes=s.algo_bytes, generated_in_model=s.generated_in_model,
+                      state_bytes=s.state_bytes, n_launches=s.n_launches,
+                      trace_text=self._text(self.lib.mc_trace), report=self._text(self.lib.mc_report),
+                      error=self.lib.mc_last_error(self.h).decode(),
+                      exit_code=self.lib.mc_exit_code(self.h))
+
+    def dump_states(self, path):
+        rc = self.lib.mc_dump_states(self.h, path.encode())
+        if rc:
+            raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None) and self.h:
+            self.lib.mc_close(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+def check(spec, config=None, **kw):
+    """Model-check `spec` with `config` (TLC: tlc2.TLC -config config spec)."""
+    with ModelChecker(spec, config, **kw) as mc:
+        return mc.run()
+
+
+def tlc_main(argv):
+    """TLC-compatible argv entry point; prints the report, returns TLC's exit code."""
+    spec, config, kw = None, None, {}
+    it = iter(argv)
+    for a in it:
+        if a == "-config":
+            config = next(it)
+        elif a == "-workers":
+            kw["workers"] = int(next(it))
+        elif a == "-deadlock":
+            kw["deadlock"] = False
+        elif a == "-depth":
+            kw["max_depth"] = int(next(it))
+        else:
+            spec = a
+    res = check(spec, config, **kw)
+    print(res.report, end="")
+    return res.exit_code

@@ -1,0 +1,88 @@
+"""GPU parity tests (MI355X): the HIP path through the C ABI against the CPU
+oracle.  Integer/index work, so the bar is bit-exact: identical generated,
+distinct, depth, per-level and per-action counts, and the identical set of
+reachable states (SHA-256 of the sorted canonical TLA+ text of every state).
+"""
+import hashlib
+import json
+import os
+import tempfile
+
+import pytest
+
+from oracle_util import CONFIGS, GOLDEN, ORIG_MC
+
+pytestmark = pytest.mark.gpu
+
+SMALL = dict(fp_table_bytes=1 << 26, state_store_bytes=1 << 28)
+FIXTURES = json.load(open(os.path.join(GOLDEN, "orig_parity.json")))
+
+
+def states_sha(mc):
+    fd, path = tempfile.mkstemp(suffix=".txt")
+    os.close(fd)
+    mc.dump_states(path)
+    lines = sorted(l.rstrip("\n") for l in open(path))
+    os.unlink(path)
+    return hashlib.sha256("\n".join(lines).encode()).hexdigest(), len(lines)
+
+
+@pytest.mark.parametrize("name", sorted(FIXTURES))
+def test_parity_against_oracle(raftmc, name):
+    g = FIXTURES[name]
+    with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, name + ".cfg"), **SMALL) as mc:
+        r = mc.run()
+        sha, n = states_sha(mc)
+    assert r.verdict == "OK", r.error
+    assert (r.generated, r.distinct, r.depth) == (g["generated"], g["distinct"], g["depth"])
+    # per-action GENERATED counts are order-independent and must match exactly;
+    # per-action DISTINCT counts depend on which successor reaches a state first
+    # (TLC: FIFO order of one worker), so only their sum is compared here
+    assert {k: v[0] for k, v in r.actions.items()} == {k: v[0] for k, v in g["actions"].items()}
+    assert sum(v[1] for v in r.actions.values()) == g["distinct"] - 1
+    assert [lv[0] for lv in r.levels] == g["levels"]
+    assert n == g["distinct"] and sha == g["states_sha256"]
+
+
+def test_depth_limit_kat(raftmc):
+    # SURVEY.md §4 KAT: expanding Init gives generated 7, distinct 5
+    r = raftmc.check(ORIG_MC, os.path.join(CONFIGS, "c1.cfg"), max_depth=2, **SMALL)
+    assert (r.generated, r.distinct, r.verdict) == (7, 5, "DEPTH_LIMIT")
+
+
+def test_violation_shortest_trace(raftmc):
+    from oracle_util import run_oracle
+    cfg = os.path.join(CONFIGS, "scenario_first_leader.cfg")
+    ref = run_oracle("bfs", ORIG_MC, cfg, "--trace")
+    r = raftmc.check(ORIG_MC, cfg, **SMALL)
+    assert r.verdict == "INVARIANT_VIOLATION" and r.violated == "NoLeader" and r.exit_code == 12
+    states = r.trace_text.strip().split("\n\n")
+    assert len(states) == ref["trace_len"] == 10
+    # the trace starts in Init and ends in a state with a leader, reached by BecomeLeader
+    assert states[0].startswith("State 1: <Initial predicate>")
+    assert ref["trace"][0]["state"] == " ".join(states[0].split("\n")[1:])
+    assert "<BecomeLeader>" in states[-1].split("\n")[0] and "Leader" in states[-1]
+
+
+def test_seed_independence_c1(raftmc):
+    cfg = os.path.join(CONFIGS, "c1.cfg")
+    a = raftmc.check(ORIG_MC, cfg, seed=1, **SMALL)
+    b = raftmc.check(ORIG_MC, cfg, seed=0xABCDEF, **SMALL)
+    assert (a.generated, a.distinct, a.depth) == (b.generated, b.distinct, b.depth)
+
+
+def test_c2_full_size_properties(raftmc):
+    """BASELINE configs[1] at full size: order-independent counts (no VIEW in
+    raft_original) must not depend on the fingerprint seed or on re-use of
+    the handle; the level sizes sum to the distinct count."""
+    cfg = os.path.join(CONFIGS, "c2.cfg")
+    with raftmc.ModelChecker(ORIG_MC, cfg, seed=7) as mc:
+        a = mc.run()
+        b = mc.run()
+    c = raftmc.check(ORIG_MC, cfg, seed=0x1234567)
+    assert a.verdict == "OK", a.error
+    assert (a.generated, a.distinct, a.depth) == (b.generated, b.distinct, b.depth) == (c.generated, c.distinct, c.depth)
+    assert sum(lv[0] for lv in a.levels) == a.distinct
+    assert sum(v[1] for v in a.actions.values()) + 1 == a.distinct
+    assert sum(v[0] for v in a.actions.values()) + 1 == a.generated
+    assert a.collision_prob_optimistic < 1e-3

@@ -1,0 +1,70 @@
+"""CPU oracle pinned against the reference's own TLC output and derived KATs.
+
+The reference has no tests; its only machine-generated results are the two
+TLC traces pasted into tlc_membership/raft.tla:1201 and :1231 (fixtures in
+tests/golden/, made by tests/golden/make_golden.py).  Counts of state spaces
+are unpinned against TLC (not runnable offline).
+"""
+import json
+import os
+
+from oracle_util import CONFIGS, GOLDEN, MEMB_MC, ORIG_MC, golden_file, run_oracle
+
+
+def test_init_expansion_kat_original():
+    # SURVEY.md §4 KAT: from Init only Restart x3 and Timeout x3 are enabled;
+    # the three Restarts yield one state (only allLogs changes), so after
+    # expanding Init generated = 1 + 6 = 7 and distinct = 1 + 1 + 3 = 5.
+    r = run_oracle("bfs", ORIG_MC, os.path.join(CONFIGS, "c1.cfg"), "--max-depth", 2)
+    assert (r["generated"], r["distinct"]) == (7, 5)
+    assert r["actions"]["Restart"] == [3, 1] and r["actions"]["Timeout"] == [3, 3]
+
+
+def test_init_expansion_kat_membership():
+    # tlc_membership, shipped cfg: Restart successors of Init violate
+    # CleanStartUntilFirstRequest; the 3 Timeout successors are one orbit
+    # under SYMMETRY perms  =>  generated 7, distinct 2.
+    r = run_oracle("bfs", MEMB_MC, os.path.join(CONFIGS, "membership_shipped.cfg"), "--max-depth", 2)
+    assert (r["generated"], r["distinct"]) == (7, 2)
+
+
+def test_concurrent_leaders_trace_replays():
+    # raft.tla:1201: TLC's ConcurrentLeaders witness, history["global"] of length 20
+    path, doc = golden_file("concurrent_leaders_trace.json")
+    r = run_oracle("replay", MEMB_MC, os.path.join(CONFIGS, "membership_shipped.cfg"), "--golden", path)
+    assert r["found"] and r["golden_len"] == 20
+    # shortest behaviour producing it: 18 transitions (TLC's "State 19"), raft.tla:1179-1180
+    assert r["transitions"] == 18
+    st = r["state"]
+    assert "hadNumLeaders |-> 2" in st and "hadNumClientRequests |-> 0" in st
+    assert "s1 :> [restarted |-> 0, timeout |-> 1] @@ s2 :> [restarted |-> 0, timeout |-> 1] @@ s3 :> [restarted |-> 0, timeout |-> 0]" in st
+
+
+def test_commit_when_concurrent_leaders_trace_replays():
+    # raft.tla:1231: TLC's CommitWhenConcurrentLeaders witness, 28 history entries,
+    # with two ClientRequests (they add no history entry, G4) and an UpdateTerm.
+    path, doc = golden_file("commit_when_concurrent_leaders_trace.json")
+    r = run_oracle("replay", MEMB_MC, os.path.join(CONFIGS, "membership_shipped.cfg"), "--golden", path)
+    assert r["found"] and r["golden_len"] == 28
+    assert r["transitions"] == 27
+    assert r["actions"].count("ClientRequest") == 2
+    assert "hadNumClientRequests |-> 2" in r["state"]
+
+
+def test_original_parity_fixtures_reproduce():
+    doc = json.load(open(os.path.join(GOLDEN, "orig_parity.json")))
+    for name in ("c1", "parity_single", "parity_pair"):
+        r = run_oracle("bfs", ORIG_MC, os.path.join(CONFIGS, name + ".cfg"))
+        g = doc[name]
+        assert (r["generated"], r["distinct"], r["depth"]) == (g["generated"], g["distinct"], g["depth"]), name
+        assert r["actions"] == g["actions"], name
+
+
+def test_first_leader_shortest_witness():
+    # NoLeader (test-only scenario invariant) on 2 servers: Timeout, RequestVote x2,
+    # HandleRequestVoteRequest (self), UpdateTerm (peer), HandleRequestVoteRequest (peer),
+    # HandleRequestVoteResponse x2, BecomeLeader = 9 steps, 10 states
+    r = run_oracle("bfs", ORIG_MC, os.path.join(CONFIGS, "scenario_first_leader.cfg"), "--trace")
+    assert r["verdict"] == "INVARIANT_VIOLATION" and r["violated"] == "NoLeader"
+    assert r["trace_len"] == 10
+    assert r["trace"][-1]["action"] == "BecomeLeader"
