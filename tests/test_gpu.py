@@ -85,4 +85,5 @@ def test_c2_full_size_properties(raftmc):
     assert sum(lv[0] for lv in a.levels) == a.distinct
     assert sum(v[1] for v in a.actions.values()) + 1 == a.distinct
     assert sum(v[0] for v in a.actions.values()) + 1 == a.generated
-    assert a.collision_prob_optimistic < 1e-3
+    # TLC's "calculated (optimistic)" collision estimate: M * (N - M) / 2^64
+    assert a.collision_prob_optimistic == pytest.approx(a.distinct * (a.generated - a.distinct) / 2.0 ** 64)
