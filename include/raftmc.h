@@ -115,6 +115,10 @@ int mc_action_stats(const mc_ctx* ctx, int32_t k, const char** name, int64_t* ge
 /* Per-BFS-level statistics of the last run, 0 <= level < depth. */
 int mc_level_stats(const mc_ctx* ctx, int32_t level, int64_t* states, int64_t* generated, double* kernel_ms);
 
+/* Per-kernel statistics of the last run (HIP-event time summed over launches, algorithmic
+ * bytes per SURVEY.md §8d), 0 <= k < number of kernels; MC_E_INVALID past the last one. */
+int mc_kernel_stats(const mc_ctx* ctx, int32_t k, const char** name, double* ms, double* algo_bytes, int64_t* launches);
+
 /* Counterexample (TLC "State k:" blocks) as text; caller frees with mc_free. */
 int mc_trace(const mc_ctx* ctx, char** text, size_t* len);
 

@@ -21,6 +21,7 @@ struct RunOpts {
 };
 
 struct LevelStat { int64_t states = 0, generated = 0; double kernel_ms = 0; };
+struct KernelStat { std::string name; double ms = 0, algo_bytes = 0; int64_t launches = 0; };
 
 struct RunResult {
   int64_t generated = 0, distinct = 0, left_on_queue = 0, depth = 0;
@@ -38,6 +39,7 @@ struct RunResult {
   int64_t generated_in_model = 0;
   int state_bytes = 0;
   int n_launches = 0;
+  std::vector<KernelStat> kernels;       // per-kernel HIP-event time and algorithmic bytes
 };
 
 struct Backend {

@@ -144,6 +144,18 @@ int mc_level_stats(const mc_ctx* c, int32_t level, int64_t* states, int64_t* gen
   return MC_OK;
 }
 
+int mc_kernel_stats(const mc_ctx* c, int32_t k, const char** name, double* ms, double* algo_bytes, int64_t* launches) {
+  if (!c) return MC_E_INVALID;
+  if (!c->ran) return MC_E_STATE;
+  if (k < 0 || k >= (int32_t)c->res.kernels.size()) return MC_E_INVALID;
+  const auto& ks = c->res.kernels[k];
+  if (name) *name = ks.name.c_str();
+  if (ms) *ms = ks.ms;
+  if (algo_bytes) *algo_bytes = ks.algo_bytes;
+  if (launches) *launches = ks.launches;
+  return MC_OK;
+}
+
 int mc_trace(const mc_ctx* c, char** text, size_t* len) {
   if (!c || !text) return MC_E_INVALID;
   if (!c->ran) return MC_E_STATE;

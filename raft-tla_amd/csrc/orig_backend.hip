@@ -1,14 +1,28 @@
 // raftmc — gfx950 BFS backend for thirdparty/raft_original.tla.
 //
-// One BFS level = one launch of orig_expand: one lane per frontier state, a
-// wave-uniform loop over the Next relation's action instances (so every lane
-// of a wave runs the same action code on a different state), and for every
-// successor: constraint filter -> canonical pack -> FP64 -> lock-free
-// open-addressing insert (atomicCAS on u64 slots) -> invariant check on
-// !seen states -> wave-aggregated slot allocation (ballot + one atomic per
-// wave per instance) and a 16-B-vector store of the new state and its
-// parent pointer.  All distinct states stay resident in HBM (the trace is
-// read back by chasing parent pointers; no host replay).
+// One BFS level is processed in frontier chunks; each chunk runs three
+// kernels on one stream:
+//
+//  1. orig_generate  (compute): one lane per frontier state, a wave-uniform
+//     loop over the Next relation's action instances (every lane of a wave
+//     runs the same action code on a different state).  Each enabled
+//     successor is constraint-filtered, canonically packed and fingerprinted
+//     (FP64); the fingerprint goes to an instance-major slot array
+//     cand[k][state] (0 = no in-model successor), so the stores of a wave are
+//     contiguous and no atomic is needed.  Out-of-model successors get their
+//     invariant check here (TLC semantics, [ext] switch).
+//  2. orig_dedup     (HBM random access): each thread takes 16 slots, issues
+//     their 16 independent seen-set loads together, then the atomicCAS
+//     inserts of the empty ones together (lock-free open addressing over u64
+//     fingerprints, linear probing); the new slots of a 4096-slot tile are
+//     compacted with one global atomic per tile into (parent, instance)
+//     records.
+//  3. orig_materialize: one lane per new state re-derives it from
+//     (parent, instance), stores the packed state + parent pointer into the
+//     HBM-resident state store and checks the invariants.
+//
+// All distinct states stay resident in HBM; counterexamples are read back by
+// chasing parent pointers (no host replay).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -26,21 +40,13 @@
 
 namespace rmc {
 
-enum { K_NEW = 0, K_GEN_IN = 1, K_ERR = 2, K_VIOL = 3, K_ERRGID = 4, K_DEADLOCK = 5, K_ACT = 8, K_NCTR = K_ACT + 2 * OA_NACT };
-enum { OE_CAP_STORE = 0x100, OE_TABLE_FULL = 0x200 };
-
-struct ExpandArgs {
-  u32* states;                 // [cap][NWP] packed states, all levels
-  u64* meta;                   // [cap] parent_gid << 24 | action << 16 | instance
-  u64 level_begin, level_count, next_base, cap;
-  u64* table;                  // seen-set, 0 = empty
-  u64 table_mask;
-  u64 seed;
-  OrigRuntime rt;
-  u32 inv_oom;
-  unsigned long long* ctr;     // K_* counters
-  void* viol;                  // ViolRec<S>
+enum {
+  K_NEW = 0, K_GEN_IN = 1, K_ERR = 2, K_VIOL = 3, K_ERRGID = 4, K_DEADLOCK = 5, K_CHUNK_NEW = 6,
+  K_ACT = 8, K_NCTR = K_ACT + 2 * OA_NACT
 };
+enum { OE_CAP_STORE = 0x100, OE_TABLE_FULL = 0x200 };
+constexpr int DEDUP_PER = 16;      // slots per dedup thread (independent probes in flight)
+constexpr int BS = 256;            // workgroup size of every kernel (4 waves)
 
 template <class S>
 struct ViolRec {
@@ -49,36 +55,30 @@ struct ViolRec {
   typename S::Work w;
 };
 
-__device__ __forceinline__ bool seen_insert(u64* table, u64 mask, u64 fp, u32& err) {
-  u64 slot = fp & mask;
-  for (int probe = 0; probe < (1 << 20); ++probe) {
-    const u64 cur = table[slot];                   // insert-only table: a non-zero read is final
-    if (cur == fp) return false;
-    if (cur == 0) {
-      const unsigned long long old = atomicCAS((unsigned long long*)&table[slot], 0ull, (unsigned long long)fp);
-      if (old == 0ull) return true;
-      if (old == (unsigned long long)fp) return false;
-    }
-    slot = (slot + 1) & mask;
-  }
-  err |= OE_TABLE_FULL;
-  return false;
-}
+struct GenArgs {
+  const u32* states;           // [cap][NWP]
+  u64 chunk_begin, chunk_count;
+  u64* cand;                   // [NI][chunk_count] fingerprints, 0 = none
+  u64 seed;
+  OrigRuntime rt;
+  u32 inv_oom;
+  unsigned long long* ctr;
+  void* viol;
+};
 
-template <class S, int BS>
-__global__ void __launch_bounds__(BS) orig_expand(ExpandArgs a) {
+template <class S>
+__global__ void __launch_bounds__(BS) orig_generate(GenArgs a) {
   using W = typename S::Work;
   constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
-  __shared__ unsigned int lds_cnt[2 * OA_NACT + 1];
-  for (int t = threadIdx.x; t < 2 * OA_NACT + 1; t += BS) lds_cnt[t] = 0;
+  __shared__ unsigned int lds_cnt[OA_NACT + 1];
+  for (int t = threadIdx.x; t < OA_NACT + 1; t += BS) lds_cnt[t] = 0;
   __syncthreads();
-
   const u64 tid = (u64)blockIdx.x * BS + threadIdx.x;
-  const bool active = tid < a.level_count;
-  const u64 gid = a.level_begin + tid;
+  const bool active = tid < a.chunk_count;
+  const u64 gid = a.chunk_begin + tid;
   W s;
   u64 al[S::AW];
-  u32 err = 0;
+  u32 err = 0, nsucc = 0;
   if (active) {
     u32 w[NWP];
     const uint4* src = reinterpret_cast<const uint4*>(a.states + gid * NWP);
@@ -91,58 +91,29 @@ __global__ void __launch_bounds__(BS) orig_expand(ExpandArgs a) {
 #pragma unroll
     for (int q = 0; q < S::AW; ++q) al[q] = 0;
   }
-  u32 nsucc = 0;
-  const int lane = __lane_id();
   for (int k = 0; k < S::NI; ++k) {
     W t;
     const int act = active ? S::apply(s, k, t, err) : -1;
-    const bool ok = act >= 0;
-    bool isnew = false;
-    u32 w[NWP];
-#pragma unroll
-    for (int q = 0; q < NWP; ++q) w[q] = 0;
-    if (ok) {
+    u64 fp = 0;
+    if (act >= 0) {
 #pragma unroll
       for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
       ++nsucc;
       atomicAdd(&lds_cnt[act], 1u);
-      const bool inm = S::in_model(t, a.rt);
-      if (inm) {
-        atomicAdd(&lds_cnt[2 * OA_NACT], 1u);
+      if (S::in_model(t, a.rt)) {
+        atomicAdd(&lds_cnt[OA_NACT], 1u);
         u32 pw[NW];
         S::pack(t, pw);
-#pragma unroll
-        for (int q = 0; q < NW; ++q) w[q] = pw[q];
-        const u64 fp = fp64(pw, a.seed);
-        isnew = seen_insert(a.table, a.table_mask, fp, err);
-        if (isnew) atomicAdd(&lds_cnt[OA_NACT + act], 1u);
-      }
-      if (isnew || (!inm && a.inv_oom)) {
+        fp = fp64(pw, a.seed);
+      } else if (a.inv_oom) {
         const u32 bad = S::violated(t, a.rt.invariants);
         if (bad && atomicCAS(&a.ctr[K_VIOL], 0ull, 1ull) == 0ull) {
           ViolRec<S>* v = reinterpret_cast<ViolRec<S>*>(a.viol);
-          v->parent = gid; v->act = (u32)act; v->inst = (u32)k; v->bad = bad; v->inmodel = inm; v->w = t;
+          v->parent = gid; v->act = (u32)act; v->inst = (u32)k; v->bad = bad; v->inmodel = 0; v->w = t;
         }
       }
     }
-    const u64 m = __ballot(isnew);
-    if (m) {
-      const int leader = __ffsll((unsigned long long)m) - 1;
-      unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(&a.ctr[K_NEW], (unsigned long long)__popcll(m));
-      base = __shfl(base, leader);
-      if (isnew) {
-        const u64 dst = a.next_base + base + (u64)__popcll(m & ((1ull << lane) - 1ull));
-        if (dst < a.cap) {
-          uint4* o = reinterpret_cast<uint4*>(a.states + dst * NWP);
-#pragma unroll
-          for (int q = 0; q < NWP / 4; ++q) o[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-          a.meta[dst] = (gid << 24) | ((u64)act << 16) | (u64)k;
-        } else {
-          err |= OE_CAP_STORE;
-        }
-      }
-    }
+    if (active) a.cand[(u64)k * a.chunk_count + tid] = fp;
   }
   if (active && nsucc == 0) atomicCAS(&a.ctr[K_DEADLOCK], 0ull, (unsigned long long)(gid + 1));
   if (err) {
@@ -150,9 +121,138 @@ __global__ void __launch_bounds__(BS) orig_expand(ExpandArgs a) {
     atomicCAS(&a.ctr[K_ERRGID], 0ull, (unsigned long long)(gid + 1));
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < 2 * OA_NACT; t += BS)
+  for (int t = threadIdx.x; t < OA_NACT; t += BS)
     if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + t], (unsigned long long)lds_cnt[t]);
-  if (threadIdx.x == 0 && lds_cnt[2 * OA_NACT]) atomicAdd(&a.ctr[K_GEN_IN], (unsigned long long)lds_cnt[2 * OA_NACT]);
+  if (threadIdx.x == 0 && lds_cnt[OA_NACT]) atomicAdd(&a.ctr[K_GEN_IN], (unsigned long long)lds_cnt[OA_NACT]);
+}
+
+struct DedupArgs {
+  const u64* cand;
+  u64 nslots, chunk_begin, chunk_count;
+  u64* table;
+  u64 table_mask;
+  u64* newrec;                 // (parent gid << 8 | instance), compacted
+  unsigned long long* ctr;
+};
+
+__global__ void __launch_bounds__(BS) orig_dedup(DedupArgs a) {
+  __shared__ unsigned int wave_tot[BS / 64];
+  __shared__ unsigned long long base_sh;
+  const u64 tile = (u64)blockIdx.x * (BS * DEDUP_PER);
+  const int lane = __lane_id(), wave = threadIdx.x >> 6;
+  u64 fp[DEDUP_PER], cur[DEDUP_PER];
+  // 1. slot loads (coalesced), then all seen-set loads back to back
+#pragma unroll
+  for (int j = 0; j < DEDUP_PER; ++j) {
+    const u64 idx = tile + (u64)j * BS + threadIdx.x;
+    fp[j] = idx < a.nslots ? a.cand[idx] : 0ull;
+  }
+#pragma unroll
+  for (int j = 0; j < DEDUP_PER; ++j) cur[j] = fp[j] ? a.table[fp[j] & a.table_mask] : ~0ull;
+  // 2. CAS the empty home slots together
+#pragma unroll
+  for (int j = 0; j < DEDUP_PER; ++j)
+    if (fp[j] && cur[j] == 0ull)
+      cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[fp[j] & a.table_mask], 0ull, (unsigned long long)fp[j]);
+  // 3. resolve; a home slot owned by another fingerprint continues linear probing
+  u32 isnew = 0, err = 0;
+#pragma unroll
+  for (int j = 0; j < DEDUP_PER; ++j) {
+    if (!fp[j]) continue;
+    if (cur[j] == 0ull) { isnew |= 1u << j; continue; }       // our CAS won on an empty home slot
+    if (cur[j] == fp[j]) continue;                            // seen (or lost the CAS race to an equal fp)
+    u64 slot = (fp[j] + 1) & a.table_mask;
+    for (int probe = 0;; ++probe) {
+      if (probe >= (1 << 20)) { err |= OE_TABLE_FULL; break; }
+      const u64 c = a.table[slot];
+      if (c == fp[j]) break;
+      if (c == 0ull) {
+        const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[slot], 0ull, (unsigned long long)fp[j]);
+        if (old == 0ull) { isnew |= 1u << j; break; }
+        if (old == fp[j]) break;
+      }
+      slot = (slot + 1) & a.table_mask;
+    }
+  }
+  // 4. tile compaction: wave prefix sums, one global atomic per tile
+  const unsigned int mine = (unsigned int)__popc(isnew);
+  unsigned int incl = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) { const unsigned int v = __shfl_up(incl, d); if (lane >= d) incl += v; }
+  if (lane == 63) wave_tot[wave] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int tot = 0;
+    for (int w = 0; w < BS / 64; ++w) { const unsigned int x = wave_tot[w]; wave_tot[w] = tot; tot += x; }
+    base_sh = tot ? atomicAdd(&a.ctr[K_CHUNK_NEW], (unsigned long long)tot) : 0ull;
+  }
+  __syncthreads();
+  u64 pos = base_sh + wave_tot[wave] + (incl - mine);
+  for (int j = 0; j < DEDUP_PER; ++j) {
+    if (!((isnew >> j) & 1u)) continue;
+    const u64 idx = tile + (u64)j * BS + threadIdx.x;
+    const u64 k = idx / a.chunk_count, st = idx - k * a.chunk_count;
+    a.newrec[pos++] = ((a.chunk_begin + st) << 8) | k;
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+}
+
+struct MatArgs {
+  u32* states;
+  u64* meta;
+  const u64* newrec;
+  u64 n_new, dst_base, cap;
+  OrigRuntime rt;
+  unsigned long long* ctr;
+  void* viol;
+};
+
+template <class S>
+__global__ void __launch_bounds__(BS) orig_materialize(MatArgs a) {
+  using W = typename S::Work;
+  constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
+  __shared__ unsigned int lds_cnt[OA_NACT];
+  for (int t = threadIdx.x; t < OA_NACT; t += BS) lds_cnt[t] = 0;
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  u32 err = 0;
+  if (i < a.n_new) {
+    const u64 rec = a.newrec[i], gid = rec >> 8;
+    const int k = (int)(rec & 0xff);
+    u32 w[NWP];
+    const uint4* src = reinterpret_cast<const uint4*>(a.states + gid * NWP);
+#pragma unroll
+    for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+    W s, t;
+    u64 al[S::AW];
+    S::unpack(w, s);
+    S::all_logs_next(s, al);
+    const int act = S::apply(s, k, t, err);
+#pragma unroll
+    for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
+    u32 pw[NW];
+    S::pack(t, pw);
+    const u64 dst = a.dst_base + i;
+    if (act >= 0 && dst < a.cap) {
+      uint4* o = reinterpret_cast<uint4*>(a.states + dst * NWP);
+#pragma unroll
+      for (int q = 0; q < NWP / 4; ++q)
+        o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
+      a.meta[dst] = (gid << 24) | ((u64)act << 16) | (u64)k;
+      atomicAdd(&lds_cnt[act], 1u);
+      const u32 bad = S::violated(t, a.rt.invariants);
+      if (bad && atomicCAS(&a.ctr[K_VIOL], 0ull, 1ull) == 0ull) {
+        ViolRec<S>* v = reinterpret_cast<ViolRec<S>*>(a.viol);
+        v->parent = gid; v->act = (u32)act; v->inst = (u32)k; v->bad = bad; v->inmodel = 1; v->w = t;
+      }
+    } else {
+      err |= dst >= a.cap ? (u32)OE_CAP_STORE : (u32)OE_EVAL_LOG_INDEX;
+    }
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+  __syncthreads();
+  for (int t = threadIdx.x; t < OA_NACT; t += BS)
+    if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + OA_NACT + t], (unsigned long long)lds_cnt[t]);
 }
 
 #define HIPCHK(x)                                                                             \
@@ -200,17 +300,22 @@ class OrigGpu : public Backend {
       uint64_t tb = o.fp_table_bytes ? o.fp_table_bytes : std::min<uint64_t>(8ull << 30, freeb / 4);
       uint64_t slots = 1; while (slots * 2 * 8 <= tb) slots *= 2;
       if (slots < 1024) slots = 1024;
-      uint64_t sb = o.state_store_bytes ? o.state_store_bytes : std::min<uint64_t>(32ull << 30, freeb / 2);
+      uint64_t sb = o.state_store_bytes ? o.state_store_bytes : std::min<uint64_t>(32ull << 30, freeb / 3);
       cap_ = sb / (NWP * 4 + 8);
       if (cap_ < 16) cap_ = 16;
+      // frontier chunk: the slot array holds chunk_states * NI fingerprints,
+      // the record array as many (worst case: every slot new); ~1/8 of the store
+      chunk_states_ = std::max<u64>(4096, std::min<u64>(cap_, (sb / 8) / (16 * (u64)S::NI)));
       table_mask_ = slots - 1;
       HIPCHK(hipMalloc(&d_table_, slots * 8));
       HIPCHK(hipMalloc(&d_states_, cap_ * NWP * 4));
       HIPCHK(hipMalloc(&d_meta_, cap_ * 8));
+      HIPCHK(hipMalloc(&d_cand_, chunk_states_ * S::NI * 8));
+      HIPCHK(hipMalloc(&d_newrec_, chunk_states_ * S::NI * 8));
       HIPCHK(hipMalloc(&d_ctr_, K_NCTR * 8));
       HIPCHK(hipMalloc(&d_viol_, sizeof(ViolRec<S>)));
       HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-      HIPCHK(hipEventCreate(&ev0_)); HIPCHK(hipEventCreate(&ev1_));
+      for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
       dev_ = o.device; req_table_ = o.fp_table_bytes; req_store_ = o.state_store_bytes;
     }
     auto t0 = std::chrono::steady_clock::now();
@@ -222,6 +327,7 @@ class OrigGpu : public Backend {
     r.state_bytes = NWP * 4;
     for (int k = 0; k < OA_NACT; ++k) r.action_names.push_back(kOrigActNames[k]);
     r.act_generated.assign(OA_NACT, 0); r.act_distinct.assign(OA_NACT, 0);
+    r.kernels = {{"orig_generate", 0, 0, 0}, {"orig_dedup", 0, 0, 0}, {"orig_materialize", 0, 0, 0}};
 
     // ---- Init (raft_original.tla:139-159): one state, generated and distinct
     W s0; S::init(s0);
@@ -242,50 +348,89 @@ class OrigGpu : public Backend {
       finish(r, t0); return 0;
     }
 
+    const u64 S_B = NWP * 4;
     u64 level_begin = 0, level_count = 1;
     while (level_count > 0) {
       if (o.max_depth && r.depth >= o.max_depth) { r.left_on_queue = (int64_t)level_count; r.verdict = MC_VERDICT_DEPTH_LIMIT; break; }
       HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
-      ExpandArgs a;
-      a.states = d_states_; a.meta = d_meta_;
-      a.level_begin = level_begin; a.level_count = level_count; a.next_base = level_begin + level_count; a.cap = cap_;
-      a.table = d_table_; a.table_mask = table_mask_; a.seed = r.seed; a.rt = m_.rt;
-      a.inv_oom = o.inv_out_of_model ? 1u : 0u; a.ctr = (unsigned long long*)d_ctr_; a.viol = d_viol_;
-      const unsigned grid = (unsigned)((level_count + 255) / 256);
-      HIPCHK(hipEventRecord(ev0_, stream_));
-      hipLaunchKernelGGL((orig_expand<S, 256>), dim3(grid), dim3(256), 0, stream_, a);
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(ev1_, stream_));
+      u64 next_write = level_begin + level_count;
+      double level_ms = 0;
+      for (u64 cb = level_begin; cb < level_begin + level_count; cb += chunk_states_) {
+        const u64 cnt = std::min<u64>(chunk_states_, level_begin + level_count - cb);
+        const u64 nslots = cnt * (u64)S::NI;
+        HIPCHK(hipMemsetAsync(d_ctr_ + K_CHUNK_NEW, 0, 8, stream_));
+        GenArgs g;
+        g.states = d_states_; g.chunk_begin = cb; g.chunk_count = cnt; g.cand = d_cand_; g.seed = r.seed; g.rt = m_.rt;
+        g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_; g.viol = d_viol_;
+        DedupArgs d;
+        d.cand = d_cand_; d.nslots = nslots; d.chunk_begin = cb; d.chunk_count = cnt; d.table = d_table_;
+        d.table_mask = table_mask_; d.newrec = d_newrec_; d.ctr = (unsigned long long*)d_ctr_;
+        HIPCHK(hipEventRecord(ev_[0], stream_));
+        hipLaunchKernelGGL((orig_generate<S>), dim3((unsigned)((cnt + BS - 1) / BS)), dim3(BS), 0, stream_, g);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ev_[1], stream_));
+        hipLaunchKernelGGL(orig_dedup, dim3((unsigned)((nslots + BS * DEDUP_PER - 1) / (BS * DEDUP_PER))), dim3(BS), 0, stream_, d);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ev_[2], stream_));
+        u64 nnew = 0;
+        HIPCHK(hipMemcpyAsync(&nnew, d_ctr_ + K_CHUNK_NEW, 8, hipMemcpyDeviceToHost, stream_));
+        HIPCHK(hipStreamSynchronize(stream_));
+        float ms_g = 0, ms_d = 0, ms_m = 0;
+        HIPCHK(hipEventElapsedTime(&ms_g, ev_[0], ev_[1]));
+        HIPCHK(hipEventElapsedTime(&ms_d, ev_[1], ev_[2]));
+        if (nnew) {
+          MatArgs m;
+          m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.n_new = nnew; m.dst_base = next_write; m.cap = cap_;
+          m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.viol = d_viol_;
+          HIPCHK(hipEventRecord(ev_[3], stream_));
+          hipLaunchKernelGGL((orig_materialize<S>), dim3((unsigned)((nnew + BS - 1) / BS)), dim3(BS), 0, stream_, m);
+          HIPCHK(hipGetLastError());
+          HIPCHK(hipEventRecord(ev_[4], stream_));
+          HIPCHK(hipEventSynchronize(ev_[4]));
+          HIPCHK(hipEventElapsedTime(&ms_m, ev_[3], ev_[4]));
+          r.kernels[2].ms += ms_m; r.kernels[2].launches += 1;
+          r.kernels[2].algo_bytes += (double)nnew * (8 + S_B + S_B + 8);
+        }
+        next_write += nnew;
+        level_ms += ms_g + ms_d + ms_m;
+        r.kernels[0].ms += ms_g; r.kernels[0].launches += 1;
+        r.kernels[0].algo_bytes += (double)cnt * S_B + (double)nslots * 8;
+        r.kernels[1].ms += ms_d; r.kernels[1].launches += 1;
+        r.kernels[1].algo_bytes += (double)nslots * 8 + (double)nnew * 16;   // + G_in*8 probe bytes added per level below
+        if (next_write > cap_) break;
+      }
       u64 c[K_NCTR];
       HIPCHK(hipMemcpyAsync(c, d_ctr_, sizeof c, hipMemcpyDeviceToHost, stream_));
       HIPCHK(hipStreamSynchronize(stream_));
-      float ms = 0; HIPCHK(hipEventElapsedTime(&ms, ev0_, ev1_));
       int64_t gen = 0;
       for (int k = 0; k < OA_NACT; ++k) { r.act_generated[k] += (int64_t)c[K_ACT + k]; r.act_distinct[k] += (int64_t)c[K_ACT + OA_NACT + k]; gen += (int64_t)c[K_ACT + k]; }
       r.generated += gen;
       r.generated_in_model += (int64_t)c[K_GEN_IN];
-      r.seconds_kernels += ms / 1000.0;
+      r.kernels[1].algo_bytes += (double)c[K_GEN_IN] * 8;
+      r.seconds_kernels += level_ms / 1000.0;
       r.n_launches += 1;
-      const u64 nnew = c[K_NEW];
-      r.algo_bytes += (double)level_count * NWP * 4 + (double)c[K_GEN_IN] * 8 + (double)nnew * (16 + NWP * 4);
+      const u64 nnew = next_write - (level_begin + level_count);
+      r.algo_bytes += (double)level_count * S_B + (double)c[K_GEN_IN] * 8 + (double)nnew * (16 + S_B);
+      if (next_write > cap_) c[K_ERR] |= OE_CAP_STORE;
       if (c[K_ERR]) {
         const u64 e = c[K_ERR];
         r.verdict = (e & (OE_CAP_STORE | OE_TABLE_FULL | OE_CAP_ELECTIONS | OE_CAP_COUNT)) ? MC_VERDICT_CAPACITY_OVERFLOW : MC_VERDICT_EVAL_ERROR;
         std::ostringstream os;
-        os << "error flags 0x" << std::hex << e << std::dec << " while expanding state " << (c[K_ERRGID] - 1) << ":";
+        os << "error flags 0x" << std::hex << e << std::dec << " while expanding state " << (c[K_ERRGID] ? (int64_t)c[K_ERRGID] - 1 : -1) << ":";
         if (e & OE_EVAL_LOG_INDEX) os << " log[i][prevLogIndex] applied outside its domain (raft_original.tla:207-210);";
         if (e & OE_CAP_ELECTIONS) os << " elections set exceeds the compiled capacity;";
         if (e & OE_CAP_COUNT) os << " message count / bag capacity exceeded;";
         if (e & OE_CAP_STORE) os << " state store full (raise state_store_bytes);";
         if (e & OE_TABLE_FULL) os << " fingerprint table full (raise fp_table_bytes);";
         r.error = os.str();
-        r.distinct = (int64_t)(total_ + std::min<u64>(nnew, cap_ - total_));
+        total_ = std::min<u64>(next_write, cap_);
+        r.distinct = (int64_t)total_;
         break;
       }
       total_ += nnew;
       r.distinct = (int64_t)total_;
       r.levels.back().generated = gen;
-      r.levels.back().kernel_ms = ms;
+      r.levels.back().kernel_ms = level_ms;
       if (nnew > 0) { r.levels.push_back({(int64_t)nnew, 0, 0.0}); r.depth += 1; }
       if (c[K_VIOL]) {
         ViolRec<S> v;
@@ -328,21 +473,19 @@ class OrigGpu : public Backend {
  private:
   OrigModel m_;
   u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr; void* d_viol_ = nullptr;
-  hipStream_t stream_ = nullptr; hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
-  u64 table_mask_ = 0, cap_ = 0, total_ = 0;
+  u64* d_cand_ = nullptr; u64* d_newrec_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  hipEvent_t ev_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  u64 table_mask_ = 0, cap_ = 0, total_ = 0, chunk_states_ = 0;
   int dev_ = -1; uint64_t req_table_ = 0, req_store_ = 0;
 
   void release() {
-    if (d_table_) (void)hipFree(d_table_);
-    if (d_states_) (void)hipFree(d_states_);
-    if (d_meta_) (void)hipFree(d_meta_);
-    if (d_ctr_) (void)hipFree(d_ctr_);
-    if (d_viol_) (void)hipFree(d_viol_);
-    if (ev0_) (void)hipEventDestroy(ev0_);
-    if (ev1_) (void)hipEventDestroy(ev1_);
+    for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, d_viol_, (void*)d_cand_, (void*)d_newrec_})
+      if (p) (void)hipFree(p);
+    for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
     if (stream_) (void)hipStreamDestroy(stream_);
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_viol_ = nullptr;
-    ev0_ = ev1_ = nullptr; stream_ = nullptr;
+    d_cand_ = nullptr; d_newrec_ = nullptr; stream_ = nullptr;
   }
 
   std::string first_violated(u32 bad) const {

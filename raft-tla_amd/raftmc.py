@@ -22,7 +22,7 @@ VERDICTS = {0: "OK", 1: "INVARIANT_VIOLATION", 2: "EVAL_ERROR", 3: "CAPACITY_OVE
 MC_COMPAT_INV_OUT_OF_MODEL = 0x1
 
 # every symbol include/raftmc.h declares
-EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stats", "mc_level_stats",
+EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stats", "mc_level_stats", "mc_kernel_stats",
            "mc_trace", "mc_report", "mc_dump_states", "mc_describe", "mc_exit_code", "mc_free",
            "mc_close", "mc_last_error"]
 
@@ -71,6 +71,8 @@ def load_library(path=LIB_PATH):
                                     ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
     lib.mc_level_stats.argtypes = [P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64),
                                    ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)]
+    lib.mc_kernel_stats.argtypes = [P, ctypes.c_int32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_double),
+                                    ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
     for f in ("mc_trace", "mc_report", "mc_describe"):
         getattr(lib, f).argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.mc_dump_states.argtypes = [P, ctypes.c_char_p]
@@ -144,7 +146,14 @@ class ModelChecker:
             st, g, ms = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_double()
             if self.lib.mc_level_stats(self.h, k, ctypes.byref(st), ctypes.byref(g), ctypes.byref(ms)) == 0:
                 levels.append((st.value, g.value, ms.value))
+        kernels = {}
+        for k in range(16):
+            name, ms, ab, nl = ctypes.c_char_p(), ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+            if self.lib.mc_kernel_stats(self.h, k, ctypes.byref(name), ctypes.byref(ms), ctypes.byref(ab), ctypes.byref(nl)):
+                break
+            kernels[name.value.decode()] = {"ms": ms.value, "algo_bytes": ab.value, "launches": nl.value}
         return Result(verdict=VERDICTS.get(s.verdict, str(s.verdict)), generated=s.generated, distinct=s.distinct,
+                      kernels=kernels,
                       left_on_queue=s.left_on_queue, depth=s.depth, violated=s.violated.decode(),
                       spec=s.spec.decode(), actions=actions, levels=levels,
                       collision_prob_optimistic=s.collision_prob_optimistic,
