@@ -138,6 +138,36 @@ void mc_free(void* p);
 void mc_close(mc_ctx* ctx);
 const char* mc_last_error(const mc_ctx* ctx);
 
+/* ---------------------------------------------------------------------------------------------
+ * Sharded BFS (multi-GPU, one process per GPU).  The state space is partitioned by fingerprint
+ * owner (owner = (fp >> 32) mod world): a rank expands its local frontier, routes every
+ * in-model successor fingerprint to its owner, the owner dedups it against its local seen-set
+ * and acknowledges the new ones, the generating rank materialises those states and ships them
+ * to the owner, which stores them as its part of the next level.  The CALLER moves the buffers
+ * between ranks (RCCL all-to-all through torch.distributed in raft-tla_amd/shard.py): every
+ * mc_shard_* call below is rank-local device work.  Records: ROUTE 16 B (fp, slot),
+ * REPLY 8 B (slot), STATES 80 B (64 B packed state, parent meta, fp).  Parent pointers carry
+ * the rank in bits [37,40) of the global state id.
+ * ------------------------------------------------------------------------------------------- */
+#define MC_SHARD_ROUTE 0
+#define MC_SHARD_REPLY 1
+#define MC_SHARD_STATES 2
+#define MC_SHARD_NSTAT 72   /* [0] new stored, [1] generated, [2] generated in model, [3] error flags,
+                               [4] violation, [5] deadlock, [6] frontier, [7] spare,
+                               [8..40) per-action generated, [40..72) per-action distinct          */
+int mc_shard_open(mc_ctx* ctx, int32_t rank, int32_t world);
+int mc_shard_record_bytes(const mc_ctx* ctx, int32_t what);
+int mc_shard_frontier(const mc_ctx* ctx, int64_t* states, int64_t* chunk_states);
+int mc_shard_generate(mc_ctx* ctx, int64_t begin, int64_t count, int64_t* route_counts);
+int mc_shard_fill(mc_ctx* ctx, int32_t what, void* dst_device, const int64_t* dst_offsets);
+int mc_shard_dedup(mc_ctx* ctx, const void* recv_device, const int64_t* recv_counts, int64_t* reply_counts);
+int mc_shard_materialize(mc_ctx* ctx, const void* acks_device, const int64_t* ack_counts);
+int mc_shard_store(mc_ctx* ctx, const void* states_device, int64_t n);
+int mc_shard_level_stats(mc_ctx* ctx, int64_t* stats);
+int mc_shard_level_commit(mc_ctx* ctx, const int64_t* global_stats, int32_t* done);
+int mc_shard_read_state(const mc_ctx* ctx, uint64_t gid, char** text, size_t* len, uint64_t* meta);
+int mc_shard_violation(const mc_ctx* ctx, uint64_t* parent_gid, char** action, char** text);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,6 +48,20 @@ struct Backend {
   virtual std::string describe_json() const = 0;
   virtual int run(const RunOpts& o, RunResult& r, std::string& err) = 0;
   virtual int dump_states(const std::string& path, std::string& err) = 0;
+  // ---- sharded BFS (include/raftmc.h mc_shard_*); rank-local device work only
+  virtual int shard_open(const RunOpts& o, int rank, int world, std::string& err) = 0;
+  virtual int shard_record_bytes(int what) const = 0;
+  virtual int shard_frontier(int64_t* states, int64_t* chunk) const = 0;
+  virtual int shard_generate(int64_t begin, int64_t count, int64_t* counts, std::string& err) = 0;
+  virtual int shard_fill(int what, void* dst, const int64_t* offsets, std::string& err) = 0;
+  virtual int shard_dedup(const void* recv, const int64_t* counts, int64_t* reply_counts, std::string& err) = 0;
+  virtual int shard_materialize(const void* acks, const int64_t* counts, std::string& err) = 0;
+  virtual int shard_store(const void* states, int64_t n, std::string& err) = 0;
+  virtual int shard_level_stats(int64_t* stats, std::string& err) = 0;
+  virtual int shard_level_commit(const int64_t* global, int* done, std::string& err) = 0;
+  virtual int shard_read_state(uint64_t gid, std::string& text, uint64_t* meta, std::string& err) const = 0;
+  virtual int shard_violation(uint64_t* parent, std::string& action, std::string& text) const = 0;
+  virtual const RunResult* shard_result() const = 0;
 };
 
 Backend* make_orig_backend(const CfgFile& cfg);   // throws CfgError

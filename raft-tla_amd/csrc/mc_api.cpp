@@ -215,6 +215,83 @@ int mc_exit_code(const mc_ctx* c) {
   }
 }
 
+// ------------------------------------------------------------------ sharded BFS
+#define SHARD_GUARD() \
+  if (!c) return MC_E_INVALID; \
+  if (!c->be) return MC_E_STATE;
+#define SHARD_RC(expr)                      \
+  do {                                      \
+    std::string err;                        \
+    int rc_ = (expr);                       \
+    if (rc_) c->last_error = err;           \
+    return rc_;                             \
+  } while (0)
+
+int mc_shard_open(mc_ctx* c, int32_t rank, int32_t world) {
+  SHARD_GUARD();
+  c->ran = false;
+  SHARD_RC(c->be->shard_open(c->ro, rank, world, err));
+}
+int mc_shard_record_bytes(const mc_ctx* c, int32_t what) {
+  if (!c || !c->be) return MC_E_INVALID;
+  return c->be->shard_record_bytes(what);
+}
+int mc_shard_frontier(const mc_ctx* c, int64_t* states, int64_t* chunk) {
+  if (!c || !c->be) return MC_E_INVALID;
+  return c->be->shard_frontier(states, chunk);
+}
+int mc_shard_generate(mc_ctx* c, int64_t begin, int64_t count, int64_t* counts) {
+  SHARD_GUARD();
+  SHARD_RC(c->be->shard_generate(begin, count, counts, err));
+}
+int mc_shard_fill(mc_ctx* c, int32_t what, void* dst, const int64_t* offsets) {
+  SHARD_GUARD();
+  SHARD_RC(c->be->shard_fill(what, dst, offsets, err));
+}
+int mc_shard_dedup(mc_ctx* c, const void* recv, const int64_t* counts, int64_t* reply_counts) {
+  SHARD_GUARD();
+  SHARD_RC(c->be->shard_dedup(recv, counts, reply_counts, err));
+}
+int mc_shard_materialize(mc_ctx* c, const void* acks, const int64_t* counts) {
+  SHARD_GUARD();
+  SHARD_RC(c->be->shard_materialize(acks, counts, err));
+}
+int mc_shard_store(mc_ctx* c, const void* states, int64_t n) {
+  SHARD_GUARD();
+  SHARD_RC(c->be->shard_store(states, n, err));
+}
+int mc_shard_level_stats(mc_ctx* c, int64_t* stats) {
+  SHARD_GUARD();
+  SHARD_RC(c->be->shard_level_stats(stats, err));
+}
+int mc_shard_level_commit(mc_ctx* c, const int64_t* global, int32_t* done) {
+  SHARD_GUARD();
+  std::string err;
+  int d = 0;
+  int rc = c->be->shard_level_commit(global, &d, err);
+  if (rc) { c->last_error = err; return rc; }
+  *done = d;
+  if (d) { c->res = *c->be->shard_result(); c->ran = true; c->last_error = c->res.error; }
+  return MC_OK;
+}
+int mc_shard_read_state(const mc_ctx* c, uint64_t gid, char** text, size_t* len, uint64_t* meta) {
+  if (!c || !c->be || !text) return MC_E_INVALID;
+  std::string t, err;
+  int rc = c->be->shard_read_state(gid, t, meta, err);
+  if (rc) { const_cast<mc_ctx*>(c)->last_error = err; return rc; }
+  *text = dup_text(t, len);
+  return *text ? MC_OK : MC_E_OOM;
+}
+int mc_shard_violation(const mc_ctx* c, uint64_t* parent, char** action, char** text) {
+  if (!c || !c->be || !action || !text) return MC_E_INVALID;
+  std::string a, t;
+  int rc = c->be->shard_violation(parent, a, t);
+  if (rc) return rc;
+  *action = dup_text(a, nullptr);
+  *text = dup_text(t, nullptr);
+  return MC_OK;
+}
+
 void mc_free(void* p) { std::free(p); }
 void mc_close(mc_ctx* c) { delete c; }
 const char* mc_last_error(const mc_ctx* c) { return c ? c->last_error.c_str() : "null handle"; }

@@ -255,6 +255,199 @@ __global__ void __launch_bounds__(BS) orig_materialize(MatArgs a) {
     if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + OA_NACT + t], (unsigned long long)lds_cnt[t]);
 }
 
+// ------------------------------------------------------------------ sharded (multi-GPU) kernels
+// owner of a fingerprint: high half mod world (the seen-set index uses the low bits)
+__device__ __host__ __forceinline__ u32 fp_owner(u64 fp, u32 world) { return (u32)((fp >> 32) % world); }
+
+struct RouteArgs {
+  const u64* cand;
+  u64 nslots;
+  u64* route;                  // [world][route_cap][2] (fp, slot)
+  u64 route_cap;
+  u32 world;
+  unsigned long long* rcnt;    // [world]
+};
+
+// bucket the chunk's in-model fingerprints by owner: LDS histogram per 4096-slot
+// tile, one global atomic per (tile, owner)
+__global__ void __launch_bounds__(BS) orig_route(RouteArgs a) {
+  __shared__ unsigned int hist[8], cur[8];
+  __shared__ unsigned long long base[8];
+  if (threadIdx.x < 8) { hist[threadIdx.x] = 0; cur[threadIdx.x] = 0; }
+  __syncthreads();
+  const u64 tile = (u64)blockIdx.x * (BS * DEDUP_PER);
+  u64 fp[DEDUP_PER];
+  int own[DEDUP_PER];
+#pragma unroll
+  for (int j = 0; j < DEDUP_PER; ++j) {
+    const u64 idx = tile + (u64)j * BS + threadIdx.x;
+    fp[j] = idx < a.nslots ? a.cand[idx] : 0ull;
+    own[j] = fp[j] ? (int)fp_owner(fp[j], a.world) : -1;
+    if (own[j] >= 0) atomicAdd(&hist[own[j]], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < a.world) base[threadIdx.x] = hist[threadIdx.x] ? atomicAdd(&a.rcnt[threadIdx.x], (unsigned long long)hist[threadIdx.x]) : 0ull;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < DEDUP_PER; ++j) {
+    if (own[j] < 0) continue;
+    const u64 pos = base[own[j]] + atomicAdd(&cur[own[j]], 1u);
+    u64* r = a.route + ((u64)own[j] * a.route_cap + pos) * 2;
+    r[0] = fp[j];
+    r[1] = tile + (u64)j * BS + threadIdx.x;
+  }
+}
+
+struct DedupShArgs {
+  const u64* recv;             // (fp, slot) records of one source rank
+  u64 n;
+  u64* table;
+  u64 table_mask;
+  u64* reply;                  // compacted slots of the new ones
+  unsigned long long* counter; // per-source reply count
+  unsigned long long* ctr;
+};
+
+__global__ void __launch_bounds__(BS) orig_dedup_sh(DedupShArgs a) {
+  __shared__ unsigned int wave_tot[BS / 64];
+  __shared__ unsigned long long base_sh;
+  const u64 tile = (u64)blockIdx.x * (BS * DEDUP_PER);
+  const int lane = __lane_id(), wave = threadIdx.x >> 6;
+  u64 fp[DEDUP_PER], cur[DEDUP_PER];
+#pragma unroll
+  for (int j = 0; j < DEDUP_PER; ++j) {
+    const u64 idx = tile + (u64)j * BS + threadIdx.x;
+    fp[j] = idx < a.n ? a.recv[2 * idx] : 0ull;
+  }
+#pragma unroll
+  for (int j = 0; j < DEDUP_PER; ++j) cur[j] = fp[j] ? a.table[fp[j] & a.table_mask] : ~0ull;
+#pragma unroll
+  for (int j = 0; j < DEDUP_PER; ++j)
+    if (fp[j] && cur[j] == 0ull)
+      cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[fp[j] & a.table_mask], 0ull, (unsigned long long)fp[j]);
+  u32 isnew = 0, err = 0;
+#pragma unroll
+  for (int j = 0; j < DEDUP_PER; ++j) {
+    if (!fp[j]) continue;
+    if (cur[j] == 0ull) { isnew |= 1u << j; continue; }
+    if (cur[j] == fp[j]) continue;
+    u64 slot = (fp[j] + 1) & a.table_mask;
+    for (int probe = 0;; ++probe) {
+      if (probe >= (1 << 20)) { err |= OE_TABLE_FULL; break; }
+      const u64 c = a.table[slot];
+      if (c == fp[j]) break;
+      if (c == 0ull) {
+        const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[slot], 0ull, (unsigned long long)fp[j]);
+        if (old == 0ull) { isnew |= 1u << j; break; }
+        if (old == fp[j]) break;
+      }
+      slot = (slot + 1) & a.table_mask;
+    }
+  }
+  const unsigned int mine = (unsigned int)__popc(isnew);
+  unsigned int incl = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) { const unsigned int v = __shfl_up(incl, d); if (lane >= d) incl += v; }
+  if (lane == 63) wave_tot[wave] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int tot = 0;
+    for (int w = 0; w < BS / 64; ++w) { const unsigned int x = wave_tot[w]; wave_tot[w] = tot; tot += x; }
+    base_sh = tot ? atomicAdd(a.counter, (unsigned long long)tot) : 0ull;
+  }
+  __syncthreads();
+  u64 pos = base_sh + wave_tot[wave] + (incl - mine);
+  for (int j = 0; j < DEDUP_PER; ++j) {
+    if (!((isnew >> j) & 1u)) continue;
+    const u64 idx = tile + (u64)j * BS + threadIdx.x;
+    a.reply[pos++] = a.recv[2 * idx + 1];
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+}
+
+struct MatShArgs {
+  const u32* states;
+  const u64* acks;             // slots acknowledged as new by one owner
+  u64 n, chunk_begin, chunk_count;
+  u32* out;                    // [n][NWP + 4] state records for that owner
+  u64 rank_bits;               // rank << 37
+  u64 seed;
+  OrigRuntime rt;
+  unsigned long long* ctr;
+  void* viol;
+};
+
+template <class S>
+__global__ void __launch_bounds__(BS) orig_materialize_sh(MatShArgs a) {
+  using W = typename S::Work;
+  constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3, RW = NWP + 4;
+  __shared__ unsigned int lds_cnt[OA_NACT];
+  for (int t = threadIdx.x; t < OA_NACT; t += BS) lds_cnt[t] = 0;
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  u32 err = 0;
+  if (i < a.n) {
+    const u64 slot = a.acks[i];
+    const u64 k = slot / a.chunk_count, gid = a.chunk_begin + (slot - k * a.chunk_count);
+    u32 w[NWP];
+    const uint4* src = reinterpret_cast<const uint4*>(a.states + gid * NWP);
+#pragma unroll
+    for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+    W s, t;
+    u64 al[S::AW];
+    S::unpack(w, s);
+    S::all_logs_next(s, al);
+    const int act = S::apply(s, (int)k, t, err);
+#pragma unroll
+    for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
+    u32 pw[NW];
+    S::pack(t, pw);
+    const u64 fp = fp64(pw, a.seed);
+    const u64 meta = ((a.rank_bits | gid) << 24) | ((u64)(act < 0 ? 0 : act) << 16) | k;
+    u32* o = a.out + i * RW;
+#pragma unroll
+    for (int q = 0; q < NWP / 4; ++q)
+      reinterpret_cast<uint4*>(o)[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
+    reinterpret_cast<uint4*>(o)[NWP / 4] = make_uint4((u32)meta, (u32)(meta >> 32), (u32)fp, (u32)(fp >> 32));
+    if (act >= 0) {
+      atomicAdd(&lds_cnt[act], 1u);
+      const u32 bad = S::violated(t, a.rt.invariants);
+      if (bad && atomicCAS(&a.ctr[K_VIOL], 0ull, 1ull) == 0ull) {
+        ViolRec<S>* v = reinterpret_cast<ViolRec<S>*>(a.viol);
+        v->parent = gid; v->act = (u32)act; v->inst = (u32)k; v->bad = bad; v->inmodel = 1; v->w = t;
+      }
+    } else {
+      err |= OE_EVAL_LOG_INDEX;
+    }
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+  __syncthreads();
+  for (int t = threadIdx.x; t < OA_NACT; t += BS)
+    if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + OA_NACT + t], (unsigned long long)lds_cnt[t]);
+}
+
+struct StoreArgs {
+  const u32* in;               // [n][NWP + 4]
+  u64 n, dst, cap;
+  u32* states;
+  u64* meta;
+  unsigned long long* ctr;
+};
+
+template <int NWP>
+__global__ void __launch_bounds__(BS) orig_store(StoreArgs a) {
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  if (i >= a.n) return;
+  const u64 dst = a.dst + i;
+  if (dst >= a.cap) { atomicOr(&a.ctr[K_ERR], (unsigned long long)OE_CAP_STORE); return; }
+  const uint4* src = reinterpret_cast<const uint4*>(a.in + i * (NWP + 4));
+  uint4* o = reinterpret_cast<uint4*>(a.states + dst * NWP);
+#pragma unroll
+  for (int q = 0; q < NWP / 4; ++q) o[q] = src[q];
+  const uint4 m = src[NWP / 4];
+  a.meta[dst] = (u64)m.x | ((u64)m.y << 32);
+}
+
 #define HIPCHK(x)                                                                             \
   do {                                                                                        \
     hipError_t e_ = (x);                                                                      \
@@ -287,37 +480,47 @@ class OrigGpu : public Backend {
     return o.str();
   }
 
-  int run(const RunOpts& o, RunResult& r, std::string& err) override {
+  // Buffers are allocated on the first run and reused (a re-run of the same
+  // handle re-zeroes the seen-set and overwrites the store).
+  int ensure_alloc(const RunOpts& o, int world, std::string& err) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= o.device) { err = "no HIP device available (raftmc has no CPU fallback)"; return MC_E_NO_DEVICE; }
     HIPCHK(hipSetDevice(o.device));
-    // ---- sizing; buffers are allocated on the first run and reused (a re-run
-    // of the same handle re-zeroes the seen-set and overwrites the store)
-    if (!d_table_ || o.device != dev_ || o.fp_table_bytes != req_table_ || o.state_store_bytes != req_store_) {
-      release();
-      size_t freeb = 0, totalb = 0;
-      HIPCHK(hipMemGetInfo(&freeb, &totalb));
-      uint64_t tb = o.fp_table_bytes ? o.fp_table_bytes : std::min<uint64_t>(8ull << 30, freeb / 4);
-      uint64_t slots = 1; while (slots * 2 * 8 <= tb) slots *= 2;
-      if (slots < 1024) slots = 1024;
-      uint64_t sb = o.state_store_bytes ? o.state_store_bytes : std::min<uint64_t>(32ull << 30, freeb / 3);
-      cap_ = sb / (NWP * 4 + 8);
-      if (cap_ < 16) cap_ = 16;
-      // frontier chunk: the slot array holds chunk_states * NI fingerprints,
-      // the record array as many (worst case: every slot new); ~1/8 of the store
-      chunk_states_ = std::max<u64>(4096, std::min<u64>(cap_, (sb / 8) / (16 * (u64)S::NI)));
-      table_mask_ = slots - 1;
-      HIPCHK(hipMalloc(&d_table_, slots * 8));
-      HIPCHK(hipMalloc(&d_states_, cap_ * NWP * 4));
-      HIPCHK(hipMalloc(&d_meta_, cap_ * 8));
-      HIPCHK(hipMalloc(&d_cand_, chunk_states_ * S::NI * 8));
-      HIPCHK(hipMalloc(&d_newrec_, chunk_states_ * S::NI * 8));
-      HIPCHK(hipMalloc(&d_ctr_, K_NCTR * 8));
-      HIPCHK(hipMalloc(&d_viol_, sizeof(ViolRec<S>)));
-      HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-      for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
-      dev_ = o.device; req_table_ = o.fp_table_bytes; req_store_ = o.state_store_bytes;
+    if (d_table_ && o.device == dev_ && o.fp_table_bytes == req_table_ && o.state_store_bytes == req_store_ && world == alloc_world_) return 0;
+    release();
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    uint64_t tb = o.fp_table_bytes ? o.fp_table_bytes : std::min<uint64_t>(8ull << 30, freeb / 4);
+    uint64_t slots = 1; while (slots * 2 * 8 <= tb) slots *= 2;
+    if (slots < 1024) slots = 1024;
+    uint64_t sb = o.state_store_bytes ? o.state_store_bytes : std::min<uint64_t>(32ull << 30, freeb / 3);
+    cap_ = sb / (NWP * 4 + 8);
+    if (cap_ < 16) cap_ = 16;
+    // frontier chunk: the slot array holds chunk_states * NI fingerprints and
+    // the record array as many (worst case: every slot new): ~1/8 of the store;
+    // sharded mode also needs world route regions of 16-B records per slot
+    chunk_states_ = std::max<u64>(4096, std::min<u64>(cap_, (sb / 8) / (16 * (u64)S::NI)));
+    if (world > 1) chunk_states_ = std::max<u64>(4096, chunk_states_ / (u64)world);
+    table_mask_ = slots - 1;
+    HIPCHK(hipMalloc(&d_table_, slots * 8));
+    HIPCHK(hipMalloc(&d_states_, cap_ * NWP * 4));
+    HIPCHK(hipMalloc(&d_meta_, cap_ * 8));
+    HIPCHK(hipMalloc(&d_cand_, chunk_states_ * S::NI * 8));
+    HIPCHK(hipMalloc(&d_newrec_, chunk_states_ * S::NI * 8));
+    HIPCHK(hipMalloc(&d_ctr_, K_NCTR * 8));
+    HIPCHK(hipMalloc(&d_viol_, sizeof(ViolRec<S>)));
+    if (world >= 1) {   // sharded mode
+      HIPCHK(hipMalloc(&d_route_, (u64)world * chunk_states_ * S::NI * 16));
+      HIPCHK(hipMalloc(&d_rcnt_, 2 * 8 * 8));
     }
+    HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
+    dev_ = o.device; req_table_ = o.fp_table_bytes; req_store_ = o.state_store_bytes; alloc_world_ = world;
+    return 0;
+  }
+
+  int run(const RunOpts& o, RunResult& r, std::string& err) override {
+    if (int rc = ensure_alloc(o, 0, err)) return rc;   // world 0 = single-GPU pipeline
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 8, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
@@ -470,22 +673,264 @@ class OrigGpu : public Backend {
     return 0;
   }
 
+  // ================================================================ sharded mode
+  int shard_open(const RunOpts& o, int rank, int world, std::string& err) override {
+    if (world < 1 || world > 8 || rank < 0 || rank >= world) { err = "sharded mode supports 1..8 ranks"; return MC_E_INVALID; }
+    if (int rc = ensure_alloc(o, world, err)) return rc;
+    rank_ = rank; world_ = world; sopts_ = o;
+    HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 8, stream_));
+    HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    sres_ = RunResult();
+    sres_.seed = o.seed ? o.seed : 0x5EED5EED2024ull;
+    sres_.state_bytes = NWP * 4;
+    for (int k = 0; k < OA_NACT; ++k) sres_.action_names.push_back(kOrigActNames[k]);
+    sres_.act_generated.assign(OA_NACT, 0); sres_.act_distinct.assign(OA_NACT, 0);
+    sres_.kernels = {{"orig_generate", 0, 0, 0}, {"orig_route", 0, 0, 0}, {"orig_dedup_sh", 0, 0, 0},
+                     {"orig_materialize_sh", 0, 0, 0}, {"orig_store", 0, 0, 0}};
+    st0_ = std::chrono::steady_clock::now();
+    // Init: one state, stored and inserted by the owner of its fingerprint
+    W s0; S::init(s0);
+    u32 w0[S::NW]; S::pack(s0, w0);
+    const u64 fp0 = fp64(w0, sres_.seed);
+    total_ = 0; sh_level_begin_ = 0; sh_level_count_ = 0; sh_new_ = 0;
+    if ((int)fp_owner(fp0, (u32)world) == rank) {
+      u32 wp[NWP] = {0}; for (int q = 0; q < S::NW; ++q) wp[q] = w0[q];
+      HIPCHK(hipMemcpy(d_table_ + (fp0 & table_mask_), &fp0, 8, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(d_states_, wp, NWP * 4, hipMemcpyHostToDevice));
+      const u64 nometa = ~0ull;
+      HIPCHK(hipMemcpy(d_meta_, &nometa, 8, hipMemcpyHostToDevice));
+      total_ = 1; sh_level_count_ = 1;
+    }
+    sres_.generated = 1; sres_.distinct = 1; sres_.depth = 1;
+    sres_.levels.push_back({1, 0, 0.0});
+    if (!S::in_model(s0, m_.rt)) { err = "the initial state violates a state constraint"; return MC_E_UNSUPPORTED; }
+    if (S::violated(s0, m_.rt.invariants)) { err = "the initial state violates an invariant"; return MC_E_UNSUPPORTED; }
+    sh_next_write_ = total_;
+    return 0;
+  }
+  int shard_record_bytes(int what) const override {
+    return what == MC_SHARD_ROUTE ? 16 : what == MC_SHARD_REPLY ? 8 : what == MC_SHARD_STATES ? (NWP + 4) * 4 : -1;
+  }
+  int shard_frontier(int64_t* states, int64_t* chunk) const override {
+    if (states) *states = (int64_t)sh_level_count_;
+    if (chunk) *chunk = (int64_t)chunk_states_;
+    return 0;
+  }
+  float time_ms(int a, int b) { float ms = 0; (void)hipEventElapsedTime(&ms, ev_[a], ev_[b]); return ms; }
+
+  int shard_generate(int64_t begin, int64_t count, int64_t* counts, std::string& err) override {
+    if (begin < 0 || count < 0 || (u64)count > chunk_states_ || (u64)(begin + count) > sh_level_count_) { err = "shard_generate: chunk outside the frontier"; return MC_E_INVALID; }
+    sh_chunk_begin_ = sh_level_begin_ + (u64)begin; sh_chunk_count_ = (u64)count;
+    HIPCHK(hipMemsetAsync(d_rcnt_, 0, 8 * 8, stream_));
+    if (count > 0) {
+      const u64 nslots = (u64)count * S::NI;
+      GenArgs g;
+      g.states = d_states_; g.chunk_begin = sh_chunk_begin_; g.chunk_count = (u64)count; g.cand = d_cand_; g.seed = sres_.seed;
+      g.rt = m_.rt; g.inv_oom = sopts_.inv_out_of_model ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_; g.viol = d_viol_;
+      RouteArgs ra;
+      ra.cand = d_cand_; ra.nslots = nslots; ra.route = d_route_; ra.route_cap = chunk_states_ * S::NI; ra.world = (u32)world_;
+      ra.rcnt = (unsigned long long*)d_rcnt_;
+      HIPCHK(hipEventRecord(ev_[0], stream_));
+      hipLaunchKernelGGL((orig_generate<S>), dim3((unsigned)((count + BS - 1) / BS)), dim3(BS), 0, stream_, g);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(ev_[1], stream_));
+      hipLaunchKernelGGL(orig_route, dim3((unsigned)((nslots + BS * DEDUP_PER - 1) / (BS * DEDUP_PER))), dim3(BS), 0, stream_, ra);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(ev_[2], stream_));
+    }
+    u64 c[8] = {0};
+    HIPCHK(hipMemcpyAsync(c, d_rcnt_, 8 * 8, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    if (count > 0) {
+      const u64 nslots = (u64)count * S::NI;
+      auto& kg = sres_.kernels[0]; kg.ms += time_ms(0, 1); kg.launches++; kg.algo_bytes += (double)count * NWP * 4 + (double)nslots * 8;
+      u64 valid = 0; for (int r = 0; r < world_; ++r) valid += c[r];
+      auto& kr = sres_.kernels[1]; kr.ms += time_ms(1, 2); kr.launches++; kr.algo_bytes += (double)nslots * 8 + (double)valid * 16;
+    }
+    for (int r = 0; r < world_; ++r) { counts[r] = (int64_t)c[r]; fill_counts_route_[r] = c[r]; }
+    return 0;
+  }
+
+  int shard_fill(int what, void* dst, const int64_t* offsets, std::string& err) override {
+    const int rb = shard_record_bytes(what);
+    if (rb < 0 || !dst) { err = "shard_fill: bad arguments"; return MC_E_INVALID; }
+    for (int r = 0; r < world_; ++r) {
+      u64 n = 0;
+      const char* src = nullptr;
+      if (what == MC_SHARD_ROUTE) { n = fill_counts_route_[r]; src = (const char*)(d_route_ + (u64)r * chunk_states_ * S::NI * 2); }
+      else if (what == MC_SHARD_REPLY) { n = fill_counts_reply_[r]; src = (const char*)(d_newrec_ + seg_off_[r]); }
+      else { n = fill_counts_states_[r]; src = (const char*)(d_stout_ + seg_off_ack_[r] * (NWP + 4)); }
+      if (n) HIPCHK(hipMemcpyAsync((char*)dst + (u64)offsets[r] * rb, src, n * rb, hipMemcpyDeviceToDevice, stream_));
+    }
+    HIPCHK(hipStreamSynchronize(stream_));
+    return 0;
+  }
+
+  int shard_dedup(const void* recv, const int64_t* counts, int64_t* reply_counts, std::string& err) override {
+    u64 off = 0;
+    HIPCHK(hipMemsetAsync(d_rcnt_ + 8, 0, 8 * 8, stream_));
+    HIPCHK(hipEventRecord(ev_[0], stream_));
+    u64 total = 0;
+    for (int r = 0; r < world_; ++r) {
+      seg_off_[r] = off;
+      const u64 n = (u64)counts[r];
+      if (off + n > chunk_states_ * S::NI) { err = "shard_dedup: received more records than one chunk holds"; return MC_E_INVALID; }
+      if (n) {
+        DedupShArgs d;
+        d.recv = (const u64*)recv + 2 * off; d.n = n; d.table = d_table_; d.table_mask = table_mask_;
+        d.reply = d_newrec_ + off; d.counter = (unsigned long long*)(d_rcnt_ + 8 + r); d.ctr = (unsigned long long*)d_ctr_;
+        hipLaunchKernelGGL(orig_dedup_sh, dim3((unsigned)((n + BS * DEDUP_PER - 1) / (BS * DEDUP_PER))), dim3(BS), 0, stream_, d);
+        HIPCHK(hipGetLastError());
+      }
+      off += n; total += n;
+    }
+    HIPCHK(hipEventRecord(ev_[1], stream_));
+    u64 c[8] = {0};
+    HIPCHK(hipMemcpyAsync(c, d_rcnt_ + 8, 8 * 8, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    u64 nnew = 0;
+    for (int r = 0; r < world_; ++r) { reply_counts[r] = (int64_t)c[r]; fill_counts_reply_[r] = c[r]; nnew += c[r]; }
+    auto& kd = sres_.kernels[2]; kd.ms += time_ms(0, 1); kd.launches++; kd.algo_bytes += (double)total * 24 + (double)nnew * 16;
+    return 0;
+  }
+
+  int shard_materialize(const void* acks, const int64_t* counts, std::string& err) override {
+    u64 total = 0;
+    for (int r = 0; r < world_; ++r) { seg_off_ack_[r] = total; total += (u64)counts[r]; fill_counts_states_[r] = (u64)counts[r]; }
+    if (total > stout_cap_) {
+      if (d_stout_) (void)hipFree(d_stout_);
+      stout_cap_ = std::max<u64>(total, 1 << 16);
+      HIPCHK(hipMalloc(&d_stout_, stout_cap_ * (NWP + 4) * 4));
+    }
+    HIPCHK(hipEventRecord(ev_[0], stream_));
+    for (int r = 0; r < world_; ++r) {
+      const u64 n = (u64)counts[r];
+      if (!n) continue;
+      MatShArgs m;
+      m.states = d_states_; m.acks = (const u64*)acks + seg_off_ack_[r]; m.n = n; m.chunk_begin = sh_chunk_begin_;
+      m.chunk_count = sh_chunk_count_; m.out = d_stout_ + seg_off_ack_[r] * (NWP + 4); m.rank_bits = (u64)rank_ << 37;
+      m.seed = sres_.seed; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.viol = d_viol_;
+      hipLaunchKernelGGL((orig_materialize_sh<S>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, m);
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(ev_[1], stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    auto& km = sres_.kernels[3]; km.ms += time_ms(0, 1); km.launches++; km.algo_bytes += (double)total * (8 + NWP * 4 + (NWP + 4) * 4);
+    return 0;
+  }
+
+  int shard_store(const void* states, int64_t n, std::string& err) override {
+    if (n <= 0) return 0;
+    StoreArgs a;
+    a.in = (const u32*)states; a.n = (u64)n; a.dst = sh_next_write_; a.cap = cap_; a.states = d_states_; a.meta = d_meta_;
+    a.ctr = (unsigned long long*)d_ctr_;
+    HIPCHK(hipEventRecord(ev_[0], stream_));
+    hipLaunchKernelGGL((orig_store<NWP>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ev_[1], stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    auto& ks = sres_.kernels[4]; ks.ms += time_ms(0, 1); ks.launches++; ks.algo_bytes += (double)n * ((NWP + 4) * 4 + NWP * 4 + 8);
+    sh_next_write_ += (u64)n; sh_new_ += (u64)n;
+    return 0;
+  }
+
+  int shard_level_stats(int64_t* st, std::string& err) override {
+    u64 c[K_NCTR];
+    HIPCHK(hipMemcpy(c, d_ctr_, sizeof c, hipMemcpyDeviceToHost));
+    std::memset(st, 0, MC_SHARD_NSTAT * sizeof(int64_t));
+    st[0] = (int64_t)sh_new_;
+    int64_t gen = 0;
+    for (int k = 0; k < OA_NACT; ++k) { st[8 + k] = (int64_t)c[K_ACT + k]; st[40 + k] = (int64_t)c[K_ACT + OA_NACT + k]; gen += (int64_t)c[K_ACT + k]; }
+    st[1] = gen; st[2] = (int64_t)c[K_GEN_IN]; st[3] = (int64_t)(c[K_ERR] | (sh_next_write_ > cap_ ? (u64)OE_CAP_STORE : 0ull));
+    st[4] = (int64_t)c[K_VIOL]; st[5] = (int64_t)c[K_DEADLOCK]; st[6] = (int64_t)sh_level_count_;
+    return 0;
+  }
+
+  int shard_level_commit(const int64_t* g, int* done, std::string& err) override {
+    sres_.generated += g[1];
+    sres_.generated_in_model += g[2];
+    for (int k = 0; k < OA_NACT; ++k) { sres_.act_generated[k] += g[8 + k]; sres_.act_distinct[k] += g[40 + k]; }
+    sres_.levels.back().generated = g[1];
+    *done = 0;
+    if (g[3]) {
+      sres_.verdict = (g[3] & (OE_CAP_STORE | OE_TABLE_FULL | OE_CAP_ELECTIONS | OE_CAP_COUNT)) ? MC_VERDICT_CAPACITY_OVERFLOW : MC_VERDICT_EVAL_ERROR;
+      std::ostringstream os; os << "error flags 0x" << std::hex << g[3] << " raised on some rank"; sres_.error = os.str();
+      *done = 1;
+    }
+    sres_.distinct += g[0];
+    if (g[0] > 0) { sres_.levels.push_back({g[0], 0, 0.0}); sres_.depth += 1; }
+    if (!*done && g[4]) { sres_.verdict = MC_VERDICT_INVARIANT_VIOLATION; *done = 1; sres_.left_on_queue = g[0]; }
+    if (!*done && sopts_.check_deadlock && g[5]) { sres_.verdict = MC_VERDICT_DEADLOCK; *done = 1; sres_.left_on_queue = g[0]; }
+    if (!*done && g[0] == 0) *done = 1;
+    if (!*done && sopts_.max_depth && sres_.depth >= sopts_.max_depth) { sres_.verdict = MC_VERDICT_DEPTH_LIMIT; sres_.left_on_queue = g[0]; *done = 1; }
+    // advance the local level
+    sh_level_begin_ += sh_level_count_;
+    sh_level_count_ = sh_new_;
+    total_ = sh_next_write_;
+    sh_new_ = 0;
+    HIPCHK(hipMemset(d_ctr_, 0, K_NCTR * 8));
+    sres_.n_launches += 1;
+    if (*done) {
+      if (sres_.verdict == MC_VERDICT_INVARIANT_VIOLATION) {
+        ViolRec<S> v; (void)hipMemcpy(&v, d_viol_, sizeof v, hipMemcpyDeviceToHost);
+        sviol_parent_ = ((u64)rank_ << 37) | v.parent; sviol_act_ = kOrigActNames[v.act]; sviol_text_ = state_text(v.w, true);
+        sviol_bad_ = v.bad;
+        sres_.violated = first_violated(v.bad);
+      }
+      double secs = 0; for (auto& k : sres_.kernels) secs += k.ms / 1000.0;
+      sres_.seconds_kernels = secs;
+      finish(sres_, st0_);
+    }
+    return 0;
+  }
+
+  int shard_read_state(uint64_t gid, std::string& text, uint64_t* meta, std::string& err) const override {
+    const u64 local = gid & ((1ull << 37) - 1);
+    if (local >= total_) { err = "shard_read_state: state id outside this rank's store"; return MC_E_INVALID; }
+    u32 w[NWP]; u64 m = 0;
+    if (hipMemcpy(w, d_states_ + local * NWP, NWP * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&m, d_meta_ + local, 8, hipMemcpyDeviceToHost) != hipSuccess) { err = "readback failed"; return MC_E_NO_DEVICE; }
+    W s; S::unpack(w, s);
+    text = state_text(s, true);
+    if (meta) *meta = m;
+    return 0;
+  }
+  int shard_violation(uint64_t* parent, std::string& action, std::string& text) const override {
+    if (parent) *parent = sviol_parent_;
+    action = sviol_act_; text = sviol_text_;
+    return sviol_act_.empty() ? MC_E_STATE : 0;
+  }
+  const RunResult* shard_result() const override { return &sres_; }
+
  private:
   OrigModel m_;
   u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr; void* d_viol_ = nullptr;
   u64* d_cand_ = nullptr; u64* d_newrec_ = nullptr;
+  u64* d_route_ = nullptr; u64* d_rcnt_ = nullptr; u32* d_stout_ = nullptr; u64 stout_cap_ = 0;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   u64 table_mask_ = 0, cap_ = 0, total_ = 0, chunk_states_ = 0;
-  int dev_ = -1; uint64_t req_table_ = 0, req_store_ = 0;
+  int dev_ = -1, alloc_world_ = 0; uint64_t req_table_ = 0, req_store_ = 0;
+  // sharded-mode state
+  int rank_ = 0, world_ = 1;
+  RunOpts sopts_;
+  RunResult sres_;
+  std::chrono::steady_clock::time_point st0_;
+  u64 sh_level_begin_ = 0, sh_level_count_ = 0, sh_next_write_ = 0, sh_new_ = 0, sh_chunk_begin_ = 0, sh_chunk_count_ = 0;
+  u64 seg_off_[8] = {0}, seg_off_ack_[8] = {0}, fill_counts_reply_[8] = {0}, fill_counts_states_[8] = {0};
+  u64 fill_counts_route_[8] = {0};
+  u64 sviol_parent_ = 0; u32 sviol_bad_ = 0; std::string sviol_act_, sviol_text_;
 
   void release() {
-    for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, d_viol_, (void*)d_cand_, (void*)d_newrec_})
+    for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, d_viol_, (void*)d_cand_, (void*)d_newrec_,
+                    (void*)d_route_, (void*)d_rcnt_, (void*)d_stout_})
       if (p) (void)hipFree(p);
     for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
     if (stream_) (void)hipStreamDestroy(stream_);
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_viol_ = nullptr;
-    d_cand_ = nullptr; d_newrec_ = nullptr; stream_ = nullptr;
+    d_cand_ = nullptr; d_newrec_ = nullptr; d_route_ = nullptr; d_rcnt_ = nullptr; d_stout_ = nullptr; stout_cap_ = 0;
+    stream_ = nullptr; alloc_world_ = 0;
   }
 
   std::string first_violated(u32 bad) const {

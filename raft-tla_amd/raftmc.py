@@ -24,7 +24,9 @@ MC_COMPAT_INV_OUT_OF_MODEL = 0x1
 # every symbol include/raftmc.h declares
 EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stats", "mc_level_stats", "mc_kernel_stats",
            "mc_trace", "mc_report", "mc_dump_states", "mc_describe", "mc_exit_code", "mc_free",
-           "mc_close", "mc_last_error"]
+           "mc_close", "mc_last_error", "mc_shard_open", "mc_shard_record_bytes", "mc_shard_frontier",
+           "mc_shard_generate", "mc_shard_fill", "mc_shard_dedup", "mc_shard_materialize", "mc_shard_store",
+           "mc_shard_level_stats", "mc_shard_level_commit", "mc_shard_read_state", "mc_shard_violation"]
 
 
 class McOpts(ctypes.Structure):
@@ -134,6 +136,10 @@ class ModelChecker:
         rc = self.lib.mc_run(self.h)
         if rc:
             raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
+        return self.summary()
+
+    def summary(self):
+        """Result of the last completed run (mc_run, or a finished sharded BFS)."""
         s = McSummary()
         self.lib.mc_summary(self.h, ctypes.byref(s))
         actions = {}

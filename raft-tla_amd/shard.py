@@ -1,0 +1,289 @@
+"""Multi-GPU BFS: owner-partitioned fingerprints, one process per GPU.
+
+Per BFS level and frontier chunk every rank runs (include/raftmc.h mc_shard_*):
+
+  generate   expand the local chunk; route in-model successor fingerprints to
+             their owner ((fp >> 32) mod world)             -> ROUTE records
+  exchange 1 all-to-all of ROUTE records (16 B: fp, slot)
+  dedup      owner inserts them into its local seen-set      -> REPLY records
+  exchange 2 all-to-all of REPLY records back (8 B: slot)
+  materialize the generating rank re-derives the acknowledged new states
+  exchange 3 all-to-all of STATES records to the owner (80 B: state, parent, fp)
+  store      the owner appends them to its part of the next level
+
+then one all-reduce of the level counters (sum; max for the error, violation
+and deadlock flags).  All payloads are device tensors moved with
+torch.distributed (backend "nccl" = RCCL over xGMI on MI355X); with the "gloo"
+backend they are staged through host memory (used by the CPU tests and to
+run several ranks on one GPU).  Parent pointers carry the owner rank, so a
+counterexample is reassembled by chasing them across ranks.
+"""
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import raftmc as _rm
+
+ROUTE, REPLY, STATES = 0, 1, 2
+NSTAT = 72
+FLAG_SLICE = slice(3, 6)   # error flags, violation, deadlock: reduced with MAX
+
+
+class LibShard:
+    """ctypes view of the mc_shard_* entry points of one raftmc handle."""
+
+    def __init__(self, checker, rank, world):
+        self.mc, self.lib, self.h = checker, checker.lib, checker.h
+        self.world = world
+        lib = self.lib
+        P, I64P = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)
+        lib.mc_shard_open.argtypes = [P, ctypes.c_int32, ctypes.c_int32]
+        lib.mc_shard_record_bytes.argtypes = [P, ctypes.c_int32]
+        lib.mc_shard_frontier.argtypes = [P, I64P, I64P]
+        lib.mc_shard_generate.argtypes = [P, ctypes.c_int64, ctypes.c_int64, I64P]
+        lib.mc_shard_fill.argtypes = [P, ctypes.c_int32, P, I64P]
+        lib.mc_shard_dedup.argtypes = [P, P, I64P, I64P]
+        lib.mc_shard_materialize.argtypes = [P, P, I64P]
+        lib.mc_shard_store.argtypes = [P, P, ctypes.c_int64]
+        lib.mc_shard_level_stats.argtypes = [P, I64P]
+        lib.mc_shard_level_commit.argtypes = [P, I64P, ctypes.POINTER(ctypes.c_int32)]
+        lib.mc_shard_read_state.argtypes = [P, ctypes.c_uint64, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t),
+                                            ctypes.POINTER(ctypes.c_uint64)]
+        lib.mc_shard_violation.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(P), ctypes.POINTER(P)]
+        self._check(lib.mc_shard_open(self.h, rank, world))
+        self.rec_bytes = {w: lib.mc_shard_record_bytes(self.h, w) for w in (ROUTE, REPLY, STATES)}
+
+    def _check(self, rc):
+        if rc:
+            raise _rm.RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
+
+    def _arr(self, xs=None):
+        a = (ctypes.c_int64 * self.world)()
+        if xs is not None:
+            for i, x in enumerate(xs):
+                a[i] = int(x)
+        return a
+
+    @staticmethod
+    def _ptr(t):
+        return ctypes.c_void_p(t.data_ptr() if t.numel() else 0)
+
+    def frontier(self):
+        s, c = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.mc_shard_frontier(self.h, ctypes.byref(s), ctypes.byref(c)))
+        return s.value, c.value
+
+    def generate(self, begin, count):
+        out = self._arr()
+        self._check(self.lib.mc_shard_generate(self.h, begin, count, out))
+        return list(out)
+
+    def fill(self, what, dst, offsets):
+        self._check(self.lib.mc_shard_fill(self.h, what, self._ptr(dst), self._arr(offsets)))
+
+    def dedup(self, recv, counts):
+        out = self._arr()
+        self._check(self.lib.mc_shard_dedup(self.h, self._ptr(recv), self._arr(counts), out))
+        return list(out)
+
+    def materialize(self, acks, counts):
+        self._check(self.lib.mc_shard_materialize(self.h, self._ptr(acks), self._arr(counts)))
+
+    def store(self, states, n):
+        self._check(self.lib.mc_shard_store(self.h, self._ptr(states), n))
+
+    def level_stats(self):
+        a = (ctypes.c_int64 * NSTAT)()
+        self._check(self.lib.mc_shard_level_stats(self.h, a))
+        return list(a)
+
+    def level_commit(self, g):
+        a = (ctypes.c_int64 * NSTAT)(*[int(x) for x in g])
+        done = ctypes.c_int32()
+        self._check(self.lib.mc_shard_level_commit(self.h, a, ctypes.byref(done)))
+        return bool(done.value)
+
+    def read_state(self, gid):
+        p, n, meta = ctypes.c_void_p(), ctypes.c_size_t(), ctypes.c_uint64()
+        self._check(self.lib.mc_shard_read_state(self.h, gid, ctypes.byref(p), ctypes.byref(n), ctypes.byref(meta)))
+        s = ctypes.string_at(p, n.value).decode()
+        self.lib.mc_free(p)
+        return s, meta.value
+
+    def violation(self):
+        parent, a, t = ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_void_p()
+        if self.lib.mc_shard_violation(self.h, ctypes.byref(parent), ctypes.byref(a), ctypes.byref(t)):
+            return None
+        act, text = ctypes.string_at(a).decode(), ctypes.string_at(t).decode()
+        self.lib.mc_free(a)
+        self.lib.mc_free(t)
+        return parent.value, act, text
+
+
+class Exchanger:
+    """all-to-all of variable-size byte payloads between the ranks of a process group."""
+
+    def __init__(self, world, device, group=None):
+        self.world, self.device, self.group = world, device, group
+        backend = dist.get_backend(group) if world > 1 else "local"
+        self.host_staged = backend == "gloo"
+
+    def counts(self, mine):
+        if self.world == 1:
+            return list(mine)
+        dev = "cpu" if self.host_staged else self.device
+        t = torch.tensor(mine, dtype=torch.int64, device=dev)
+        out = torch.empty_like(t)
+        dist.all_to_all_single(out, t, group=self.group)
+        return out.tolist()
+
+    def payload(self, send, send_counts, recv_counts, rec_bytes):
+        """send: uint8 device tensor holding the per-destination segments in rank order."""
+        rb = [c * rec_bytes for c in recv_counts]
+        if self.world == 1:
+            return send
+        if self.host_staged:
+            s = send.cpu()
+            r = torch.empty(sum(rb), dtype=torch.uint8)
+            dist.all_to_all_single(r, s, rb, [c * rec_bytes for c in send_counts], group=self.group)
+            return r.to(self.device)
+        r = torch.empty(sum(rb), dtype=torch.uint8, device=self.device)
+        dist.all_to_all_single(r, send, rb, [c * rec_bytes for c in send_counts], group=self.group)
+        torch.cuda.synchronize(self.device)
+        return r
+
+    def allreduce_stats(self, st):
+        if self.world == 1:
+            return list(st)
+        dev = "cpu" if self.host_staged else self.device
+        t = torch.tensor(st, dtype=torch.int64, device=dev)
+        m = t[FLAG_SLICE].clone()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
+        t[FLAG_SLICE] = m
+        return t.tolist()
+
+    def allreduce_max(self, x):
+        if self.world == 1:
+            return x
+        dev = "cpu" if self.host_staged else self.device
+        t = torch.tensor([x], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+    def broadcast_obj(self, obj, src):
+        if self.world == 1:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=src, group=self.group)
+        return box[0]
+
+
+def _offsets(counts):
+    off, acc = [], 0
+    for c in counts:
+        off.append(acc)
+        acc += c
+    return off
+
+
+def sharded_bfs(shard, ex, rank, device):
+    """Drive the level loop; returns the (rank-0) trace list on a violation."""
+    world = ex.world
+    while True:
+        front, chunk = shard.frontier()
+        nchunks = ex.allreduce_max((front + chunk - 1) // chunk if front else 0)
+        for c in range(nchunks):
+            begin = c * chunk
+            count = max(0, min(chunk, front - begin))
+            send_counts = shard.generate(min(begin, front), count)
+            recv_counts = ex.counts(send_counts)
+            rb = shard.rec_bytes[ROUTE]
+            send = torch.empty(sum(send_counts) * rb, dtype=torch.uint8, device=device)
+            shard.fill(ROUTE, send, _offsets(send_counts))
+            recv = ex.payload(send, send_counts, recv_counts, rb)
+            reply_counts = shard.dedup(recv, recv_counts)           # replies[r] go back to rank r
+            ack_counts = ex.counts(reply_counts)
+            rb = shard.rec_bytes[REPLY]
+            send = torch.empty(sum(reply_counts) * rb, dtype=torch.uint8, device=device)
+            shard.fill(REPLY, send, _offsets(reply_counts))
+            acks = ex.payload(send, reply_counts, ack_counts, rb)
+            shard.materialize(acks, ack_counts)                      # states for owner r = acks from r
+            rb = shard.rec_bytes[STATES]
+            send = torch.empty(sum(ack_counts) * rb, dtype=torch.uint8, device=device)
+            shard.fill(STATES, send, _offsets(ack_counts))
+            states = ex.payload(send, ack_counts, reply_counts, rb)
+            shard.store(states, sum(reply_counts))
+        g = ex.allreduce_stats(shard.level_stats())
+        if shard.level_commit(g):
+            break
+    return _trace(shard, ex, rank, world)
+
+
+def _trace(shard, ex, rank, world):
+    v = shard.violation()
+    # the lowest rank that recorded a violation reports it
+    top = ex.allreduce_max(world - rank if v is not None else 0)
+    if top == 0:
+        return None
+    src = world - top
+    head = ex.broadcast_obj(v, src)
+    if head is None:
+        return None
+    parent, act, text = head
+    trace = [(act, text)]
+    gid = parent
+    for _ in range(1 << 20):
+        owner = (gid >> 37) & 7
+        mine = shard.read_state(gid) if owner == rank else None
+        text, meta = ex.broadcast_obj(mine, owner)
+        if meta == (1 << 64) - 1:
+            trace.append(("<Initial predicate>", text))
+            break
+        act_id = (meta >> 16) & 0xFF
+        trace.append((shard.mc.describe()["actions"][act_id], text))
+        gid = meta >> 24
+    trace.reverse()
+    return trace
+
+
+def trace_text(trace):
+    out = []
+    for k, (act, text) in enumerate(trace):
+        out.append("State %d: %s\n%s\n" % (k + 1, "<Initial predicate>" if k == 0 else "<%s>" % act, text))
+    return "\n".join(out) + ("\n" if out else "")
+
+
+class ShardedChecker:
+    """One rank of a sharded model-checking job; run() may be called repeatedly
+    (device buffers are kept, the seen-set is re-zeroed by mc_shard_open)."""
+
+    def __init__(self, spec, config, rank, world, device_index=0, group=None, **kw):
+        self.rank, self.world = rank, world
+        self.device = torch.device("cuda", device_index)
+        self.mc = _rm.ModelChecker(spec, config, device=device_index, **kw)
+        self.ex = Exchanger(world, self.device, group)
+
+    def run(self):
+        shard = LibShard(self.mc, self.rank, self.world)
+        trace = sharded_bfs(shard, self.ex, self.rank, self.device)
+        res = self.mc.summary()
+        if trace:
+            res.trace_text = trace_text(trace)
+        return res
+
+    def close(self):
+        self.mc.close()
+
+
+def check_sharded(spec, config, rank, world, device_index=0, group=None, **kw):
+    """Run one sharded BFS on this rank (call on every rank of the group).
+
+    Returns the raftmc Result (identical on every rank) with .trace_text
+    assembled across ranks."""
+    sc = ShardedChecker(spec, config, rank, world, device_index, group, **kw)
+    try:
+        return sc.run()
+    finally:
+        sc.close()

@@ -1,0 +1,85 @@
+"""GPU tests of the sharded (multi-GPU) BFS through the C ABI.
+
+On a one-GPU box the N>1 path runs as several ranks on cuda:0 with the gloo
+backend (payloads staged through host memory); on a node, bench.py runs the
+same code with RCCL.  The sharded result must equal the single-GPU result:
+identical generated / distinct / depth and per-action generated counts, and
+on a violation a shortest counterexample reassembled across ranks."""
+import importlib
+import json
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle_util import CONFIGS, GOLDEN, ORIG_MC
+
+pytestmark = pytest.mark.gpu
+
+SMALL = dict(fp_table_bytes=1 << 26, state_store_bytes=1 << 28)
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cfg, kw, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shard = importlib.import_module("raft-tla_amd.shard")
+    try:
+        r = shard.check_sharded(ORIG_MC, cfg, rank, world, device_index=0, **kw)
+        q.put((rank, r.verdict, r.generated, r.distinct, r.depth, {k: v[0] for k, v in r.actions.items()},
+               r.violated, getattr(r, "trace_text", "")))
+    except Exception as e:   # surface the error instead of hanging the parent
+        q.put((rank, "ERROR: %r" % e, 0, 0, 0, {}, "", ""))
+    dist.destroy_process_group()
+
+
+def run_sharded(cfg, world, **kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, cfg, {**SMALL, **kw}, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    return out
+
+
+def test_sharded_world1_equals_single(raftmc):
+    shard = importlib.import_module("raft-tla_amd.shard")
+    cfg = os.path.join(CONFIGS, "parity_pair.cfg")
+    g = json.load(open(os.path.join(GOLDEN, "orig_parity.json")))["parity_pair"]
+    r = shard.check_sharded(ORIG_MC, cfg, 0, 1, **SMALL)
+    assert (r.verdict, r.generated, r.distinct, r.depth) == ("OK", g["generated"], g["distinct"], g["depth"])
+    assert {k: v[0] for k, v in r.actions.items()} == {k: v[0] for k, v in g["actions"].items()}
+
+
+@pytest.mark.parametrize("name,world", [("parity_pair", 2), ("parity_trio", 2), ("parity_pair_neg", 3)])
+def test_sharded_ranks_on_one_gpu(name, world):
+    g = json.load(open(os.path.join(GOLDEN, "orig_parity.json")))[name]
+    out = run_sharded(os.path.join(CONFIGS, name + ".cfg"), world)
+    for rank, verdict, gen, dist_, depth, acts, _, _ in out:
+        assert verdict == "OK", verdict
+        assert (gen, dist_, depth) == (g["generated"], g["distinct"], g["depth"])
+        assert acts == {k: v[0] for k, v in g["actions"].items()}
+
+
+def test_sharded_violation_trace():
+    out = run_sharded(os.path.join(CONFIGS, "scenario_first_leader.cfg"), 2)
+    rank0 = out[0]
+    assert rank0[1] == "INVARIANT_VIOLATION" and rank0[6] == "NoLeader"
+    states = rank0[7].strip().split("\n\n")
+    assert len(states) == 10                     # same shortest length as the single-GPU / oracle run
+    assert states[0].startswith("State 1: <Initial predicate>")
+    assert "<BecomeLeader>" in states[-1].split("\n")[0]
