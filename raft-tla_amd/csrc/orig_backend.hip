@@ -754,13 +754,14 @@ class OrigGpu : public Backend {
 
   int shard_fill(int what, void* dst, const int64_t* offsets, std::string& err) override {
     const int rb = shard_record_bytes(what);
-    if (rb < 0 || !dst) { err = "shard_fill: bad arguments"; return MC_E_INVALID; }
+    if (rb < 0) { err = "shard_fill: bad record kind"; return MC_E_INVALID; }
     for (int r = 0; r < world_; ++r) {
       u64 n = 0;
       const char* src = nullptr;
       if (what == MC_SHARD_ROUTE) { n = fill_counts_route_[r]; src = (const char*)(d_route_ + (u64)r * chunk_states_ * S::NI * 2); }
       else if (what == MC_SHARD_REPLY) { n = fill_counts_reply_[r]; src = (const char*)(d_newrec_ + seg_off_[r]); }
       else { n = fill_counts_states_[r]; src = (const char*)(d_stout_ + seg_off_ack_[r] * (NWP + 4)); }
+      if (n && !dst) { err = "shard_fill: null destination for a non-empty segment"; return MC_E_INVALID; }
       if (n) HIPCHK(hipMemcpyAsync((char*)dst + (u64)offsets[r] * rb, src, n * rb, hipMemcpyDeviceToDevice, stream_));
     }
     HIPCHK(hipStreamSynchronize(stream_));
