@@ -146,6 +146,8 @@ struct Spec {
   virtual std::vector<int> view_vars(const std::string& view) const { (void)view; return {}; }
   // SYMMETRY: permutations of model values (each a full mv-id map), empty => none
   virtual std::vector<std::vector<int>> symmetry_perms(const std::string& sym) const { (void)sym; return {}; }
+  // the text written by --dump and in traces (default: every variable, see state_text)
+  virtual std::string dump_line(const State& s) const;
 };
 
 // ----------------------------------------------------------------- BFS
@@ -177,6 +179,7 @@ inline std::string state_text(const Spec& sp, const State& s) {
   for (size_t q = 0; q < s.size(); ++q) { if (q) t += " /\\ "; t += vn[q] + " = " + show(s[q]); }
   return t;
 }
+inline std::string Spec::dump_line(const State& s) const { return state_text(*this, s); }
 
 // Canonical key of a state under SYMMETRY/VIEW (the text replaces TLC's FP64).
 inline std::string canon_key(const Spec& sp, const Cfg& cfg, const Options& o, const State& s,
@@ -256,7 +259,7 @@ inline Result bfs(const Spec& sp, const Cfg& cfg, const Options& o) {
         if (isnew) {
           store.push_back(s); nodes.push_back({-1, -1, 1});
           frontier.push_back((int64_t)store.size() - 1);
-          if (dump) std::fprintf(dump, "%s\n", state_text(sp, s).c_str());
+          if (dump) std::fprintf(dump, "%s\n", sp.dump_line(s).c_str());
         }
       }
       if (isnew || (!im && o.inv_out_of_model)) {
@@ -296,7 +299,7 @@ inline Result bfs(const Spec& sp, const Cfg& cfg, const Options& o) {
               store.push_back(su.s); nodes.push_back({idx, su.action, level + 1});
               nextf.push_back((int64_t)store.size() - 1);
               r.act_distinct[su.action]++;
-              if (dump) std::fprintf(dump, "%s\n", state_text(sp, su.s).c_str());
+              if (dump) std::fprintf(dump, "%s\n", sp.dump_line(su.s).c_str());
             }
           }
           if (isnew || (!im && o.inv_out_of_model)) {

@@ -96,7 +96,7 @@ int main(int argc, char** argv) {
         js += ", \"trace\": [";
         for (size_t q = 0; q < r.trace.size(); ++q)
           js += (q ? ", " : "") + std::string("{\"action\": ") + json_str(r.trace[q].first < 0 ? "Init" : an[r.trace[q].first]) +
-                ", \"state\": " + json_str(state_text(*sp, r.trace[q].second)) + "}";
+                ", \"state\": " + json_str(sp->dump_line(r.trace[q].second)) + "}";
         js += "]";
       }
       js += "}";

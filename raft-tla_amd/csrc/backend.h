@@ -65,5 +65,6 @@ struct Backend {
 };
 
 Backend* make_orig_backend(const CfgFile& cfg);   // throws CfgError
+Backend* make_memb_backend(const CfgFile& cfg);   // throws CfgError
 
 }  // namespace rmc

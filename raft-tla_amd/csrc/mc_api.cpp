@@ -82,7 +82,8 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
     std::string fam = rmc::detect_spec_family(rmc::read_text_file(tla_path));
     rmc::CfgFile cfg = rmc::parse_cfg_text(rmc::read_text_file(cfg_path));
     if (fam == "raft_original") c->be.reset(rmc::make_orig_backend(cfg));
-    else throw rmc::CfgError(MC_E_UNSUPPORTED, "spec family '" + fam + "' has no GPU backend in this build (raft_original only)");
+    else if (fam == "tlc_membership") c->be.reset(rmc::make_memb_backend(cfg));
+    else throw rmc::CfgError(MC_E_UNSUPPORTED, "spec family '" + fam + "' has no GPU backend in this build");
   } catch (const rmc::CfgError& e) {
     c->last_error = e.what();
     int code = e.code;

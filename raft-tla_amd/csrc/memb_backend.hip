@@ -1,0 +1,787 @@
+// raftmc — gfx950 BFS backend for tlc_membership/raft.tla (SYMMETRY perms,
+// VIEW vars, history summary automaton, scenario properties).
+//
+// Under VIEW the reachable set depends on WHICH successor of a view class is
+// kept (history is outside the view but read by constraints, raft.tla:1105-1137),
+// so the search reproduces TLC's single-worker FIFO first-found order
+// (SURVEY.md §7 hard part 2): every successor has a key
+//     key = (rank of its parent in the level) * NSLOT + slot(instance, sub)
+// equal to its position in the oracle's enumeration order, the seen-set keeps
+// the minimum key per fingerprint of the level (atomicMax on the complement),
+// and the next level is written in key order.  Per frontier chunk:
+//
+//  1. memb_expand     lane per state, wave-uniform loop over the Next
+//                     instances; constraint filter, out-of-model invariant
+//                     checks; in-model cells compacted with wave ballots
+//  1b memb_fingerprint lane per in-model successor (full lanes): re-derive it,
+//                     symmetric FP64 of the view (min over Permutations(Server))
+//                     into cand[slot][state]
+//  2. memb_dedup      16 independent seen-set probes per thread over 16-B
+//                     entries (fp, ~level|key); insert-if-absent with CAS,
+//                     then atomicMax of ~(level << 40 | key); cand := entry+1
+//  3. memb_select     lane per state: which of its slots won its fingerprint
+//                     (entry still holds its own key), per-block exclusive scan
+//  4. memb_scan_blocks exclusive scan of the block totals (one workgroup)
+//  5. memb_compact    lane per state: winners' (parent, slot) records in key order
+//  6. memb_materialize lane per new state: re-derive, store packed state and
+//                     parent pointer, per-action distinct counts, invariants
+//
+// The first "event" of a level in key order (TLC evaluation error while
+// computing successors, deadlock, invariant error, invariant violation) is the
+// 64-bit atomicMin of (key << 2 | kind); the host re-derives that successor
+// with the same spec code to name the invariant and build the trace.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+
+#include "../../include/raftmc.h"
+#include "backend.h"
+#include "memb_spec.h"
+#include "memb_text.h"
+
+namespace rmc {
+
+namespace {
+enum {
+  C_CELLS = 0, C_ERR = 1, C_EVENT = 2, C_NEW = 3, C_ERRGID = 4, C_GEN_IN = 5,
+  C_ACT = 8, C_NCTR = C_ACT + 2 * MA_NACT
+};
+enum { EV_NEXT_ERROR = 0, EV_DEADLOCK = 1, EV_INV_ERROR = 2, EV_VIOLATION = 3 };
+enum { MERR_TABLE_FULL = 0x100, MERR_STORE = 0x200 };
+constexpr int BS = 256;
+constexpr int DPER = 16;               // probes in flight per dedup thread
+constexpr u64 WINBIT = 1ull << 63;
+constexpr u32 OOM_BIT = 1u << 31;      // a compacted cell holding an out-of-model successor
+constexpr int SCAN_MAX_BLOCKS = 4096;  // chunk <= 4096 * BS states
+}  // namespace
+
+struct MGenArgs {
+  const u32* states;
+  u64 chunk_begin, chunk_count, rank0;     // first state of the chunk: gid and rank in its level
+  u64* cand;                               // [NSLOT][chunk] fingerprints, 0 = none
+  u32* cells;                              // compacted cells (slot * chunk + state) of in-model successors
+  unsigned short* nsucc;                   // [chunk] successors per state (TLC "generated")
+  u64 seed;
+  MembRuntime rt;
+  u32 inv_oom, deadlock;
+  unsigned long long* ctr;
+};
+
+// Phase 1 for one instance group [K0, K1) with NS successors per instance.  The group bounds
+// are compile-time so the instance dispatch folds away; launder() keeps the per-state decodes
+// inside the loop body (hoisting them over ~100 instances exhausts the register file).
+template <class S, int K0, int K1, int NS>
+__device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs& a, bool active, u64 tid, u32& err,
+                                             u32& nsucc, u32& nin, unsigned int* lds_cnt) {
+  using W = typename S::Work;
+  const int lane = __lane_id();
+  const bool en = S::group_enabled(K0, a.rt.next);                   // wave-uniform
+  for (int k = K0; k < K1; ++k) {
+    for (int sub = 0; sub < NS; ++sub) {
+      const int slot = S::slot_of(k, sub);
+      if (active) a.cand[(u64)slot * a.chunk_count + tid] = 0;
+      if (!en) continue;
+      S::launder(s);
+      bool need = false, oom = false;
+      if (active) {
+        W t;
+        const int act = S::apply(s, k, sub, t, err, a.rt);
+        if (act >= 0) {
+          ++nsucc;
+          atomicAdd(&lds_cnt[act], 1u);
+          if (S::in_model(t, s, a.rt)) {
+            if (t.bag.v[S::MK] != S::EMPTY) err |= ME_CAP;           // bag domain beyond the compiled capacity
+            need = true;
+            ++nin;
+          } else if (a.inv_oom) {
+            need = oom = true;                                       // invariants checked in phase 2
+          }
+        }
+      }
+      const u64 mask = __ballot(need);
+      if (mask) {
+        const int leader = __ffsll((unsigned long long)mask) - 1;
+        u32 base = 0;
+        if (lane == leader) base = (u32)atomicAdd(&a.ctr[C_CELLS], (unsigned long long)__popcll(mask));
+        base = __shfl(base, leader);
+        if (need) a.cells[base + __popcll(mask & ((1ull << lane) - 1ull))] = (u32)((u64)slot * a.chunk_count + tid) | (oom ? OOM_BIT : 0u);
+      }
+    }
+  }
+}
+
+// Phase 1: successors, constraints and TLC "generated" counts; in-model (and, for the
+// invariant check, out-of-model) cells are appended with one atomic per wave and slot.
+template <class S>
+__global__ void __launch_bounds__(BS) memb_expand(MGenArgs a) {
+  using W = typename S::Work;
+  constexpr int NWP = S::NWP;
+  __shared__ unsigned int lds_cnt[MA_NACT + 1];
+  for (int t = threadIdx.x; t < MA_NACT + 1; t += BS) lds_cnt[t] = 0;
+  __syncthreads();
+  const u64 tid = (u64)blockIdx.x * BS + threadIdx.x;
+  const bool active = tid < a.chunk_count;
+  const u64 gid = a.chunk_begin + tid, kbase = (a.rank0 + tid) * (u64)S::NSLOT;
+  W s;
+  if (active) {
+    u32 w[NWP];
+    const uint4* src = reinterpret_cast<const uint4*>(a.states + gid * NWP);
+#pragma unroll
+    for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+    S::unpack(w, s);
+  } else {
+    S::init(s);
+  }
+  u32 err = 0, nsucc = 0, nin = 0;
+  expand_group<S, S::G_RV, S::G_BL, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_BL, S::G_CR, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_CR, S::G_ACI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_ACI, S::G_AE, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_AE, S::G_RECV, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_RECV, S::G_TO, 2>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_TO, S::G_RS, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_RS, S::G_DUP, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_DUP, S::G_DROP, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_DROP, S::G_ADD, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_ADD, S::G_DEL, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_DEL, S::NI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  unsigned long long ev = ~0ull;
+  if (active) {
+    a.nsucc[tid] = (unsigned short)nsucc;
+    if (err & ME_EVAL) { const u64 e = (kbase << 2) | EV_NEXT_ERROR; ev = e < ev ? e : ev; }
+    if (nsucc == 0 && a.deadlock) { const u64 e = (kbase << 2) | EV_DEADLOCK; ev = e < ev ? e : ev; }
+    if (err & ME_CAP) {
+      atomicOr(&a.ctr[C_ERR], (unsigned long long)ME_CAP);
+      atomicCAS(&a.ctr[C_ERRGID], 0ull, (unsigned long long)(gid + 1));
+    }
+  }
+  if (ev != ~0ull) atomicMin(&a.ctr[C_EVENT], ev);
+  if (nin) atomicAdd(&lds_cnt[MA_NACT], nin);
+  __syncthreads();
+  for (int t = threadIdx.x; t < MA_NACT; t += BS)
+    if (lds_cnt[t]) atomicAdd(&a.ctr[C_ACT + t], (unsigned long long)lds_cnt[t]);
+  if (threadIdx.x == 0 && lds_cnt[MA_NACT]) atomicAdd(&a.ctr[C_GEN_IN], (unsigned long long)lds_cnt[MA_NACT]);
+}
+
+// Phase 2: one lane per in-model successor (full lanes): re-derive it and store its
+// symmetric FP64 into its cell (cand[slot][state], coalesced order is not needed here).
+template <class S>
+__global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a, u64 ncells) {
+  using W = typename S::Work;
+  constexpr int NWP = S::NWP;
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  if (i >= ncells) return;
+  const u32 cw = a.cells[i], cell = cw & ~OOM_BIT;
+  const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
+  int k, sub;
+  S::inst_of_slot((int)slot, k, sub);
+  u32 w[NWP];
+  const uint4* src = reinterpret_cast<const uint4*>(a.states + (a.chunk_begin + st) * NWP);
+#pragma unroll
+  for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+  W s, t;
+  S::unpack(w, s);
+  u32 err = 0;
+  S::apply(s, k, sub, t, err, a.rt);
+  if (!(cw & OOM_BIT)) {
+    a.cand[cell] = S::fingerprint(t, a.seed, a.rt);
+    return;
+  }
+  // an out-of-model successor: TLC still checks the invariants on it ([ext] switch (ii))
+  const u32 r = S::check_invariants(t, a.rt);
+  if (r) {
+    const u64 e = (((a.rank0 + st) * (u64)S::NSLOT + slot) << 2) | ((r >> 8) == IV_BAD ? EV_VIOLATION : EV_INV_ERROR);
+    atomicMin(&a.ctr[C_EVENT], (unsigned long long)e);
+  }
+}
+
+struct MDedupArgs {
+  u64* cand;
+  u64 nslots, chunk_count, rank0, nslot, level;
+  u64* table;                  // [2 * slots] (fp, ~(level << 40 | key)); zero = empty
+  u64 table_mask;
+  unsigned long long* ctr;
+};
+
+__global__ void __launch_bounds__(BS) memb_dedup(MDedupArgs a) {
+  const u64 tile = (u64)blockIdx.x * (BS * DPER);
+  u64 fp[DPER], cur[DPER], pos[DPER];
+#pragma unroll
+  for (int j = 0; j < DPER; ++j) {
+    const u64 idx = tile + (u64)j * BS + threadIdx.x;
+    fp[j] = idx < a.nslots ? a.cand[idx] : 0ull;
+    pos[j] = fp[j] & a.table_mask;
+  }
+#pragma unroll
+  for (int j = 0; j < DPER; ++j) cur[j] = fp[j] ? a.table[2 * pos[j]] : ~0ull;
+#pragma unroll
+  for (int j = 0; j < DPER; ++j)
+    if (fp[j] && cur[j] == 0ull)
+      cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[2 * pos[j]], 0ull, (unsigned long long)fp[j]);
+  u32 err = 0;
+#pragma unroll
+  for (int j = 0; j < DPER; ++j) {
+    if (!fp[j]) continue;
+    if (cur[j] == 0ull || cur[j] == fp[j]) continue;          // inserted here, or already present
+    u64 slot = (pos[j] + 1) & a.table_mask;
+    for (int probe = 0;; ++probe) {
+      if (probe >= (1 << 20)) { err |= MERR_TABLE_FULL; break; }
+      const u64 c = a.table[2 * slot];
+      if (c == fp[j]) break;
+      if (c == 0ull) {
+        const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[2 * slot], 0ull, (unsigned long long)fp[j]);
+        if (old == 0ull || old == fp[j]) break;
+      }
+      slot = (slot + 1) & a.table_mask;
+    }
+    pos[j] = slot;
+  }
+  // FIFO first-found: keep the minimum (level, key) per fingerprint (older levels always win)
+#pragma unroll
+  for (int j = 0; j < DPER; ++j) {
+    if (!fp[j]) continue;
+    const u64 idx = tile + (u64)j * BS + threadIdx.x;
+    const u64 sl = idx / a.chunk_count, st = idx - sl * a.chunk_count;
+    const u64 key = (a.rank0 + st) * a.nslot + sl;
+    atomicMax((unsigned long long*)&a.table[2 * pos[j] + 1], (unsigned long long)~((a.level << 40) | key));
+    a.cand[idx] = pos[j] + 1;
+  }
+  if (err) atomicOr(&a.ctr[C_ERR], (unsigned long long)err);
+}
+
+struct MSelArgs {
+  u64* cand;
+  u64 chunk_count, rank0, nslot, level;
+  const u64* table;
+  unsigned int* woff;          // [chunk] block-local exclusive offsets
+  unsigned long long* bsum;    // [blocks] block totals
+};
+
+__global__ void __launch_bounds__(BS) memb_select(MSelArgs a) {
+  __shared__ unsigned int wave_tot[BS / 64];
+  const u64 tid = (u64)blockIdx.x * BS + threadIdx.x;
+  const int lane = __lane_id(), wave = threadIdx.x >> 6;
+  unsigned int mine = 0;
+  if (tid < a.chunk_count) {
+    const u64 kb = (a.rank0 + tid) * a.nslot;
+    for (u64 sl = 0; sl < a.nslot; ++sl) {
+      const u64 c = a.cand[sl * a.chunk_count + tid];
+      if (!c) continue;
+      const u64 want = ~((a.level << 40) | (kb + sl));
+      if (a.table[2 * (c - 1) + 1] == want) { a.cand[sl * a.chunk_count + tid] = c | WINBIT; ++mine; }
+    }
+  }
+  unsigned int incl = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) { const unsigned int v = __shfl_up(incl, d); if (lane >= d) incl += v; }
+  if (lane == 63) wave_tot[wave] = incl;
+  __syncthreads();
+  unsigned int base = 0;
+  for (int w = 0; w < wave; ++w) base += wave_tot[w];
+  if (tid < a.chunk_count) a.woff[tid] = base + incl - mine;
+  if (threadIdx.x == BS - 1) a.bsum[blockIdx.x] = base + incl;
+}
+
+// exclusive scan of up to SCAN_MAX_BLOCKS block totals in one workgroup; total -> ctr[C_NEW]
+__global__ void __launch_bounds__(BS) memb_scan_blocks(unsigned long long* bsum, u32 nblocks, unsigned long long* ctr) {
+  __shared__ unsigned long long part[BS];
+  constexpr int PER = SCAN_MAX_BLOCKS / BS;
+  unsigned long long v[PER], s = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) { const u32 b = threadIdx.x * PER + j; v[j] = b < nblocks ? bsum[b] : 0ull; s += v[j]; }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 1; d < BS; d <<= 1) {
+    const unsigned long long x = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0ull;
+    __syncthreads();
+    part[threadIdx.x] += x;
+    __syncthreads();
+  }
+  unsigned long long run = part[threadIdx.x] - s;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) { const u32 b = threadIdx.x * PER + j; if (b < nblocks) bsum[b] = run; run += v[j]; }
+  if (threadIdx.x == BS - 1) ctr[C_NEW] = part[BS - 1];
+}
+
+struct MCompArgs {
+  const u64* cand;
+  u64 chunk_count, chunk_begin, nslot;
+  const unsigned int* woff;
+  const unsigned long long* bsum;
+  u64* newrec;                 // (parent gid << 10 | slot), key order
+};
+
+__global__ void __launch_bounds__(BS) memb_compact(MCompArgs a) {
+  const u64 tid = (u64)blockIdx.x * BS + threadIdx.x;
+  if (tid >= a.chunk_count) return;
+  u64 o = a.bsum[blockIdx.x] + a.woff[tid];
+  const u64 gid = a.chunk_begin + tid;
+  for (u64 sl = 0; sl < a.nslot; ++sl)
+    if (a.cand[sl * a.chunk_count + tid] & WINBIT) a.newrec[o++] = (gid << 10) | sl;
+}
+
+struct MMatArgs {
+  u32* states;
+  u64* meta;
+  const u64* newrec;
+  u64 n_new, dst_base, cap, level_begin;
+  MembRuntime rt;
+  unsigned long long* ctr;
+};
+
+template <class S>
+__global__ void __launch_bounds__(BS) memb_materialize(MMatArgs a) {
+  using W = typename S::Work;
+  constexpr int NW = S::NW, NWP = S::NWP;
+  __shared__ unsigned int lds_cnt[MA_NACT];
+  for (int t = threadIdx.x; t < MA_NACT; t += BS) lds_cnt[t] = 0;
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  u32 err = 0;
+  unsigned long long ev = ~0ull;
+  if (i < a.n_new) {
+    const u64 rec = a.newrec[i], gid = rec >> 10;
+    const int slot = (int)(rec & 1023);
+    int k, sub;
+    S::inst_of_slot(slot, k, sub);
+    u32 w[NWP];
+    const uint4* src = reinterpret_cast<const uint4*>(a.states + gid * NWP);
+#pragma unroll
+    for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+    W s, t;
+    S::unpack(w, s);
+    const int act = S::apply(s, k, sub, t, err, a.rt);
+    const u64 dst = a.dst_base + i;
+    if (act >= 0 && dst < a.cap) {
+      u32 pw[NW];
+      S::pack(t, pw);
+      uint4* o = reinterpret_cast<uint4*>(a.states + dst * NWP);
+#pragma unroll
+      for (int q = 0; q < NWP / 4; ++q)
+        o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
+      a.meta[dst] = (gid << 20) | ((u64)act << 10) | (u64)slot;
+      atomicAdd(&lds_cnt[act], 1u);
+      const u32 r = S::check_invariants(t, a.rt);
+      if (r) ev = ((((gid - a.level_begin) * (u64)S::NSLOT + (u64)slot)) << 2) | ((r >> 8) == IV_BAD ? EV_VIOLATION : EV_INV_ERROR);
+    } else {
+      err |= dst >= a.cap ? (u32)MERR_STORE : (u32)ME_CAP;
+    }
+  }
+  if (err) atomicOr(&a.ctr[C_ERR], (unsigned long long)err);
+  if (ev != ~0ull) atomicMin(&a.ctr[C_EVENT], ev);
+  __syncthreads();
+  for (int t = threadIdx.x; t < MA_NACT; t += BS)
+    if (lds_cnt[t]) atomicAdd(&a.ctr[C_ACT + MA_NACT + t], (unsigned long long)lds_cnt[t]);
+}
+
+#define HIPCHK(x)                                                                             \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) { err = std::string(#x) + ": " + hipGetErrorString(e_); return MC_E_NO_DEVICE; } \
+  } while (0)
+
+template <class S>
+class MembGpu : public Backend {
+ public:
+  using W = typename S::Work;
+  static constexpr int NWP = S::NWP;
+  explicit MembGpu(const MembModel& m) : m_(m), text_(m_) {}
+  ~MembGpu() override { release(); }
+
+  std::string family() const override { return "tlc_membership"; }
+
+  std::string describe_json() const override {
+    std::ostringstream o;
+    o << "{\"spec\": \"tlc_membership\", \"N\": " << S::N << ", \"NV\": " << S::NV << ", \"MK\": " << S::MK
+      << ", \"next\": \"" << m_.next_name << "\", \"symmetry\": " << (m_.rt.symmetry ? "true" : "false")
+      << ", \"permutations\": " << (m_.rt.symmetry ? S::NPERM : 1) << ", \"view\": \"vars\", \"init_server_mask\": " << m_.rt.init_cfg
+      << ", \"num_rounds\": " << m_.rt.num_rounds << ", \"state_words\": " << S::NW << ", \"state_bytes_stored\": " << NWP * 4
+      << ", \"instances\": " << S::NI << ", \"slots\": " << S::NSLOT << ", \"constraints\": [";
+    for (size_t k = 0; k < m_.constraint_names.size(); ++k) o << (k ? ", " : "") << "\"" << m_.constraint_names[k] << "\"";
+    o << "], \"action_constraints\": [";
+    for (size_t k = 0; k < m_.action_constraint_names.size(); ++k) o << (k ? ", " : "") << "\"" << m_.action_constraint_names[k] << "\"";
+    o << "], \"invariants\": [";
+    for (size_t k = 0; k < m_.inv_names.size(); ++k) o << (k ? ", " : "") << "\"" << m_.inv_names[k] << "\"";
+    o << "], \"actions\": [";
+    for (int k = 0; k < MA_NACT; ++k) o << (k ? ", " : "") << "\"" << kMembActNames[k] << "\"";
+    o << "]}";
+    return o.str();
+  }
+
+  int ensure_alloc(const RunOpts& o, std::string& err) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= o.device) { err = "no HIP device available (raftmc has no CPU fallback)"; return MC_E_NO_DEVICE; }
+    HIPCHK(hipSetDevice(o.device));
+    if (d_table_ && o.device == dev_ && o.fp_table_bytes == req_table_ && o.state_store_bytes == req_store_) return 0;
+    release();
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    const uint64_t tb = o.fp_table_bytes ? o.fp_table_bytes : std::min<uint64_t>(16ull << 30, freeb / 4);
+    uint64_t slots = 1; while (slots * 2 * 16 <= tb) slots *= 2;
+    if (slots < 1024) slots = 1024;
+    const uint64_t sb = o.state_store_bytes ? o.state_store_bytes : std::min<uint64_t>(64ull << 30, freeb / 3);
+    cap_ = std::max<u64>(16, sb / (NWP * 4 + 8));
+    // chunk: cand + newrec hold NSLOT u64 per state; ~1/8 of the store bytes, <= SCAN_MAX_BLOCKS blocks
+    chunk_ = std::max<u64>(BS, std::min<u64>({cap_, (sb / 8) / (16 * (u64)S::NSLOT), (u64)SCAN_MAX_BLOCKS * BS}));
+    chunk_ = (chunk_ / BS) * BS;
+    table_mask_ = slots - 1;
+    HIPCHK(hipMalloc(&d_table_, slots * 16));
+    HIPCHK(hipMalloc(&d_states_, cap_ * NWP * 4));
+    HIPCHK(hipMalloc(&d_meta_, cap_ * 8));
+    HIPCHK(hipMalloc(&d_cand_, chunk_ * S::NSLOT * 8));
+    HIPCHK(hipMalloc(&d_newrec_, chunk_ * S::NSLOT * 8));
+    HIPCHK(hipMalloc(&d_nsucc_, chunk_ * 2));
+    HIPCHK(hipMalloc(&d_cells_, chunk_ * S::NSLOT * 4));
+    HIPCHK(hipMalloc(&d_woff_, chunk_ * 4));
+    HIPCHK(hipMalloc(&d_bsum_, SCAN_MAX_BLOCKS * 8));
+    HIPCHK(hipMalloc(&d_ctr_, C_NCTR * 8));
+    HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
+    dev_ = o.device; req_table_ = o.fp_table_bytes; req_store_ = o.state_store_bytes;
+    return 0;
+  }
+
+  float ms(int a, int b) { float x = 0; (void)hipEventElapsedTime(&x, ev_[a], ev_[b]); return x; }
+
+  int run(const RunOpts& o, RunResult& r, std::string& err) override {
+    if (int rc = ensure_alloc(o, err)) return rc;
+    auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    r = RunResult();
+    r.seed = o.seed ? o.seed : 0x5EED5EED2024ull;
+    r.state_bytes = NWP * 4;
+    for (int k = 0; k < MA_NACT; ++k) r.action_names.push_back(kMembActNames[k]);
+    r.act_generated.assign(MA_NACT, 0); r.act_distinct.assign(MA_NACT, 0);
+    r.kernels = {{"memb_expand", 0, 0, 0}, {"memb_fingerprint", 0, 0, 0}, {"memb_dedup", 0, 0, 0},
+                 {"memb_select", 0, 0, 0}, {"memb_compact", 0, 0, 0}, {"memb_materialize", 0, 0, 0}};
+    const MembRuntime& rt = m_.rt;
+
+    // ---- Init (raft.tla:388-393): generated 1; constraints; invariants (TLC checks them on initial states)
+    W s0; S::init(s0);
+    r.generated = 1; r.depth = 1;
+    r.levels.push_back({1, 0, 0.0});
+    total_ = 0;
+    if (!S::in_model(s0, s0, rt)) { r.distinct = 0; r.depth = 0; finish(r, t0); return 0; }
+    {
+      u32 w0[S::NW]; S::pack(s0, w0);
+      u32 wp[NWP] = {0}; for (int q = 0; q < S::NW; ++q) wp[q] = w0[q];
+      const u64 fp0 = S::fingerprint(s0, r.seed, rt);
+      u64 e2[2] = {fp0, ~0ull};   // level 0, key 0: the stored side value is ~(0 << 40 | 0)
+      HIPCHK(hipMemcpy(d_table_ + 2 * (fp0 & table_mask_), e2, 16, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(d_states_, wp, NWP * 4, hipMemcpyHostToDevice));
+      const u64 nometa = ~0ull;
+      HIPCHK(hipMemcpy(d_meta_, &nometa, 8, hipMemcpyHostToDevice));
+      total_ = 1; r.distinct = 1;
+      if (u32 bad = S::check_invariants(s0, rt)) {
+        if ((bad >> 8) == IV_BAD) { r.verdict = MC_VERDICT_INVARIANT_VIOLATION; r.violated = kMembInvNames[bad & 255]; }
+        else { r.verdict = MC_VERDICT_EVAL_ERROR; r.error = std::string("TLC evaluation error in invariant ") + kMembInvNames[bad & 255]; }
+        r.trace.push_back({"<Initial predicate>", text_.text(s0, true)});
+        finish(r, t0); return 0;
+      }
+    }
+
+    const u64 S_B = NWP * 4;
+    u64 level_begin = 0, level_count = 1;
+    u32 level = 0;
+    while (level_count > 0) {
+      if (o.max_depth && r.depth >= o.max_depth) { r.left_on_queue = (int64_t)level_count; r.verdict = MC_VERDICT_DEPTH_LIMIT; break; }
+      HIPCHK(hipMemsetAsync(d_ctr_, 0, C_NCTR * 8, stream_));
+      HIPCHK(hipMemsetAsync(d_ctr_ + C_EVENT, 0xFF, 8, stream_));
+      u64 next_write = level_begin + level_count;
+      double level_ms = 0;
+      int64_t gen_before_chunk = 0;       // generated in earlier chunks of this level
+      u64 gen_in_level = 0;               // in-model successors of this level (G_in)
+      u64 c[C_NCTR] = {0};
+      bool stop = false;
+      for (u64 cb = level_begin; cb < level_begin + level_count; cb += chunk_) {
+        const u64 cnt = std::min<u64>(chunk_, level_begin + level_count - cb), rank0 = cb - level_begin;
+        const u64 nslots = cnt * (u64)S::NSLOT;
+        const u32 nblk = (u32)((cnt + BS - 1) / BS);
+        MGenArgs g;
+        g.states = d_states_; g.chunk_begin = cb; g.chunk_count = cnt; g.rank0 = rank0; g.cand = d_cand_; g.cells = d_cells_; g.nsucc = d_nsucc_;
+        g.seed = r.seed; g.rt = rt; g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.deadlock = o.check_deadlock ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_;
+        MDedupArgs d;
+        d.cand = d_cand_; d.nslots = nslots; d.chunk_count = cnt; d.rank0 = rank0; d.nslot = S::NSLOT; d.level = level + 1;
+        d.table = d_table_; d.table_mask = table_mask_; d.ctr = (unsigned long long*)d_ctr_;
+        MSelArgs sa;
+        sa.cand = d_cand_; sa.chunk_count = cnt; sa.rank0 = rank0; sa.nslot = S::NSLOT; sa.level = level + 1; sa.table = d_table_;
+        sa.woff = d_woff_; sa.bsum = (unsigned long long*)d_bsum_;
+        MCompArgs ca;
+        ca.cand = d_cand_; ca.chunk_count = cnt; ca.chunk_begin = cb; ca.nslot = S::NSLOT; ca.woff = d_woff_;
+        ca.bsum = (const unsigned long long*)d_bsum_; ca.newrec = d_newrec_;
+        HIPCHK(hipMemsetAsync(d_ctr_ + C_CELLS, 0, 8, stream_));
+        HIPCHK(hipEventRecord(ev_[7], stream_));
+        hipLaunchKernelGGL((memb_expand<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ev_[8], stream_));
+        u64 ncells = 0;
+        HIPCHK(hipMemcpyAsync(&ncells, d_ctr_ + C_CELLS, 8, hipMemcpyDeviceToHost, stream_));
+        HIPCHK(hipStreamSynchronize(stream_));
+        HIPCHK(hipEventRecord(ev_[0], stream_));
+        if (ncells) hipLaunchKernelGGL((memb_fingerprint<S>), dim3((unsigned)((ncells + BS - 1) / BS)), dim3(BS), 0, stream_, g, ncells);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ev_[1], stream_));
+        hipLaunchKernelGGL(memb_dedup, dim3((unsigned)((nslots + BS * DPER - 1) / (BS * DPER))), dim3(BS), 0, stream_, d);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ev_[2], stream_));
+        hipLaunchKernelGGL(memb_select, dim3(nblk), dim3(BS), 0, stream_, sa);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(memb_scan_blocks, dim3(1), dim3(BS), 0, stream_, (unsigned long long*)d_bsum_, nblk, (unsigned long long*)d_ctr_);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ev_[3], stream_));
+        hipLaunchKernelGGL(memb_compact, dim3(nblk), dim3(BS), 0, stream_, ca);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ev_[4], stream_));
+        u64 nnew = 0;
+        HIPCHK(hipMemcpyAsync(&nnew, d_ctr_ + C_NEW, 8, hipMemcpyDeviceToHost, stream_));
+        HIPCHK(hipStreamSynchronize(stream_));
+        const float ms_x = ms(7, 8), ms_g = ms(0, 1), ms_d = ms(1, 2), ms_s = ms(2, 3), ms_c = ms(3, 4);
+
+        float ms_m = 0;
+        if (nnew && next_write + nnew <= cap_) {
+          MMatArgs m;
+          m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.n_new = nnew; m.dst_base = next_write; m.cap = cap_;
+          m.level_begin = level_begin; m.rt = rt; m.ctr = (unsigned long long*)d_ctr_;
+          HIPCHK(hipEventRecord(ev_[5], stream_));
+          hipLaunchKernelGGL((memb_materialize<S>), dim3((unsigned)((nnew + BS - 1) / BS)), dim3(BS), 0, stream_, m);
+          HIPCHK(hipGetLastError());
+          HIPCHK(hipEventRecord(ev_[6], stream_));
+          HIPCHK(hipEventSynchronize(ev_[6]));
+          ms_m = ms(5, 6);
+        }
+        HIPCHK(hipMemcpyAsync(c, d_ctr_, sizeof c, hipMemcpyDeviceToHost, stream_));
+        HIPCHK(hipStreamSynchronize(stream_));
+        level_ms += ms_x + ms_g + ms_d + ms_s + ms_c + ms_m;
+        r.kernels[0].ms += ms_x; r.kernels[0].launches++; r.kernels[0].algo_bytes += (double)cnt * S_B + (double)nslots * 8 + (double)ncells * 4;
+        r.kernels[1].ms += ms_g; r.kernels[1].launches++; r.kernels[1].algo_bytes += (double)ncells * (4 + S_B + 8);
+        r.kernels[2].ms += ms_d; r.kernels[2].launches++; r.kernels[2].algo_bytes += (double)nslots * 16 + (double)ncells * 16;
+        r.kernels[3].ms += ms_s; r.kernels[3].launches++; r.kernels[3].algo_bytes += (double)nslots * 8 + (double)ncells * 16 + (double)cnt * 4;
+        r.kernels[4].ms += ms_c; r.kernels[4].launches++; r.kernels[4].algo_bytes += (double)nslots * 8 + (double)nnew * 8;
+        if (ms_m > 0) { r.kernels[5].ms += ms_m; r.kernels[5].launches++; r.kernels[5].algo_bytes += (double)nnew * (8 + 2 * S_B + 8); }
+        if (next_write + nnew > cap_) { c[C_ERR] |= MERR_STORE; stop = true; }
+        if (c[C_EVENT] != ~0ull) {
+          // first event of this chunk in key order (earlier chunks had none)
+          handle_event(c, cnt, level_begin, level_count, rank0, gen_before_chunk, next_write - (level_begin + level_count), nnew, level, r);
+          stop = true;
+        }
+        if (c[C_ERR]) stop = true;
+        if (stop) break;
+        next_write += nnew;
+        int64_t g_all = 0; for (int k = 0; k < MA_NACT; ++k) g_all += (int64_t)c[C_ACT + k];
+        gen_before_chunk = g_all;
+      }
+      r.seconds_kernels += level_ms / 1000.0;
+      r.n_launches += 1;
+      if (c[C_ERR] && r.verdict == MC_VERDICT_OK) {
+        const u64 e = c[C_ERR];
+        r.verdict = MC_VERDICT_CAPACITY_OVERFLOW;
+        std::ostringstream os;
+        os << "error flags 0x" << std::hex << e << std::dec << ":";
+        if (e & ME_CAP) os << " a field, message count or the message bag exceeded its compiled capacity (state "
+                           << (c[C_ERRGID] ? (int64_t)c[C_ERRGID] - 1 : -1) << ");";
+        if (e & MERR_STORE) os << " state store full (raise state_store_bytes);";
+        if (e & MERR_TABLE_FULL) os << " fingerprint table full (raise fp_table_bytes);";
+        r.error = os.str();
+      }
+      if (stop) {
+        if (r.verdict == MC_VERDICT_OK) r.verdict = MC_VERDICT_CAPACITY_OVERFLOW;
+        break;
+      }
+      int64_t gen = 0;
+      for (int k = 0; k < MA_NACT; ++k) { r.act_generated[k] += (int64_t)c[C_ACT + k]; r.act_distinct[k] += (int64_t)c[C_ACT + MA_NACT + k]; gen += (int64_t)c[C_ACT + k]; }
+      r.generated += gen;
+      gen_in_level = c[C_GEN_IN];
+      r.generated_in_model += (int64_t)gen_in_level;
+      const u64 nnew = next_write - (level_begin + level_count);
+      r.algo_bytes += (double)level_count * S_B + (double)gen_in_level * 8 + (double)nnew * (16 + S_B);
+      total_ = next_write;
+      r.distinct = (int64_t)total_;
+      r.levels.back().generated = gen;
+      r.levels.back().kernel_ms = level_ms;
+      if (nnew > 0) { r.levels.push_back({(int64_t)nnew, 0, 0.0}); r.depth += 1; }
+      level_begin += level_count;
+      level_count = nnew;
+      ++level;
+    }
+    finish(r, t0);
+    return 0;
+  }
+
+  // The first event of the level: reproduce TLC's (the oracle's) stop point, counts and trace.
+  void handle_event(const u64* c, u64 cnt, u64 level_begin, u64 level_count, u64 rank0, int64_t gen_before_chunk,
+                    u64 new_before_chunk, u64 nnew, u32 level, RunResult& r) {
+    const u64 ev = c[C_EVENT], key = ev >> 2;
+    const int kind = (int)(ev & 3);
+    const u64 rank = key / S::NSLOT, slot = key % S::NSLOT, gid = level_begin + rank;
+    // generated: whole successor lists of parents up to this one (next() errors abort before counting)
+    std::vector<unsigned short> ns(cnt);
+    (void)hipMemcpy(ns.data(), d_nsucc_, cnt * 2, hipMemcpyDeviceToHost);
+    int64_t gen = gen_before_chunk;
+    for (u64 q = 0; q < rank - rank0; ++q) gen += ns[q];
+    if (kind != EV_NEXT_ERROR) gen += ns[rank - rank0];
+    // distinct: this level's winners with key < k (<= k when the event state itself may be new)
+    std::vector<u64> nr(nnew);
+    if (nnew) (void)hipMemcpy(nr.data(), d_newrec_, nnew * 8, hipMemcpyDeviceToHost);
+    auto key_of = [&](u64 rec) { return ((rec >> 10) - level_begin) * S::NSLOT + (rec & 1023); };
+    u64 before = 0;
+    for (u64 q = 0; q < nnew; ++q) {
+      const u64 k = key_of(nr[q]);
+      if (k < key || (k == key && kind >= EV_INV_ERROR)) ++before;
+    }
+    r.generated += gen;
+    r.distinct = (int64_t)(total_ + new_before_chunk + before);
+    W s;
+    read_state(gid, s);
+    int k, sub;
+    S::inst_of_slot((int)slot, k, sub);
+    if (kind == EV_DEADLOCK) {
+      r.verdict = MC_VERDICT_DEADLOCK;
+      build_trace(gid, nullptr, s, r);
+      return;
+    }
+    if (kind == EV_NEXT_ERROR) {
+      r.verdict = MC_VERDICT_EVAL_ERROR;
+      r.error = "TLC evaluation error while computing the successors of state " + std::to_string(gid) +
+                " (SubSeq index out of domain, raft.tla:551/764)";
+      build_trace(gid, nullptr, s, r);
+      return;
+    }
+    W t; u32 e2 = 0;
+    const int act = S::apply(s, k, sub, t, e2, m_.rt);
+    const u32 res = S::check_invariants(t, m_.rt);
+    const int id = (int)(res & 255);
+    if (kind == EV_INV_ERROR) {
+      r.verdict = MC_VERDICT_EVAL_ERROR;
+      r.error = std::string("TLC evaluation error while checking invariant ") + kMembInvNames[id] +
+                " (Committed(i) = SubSeq(log[i], 1, commitIndex[i]) or log[l][idx] outside its domain)";
+    } else {
+      r.verdict = MC_VERDICT_INVARIANT_VIOLATION;
+      r.violated = kMembInvNames[id];
+      r.depth = (int64_t)level + 2;
+      r.left_on_queue = (int64_t)(level_count - rank - 1 + new_before_chunk + before);
+    }
+    build_trace(gid, act >= 0 ? kMembActNames[act] : "?", t, r);
+  }
+
+  int dump_states(const std::string& path, std::string& err) override {
+    if (!d_states_) { err = "mc_dump_states before mc_run"; return MC_E_STATE; }
+    std::vector<u32> h(total_ * NWP);
+    HIPCHK(hipMemcpy(h.data(), d_states_, h.size() * 4, hipMemcpyDeviceToHost));
+    FILE* f = std::fopen(path.c_str(), "w");
+    if (!f) { err = "cannot write " + path; return MC_E_IO; }
+    for (u64 g = 0; g < total_; ++g) {
+      u32 w[NWP];
+      for (int q = 0; q < NWP; ++q) w[q] = h[g * NWP + q];
+      W s; S::unpack(w, s);
+      std::fprintf(f, "%s\n", text_.text(s, false).c_str());
+    }
+    std::fclose(f);
+    return 0;
+  }
+
+  // ---- sharded mode: not available for this spec yet (FIFO ranking across ranks)
+  int shard_open(const RunOpts&, int, int, std::string& err) override {
+    err = "sharded (multi-GPU) BFS is implemented for raft_original only; tlc_membership runs on one GPU";
+    return MC_E_UNSUPPORTED;
+  }
+  int shard_record_bytes(int) const override { return -1; }
+  int shard_frontier(int64_t*, int64_t*) const override { return MC_E_STATE; }
+  int shard_generate(int64_t, int64_t, int64_t*, std::string&) override { return MC_E_STATE; }
+  int shard_fill(int, void*, const int64_t*, std::string&) override { return MC_E_STATE; }
+  int shard_dedup(const void*, const int64_t*, int64_t*, std::string&) override { return MC_E_STATE; }
+  int shard_materialize(const void*, const int64_t*, std::string&) override { return MC_E_STATE; }
+  int shard_store(const void*, int64_t, std::string&) override { return MC_E_STATE; }
+  int shard_level_stats(int64_t*, std::string&) override { return MC_E_STATE; }
+  int shard_level_commit(const int64_t*, int*, std::string&) override { return MC_E_STATE; }
+  int shard_read_state(uint64_t, std::string&, uint64_t*, std::string&) const override { return MC_E_STATE; }
+  int shard_violation(uint64_t*, std::string&, std::string&) const override { return MC_E_STATE; }
+  const RunResult* shard_result() const override { return nullptr; }
+
+ private:
+  MembModel m_;
+  MembText<S> text_;
+  u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr;
+  u64* d_cand_ = nullptr; u64* d_newrec_ = nullptr; unsigned short* d_nsucc_ = nullptr; unsigned int* d_woff_ = nullptr;
+  u32* d_cells_ = nullptr;
+  u64* d_bsum_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  hipEvent_t ev_[9] = {};
+  u64 table_mask_ = 0, cap_ = 0, total_ = 0, chunk_ = 0;
+  int dev_ = -1; uint64_t req_table_ = 0, req_store_ = 0;
+
+  void release() {
+    for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_cand_, (void*)d_newrec_,
+                    (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_})
+      if (p) (void)hipFree(p);
+    for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
+    if (stream_) (void)hipStreamDestroy(stream_);
+    d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_cand_ = nullptr; d_newrec_ = nullptr;
+    d_nsucc_ = nullptr; d_woff_ = nullptr; d_bsum_ = nullptr; d_cells_ = nullptr; stream_ = nullptr;
+  }
+  void read_state(u64 gid, W& s) const {
+    u32 w[NWP];
+    (void)hipMemcpy(w, d_states_ + gid * NWP, NWP * 4, hipMemcpyDeviceToHost);
+    S::unpack(w, s);
+  }
+  void finish(RunResult& r, std::chrono::steady_clock::time_point t0) {
+    const double M = (double)r.distinct, Ng = (double)r.generated;
+    r.collision_optimistic = M * (Ng - M) / 18446744073709551616.0;
+    r.seconds_total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  // parent-pointer chase on the host (<= depth device reads)
+  void build_trace(u64 parent, const char* last_act, const W& last, RunResult& r) {
+    std::vector<std::pair<std::string, std::string>> tr;
+    if (last_act) tr.push_back({last_act, text_.text(last, true)});
+    u64 g = parent;
+    while (true) {
+      W s; u64 meta = 0;
+      read_state(g, s);
+      (void)hipMemcpy(&meta, d_meta_ + g, 8, hipMemcpyDeviceToHost);
+      if (meta == ~0ull) { tr.push_back({"<Initial predicate>", text_.text(s, true)}); break; }
+      tr.push_back({kMembActNames[(meta >> 10) & 1023], text_.text(s, true)});
+      g = meta >> 20;
+    }
+    std::reverse(tr.begin(), tr.end());
+    r.trace = tr;
+  }
+};
+
+// ------------------------------------------------------------------ shapes compiled into this build: (N, NV)
+#ifdef RMC_QUICK_BUILD
+#define RMC_MEMB_SHAPES(X) X(3, 2)
+#else
+#define RMC_MEMB_SHAPES(X) \
+  X(3, 2) /* shipped raft.cfg */ \
+  X(2, 1)                        \
+  X(2, 2)                        \
+  X(3, 1)                        \
+  X(4, 2) /* C3: 4 servers */
+#endif
+
+static Backend* memb_factory(const MembModel& m) {
+#define X(n, nv) if (m.N == n && m.NV == nv) return new MembGpu<Memb<n, nv, 2 * n * n>>(m);
+  RMC_MEMB_SHAPES(X)
+#undef X
+  return nullptr;
+}
+
+Backend* make_memb_backend(const CfgFile& cfg) {
+  MembModel m = resolve_memb_model(cfg);
+  Backend* b = memb_factory(m);
+  if (!b) {
+    std::string o;
+#define X(n, nv) o += std::string(o.empty() ? "" : ", ") + "(" #n "," #nv ")";
+    RMC_MEMB_SHAPES(X)
+#undef X
+    throw CfgError(MC_E_UNSUPPORTED, "tlc_membership shape (N=" + std::to_string(m.N) + ", |Value|=" + std::to_string(m.NV) +
+                                         ") is not compiled into this build; compiled (N,|Value|): " + o);
+  }
+  return b;
+}
+
+}  // namespace rmc

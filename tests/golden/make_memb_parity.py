@@ -1,0 +1,66 @@
+"""Generate tlc_membership parity fixtures with the CPU oracle (test infrastructure).
+
+For each (cfg, max depth) case the oracle (oracle/raft_membership.h, a literal
+restatement of tlc_membership/raft.tla with TLC BFS semantics) runs BFS with
+SYMMETRY in orbit ("view") mode and FIFO single-worker order, and the fixture
+records generated / distinct / depth / left on queue / per-level sizes /
+per-action (generated, distinct), the verdict, the counterexample trace, and
+the SHA-256 of the sorted canonical text of every distinct state (the VIEW
+plus every history counter; history["global"] is summarised, see
+raft-tla_amd/csrc/memb_spec.h).  TLC itself is unavailable offline
+(SURVEY.md §8c): the counts are oracle-pinned; the oracle is pinned by the
+reference's two TLC traces (tests/test_oracle.py).
+
+    python tests/golden/make_memb_parity.py [case ...]
+"""
+import hashlib
+import json
+import os
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from oracle_util import CONFIGS, GOLDEN, MEMB_MC, run_oracle  # noqa: E402
+
+CASES = {
+    "membership_shipped@14": ("membership_shipped", 14),
+    "memb_two@16": ("memb_two", 16),
+    "memb_dynamic3@14": ("memb_dynamic3", 14),
+    "memb_nosym@13": ("memb_nosym", 13),
+    "memb_four@10": ("memb_four", 10),
+    "scen_FirstBecomeLeader": ("scen_FirstBecomeLeader", 0),
+    "scen_FirstCommit": ("scen_FirstCommit", 0),
+    "scen_EntryCommitted": ("scen_EntryCommitted", 0),
+}
+OUT = os.path.join(GOLDEN, "memb_parity.json")
+
+
+def digest_lines(path):
+    lines = sorted(l.rstrip("\n") for l in open(path))
+    return hashlib.sha256("\n".join(lines).encode()).hexdigest(), len(lines)
+
+
+def main(names):
+    doc = json.load(open(OUT)) if os.path.exists(OUT) else {}
+    for n in names:
+        cfg, depth = CASES[n]
+        fd, dump = tempfile.mkstemp(suffix=".txt")
+        os.close(fd)
+        args = ["--sym", "view", "--dump", dump, "--trace"]
+        if depth:
+            args += ["--max-depth", depth]
+        r = run_oracle("bfs", MEMB_MC, os.path.join(CONFIGS, cfg + ".cfg"), *args, timeout=100000)
+        assert r["verdict"] in ("OK", "INVARIANT_VIOLATION"), r
+        sha, cnt = digest_lines(dump)
+        os.unlink(dump)
+        doc[n] = {"cfg": cfg, "max_depth": depth, "verdict": r["verdict"], "violated": r["violated"],
+                  "generated": r["generated"], "distinct": r["distinct"], "depth": r["depth"],
+                  "left_on_queue": r["left_on_queue"], "levels": r["levels"], "actions": r["actions"],
+                  "states_sha256": sha, "states_dumped": cnt,
+                  "trace": r.get("trace", []), "oracle_seconds": round(r["seconds"], 2)}
+        print(n, r["verdict"], r["distinct"], doc[n]["oracle_seconds"], "s", flush=True)
+        json.dump(doc, open(OUT, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or list(CASES))

@@ -1,0 +1,88 @@
+// TEST HARNESS ONLY (never part of the product).  Runs a single-worker FIFO BFS
+// on the host with the product's packed tlc_membership successor function,
+// constraints, invariants and symmetric fingerprint (raft-tla_amd/csrc/
+// memb_spec.h, the same header the gfx950 kernels compile), so its semantics
+// can be checked against the oracle on CPU before a GPU run.
+// Shape: -DSHAPE_N=.. -DSHAPE_NV=..
+//   memb_host_bfs CFG MAX_DEPTH [DUMP]  -> JSON {generated, distinct, depth, left_on_queue, verdict, actions}
+#include <cstdio>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "../../raft-tla_amd/csrc/memb_text.h"
+
+using namespace rmc;
+using S = Memb<SHAPE_N, SHAPE_NV, 2 * SHAPE_N * SHAPE_N>;
+using W = S::Work;
+
+int main(int argc, char** argv) {
+  CfgFile cfg = parse_cfg_text(read_text_file(argv[1]));
+  MembModel m = resolve_memb_model(cfg);
+  const long long max_depth = argc > 2 ? std::atoll(argv[2]) : 0;
+  FILE* dump = argc > 3 ? std::fopen(argv[3], "w") : nullptr;
+  MembText<S> text(m);
+  const MembRuntime& rt = m.rt;
+  const u64 seed = 0x5EED5EED2024ull;
+  std::unordered_set<u64> seen;
+  std::vector<W> frontier(1);
+  S::init(frontier[0]);
+  seen.insert(S::fingerprint(frontier[0], seed, rt));
+  if (dump) std::fprintf(dump, "%s\n", text.text(frontier[0], false).c_str());
+  long long generated = 1, gen_act[MA_NACT] = {0}, dist_act[MA_NACT] = {0}, left = 0;
+  int depth = 1;
+  u32 err = 0;
+  std::string verdict = "OK", violated;
+  while (!frontier.empty()) {
+    if (max_depth && depth >= max_depth) { left = (long long)frontier.size(); break; }
+    std::vector<W> next;
+    for (size_t fi = 0; fi < frontier.size() && verdict == "OK"; ++fi) {
+      const W& s = frontier[fi];
+      { u32 a[S::NW]; S::pack(s, a); W b; S::unpack(a, b); u32 c[S::NW]; S::pack(b, c);
+        for (int q = 0; q < S::NW; ++q) if (a[q] != c[q]) { std::printf("{\"error\": \"pack/unpack mismatch\"}\n"); return 1; } }
+      // TLC (oracle) counts a state's whole successor list before checking any of them
+      for (int k = 0; k < S::NI; ++k) {
+        if (!S::group_enabled(k, rt.next)) continue;
+        for (int sub = 0; sub < S::nsub(k); ++sub) { W t; if (S::apply(s, k, sub, t, err, rt) >= 0) generated++; }
+      }
+      for (int k = 0; k < S::NI && verdict == "OK"; ++k) {
+        if (!S::group_enabled(k, rt.next)) continue;
+        for (int sub = 0; sub < S::nsub(k); ++sub) {
+          W t;
+          const int act = S::apply(s, k, sub, t, err, rt);
+          if (act < 0) continue;
+          gen_act[act]++;
+          const bool im = S::in_model(t, s, rt);
+          bool isnew = false;
+          if (im) {
+            isnew = seen.insert(S::fingerprint(t, seed, rt)).second;
+            if (isnew) {
+              dist_act[act]++; next.push_back(t);
+              if (dump) std::fprintf(dump, "%s\n", text.text(t, false).c_str());
+            }
+          }
+          if (isnew || !im) {
+            const u32 r = S::check_invariants(t, rt);
+            if (r) {
+              verdict = (r >> 8) == IV_BAD ? "INVARIANT_VIOLATION" : "EVAL_ERROR";
+              violated = kMembInvNames[r & 255];
+              left = (long long)(frontier.size() - fi - 1 + next.size());
+              depth++;
+              break;
+            }
+          }
+        }
+      }
+    }
+    if (verdict != "OK") break;
+    if (!next.empty()) depth++;
+    frontier.swap(next);
+  }
+  if (dump) std::fclose(dump);
+  std::printf("{\"generated\": %lld, \"distinct\": %zu, \"depth\": %d, \"left_on_queue\": %lld, \"err\": %u, \"verdict\": \"%s\", "
+              "\"violated\": \"%s\", \"actions\": {",
+              generated, seen.size(), depth, left, err, verdict.c_str(), violated.c_str());
+  for (int k = 0; k < MA_NACT; ++k) std::printf("%s\"%s\": [%lld, %lld]", k ? ", " : "", kMembActNames[k], gen_act[k], dist_act[k]);
+  std::printf("}}\n");
+  return 0;
+}

@@ -47,11 +47,37 @@ def test_open_rejects_unsupported(raftmc, edit, code):
     assert e.value.code == code
 
 
-def test_membership_has_no_gpu_backend_yet(raftmc):
+def test_describe_membership_shipped(raftmc):
     from oracle_util import MEMB_MC
+    with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, "membership_shipped.cfg")) as mc:
+        d = mc.describe()
+    assert d["spec"] == "tlc_membership" and (d["N"], d["NV"], d["MK"]) == (3, 2, 18)
+    assert d["symmetry"] is True and d["permutations"] == 6 and d["next"] == "NextAsyncCrash"
+    assert d["init_server_mask"] == 7 and d["invariants"][:3] == ["LeaderVotesQuorum", "CandidateTermNotInLog", "ElectionSafety"]
+    assert d["state_bytes_stored"] % 16 == 0
+
+
+def test_describe_membership_four_servers(raftmc):
+    from oracle_util import MEMB_MC
+    with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, "memb_four.cfg")) as mc:
+        d = mc.describe()
+    assert (d["N"], d["MK"], d["permutations"], d["next"], d["init_server_mask"]) == (4, 32, 24, "NextDynamic", 7)
+
+
+@pytest.mark.parametrize("edit,code", [
+    ((("VIEW vars\n", ""),), -4),                                           # history would be fingerprinted
+    ((("    BoundedLogSize\n", ""),), -4),                                  # unbounded logs
+    ((("    LogMatching\n", "    LogMatching\n    NotAnInvariant\n"),), -4),
+    ((("NEXT NextAsyncCrash", "NEXT NextFoo"),), -4),
+    ((("    Server = {s1, s2, s3}", "    Server = {s1, s2, s3, s4, s5}"),), -4),   # shape not compiled in
+    ((("    CleanStartUntilTwoLeaders\n", "    CleanStartUntilTwoLeaders\n    MajorityOfClusterRestarts_constraint\n"),), -4),
+])
+def test_membership_open_rejects_unsupported(raftmc, edit, code):
+    from oracle_util import MEMB_MC
+    cfg = cfg_variant(os.path.join(CONFIGS, "membership_shipped.cfg"), edit)
     with pytest.raises(raftmc.RaftMCError) as e:
-        raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, "membership_shipped.cfg"))
-    assert e.value.code == -4
+        raftmc.ModelChecker(MEMB_MC, cfg)
+    assert e.value.code == code
 
 
 def test_run_without_device_fails_loudly(raftmc):

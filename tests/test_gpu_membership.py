@@ -1,0 +1,85 @@
+"""GPU parity tests for tlc_membership/raft.tla (SYMMETRY perms, VIEW vars,
+history summary, scenario properties) through the C ABI against the CPU
+oracle's committed fixtures (tests/golden/make_memb_parity.py).
+
+Integer work, so the bar is bit-exact.  With TLC's FIFO first-found order
+reproduced on the GPU (memb_backend.hip), even the order-dependent figures
+match: per-action DISTINCT counts, the history counters of every kept state
+(they are part of the dumped text) and the counterexample trace, state by
+state.  The oracle runs SYMMETRY in orbit ("view") mode, which is what the
+GPU implements.
+"""
+import hashlib
+import json
+import os
+import tempfile
+
+import pytest
+
+from oracle_util import CONFIGS, GOLDEN, MEMB_MC
+
+pytestmark = pytest.mark.gpu
+
+SMALL = dict(fp_table_bytes=1 << 26, state_store_bytes=1 << 29, deadlock=False)
+FIX = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))
+EXHAUSTIVE = sorted(k for k, v in FIX.items() if v["verdict"] == "OK")
+VIOLATIONS = sorted(k for k, v in FIX.items() if v["verdict"] == "INVARIANT_VIOLATION")
+
+
+def states_sha(mc):
+    fd, path = tempfile.mkstemp(suffix=".txt")
+    os.close(fd)
+    mc.dump_states(path)
+    lines = sorted(l.rstrip("\n") for l in open(path))
+    os.unlink(path)
+    return hashlib.sha256("\n".join(lines).encode()).hexdigest(), len(lines)
+
+
+@pytest.mark.parametrize("case", EXHAUSTIVE)
+def test_membership_parity(raftmc, case):
+    g = FIX[case]
+    with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), max_depth=g["max_depth"], **SMALL) as mc:
+        r = mc.run()
+        sha, n = states_sha(mc)
+    assert r.verdict in ("OK", "DEPTH_LIMIT"), r.error
+    assert (r.generated, r.distinct, r.depth, r.left_on_queue) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
+    assert [lv[0] for lv in r.levels] == g["levels"]
+    assert r.actions == g["actions"]                      # generated AND distinct per action (FIFO first-found)
+    assert n == g["distinct"] and sha == g["states_sha256"]
+
+
+@pytest.mark.parametrize("case", VIOLATIONS)
+def test_scenario_shortest_counterexample(raftmc, case):
+    g = FIX[case]
+    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), **SMALL)
+    assert r.verdict == "INVARIANT_VIOLATION" and r.violated == g["violated"] and r.exit_code == 12, (r, r.error)
+    assert (r.depth, r.generated, r.distinct, r.left_on_queue) == (g["depth"], g["generated"], g["distinct"], g["left_on_queue"])
+    blocks = r.trace_text.strip().split("\n\n")
+    assert len(blocks) == len(g["trace"]) == g["depth"]
+    for k, (blk, ref) in enumerate(zip(blocks, g["trace"])):
+        head, *body = blk.split("\n")
+        assert " ".join(body) == ref["state"], "trace state %d differs" % (k + 1)
+        if k:
+            assert head == "State %d: <%s>" % (k + 1, ref["action"])
+
+
+def test_membership_seed_independence(raftmc):
+    cfg = os.path.join(CONFIGS, "memb_dynamic3.cfg")
+    a = raftmc.check(MEMB_MC, cfg, max_depth=12, seed=3, **SMALL)
+    b = raftmc.check(MEMB_MC, cfg, max_depth=12, seed=0xFEEDFACE, **SMALL)
+    assert (a.generated, a.distinct, a.depth, a.actions) == (b.generated, b.distinct, b.depth, b.actions)
+
+
+def test_membership_kat_init_expansion(raftmc):
+    # SURVEY.md §4 KAT: with the shipped cfg, expanding Init gives generated 7,
+    # distinct 2 (Restart successors violate CleanStartUntilFirstRequest; the
+    # three Timeouts are one orbit under perms)
+    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, "membership_shipped.cfg"), max_depth=2, **SMALL)
+    assert (r.generated, r.distinct, r.verdict) == (7, 2, "DEPTH_LIMIT")
+
+
+def test_membership_handle_rerun(raftmc):
+    with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, "memb_two.cfg"), max_depth=14, **SMALL) as mc:
+        a = mc.run()
+        b = mc.run()
+    assert (a.generated, a.distinct, a.actions) == (b.generated, b.distinct, b.actions)

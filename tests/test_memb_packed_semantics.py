@@ -1,0 +1,58 @@
+"""The product's packed tlc_membership spec (raft-tla_amd/csrc/memb_spec.h: the
+successor relation, constraints, invariants, history summary and symmetric
+fingerprint that the gfx950 kernels compile) run on the host by a test-only
+FIFO BFS harness (tests/native/memb_host_bfs.cpp), checked against the oracle
+fixtures: identical counts, per-action (generated, distinct) counts, depth,
+states left on queue and the identical set of kept states (SHA-256 of the
+sorted canonical text, history counters included)."""
+import hashlib
+import json
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+from oracle_util import CONFIGS, GOLDEN, ROOT
+
+SHAPES = {"membership_shipped": (3, 2), "memb_dynamic3": (3, 2), "memb_nosym": (3, 2), "memb_two": (2, 1),
+          "memb_four": (4, 2)}
+FIX = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))
+
+
+def build_harness(shape):
+    out = os.path.join(tempfile.gettempdir(), "memb_host_bfs_%d%d" % shape)
+    csrc = os.path.join(ROOT, "raft-tla_amd", "csrc")
+    src = [os.path.join(ROOT, "tests", "native", "memb_host_bfs.cpp"), os.path.join(csrc, "model.cpp"),
+           os.path.join(csrc, "memb_model.cpp")]
+    deps = src + [os.path.join(csrc, f) for f in ("memb_spec.h", "memb_text.h", "common.h")]
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(p) for p in deps):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-DSHAPE_N=%d" % shape[0], "-DSHAPE_NV=%d" % shape[1], "-o", out, *src],
+                       check=True)
+    return out
+
+
+@pytest.mark.parametrize("case", sorted(k for k, v in FIX.items() if v["verdict"] == "OK"))
+def test_packed_membership_matches_oracle(case):
+    g = FIX[case]
+    exe = build_harness(SHAPES[g["cfg"]])
+    fd, dump = tempfile.mkstemp(suffix=".txt")
+    os.close(fd)
+    r = json.loads(subprocess.run([exe, os.path.join(CONFIGS, g["cfg"] + ".cfg"), str(g["max_depth"]), dump],
+                                  capture_output=True, text=True, check=True).stdout)
+    assert r["err"] == 0 and r["verdict"] == "OK"
+    assert (r["generated"], r["distinct"], r["depth"], r["left_on_queue"]) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
+    assert r["actions"] == g["actions"]
+    lines = sorted(l.rstrip("\n") for l in open(dump))
+    os.unlink(dump)
+    assert hashlib.sha256("\n".join(lines).encode()).hexdigest() == g["states_sha256"]
+
+
+@pytest.mark.parametrize("case", ["scen_FirstBecomeLeader"])
+def test_packed_membership_first_violation(case):
+    g = FIX[case]
+    exe = build_harness(SHAPES["membership_shipped"])
+    r = json.loads(subprocess.run([exe, os.path.join(CONFIGS, g["cfg"] + ".cfg"), "0"], capture_output=True, text=True,
+                                  check=True).stdout)
+    assert (r["verdict"], r["violated"], r["depth"], r["generated"], r["distinct"], r["left_on_queue"]) == \
+        (g["verdict"], g["violated"], g["depth"], g["generated"], g["distinct"], g["left_on_queue"])
