@@ -6,6 +6,7 @@
 //                      [--dump states.txt] [--sym tlc|view] [--no-inv-oom]
 //                      [--deadlock] [--golden-cwcl F] [--golden-morc F] [--trace]
 //   raft_oracle replay --tla F.tla --cfg F.cfg --golden F [--max-steps N]
+//   raft_oracle check-trace --tla F.tla --cfg F.cfg --golden TRACE.txt   (one state per line)
 //
 // Output: one JSON object on stdout.
 // ============================================================================
@@ -160,6 +161,48 @@ int main(int argc, char** argv) {
                        ", \"bindings_matched\": " + std::to_string(nbind) + ", \"golden_len\": " + std::to_string(gg.size()) +
                        ", \"actions\": " + json_str(best_actions) + ", \"state\": " + json_str(best_state) + "}";
       std::cout << js << std::endl;
+      return 0;
+    }
+    if (mode == "check-trace") {
+      // Independent validation of a counterexample found elsewhere (e.g. by the GPU at a
+      // depth the oracle's BFS cannot reach): the trace file holds one state per line in
+      // dump_line text.  Line 1 must be an initial state; every next line must be the text
+      // of an in-model successor (oracle Next, constraints, action constraints) of the
+      // current state; no earlier state may violate an invariant; the last must.
+      std::ifstream f(golden);
+      if (!f) throw EvalError("cannot open trace file " + golden);
+      std::vector<std::string> lines;
+      for (std::string l; std::getline(f, l);) if (!l.empty()) lines.push_back(l);
+      auto check_inv = [&](const State& st) -> std::string {
+        for (auto& inv : cfg.invariants) if (!sp->invariant(inv, st)) return inv;
+        return "";
+      };
+      auto in_model = [&](const State& a, const State& b) {
+        for (auto& c : cfg.constraints) if (!sp->constraint(c, b)) return false;
+        for (auto& c : cfg.action_constraints) if (!sp->action_constraint(c, a, b)) return false;
+        return true;
+      };
+      int64_t bad_step = -1; std::string violated, actions;
+      State cur;
+      bool ok = false;
+      for (auto& s0 : sp->init()) if (sp->dump_line(s0) == lines.at(0)) { cur = s0; ok = true; break; }
+      if (!ok) bad_step = 0;
+      std::vector<Succ> succ;
+      for (size_t k = 1; ok && k < lines.size(); ++k) {
+        std::string early = check_inv(cur);
+        if (!early.empty()) { ok = false; bad_step = (int64_t)k - 1; violated = early; break; }
+        succ.clear(); sp->next(cur, succ);
+        bool found = false;
+        for (auto& su : succ)
+          if (sp->dump_line(su.s) == lines[k] && in_model(cur, su.s)) {
+            cur = su.s; found = true; actions += (actions.empty() ? "" : ",") + sp->action_names()[su.action]; break;
+          }
+        if (!found) { ok = false; bad_step = (int64_t)k; }
+      }
+      if (ok) violated = check_inv(cur);
+      std::cout << "{\"valid\": " << ((ok && !violated.empty()) ? "true" : "false") << ", \"length\": " << lines.size()
+                << ", \"violated\": " << json_str(violated) << ", \"bad_step\": " << bad_step
+                << ", \"actions\": " << json_str(actions) << "}" << std::endl;
       return 0;
     }
     std::fprintf(stderr, "unknown mode %s\n", mode.c_str());

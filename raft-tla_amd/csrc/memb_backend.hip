@@ -420,10 +420,11 @@ class MembGpu : public Backend {
     release();
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
-    const uint64_t tb = o.fp_table_bytes ? o.fp_table_bytes : std::min<uint64_t>(16ull << 30, freeb / 4);
+    // defaults sized for one 288 GB MI355X: seen-set ~1/8 of free HBM (16-B entries), state store ~1/2
+    const uint64_t tb = o.fp_table_bytes ? o.fp_table_bytes : std::min<uint64_t>(32ull << 30, freeb / 8);
     uint64_t slots = 1; while (slots * 2 * 16 <= tb) slots *= 2;
     if (slots < 1024) slots = 1024;
-    const uint64_t sb = o.state_store_bytes ? o.state_store_bytes : std::min<uint64_t>(64ull << 30, freeb / 3);
+    const uint64_t sb = o.state_store_bytes ? o.state_store_bytes : std::min<uint64_t>(160ull << 30, freeb / 2);
     cap_ = std::max<u64>(16, sb / (NWP * 4 + 8));
     // chunk: cand + newrec hold NSLOT u64 per state; ~1/8 of the store bytes, <= SCAN_MAX_BLOCKS blocks
     chunk_ = std::max<u64>(BS, std::min<u64>({cap_, (sb / 8) / (16 * (u64)S::NSLOT), (u64)SCAN_MAX_BLOCKS * BS}));

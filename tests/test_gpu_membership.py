@@ -83,3 +83,15 @@ def test_membership_handle_rerun(raftmc):
         a = mc.run()
         b = mc.run()
     assert (a.generated, a.distinct, a.actions) == (b.generated, b.distinct, b.actions)
+
+
+def test_c3_counterexample_matches_committed_trace(raftmc):
+    """C3 (BASELINE configs[2], 4 servers, NextDynamic) to completion: the first
+    violation in TLC FIFO order is LeaderVotesQuorum at depth 21; the trace equals
+    the committed one, which the oracle validates (tests/test_oracle.py)."""
+    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, "memb_four.cfg"), deadlock=False)
+    assert r.verdict == "INVARIANT_VIOLATION" and r.violated == "LeaderVotesQuorum", (r, r.error)
+    assert (r.depth, r.distinct, r.generated) == (21, 162883559, 1113410993)
+    got = [" ".join(b.split("\n")[1:]) for b in r.trace_text.strip().split("\n\n")]
+    want = open(os.path.join(GOLDEN, "c3_leader_votes_quorum_trace.txt")).read().strip().split("\n")
+    assert got == want

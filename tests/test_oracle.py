@@ -68,3 +68,25 @@ def test_first_leader_shortest_witness():
     assert r["verdict"] == "INVARIANT_VIOLATION" and r["violated"] == "NoLeader"
     assert r["trace_len"] == 10
     assert r["trace"][-1]["action"] == "BecomeLeader"
+
+
+def test_oracle_validates_gpu_c3_counterexample():
+    """BASELINE configs[2] (C3, 4 servers, NextDynamic): the GPU found a
+    LeaderVotesQuorum violation at depth 21 (162.9M distinct states, beyond the
+    oracle's reach).  The oracle replays the committed trace step by step through
+    its own Next relation, constraints and invariants (check-trace mode)."""
+    from oracle_util import MEMB_MC, run_oracle
+    r = run_oracle("check-trace", MEMB_MC, os.path.join(CONFIGS, "memb_four.cfg"), "--golden",
+                   os.path.join(GOLDEN, "c3_leader_votes_quorum_trace.txt"))
+    assert r["valid"] and r["length"] == 21 and r["violated"] == "LeaderVotesQuorum"
+    assert r["actions"].split(",")[-2:] == ["AddNewServer", "UpdateTerm"]
+
+
+def test_oracle_check_trace_rejects_a_broken_trace(tmp_path):
+    from oracle_util import MEMB_MC, run_oracle
+    lines = open(os.path.join(GOLDEN, "c3_leader_votes_quorum_trace.txt")).read().strip().split("\n")
+    lines[7] = lines[6]
+    p = tmp_path / "broken.txt"
+    p.write_text("\n".join(lines) + "\n")
+    r = run_oracle("check-trace", MEMB_MC, os.path.join(CONFIGS, "memb_four.cfg"), "--golden", str(p))
+    assert not r["valid"] and r["bad_step"] == 7
