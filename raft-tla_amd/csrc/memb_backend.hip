@@ -16,6 +16,7 @@
 //  1b memb_fingerprint lane per in-model successor (full lanes): re-derive it,
 //                     symmetric FP64 of the view (min over Permutations(Server))
 //                     into cand[slot][state]
+//  1c memb_oom_check  lane per out-of-model successor: invariants (TLC [ext] (ii))
 //  2. memb_dedup      16 independent seen-set probes per thread over 16-B
 //                     entries (fp, ~level|key); insert-if-absent with CAS,
 //                     then atomicMax of ~(level << 40 | key); cand := entry+1
@@ -47,7 +48,7 @@ namespace rmc {
 
 namespace {
 enum {
-  C_CELLS = 0, C_ERR = 1, C_EVENT = 2, C_NEW = 3, C_ERRGID = 4, C_GEN_IN = 5,
+  C_CELLS = 0, C_ERR = 1, C_EVENT = 2, C_NEW = 3, C_ERRGID = 4, C_GEN_IN = 5, C_CELLS_OOM = 6,
   C_ACT = 8, C_NCTR = C_ACT + 2 * MA_NACT
 };
 enum { EV_NEXT_ERROR = 0, EV_DEADLOCK = 1, EV_INV_ERROR = 2, EV_VIOLATION = 3 };
@@ -55,7 +56,6 @@ enum { MERR_TABLE_FULL = 0x100, MERR_STORE = 0x200 };
 constexpr int BS = 256;
 constexpr int DPER = 16;               // probes in flight per dedup thread
 constexpr u64 WINBIT = 1ull << 63;
-constexpr u32 OOM_BIT = 1u << 31;      // a compacted cell holding an out-of-model successor
 constexpr int SCAN_MAX_BLOCKS = 4096;  // chunk <= 4096 * BS states
 }  // namespace
 
@@ -64,6 +64,7 @@ struct MGenArgs {
   u64 chunk_begin, chunk_count, rank0;     // first state of the chunk: gid and rank in its level
   u64* cand;                               // [NSLOT][chunk] fingerprints, 0 = none
   u32* cells;                              // compacted cells (slot * chunk + state) of in-model successors
+  u32* cells_oom;                          // ... of out-of-model successors (TLC checks their invariants, [ext] (ii))
   unsigned short* nsucc;                   // [chunk] successors per state (TLC "generated")
   u64 seed;
   MembRuntime rt;
@@ -71,16 +72,16 @@ struct MGenArgs {
   unsigned long long* ctr;
 };
 
-// Phase 1 for one instance group [K0, K1) with NS successors per instance.  The group bounds
-// are compile-time so the instance dispatch folds away; launder() keeps the per-state decodes
-// inside the loop body (hoisting them over ~100 instances exhausts the register file).
+// Phase 1 for the instances [K0, K1) with NS successors each.  The bounds are compile-time so
+// apply's dispatch is pruned to the range; launder() keeps the per-state decodes inside the
+// loop body (hoisting them over ~100 instances exhausts the register file).
 template <class S, int K0, int K1, int NS>
 __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs& a, bool active, u64 tid, u32& err,
                                              u32& nsucc, u32& nin, unsigned int* lds_cnt) {
   using W = typename S::Work;
   const int lane = __lane_id();
-  const bool en = S::group_enabled(K0, a.rt.next);                   // wave-uniform
   for (int k = K0; k < K1; ++k) {
+    const bool en = S::group_enabled(k, a.rt.next);                 // wave-uniform
     for (int sub = 0; sub < NS; ++sub) {
       const int slot = S::slot_of(k, sub);
       if (active) a.cand[(u64)slot * a.chunk_count + tid] = 0;
@@ -98,17 +99,26 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
             need = true;
             ++nin;
           } else if (a.inv_oom) {
-            need = oom = true;                                       // invariants checked in phase 2
+            oom = true;                                              // invariants checked by memb_oom_check
           }
         }
       }
+      const u32 cell = (u32)((u64)slot * a.chunk_count + tid);
       const u64 mask = __ballot(need);
       if (mask) {
         const int leader = __ffsll((unsigned long long)mask) - 1;
         u32 base = 0;
         if (lane == leader) base = (u32)atomicAdd(&a.ctr[C_CELLS], (unsigned long long)__popcll(mask));
         base = __shfl(base, leader);
-        if (need) a.cells[base + __popcll(mask & ((1ull << lane) - 1ull))] = (u32)((u64)slot * a.chunk_count + tid) | (oom ? OOM_BIT : 0u);
+        if (need) a.cells[base + __popcll(mask & ((1ull << lane) - 1ull))] = cell;
+      }
+      const u64 omask = __ballot(oom);
+      if (omask) {
+        const int leader = __ffsll((unsigned long long)omask) - 1;
+        u32 base = 0;
+        if (lane == leader) base = (u32)atomicAdd(&a.ctr[C_CELLS_OOM], (unsigned long long)__popcll(omask));
+        base = __shfl(base, leader);
+        if (oom) a.cells_oom[base + __popcll(omask & ((1ull << lane) - 1ull))] = cell;
       }
     }
   }
@@ -137,18 +147,11 @@ __global__ void __launch_bounds__(BS) memb_expand(MGenArgs a) {
     S::init(s);
   }
   u32 err = 0, nsucc = 0, nin = 0;
-  expand_group<S, S::G_RV, S::G_BL, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_BL, S::G_CR, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_CR, S::G_ACI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_ACI, S::G_AE, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_AE, S::G_RECV, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  // three loops (instances before Receive, Receive with its two successor slots, the rest): the
+  // compile-time ranges prune apply's dispatch while keeping the kernel within short-branch range
+  expand_group<S, S::G_RV, S::G_RECV, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
   expand_group<S, S::G_RECV, S::G_TO, 2>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_TO, S::G_RS, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_RS, S::G_DUP, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_DUP, S::G_DROP, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_DROP, S::G_ADD, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_ADD, S::G_DEL, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_DEL, S::NI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_TO, S::NI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
   unsigned long long ev = ~0ull;
   if (active) {
     a.nsucc[tid] = (unsigned short)nsucc;
@@ -168,14 +171,14 @@ __global__ void __launch_bounds__(BS) memb_expand(MGenArgs a) {
 }
 
 // Phase 2: one lane per in-model successor (full lanes): re-derive it and store its
-// symmetric FP64 into its cell (cand[slot][state], coalesced order is not needed here).
+// symmetric FP64 into its cell (cand[slot][state]).
 template <class S>
 __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a, u64 ncells) {
   using W = typename S::Work;
   constexpr int NWP = S::NWP;
   const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
   if (i >= ncells) return;
-  const u32 cw = a.cells[i], cell = cw & ~OOM_BIT;
+  const u32 cell = a.cells[i];
   const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
   int k, sub;
   S::inst_of_slot((int)slot, k, sub);
@@ -187,11 +190,29 @@ __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a, u64 ncells) {
   S::unpack(w, s);
   u32 err = 0;
   S::apply(s, k, sub, t, err, a.rt);
-  if (!(cw & OOM_BIT)) {
-    a.cand[cell] = S::fingerprint(t, a.seed, a.rt);
-    return;
-  }
-  // an out-of-model successor: TLC still checks the invariants on it ([ext] switch (ii))
+  a.cand[cell] = S::fingerprint(t, a.seed, a.rt);
+}
+
+// Out-of-model successors: TLC still checks the invariants on them ([ext] switch (ii)); the
+// first violation / evaluation error in key order becomes the level's event.
+template <class S>
+__global__ void __launch_bounds__(BS) memb_oom_check(MGenArgs a, u64 ncells) {
+  using W = typename S::Work;
+  constexpr int NWP = S::NWP;
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  if (i >= ncells) return;
+  const u32 cell = a.cells_oom[i];
+  const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
+  int k, sub;
+  S::inst_of_slot((int)slot, k, sub);
+  u32 w[NWP];
+  const uint4* src = reinterpret_cast<const uint4*>(a.states + (a.chunk_begin + st) * NWP);
+#pragma unroll
+  for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+  W s, t;
+  S::unpack(w, s);
+  u32 err = 0;
+  S::apply(s, k, sub, t, err, a.rt);
   const u32 r = S::check_invariants(t, a.rt);
   if (r) {
     const u64 e = (((a.rank0 + st) * (u64)S::NSLOT + slot) << 2) | ((r >> 8) == IV_BAD ? EV_VIOLATION : EV_INV_ERROR);
@@ -437,6 +458,7 @@ class MembGpu : public Backend {
     HIPCHK(hipMalloc(&d_newrec_, chunk_ * S::NSLOT * 8));
     HIPCHK(hipMalloc(&d_nsucc_, chunk_ * 2));
     HIPCHK(hipMalloc(&d_cells_, chunk_ * S::NSLOT * 4));
+    HIPCHK(hipMalloc(&d_cells_oom_, chunk_ * S::NSLOT * 4));
     HIPCHK(hipMalloc(&d_woff_, chunk_ * 4));
     HIPCHK(hipMalloc(&d_bsum_, SCAN_MAX_BLOCKS * 8));
     HIPCHK(hipMalloc(&d_ctr_, C_NCTR * 8));
@@ -504,7 +526,8 @@ class MembGpu : public Backend {
         const u64 nslots = cnt * (u64)S::NSLOT;
         const u32 nblk = (u32)((cnt + BS - 1) / BS);
         MGenArgs g;
-        g.states = d_states_; g.chunk_begin = cb; g.chunk_count = cnt; g.rank0 = rank0; g.cand = d_cand_; g.cells = d_cells_; g.nsucc = d_nsucc_;
+        g.states = d_states_; g.chunk_begin = cb; g.chunk_count = cnt; g.rank0 = rank0; g.cand = d_cand_; g.cells = d_cells_;
+        g.cells_oom = d_cells_oom_; g.nsucc = d_nsucc_;
         g.seed = r.seed; g.rt = rt; g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.deadlock = o.check_deadlock ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_;
         MDedupArgs d;
         d.cand = d_cand_; d.nslots = nslots; d.chunk_count = cnt; d.rank0 = rank0; d.nslot = S::NSLOT; d.level = level + 1;
@@ -516,13 +539,18 @@ class MembGpu : public Backend {
         ca.cand = d_cand_; ca.chunk_count = cnt; ca.chunk_begin = cb; ca.nslot = S::NSLOT; ca.woff = d_woff_;
         ca.bsum = (const unsigned long long*)d_bsum_; ca.newrec = d_newrec_;
         HIPCHK(hipMemsetAsync(d_ctr_ + C_CELLS, 0, 8, stream_));
+        HIPCHK(hipMemsetAsync(d_ctr_ + C_CELLS_OOM, 0, 8, stream_));
         HIPCHK(hipEventRecord(ev_[7], stream_));
         hipLaunchKernelGGL((memb_expand<S>), dim3(nblk), dim3(BS), 0, stream_, g);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ev_[8], stream_));
-        u64 ncells = 0;
+        u64 ncells = 0, noom = 0;
         HIPCHK(hipMemcpyAsync(&ncells, d_ctr_ + C_CELLS, 8, hipMemcpyDeviceToHost, stream_));
+        HIPCHK(hipMemcpyAsync(&noom, d_ctr_ + C_CELLS_OOM, 8, hipMemcpyDeviceToHost, stream_));
         HIPCHK(hipStreamSynchronize(stream_));
+        if (ncells > cnt * (u64)S::NSLOT || noom > cnt * (u64)S::NSLOT) { err = "memb_expand: cell count beyond the chunk"; return MC_E_NO_DEVICE; }
+        if (noom) hipLaunchKernelGGL((memb_oom_check<S>), dim3((unsigned)((noom + BS - 1) / BS)), dim3(BS), 0, stream_, g, noom);
+        HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ev_[0], stream_));
         if (ncells) hipLaunchKernelGGL((memb_fingerprint<S>), dim3((unsigned)((ncells + BS - 1) / BS)), dim3(BS), 0, stream_, g, ncells);
         HIPCHK(hipGetLastError());
@@ -708,7 +736,7 @@ class MembGpu : public Backend {
   MembText<S> text_;
   u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr;
   u64* d_cand_ = nullptr; u64* d_newrec_ = nullptr; unsigned short* d_nsucc_ = nullptr; unsigned int* d_woff_ = nullptr;
-  u32* d_cells_ = nullptr;
+  u32* d_cells_ = nullptr; u32* d_cells_oom_ = nullptr;
   u64* d_bsum_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_[9] = {};
@@ -717,12 +745,12 @@ class MembGpu : public Backend {
 
   void release() {
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_cand_, (void*)d_newrec_,
-                    (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_})
+                    (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_, (void*)d_cells_oom_})
       if (p) (void)hipFree(p);
     for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
     if (stream_) (void)hipStreamDestroy(stream_);
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_cand_ = nullptr; d_newrec_ = nullptr;
-    d_nsucc_ = nullptr; d_woff_ = nullptr; d_bsum_ = nullptr; d_cells_ = nullptr; stream_ = nullptr;
+    d_nsucc_ = nullptr; d_woff_ = nullptr; d_bsum_ = nullptr; d_cells_ = nullptr; d_cells_oom_ = nullptr; stream_ = nullptr;
   }
   void read_state(u64 gid, W& s) const {
     u32 w[NWP];

@@ -403,20 +403,24 @@ struct Memb {
   RMC_HD static int glen(const Work& s) { return hget(s.h0, H_GLEN, 10); }
   RMC_HD static void h_bump(Work& t, int off, int w, u32& err) { hset(t.h0, off, w, hget(t.h0, off, w) + 1, err); }
   RMC_HD static int h_append(Work& t, int d, u32& err) { const int g = glen(t) + d; hset(t.h0, H_GLEN, 10, g, err); return g; }
+  // Bag changes of one successor are recorded as a delta (at most one message added, one
+  // removed) and applied once at the end of apply(): one inlined copy of the 33-entry bag
+  // loops instead of one per call site keeps every kernel within short-branch range.
+  struct Delta { u64 add, rem; bool a, r; };
   // Send (raft.tla:247-263): TryAddServer/TryRemoveServer precede Send for CatchupRequest/CheckOldConfig
-  RMC_HD static void send(Work& t, u64 code, u32& err) {
-    with_msg(t.bag, code, err);
+  RMC_HD static void send(Work& t, Delta& d, u64 code, u32& err) {
+    d.add = code; d.a = true;
     const int c = mcls(code);
     if (c == K_CRQ7 || c == K_CRQ8 || c == K_COC) { h_bump(t, H_TMC, 3, err); h_append(t, 2, err); }
     else h_append(t, 1, err);
   }
-  RMC_HD static void discard(Work& t, u64 code, u32& err) { without_msg(t.bag, code); h_append(t, 1, err); }   // :280-283
-  RMC_HD static void reply(Work& t, u64 resp, u64 req, u32& err) {   // :308-314
-    with_msg(t.bag, resp, err); without_msg(t.bag, req); h_append(t, 2, err);
+  RMC_HD static void discard(Work& t, Delta& d, u64 code, u32& err) { d.rem = code; d.r = true; h_append(t, 1, err); }   // :280-283
+  RMC_HD static void reply(Work& t, Delta& d, u64 resp, u64 req, u32& err) {   // :308-314: WithoutMessage(req, WithMessage(resp, .))
+    d.add = resp; d.a = true; d.rem = req; d.r = true; h_append(t, 2, err);
   }
   // DiscardDirectWithMembershipChange (:285-290) with AddServer/RemoveServer
-  RMC_HD static void discard_mc(Work& t, u64 code, bool add, int srv, u32& err) {
-    without_msg(t.bag, code);
+  RMC_HD static void discard_mc(Work& t, Delta& d, u64 code, bool add, int srv, u32& err) {
+    d.rem = code; d.r = true;
     h_bump(t, H_MC, 3, err);
     h_append(t, 2, err);
     if (add) {
@@ -497,6 +501,15 @@ struct Memb {
   // Returns its MembAct, or -1 when it does not exist.
   RMC_HD static int apply(const Work& s, int k, int sub, Work& t, u32& err, const MembRuntime& rt) {
     t = s;
+    Delta d{0, 0, false, false};
+    const int act = apply_inner(s, k, sub, t, d, err, rt);
+    if (act >= 0) {
+      if (d.a) with_msg(t.bag, d.add, err);
+      if (d.r) without_msg(t.bag, d.rem);
+    }
+    return act;
+  }
+  RMC_HD static int apply_inner(const Work& s, int k, int sub, Work& t, Delta& d, u32& err, const MembRuntime& rt) {
     const u32 cfgt = rt.cfg_type;
     if (k < G_BL) {                                                   // RequestVote(i, j) :431-440
       const int i = k / N, j = k % N;
@@ -504,7 +517,7 @@ struct Memb {
       const LogV li = getlog(s, i);
       const u32 cfg = config_of<MAXLOG>(li, llen(li), rt.init_cfg, cfgt, nullptr);
       if (!((cfg >> j) & 1u) || ((g_vr(s, i) >> j) & 1u)) return -1;
-      send(t, m_rvq(j, llen(li), last_term(li), i, g_term(s, i), err), err);
+      send(t, d, m_rvq(j, llen(li), last_term(li), i, g_term(s, i), err), err);
       return MA_RequestVote;
     }
     if (k < G_CR) {                                                   // BecomeLeader(i) :472-484
@@ -563,13 +576,13 @@ struct Memb {
       const int last = n < ni ? n : ni;
       const u32 ents = (ni <= last) ? ((1u << EW) | lent(li, ni - 1)) : 0u;   // SubSeq(log[i], ni, lastEntry): <= 1 entry
       const int ci = g_commit(s, i);
-      send(t, m_aeq(ci < last ? ci : last, j, ents, pli, plt, i, g_term(s, i), err), err);
+      send(t, d, m_aeq(ci < last ? ci : last, j, ents, pli, plt, i, g_term(s, i), err), err);
       return MA_AppendEntries;
     }
     if (k < G_TO) {                                                   // Receive(m) :842-863
       const u64 ent = sel(s.bag, k - G_RECV);
       if (ent == EMPTY) return -1;
-      return receive(s, mcode(ent), sub, t, err, rt);
+      return receive(s, mcode(ent), sub, t, d, err, rt);
     }
     if (k < G_RS) {                                                   // Timeout(i) :415-427
       const int i = k - G_TO, st = g_st(s, i);
@@ -597,13 +610,13 @@ struct Memb {
     if (k < G_DROP) {                                                 // DuplicateMessage(m), messages[m] = 1 :892-896, :926-928
       const u64 ent = sel(s.bag, k - G_DUP);
       if (ent == EMPTY || mcount(ent) != 1) return -1;
-      with_msg(t.bag, mcode(ent), err);
+      d.add = mcode(ent); d.a = true;
       return MA_DuplicateMessage;
     }
     if (k < G_ADD) {                                                  // DropMessage(m), messages[m] = 1 :900-904, :930-932
       const u64 ent = sel(s.bag, k - G_DROP);
       if (ent == EMPTY || mcount(ent) != 1) return -1;
-      without_msg(t.bag, mcode(ent));
+      d.rem = mcode(ent); d.r = true;
       return MA_DropMessage;
     }
     if (k < G_DEL) {                                                  // AddNewServer(i, j) :542-555 (G7, G8)
@@ -615,7 +628,7 @@ struct Memb {
       s_voted(t, j, N);
       const int ci = g_commit(s, i);
       const u64 ents = sub_to_mlog(li, g_next(s, i, j), ci, err);
-      send(t, m_crq8(ci, j, ents, g_match(s, i, j), (int)rt.num_rounds, i, g_term(s, i), err), err);
+      send(t, d, m_crq8(ci, j, ents, g_match(s, i, j), (int)rt.num_rounds, i, g_term(s, i), err), err);
       return MA_AddNewServer;
     }
     {                                                                 // DeleteServer(i, j) :558-569
@@ -625,14 +638,14 @@ struct Memb {
       if (!(sj == (int)F || sj == (int)C) || j == i) return -1;
       const LogV li = getlog(s, i);
       if (!((config_of<MAXLOG>(li, llen(li), rt.init_cfg, cfgt, nullptr) >> j) & 1u)) return -1;
-      send(t, m_coc(false, i, j, i, g_term(s, i), err), err);
+      send(t, d, m_coc(false, i, j, i, g_term(s, i), err), err);
       return MA_DeleteServer;
     }
   }
 
   // ReceiveDirect(m) :842-863: UpdateTerm first, then the type handler's successors in disjunct order.
 #define RMC_EMIT(cond) if ((cond) && (idx++ == sub))
-  RMC_HD static int receive(const Work& s, u64 m, int sub, Work& t, u32& err, const MembRuntime& rt) {
+  RMC_HD static int receive(const Work& s, u64 m, int sub, Work& t, Delta& d, u32& err, const MembRuntime& rt) {
     const int cls = mcls(m);
     const u64 dp = mdesc_packed(cls);
     const int i = (int)fld(m, (int)(dp & 127), SB), j = (int)fld(m, (int)((dp >> 7) & 127), SB);
@@ -653,17 +666,17 @@ struct Memb {
           const int vf = g_voted(s, i);
           const bool grant = mt == ct && logOk && (vf == N || vf == j);
           if (grant) s_voted(t, i, j);
-          reply(t, m_rvp(j, sub_to_mlog(li, 1, n, err), i, ct, grant, err), m, err);
+          reply(t, d, m_rvp(j, sub_to_mlog(li, 1, n, err), i, ct, grant, err), m, err);
           return MA_HandleRequestVoteRequest;
         }
         return -1;
       }
       case K_RVP: {
-        RMC_EMIT(mt < ct) { discard(t, m, err); return MA_DropStaleResponse; }          // :836-839
+        RMC_EMIT(mt < ct) { discard(t, d, m, err); return MA_DropStaleResponse; }          // :836-839
         RMC_EMIT(mt == ct) {                                          // HandleRequestVoteResponse :602-614
           fset<N>(t.vr, i, g_vr(s, i) | (1u << j));
           if (fld(m, O_RVP_GR, 1)) fset<N>(t.vg, i, g_vg(s, i) | (1u << j));
-          discard(t, m, err);
+          discard(t, d, m, err);
           return MA_HandleRequestVoteResponse;
         }
         return -1;
@@ -675,7 +688,7 @@ struct Memb {
         const u32 e = ents & EM;
         const bool logOk = pli == 0 || (pli > 0 && pli <= n && plt == eterm(lent(li, pli - 1)));
         RMC_EMIT(mt <= ct && (mt < ct || (st == (int)F && !logOk))) {  // Reject :617-629
-          reply(t, m_aep(j, 0, i, false, ct, err), m, err);
+          reply(t, d, m_aep(j, 0, i, false, ct, err), m, err);
           return MA_HandleAppendEntriesRequest;
         }
         RMC_EMIT(mt == ct && st == (int)C) { s_st(t, i, F); return MA_HandleAppendEntriesRequest; }   // :632-636
@@ -685,7 +698,7 @@ struct Memb {
         const bool same = has && eterm(lent(li, index - 1)) == eterm(e);
         RMC_EMIT(acc && (elen == 0 || same)) {                        // AppendEntriesAlreadyDone :639-655
           s_commit(t, i, (int)fld(m, O_AEQ_CI, IB), err);
-          reply(t, m_aep(j, pli + elen, i, true, ct, err), m, err);
+          reply(t, d, m_aep(j, pli + elen, i, true, ct, err), m, err);
           return MA_HandleAppendEntriesRequest;
         }
         RMC_EMIT(acc && has && !same) { putlog(t, i, lprefix(li, n - 1)); return MA_HandleAppendEntriesRequest; }   // :658-665
@@ -693,12 +706,12 @@ struct Memb {
         return -1;
       }
       case K_AEP: {
-        RMC_EMIT(mt < ct) { discard(t, m, err); return MA_DropStaleResponse; }
+        RMC_EMIT(mt < ct) { discard(t, d, m, err); return MA_DropStaleResponse; }
         RMC_EMIT(mt == ct) {                                          // HandleAppendEntriesResponse :705-715
           const int mmi = (int)fld(m, O_AEP_MMI, IB);
           if (fld(m, O_AEP_SUC, 1)) { s_next(t, i, j, mmi + 1, err); s_match(t, i, j, mmi, err); }
           else { const int ni = g_next(s, i, j); s_next(t, i, j, ni - 1 > 1 ? ni - 1 : 1, err); }
-          discard(t, m, err);
+          discard(t, d, m, err);
           return MA_HandleAppendEntriesResponse;
         }
         return -1;
@@ -706,7 +719,7 @@ struct Memb {
       case K_CRQ7:
       case K_CRQ8: {                                                  // HandleCatchupRequest :718-745 (G5)
         RMC_EMIT(mt < ct) {
-          reply(t, m_crp(j, 0, 0, i, false, ct, err), m, err);
+          reply(t, d, m_crp(j, 0, 0, i, false, ct, err), m, err);
           return MA_HandleCatchupRequest;
         }
         RMC_EMIT(mt >= ct) {
@@ -716,7 +729,7 @@ struct Memb {
           s_term(t, i, mt, err);
           LogV nl = n == 0 ? LogV{0ull, 0u} : lprefix(li, mll < n ? mll : n);
           putlog(t, i, mlog_append(nl, ments, err));
-          reply(t, m_crp(j, n, rnd - 1, i, true, mt, err), m, err);
+          reply(t, d, m_crp(j, n, rnd - 1, i, true, mt, err), m, err);
           return MA_HandleCatchupRequest;
         }
         return -1;
@@ -729,16 +742,16 @@ struct Memb {
         const bool c1 = succ && ((mmi != ci && mmi != mi) || mmi == ci) && isLeader && termEq && !inCfg;
         RMC_EMIT(c1) {
           s_next(t, i, j, mmi + 1, err); s_match(t, i, j, mmi, err);
-          if (rl != 0) reply(t, m_crq7(j, sub_to_mlog(li, ni, ci, err), ni - 1, rl, i, ct, err), m, err);
-          else reply(t, m_coc(true, i, j, i, ct, err), m, err);
+          if (rl != 0) reply(t, d, m_crq7(j, sub_to_mlog(li, ni, ci, err), ni - 1, rl, i, ct, err), m, err);
+          else reply(t, d, m_coc(true, i, j, i, ct, err), m, err);
           return MA_HandleCatchupResponse;
         }
-        RMC_EMIT(!c1) { discard(t, m, err); return MA_HandleCatchupResponse; }
+        RMC_EMIT(!c1) { discard(t, d, m, err); return MA_HandleCatchupResponse; }
         return -1;
       }
       default: {                                                      // K_COC: HandleCheckOldConfig :795-822 (G6)
         const bool isLeader = st == (int)L, termEq = mt == ct;
-        RMC_EMIT(!isLeader || termEq) { discard(t, m, err); return MA_HandleCheckOldConfig; }
+        RMC_EMIT(!isLeader || termEq) { discard(t, d, m, err); return MA_HandleCheckOldConfig; }
         RMC_EMIT(isLeader && termEq) {
           int mci = 0;
           const u32 cfg = config_of<MAXLOG>(li, n, rt.init_cfg, cfgt, &mci);
@@ -748,12 +761,12 @@ struct Memb {
             const u32 nc = add ? (cfg | (1u << srv)) : (cfg & ~(1u << srv));
             if (nc != cfg) {
               putlog(t, i, lappend(li, mkentry(ct, cfgt, m2r(nc), err), err));
-              discard_mc(t, m, add, srv, err);
+              discard_mc(t, d, m, add, srv, err);
             } else {
-              discard(t, m, err);
+              discard(t, d, m, err);
             }
           } else {
-            reply(t, m_coc(add, i, srv, i, ct, err), m, err);
+            reply(t, d, m_coc(add, i, srv, i, ct, err), m, err);
           }
           return MA_HandleCheckOldConfig;
         }
@@ -834,7 +847,7 @@ struct Memb {
 #pragma unroll
           for (int j = 0; j < N; ++j) {
             const LogV lj = getlog(t, j);
-#pragma unroll
+#pragma unroll 1
             for (int p = 0; p < LMAXW; ++p) if (p < llen(lj) && eterm(lent(lj, p)) == g_term(t, i)) return IV_BAD;
           }
         }
@@ -850,7 +863,7 @@ struct Memb {
           for (int j = 0; j < N; ++j) {
             const LogV lj = getlog(t, j);
             int mx = 0;
-#pragma unroll
+#pragma unroll 1
             for (int p = 0; p < LMAXW; ++p) if (p < llen(lj) && eterm(lent(lj, p)) == ti) mx = p + 1;
             mo[j] = mx;
           }
@@ -867,7 +880,7 @@ struct Memb {
             const LogV li = getlog(t, i), lj = getlog(t, j);
             const int mn = llen(li) < llen(lj) ? llen(li) : llen(lj);
             bool pref = true;
-#pragma unroll
+#pragma unroll 1
             for (int p = 0; p < LMAXW; ++p) {
               if (p < mn) {
                 const u32 x = lent(li, p), y = lent(lj, p);
@@ -948,7 +961,7 @@ struct Memb {
           const LogV li = getlog(t, i);
           const int ci = g_commit(t, i);
           if (ci > llen(li)) return IV_ERR;
-#pragma unroll
+#pragma unroll 1
           for (int idx = 1; idx <= LMAXW; ++idx) {
             if (idx > ci) continue;
             const u32 e = lent(li, idx - 1);
@@ -1145,22 +1158,115 @@ struct Memb {
       }
     }
   }
-  // FP64 of raftmc for this spec: min over Permutations(Server) (identity only without SYMMETRY)
+  // hash of pi(view) for one runtime permutation pi (same element hashes as view_acc)
+  template <bool CE>
+  RMC_HD static u64 view_hash1(const Work& t, u32 pi, u64 seed, u32 cfgt) {
+    u64 acc = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const LogV l = getlog(t, i);
+      acc += fmix(server_word(t, i, pi) ^ log_hash(CE ? perm_log(l, pi, cfgt) : l, seed));
+    }
+#pragma unroll 1
+    for (int q = 0; q < MK; ++q) {
+      const u64 e = sel(t.bag, q);
+      if (e == EMPTY) break;
+      const u64 dp = mdesc_packed(mcls(mcode(e)));
+      const int sd = CODEB + CNTB - (int)(dp & 127) - SB, ss = CODEB + CNTB - (int)((dp >> 7) & 127) - SB;
+      const int ov = (int)((dp >> 21) & 127), sv = CODEB + CNTB - ov - SB;
+      u64 x = e & ~(lomask(SB) << sd) & ~(lomask(SB) << ss);
+      if (ov) x &= ~(lomask(SB) << sv);
+      if (CE) x = (perm_entries(mcode(x), pi, cfgt) << CNTB) | (x & lomask(CNTB));
+      x |= (u64)pi_of(pi, (int)((e >> sd) & lomask(SB))) << sd | (u64)pi_of(pi, (int)((e >> ss) & lomask(SB))) << ss;
+      if (ov) x |= (u64)pi_of(pi, (int)((e >> sv) & lomask(SB))) << sv;
+      acc += fmix(x ^ seed ^ K_MSG);
+    }
+    return acc;
+  }
+  // Permutation-invariant signature of server i (partition refinement): its own scalars, vote
+  // counts and self-relations, the multiset of its nextIndex/matchIndex row, its log with config
+  // values reduced to (cardinality, self-membership), and the multiset of (class, term, count,
+  // role) of the messages it sends or receives.  sig(pi(s), pi(i)) = sig(s, i) for every pi.
+  RMC_HD static u64 server_sig(const Work& t, int i, u32 cfgt) {
+    const int vo = g_voted(t, i);
+    const u32 vr = g_vr(t, i), vg = g_vg(t, i);
+    const u64 w = (u64)g_term(t, i) | (u64)g_st(t, i) << 3 | (u64)g_commit(t, i) << 5 | (u64)(vo == N) << 8 | (u64)(vo == i) << 9 |
+                  (u64)popc32(vr) << 10 | (u64)popc32(vg) << 13 | (u64)((vr >> i) & 1u) << 16 | (u64)((vg >> i) & 1u) << 17 |
+                  (u64)g_next(t, i, i) << 18 | (u64)g_match(t, i, i) << 21;
+    u64 rows = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if (j != i) rows += fmix((u64)g_next(t, i, j) | (u64)g_match(t, i, j) << 3 | 0x5151ull << 8);
+    const LogV l = getlog(t, i);
+    u64 lh = (u64)llen(l);
+#pragma unroll
+    for (int p = 0; p < MAXLOG; ++p) {
+      if (p >= llen(l)) continue;
+      u32 e = lent(l, p);
+      if (etype(e) == cfgt) { const u32 m = r2m(evalue(e)); e = (e & ~(u32)lomask(VW)) | (u32)popc32(m) << 1 | ((m >> i) & 1u); }
+      lh = lh * P1 + (u64)e + 1;
+    }
+    u64 ms = 0;
+#pragma unroll 1
+    for (int q = 0; q < MK; ++q) {
+      const u64 e = sel(t.bag, q);
+      if (e == EMPTY) break;
+      const u64 c = mcode(e), dp = mdesc_packed(mcls(c));
+      const int d = (int)fld(c, (int)(dp & 127), SB), sr = (int)fld(c, (int)((dp >> 7) & 127), SB);
+      if (d == i || sr == i)
+        ms += fmix((u64)mcls(c) | (u64)fld(c, (int)((dp >> 14) & 127), TB) << 3 | (u64)mcount(e) << 6 | (u64)(d == i) << 13 |
+                   (u64)(sr == i) << 14 | (u64)(d == sr) << 15 | 0xA5ull << 16);
+    }
+    return fmix(w ^ fmix(rows ^ 0x9E37ull) ^ rotl64(fmix(lh), 17) ^ rotl64(ms, 31));
+  }
+  // FP64 of raftmc for this spec.  With SYMMETRY: min over the permutations that respect the
+  // order of the server signatures (ties permuted among themselves).  For pi(s) in the orbit of
+  // s those are exactly the signature-respecting permutations of s composed with pi^-1, so the
+  // minimum runs over the same set of permuted views: canonical, and usually over one
+  // permutation instead of N!.  Without SYMMETRY: the identity.
   RMC_HD static u64 fingerprint(const Work& t, u64 seed, const MembRuntime& rt) {
-    u64 acc[NPERM];
     const bool ce = has_config_entries(t, rt.cfg_type);
-    int np = 1;
-    if (rt.symmetry) {
-      np = NPERM;
-      if (ce) view_acc<NPERM, true>(t, seed, rt.cfg_type, acc);
-      else view_acc<NPERM, false>(t, seed, rt.cfg_type, acc);
-    } else {
+    u64 best;
+    if (!rt.symmetry) {
+      u64 acc[NPERM];
       if (ce) view_acc<1, true>(t, seed, rt.cfg_type, acc);
       else view_acc<1, false>(t, seed, rt.cfg_type, acc);
-    }
-    u64 best = acc[0];
+      best = acc[0];
+    } else {
+      u64 sig[N];
 #pragma unroll
-    for (int p = 1; p < NPERM; ++p) if (p < np) best = acc[p] < best ? acc[p] : best;
+      for (int i = 0; i < N; ++i) sig[i] = server_sig(t, i, rt.cfg_type);
+      u32 lo = 0, hi = 0;                                              // packed 3-bit bounds per server
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        u32 l = 0, e = 0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) { l += sig[j] < sig[i]; e += sig[j] == sig[i]; }
+        lo |= l << (3 * i); hi |= (l + e) << (3 * i);
+      }
+      auto valid = [&](u32 pi) {
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          const u32 x = (u32)pi_of(pi, i);
+          ok &= x >= ((lo >> (3 * i)) & 7u) && x < ((hi >> (3 * i)) & 7u);
+        }
+        return ok;
+      };
+      int nvalid = 0;
+#pragma unroll 1
+      for (int p = 0; p < NPERM; ++p) nvalid += valid(perm_of(p));
+      best = ~0ull;
+#pragma unroll 1
+      for (int k = 0; k < nvalid; ++k) {
+        u32 pi = 0;
+        int c = 0;
+#pragma unroll 1
+        for (int p = 0; p < NPERM; ++p) { const u32 q = perm_of(p); if (valid(q)) { if (c == k) pi = q; ++c; } }
+        const u64 h = ce ? view_hash1<true>(t, pi, seed, rt.cfg_type) : view_hash1<false>(t, pi, seed, rt.cfg_type);
+        best = h < best ? h : best;
+      }
+    }
     const u64 fp = fmix(best ^ seed);
     return fp ? fp : 1ull;
   }

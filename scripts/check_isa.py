@@ -1,0 +1,79 @@
+"""Static checks of the gfx950 code object inside libraftmc.so (no GPU needed).
+
+    python scripts/check_isa.py [path/to/libraftmc.so]
+
+For every kernel: instruction count, long-branch sequences (s_getpc_b64 +
+s_setpc_b64, emitted when a kernel outgrows the 16-bit branch range) and the
+private (scratch) segment size.  Round 1 found that kernels large enough to
+need long branches computed wrong results and faulted on MI355X, so the build
+keeps every kernel within short-branch range and free of scratch; the CPU test
+suite runs this check (tests/test_abi.py).
+"""
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+DEFAULT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raft-tla_amd", "_build", "libraftmc.so")
+
+
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def code_objects(lib):
+    """The .hip_fatbin section holds one offload bundle per translation unit; unbundle each."""
+    d = tempfile.mkdtemp()
+    fat = os.path.join(d, "fat.bin")
+    subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=" + fat, lib], check=True)
+    blob = open(fat, "rb").read()
+    starts = [m.start() for m in re.finditer(re.escape(MAGIC), blob)]
+    out = []
+    for n, st in enumerate(starts):
+        part = os.path.join(d, "part%d.bin" % n)
+        open(part, "wb").write(blob[st:starts[n + 1] if n + 1 < len(starts) else len(blob)])
+        co = os.path.join(d, "part%d.co" % n)
+        subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", "--input=" + part,
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True)
+        out.append(co)
+    return out
+
+
+def kernels(co):
+    dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", co], capture_output=True,
+                         text=True, check=True).stdout
+    out, cur = {}, None
+    for line in dis.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            cur = m.group(1)
+            out[cur] = {"instructions": 0, "long_branches": 0}
+            continue
+        if cur and line.startswith("\t"):
+            out[cur]["instructions"] += 1
+            if "s_setpc_b64" in line:
+                out[cur]["long_branches"] += 1
+    notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], capture_output=True, text=True, check=True).stdout
+    # amdhsa metadata: a list of kernel maps (keys sorted): private segment size, then symbol
+    priv = re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)
+    syms = re.findall(r"\.symbol:\s+(\S+)\.kd", notes)
+    for s, p in zip(syms, priv):
+        if s in out:
+            out[s]["scratch_bytes"] = int(p)
+    return {k: v for k, v in out.items() if "scratch_bytes" in v}
+
+
+def main():
+    lib = sys.argv[1] if len(sys.argv) > 1 else DEFAULT
+    ks = {}
+    for co in code_objects(lib):
+        ks.update(kernels(co))
+    print(json.dumps(ks, indent=1, sort_keys=True))
+    bad = {k: v for k, v in ks.items() if v["long_branches"] or v["scratch_bytes"]}
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -88,3 +88,18 @@ def test_run_without_device_fails_loudly(raftmc):
         with pytest.raises(raftmc.RaftMCError) as e:
             mc.run()
     assert e.value.code == -5
+
+
+def test_kernels_short_branch_and_no_scratch():
+    """Every gfx950 kernel in libraftmc.so stays within the short-branch range
+    (no s_getpc/s_setpc long-branch sequences) and uses no scratch: round 1
+    found a membership kernel that outgrew the branch range computing wrong
+    fingerprints and faulting."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_isa.py")], capture_output=True, text=True)
+    import json
+    ks = json.loads(r.stdout)
+    assert len(ks) > 40 and any("memb_fingerprint" in k for k in ks) and any("orig_generate" in k for k in ks)
+    bad = {k: v for k, v in ks.items() if v["long_branches"] or v["scratch_bytes"]}
+    assert not bad, bad
