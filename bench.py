@@ -16,7 +16,7 @@ all-to-alls (raft-tla_amd/shard.py); value = the model's distinct states /
 max-over-ranks time of one run, "scaling": "strong" (total work fixed).
 
 The JSON line adds:
-  roofline      expand kernel (orig_expand): algorithmic bytes F*S + G_in*8 +
+  roofline      dominant kernel (orig_generate): algorithmic bytes F*S + G_in*8 +
                 D*(16+S) / summed HIP-event kernel time,
                 against the 8 TB/s HBM peak; traffic from rocprofv3 PMC passes
                 when --traffic-json points at their summary (else null)
@@ -60,7 +60,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default=os.path.join(ROOT, "configs", "c2.cfg"))
-    ap.add_argument("--cpu-states", type=int, default=150000)
+    ap.add_argument("--cpu-states", type=int, default=400000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     args = ap.parse_args()

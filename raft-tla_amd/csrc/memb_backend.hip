@@ -63,8 +63,9 @@ struct MGenArgs {
   const u32* states;
   u64 chunk_begin, chunk_count, rank0;     // first state of the chunk: gid and rank in its level
   u64* cand;                               // [NSLOT][chunk] fingerprints, 0 = none
-  u32* cells;                              // compacted cells (slot * chunk + state) of in-model successors
+  u32* cells;                              // per workgroup: BS*NSLOT cells (slot * chunk + state) of in-model successors
   u32* cells_oom;                          // ... of out-of-model successors (TLC checks their invariants, [ext] (ii))
+  u32* cell_count;                         // per workgroup: [in-model, out-of-model] cell counts
   unsigned short* nsucc;                   // [chunk] successors per state (TLC "generated")
   u64 seed;
   MembRuntime rt;
@@ -77,9 +78,11 @@ struct MGenArgs {
 // loop body (hoisting them over ~100 instances exhausts the register file).
 template <class S, int K0, int K1, int NS>
 __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs& a, bool active, u64 tid, u32& err,
-                                             u32& nsucc, u32& nin, unsigned int* lds_cnt) {
+                                             u32& nsucc, u32& nin, unsigned int* lds_cnt, unsigned int* lds_cells) {
   using W = typename S::Work;
   const int lane = __lane_id();
+  u32* cells = a.cells + (u64)blockIdx.x * (BS * S::NSLOT);
+  u32* cells_oom = a.cells_oom + (u64)blockIdx.x * (BS * S::NSLOT);
   for (int k = K0; k < K1; ++k) {
     const bool en = S::group_enabled(k, a.rt.next);                 // wave-uniform
     for (int sub = 0; sub < NS; ++sub) {
@@ -108,17 +111,17 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
       if (mask) {
         const int leader = __ffsll((unsigned long long)mask) - 1;
         u32 base = 0;
-        if (lane == leader) base = (u32)atomicAdd(&a.ctr[C_CELLS], (unsigned long long)__popcll(mask));
+        if (lane == leader) base = atomicAdd(&lds_cells[0], (unsigned int)__popcll(mask));   // LDS: no global contention
         base = __shfl(base, leader);
-        if (need) a.cells[base + __popcll(mask & ((1ull << lane) - 1ull))] = cell;
+        if (need) cells[base + __popcll(mask & ((1ull << lane) - 1ull))] = cell;
       }
       const u64 omask = __ballot(oom);
       if (omask) {
         const int leader = __ffsll((unsigned long long)omask) - 1;
         u32 base = 0;
-        if (lane == leader) base = (u32)atomicAdd(&a.ctr[C_CELLS_OOM], (unsigned long long)__popcll(omask));
+        if (lane == leader) base = atomicAdd(&lds_cells[1], (unsigned int)__popcll(omask));
         base = __shfl(base, leader);
-        if (oom) a.cells_oom[base + __popcll(omask & ((1ull << lane) - 1ull))] = cell;
+        if (oom) cells_oom[base + __popcll(omask & ((1ull << lane) - 1ull))] = cell;
       }
     }
   }
@@ -131,7 +134,9 @@ __global__ void __launch_bounds__(BS) memb_expand(MGenArgs a) {
   using W = typename S::Work;
   constexpr int NWP = S::NWP;
   __shared__ unsigned int lds_cnt[MA_NACT + 1];
+  __shared__ unsigned int lds_cells[2];
   for (int t = threadIdx.x; t < MA_NACT + 1; t += BS) lds_cnt[t] = 0;
+  if (threadIdx.x < 2) lds_cells[threadIdx.x] = 0;
   __syncthreads();
   const u64 tid = (u64)blockIdx.x * BS + threadIdx.x;
   const bool active = tid < a.chunk_count;
@@ -149,9 +154,9 @@ __global__ void __launch_bounds__(BS) memb_expand(MGenArgs a) {
   u32 err = 0, nsucc = 0, nin = 0;
   // three loops (instances before Receive, Receive with its two successor slots, the rest): the
   // compile-time ranges prune apply's dispatch while keeping the kernel within short-branch range
-  expand_group<S, S::G_RV, S::G_RECV, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_RECV, S::G_TO, 2>(s, a, active, tid, err, nsucc, nin, lds_cnt);
-  expand_group<S, S::G_TO, S::NI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt);
+  expand_group<S, S::G_RV, S::G_RECV, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, lds_cells);
+  expand_group<S, S::G_RECV, S::G_TO, 2>(s, a, active, tid, err, nsucc, nin, lds_cnt, lds_cells);
+  expand_group<S, S::G_TO, S::NI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, lds_cells);
   unsigned long long ev = ~0ull;
   if (active) {
     a.nsucc[tid] = (unsigned short)nsucc;
@@ -167,18 +172,23 @@ __global__ void __launch_bounds__(BS) memb_expand(MGenArgs a) {
   __syncthreads();
   for (int t = threadIdx.x; t < MA_NACT; t += BS)
     if (lds_cnt[t]) atomicAdd(&a.ctr[C_ACT + t], (unsigned long long)lds_cnt[t]);
-  if (threadIdx.x == 0 && lds_cnt[MA_NACT]) atomicAdd(&a.ctr[C_GEN_IN], (unsigned long long)lds_cnt[MA_NACT]);
+  if (threadIdx.x == 0) {
+    if (lds_cnt[MA_NACT]) atomicAdd(&a.ctr[C_GEN_IN], (unsigned long long)lds_cnt[MA_NACT]);
+    a.cell_count[2 * blockIdx.x] = lds_cells[0];
+    a.cell_count[2 * blockIdx.x + 1] = lds_cells[1];
+  }
 }
 
 // Phase 2: one lane per in-model successor (full lanes): re-derive it and store its
 // symmetric FP64 into its cell (cand[slot][state]).
 template <class S>
-__global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a, u64 ncells) {
+__global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
   using W = typename S::Work;
   constexpr int NWP = S::NWP;
-  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
-  if (i >= ncells) return;
-  const u32 cell = a.cells[i];
+  const u32 n = a.cell_count[2 * blockIdx.x];
+  const u32* cells = a.cells + (u64)blockIdx.x * (BS * S::NSLOT);
+  for (u32 i = threadIdx.x; i < n; i += BS) {
+  const u32 cell = cells[i];
   const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
   int k, sub;
   S::inst_of_slot((int)slot, k, sub);
@@ -191,17 +201,19 @@ __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a, u64 ncells) {
   u32 err = 0;
   S::apply(s, k, sub, t, err, a.rt);
   a.cand[cell] = S::fingerprint(t, a.seed, a.rt);
+  }
 }
 
 // Out-of-model successors: TLC still checks the invariants on them ([ext] switch (ii)); the
 // first violation / evaluation error in key order becomes the level's event.
 template <class S>
-__global__ void __launch_bounds__(BS) memb_oom_check(MGenArgs a, u64 ncells) {
+__global__ void __launch_bounds__(BS) memb_oom_check(MGenArgs a) {
   using W = typename S::Work;
   constexpr int NWP = S::NWP;
-  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
-  if (i >= ncells) return;
-  const u32 cell = a.cells_oom[i];
+  const u32 n = a.cell_count[2 * blockIdx.x + 1];
+  const u32* cells = a.cells_oom + (u64)blockIdx.x * (BS * S::NSLOT);
+  for (u32 i = threadIdx.x; i < n; i += BS) {
+  const u32 cell = cells[i];
   const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
   int k, sub;
   S::inst_of_slot((int)slot, k, sub);
@@ -217,6 +229,7 @@ __global__ void __launch_bounds__(BS) memb_oom_check(MGenArgs a, u64 ncells) {
   if (r) {
     const u64 e = (((a.rank0 + st) * (u64)S::NSLOT + slot) << 2) | ((r >> 8) == IV_BAD ? EV_VIOLATION : EV_INV_ERROR);
     atomicMin(&a.ctr[C_EVENT], (unsigned long long)e);
+  }
   }
 }
 
@@ -459,6 +472,7 @@ class MembGpu : public Backend {
     HIPCHK(hipMalloc(&d_nsucc_, chunk_ * 2));
     HIPCHK(hipMalloc(&d_cells_, chunk_ * S::NSLOT * 4));
     HIPCHK(hipMalloc(&d_cells_oom_, chunk_ * S::NSLOT * 4));
+    HIPCHK(hipMalloc(&d_cell_count_, 2 * ((chunk_ + BS - 1) / BS) * 4));
     HIPCHK(hipMalloc(&d_woff_, chunk_ * 4));
     HIPCHK(hipMalloc(&d_bsum_, SCAN_MAX_BLOCKS * 8));
     HIPCHK(hipMalloc(&d_ctr_, C_NCTR * 8));
@@ -519,6 +533,7 @@ class MembGpu : public Backend {
       double level_ms = 0;
       int64_t gen_before_chunk = 0;       // generated in earlier chunks of this level
       u64 gen_in_level = 0;               // in-model successors of this level (G_in)
+      u64 gin_seen = 0;                   // ... counted up to the previous chunk
       u64 c[C_NCTR] = {0};
       bool stop = false;
       for (u64 cb = level_begin; cb < level_begin + level_count; cb += chunk_) {
@@ -527,7 +542,7 @@ class MembGpu : public Backend {
         const u32 nblk = (u32)((cnt + BS - 1) / BS);
         MGenArgs g;
         g.states = d_states_; g.chunk_begin = cb; g.chunk_count = cnt; g.rank0 = rank0; g.cand = d_cand_; g.cells = d_cells_;
-        g.cells_oom = d_cells_oom_; g.nsucc = d_nsucc_;
+        g.cells_oom = d_cells_oom_; g.cell_count = d_cell_count_; g.nsucc = d_nsucc_;
         g.seed = r.seed; g.rt = rt; g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.deadlock = o.check_deadlock ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_;
         MDedupArgs d;
         d.cand = d_cand_; d.nslots = nslots; d.chunk_count = cnt; d.rank0 = rank0; d.nslot = S::NSLOT; d.level = level + 1;
@@ -538,21 +553,14 @@ class MembGpu : public Backend {
         MCompArgs ca;
         ca.cand = d_cand_; ca.chunk_count = cnt; ca.chunk_begin = cb; ca.nslot = S::NSLOT; ca.woff = d_woff_;
         ca.bsum = (const unsigned long long*)d_bsum_; ca.newrec = d_newrec_;
-        HIPCHK(hipMemsetAsync(d_ctr_ + C_CELLS, 0, 8, stream_));
-        HIPCHK(hipMemsetAsync(d_ctr_ + C_CELLS_OOM, 0, 8, stream_));
         HIPCHK(hipEventRecord(ev_[7], stream_));
         hipLaunchKernelGGL((memb_expand<S>), dim3(nblk), dim3(BS), 0, stream_, g);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ev_[8], stream_));
-        u64 ncells = 0, noom = 0;
-        HIPCHK(hipMemcpyAsync(&ncells, d_ctr_ + C_CELLS, 8, hipMemcpyDeviceToHost, stream_));
-        HIPCHK(hipMemcpyAsync(&noom, d_ctr_ + C_CELLS_OOM, 8, hipMemcpyDeviceToHost, stream_));
-        HIPCHK(hipStreamSynchronize(stream_));
-        if (ncells > cnt * (u64)S::NSLOT || noom > cnt * (u64)S::NSLOT) { err = "memb_expand: cell count beyond the chunk"; return MC_E_NO_DEVICE; }
-        if (noom) hipLaunchKernelGGL((memb_oom_check<S>), dim3((unsigned)((noom + BS - 1) / BS)), dim3(BS), 0, stream_, g, noom);
+        if (o.inv_out_of_model) hipLaunchKernelGGL((memb_oom_check<S>), dim3(nblk), dim3(BS), 0, stream_, g);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ev_[0], stream_));
-        if (ncells) hipLaunchKernelGGL((memb_fingerprint<S>), dim3((unsigned)((ncells + BS - 1) / BS)), dim3(BS), 0, stream_, g, ncells);
+        hipLaunchKernelGGL((memb_fingerprint<S>), dim3(nblk), dim3(BS), 0, stream_, g);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ev_[1], stream_));
         hipLaunchKernelGGL(memb_dedup, dim3((unsigned)((nslots + BS * DPER - 1) / (BS * DPER))), dim3(BS), 0, stream_, d);
@@ -586,6 +594,8 @@ class MembGpu : public Backend {
         HIPCHK(hipMemcpyAsync(c, d_ctr_, sizeof c, hipMemcpyDeviceToHost, stream_));
         HIPCHK(hipStreamSynchronize(stream_));
         level_ms += ms_x + ms_g + ms_d + ms_s + ms_c + ms_m;
+        const u64 ncells = c[C_GEN_IN] - gin_seen;        // in-model successors of this chunk
+        gin_seen = c[C_GEN_IN];
         r.kernels[0].ms += ms_x; r.kernels[0].launches++; r.kernels[0].algo_bytes += (double)cnt * S_B + (double)nslots * 8 + (double)ncells * 4;
         r.kernels[1].ms += ms_g; r.kernels[1].launches++; r.kernels[1].algo_bytes += (double)ncells * (4 + S_B + 8);
         r.kernels[2].ms += ms_d; r.kernels[2].launches++; r.kernels[2].algo_bytes += (double)nslots * 16 + (double)ncells * 16;
@@ -736,7 +746,7 @@ class MembGpu : public Backend {
   MembText<S> text_;
   u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr;
   u64* d_cand_ = nullptr; u64* d_newrec_ = nullptr; unsigned short* d_nsucc_ = nullptr; unsigned int* d_woff_ = nullptr;
-  u32* d_cells_ = nullptr; u32* d_cells_oom_ = nullptr;
+  u32* d_cells_ = nullptr; u32* d_cells_oom_ = nullptr; u32* d_cell_count_ = nullptr;
   u64* d_bsum_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_[9] = {};
@@ -745,12 +755,12 @@ class MembGpu : public Backend {
 
   void release() {
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_cand_, (void*)d_newrec_,
-                    (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_, (void*)d_cells_oom_})
+                    (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_, (void*)d_cells_oom_, (void*)d_cell_count_})
       if (p) (void)hipFree(p);
     for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
     if (stream_) (void)hipStreamDestroy(stream_);
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_cand_ = nullptr; d_newrec_ = nullptr;
-    d_nsucc_ = nullptr; d_woff_ = nullptr; d_bsum_ = nullptr; d_cells_ = nullptr; d_cells_oom_ = nullptr; stream_ = nullptr;
+    d_nsucc_ = nullptr; d_woff_ = nullptr; d_bsum_ = nullptr; d_cells_ = nullptr; d_cells_oom_ = nullptr; d_cell_count_ = nullptr; stream_ = nullptr;
   }
   void read_state(u64 gid, W& s) const {
     u32 w[NWP];

@@ -112,7 +112,8 @@ MembModel resolve_memb_model(const CfgFile& cfg) {
     for (int k = 0; k < MI_NINV; ++k) if (n == kMembInvNames[k]) id = k;
     if (id < 0) throw CfgError(MC_E_UNSUPPORTED, "unknown invariant '" + n + "' for tlc_membership");
     if (m.rt.n_inv >= 32) throw CfgError(MC_E_UNSUPPORTED, "at most 32 invariants");
-    m.rt.inv_order[m.rt.n_inv++] = (unsigned char)id;
+    m.rt.inv_order[m.rt.n_inv / 8] |= (u64)id << (8 * (m.rt.n_inv % 8));
+    ++m.rt.n_inv;
     m.inv_names.push_back(n);
   }
   return m;

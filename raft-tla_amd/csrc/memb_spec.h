@@ -97,7 +97,8 @@ struct MembRuntime {
   u32 cfg_type;             // entry type bit of ConfigEntry (0 iff ConfigEntry sorts before ValueEntry)
   u32 symmetry;             // 1 = SYMMETRY perms
   u32 n_inv;                // invariants in cfg order
-  unsigned char inv_order[32];
+  u64 inv_order[4];         // invariant ids in cfg order, one byte each (read with selects, never a
+                            // runtime-indexed array: that would put the kernel argument in scratch)
 };
 
 // ------------------------------------------------------------------ small constexpr tables
@@ -1020,7 +1021,8 @@ struct Memb {
   // Returns 0 if all hold, else (kind << 8 | invariant id) with kind IV_BAD / IV_ERR.
   RMC_HD static u32 check_invariants(const Work& t, const MembRuntime& rt) {
     for (u32 q = 0; q < rt.n_inv; ++q) {
-      const int id = rt.inv_order[q];
+      const u64 w = q < 8 ? rt.inv_order[0] : q < 16 ? rt.inv_order[1] : q < 24 ? rt.inv_order[2] : rt.inv_order[3];
+      const int id = (int)((w >> (8 * (q & 7))) & 255u);
       const int r = inv(t, id, rt);
       if (r != IV_OK) return ((u32)r << 8) | (u32)id;
     }

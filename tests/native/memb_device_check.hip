@@ -118,26 +118,24 @@ int main(int argc, char** argv) {
     for (u64 q = 0; q < n; ++q) for (int j = 0; j < S::NW; ++j) h4[q * S::NWP + j] = hs[q * S::NW + j];
     (void)hipMemcpy(dst4, h4.data(), h4.size() * 4, hipMemcpyHostToDevice);
     MGenArgs g{};
-    u32 *dcells, *dcells_oom;
-    (void)hipMalloc(&dcells, np * 4);
-    (void)hipMalloc(&dcells_oom, np * 4);
+    const u64 nblk = (n + 255) / 256;
+    u32 *dcells, *dcells_oom, *dcount;
+    (void)hipMalloc(&dcells, nblk * 256 * S::NSLOT * 4);
+    (void)hipMalloc(&dcells_oom, nblk * 256 * S::NSLOT * 4);
+    (void)hipMalloc(&dcount, nblk * 2 * 4);
     g.states = dst4; g.chunk_begin = 0; g.chunk_count = n; g.rank0 = 0; g.cand = dcand; g.cells = dcells; g.cells_oom = dcells_oom;
-    g.nsucc = dns; g.seed = seed; g.rt = rt; g.inv_oom = 1; g.deadlock = 0; g.ctr = (unsigned long long*)dctr;
-    hipLaunchKernelGGL((memb_expand<S>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, g);
+    g.cell_count = dcount; g.nsucc = dns; g.seed = seed; g.rt = rt; g.inv_oom = 1; g.deadlock = 0; g.ctr = (unsigned long long*)dctr;
+    hipLaunchKernelGGL((memb_expand<S>), dim3((unsigned)nblk), dim3(256), 0, 0, g);
     if (hipDeviceSynchronize() != hipSuccess) { std::printf("{\"error\": \"expand kernel\"}\n"); return 1; }
-    u64 cnt[7] = {0};
-    (void)hipMemcpy(cnt, dctr, sizeof cnt, hipMemcpyDeviceToHost);
-    const u64 ncells = cnt[0], noom = cnt[6];
-    // validate both compacted cell lists on the host before any kernel dereferences them
+    // validate every workgroup's two cell lists on the host before any kernel dereferences them
     {
-      std::vector<u32> cells(ncells), oc(noom);
-      if (ncells) (void)hipMemcpy(cells.data(), dcells, ncells * 4, hipMemcpyDeviceToHost);
-      if (noom) (void)hipMemcpy(oc.data(), dcells_oom, noom * 4, hipMemcpyDeviceToHost);
-      u64 nbad = 0, nwant_in = 0, nwant_oom = 0;
+      std::vector<u32> cnts(nblk * 2);
+      (void)hipMemcpy(cnts.data(), dcount, nblk * 2 * 4, hipMemcpyDeviceToHost);
+      u64 nbad = 0, nwant_in = 0, nwant_oom = 0, ncells = 0, noom = 0;
       std::vector<char> seen_cell(np, 0);
-      auto check = [&](u32 c, bool want_in) {
+      auto check = [&](u32 c, bool want_in, u64 blk) {
         const u64 sl = c / n, st = c - sl * n;
-        bool ok = c < np && sl < (u64)S::NSLOT && !seen_cell[c];
+        bool ok = c < np && sl < (u64)S::NSLOT && !seen_cell[c] && st / 256 == blk;
         if (ok) {
           seen_cell[c] = 1;
           int k, sub; S::inst_of_slot((int)sl, k, sub);
@@ -146,8 +144,15 @@ int main(int argc, char** argv) {
         }
         if (!ok) { if (!nbad) std::fprintf(stderr, "bad cell %08x (in-model list: %d)\n", c, (int)want_in); ++nbad; }
       };
-      for (u32 c : cells) check(c, true);
-      for (u32 c : oc) check(c, false);
+      for (u64 b = 0; b < nblk; ++b) {
+        if (cnts[2 * b] > 256u * S::NSLOT || cnts[2 * b + 1] > 256u * S::NSLOT) { std::printf("{\"error\": \"cell count out of range\"}\n"); return 4; }
+        std::vector<u32> cl(cnts[2 * b]), co(cnts[2 * b + 1]);
+        if (!cl.empty()) (void)hipMemcpy(cl.data(), dcells + b * 256 * S::NSLOT, cl.size() * 4, hipMemcpyDeviceToHost);
+        if (!co.empty()) (void)hipMemcpy(co.data(), dcells_oom + b * 256 * S::NSLOT, co.size() * 4, hipMemcpyDeviceToHost);
+        for (u32 c : cl) check(c, true, b);
+        for (u32 c : co) check(c, false, b);
+        ncells += cl.size(); noom += co.size();
+      }
       for (u64 i = 0; i < np; ++i) {
         const u64 st = i / S::NSLOT; const int sl = (int)(i % S::NSLOT);
         int k, sub; S::inst_of_slot(sl, k, sub);
@@ -161,9 +166,9 @@ int main(int argc, char** argv) {
         return 4;
       }
     }
-    if (ncells) hipLaunchKernelGGL((memb_fingerprint<S>), dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, 0, g, ncells);
+    hipLaunchKernelGGL((memb_fingerprint<S>), dim3((unsigned)nblk), dim3(256), 0, 0, g);
     if (hipDeviceSynchronize() != hipSuccess) { std::printf("{\"error\": \"fingerprint kernel\"}\n"); return 1; }
-    if (noom) hipLaunchKernelGGL((memb_oom_check<S>), dim3((unsigned)((noom + 255) / 256)), dim3(256), 0, 0, g, noom);
+    hipLaunchKernelGGL((memb_oom_check<S>), dim3((unsigned)nblk), dim3(256), 0, 0, g);
     if (hipDeviceSynchronize() != hipSuccess) { std::printf("{\"error\": \"oom check kernel\"}\n"); return 1; }
     std::vector<u64> cand(np);
     (void)hipMemcpy(cand.data(), dcand, np * 8, hipMemcpyDeviceToHost);
