@@ -103,6 +103,14 @@ void mc_default_opts(mc_opts* o);
 /* Load a spec module (.tla) and a TLC model config (.cfg); no GPU work yet. */
 int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx** out);
 
+/* Golden history trace of a punctuated-search constraint (CommitWhenConcurrentLeaders_unique,
+ * MajorityOfClusterRestarts_constraint; tlc_membership/raft.tla:1198-1204, :1228-1234), as
+ * TLA+ value text: the `[global |-> << ... >>]` record the operator's definition embeds
+ * (raft.tla:1201, :1231) or the sequence alone.  mc_open already takes it from the module (or
+ * the module it EXTENDS, next to it) when the definition is there; this call supplies or
+ * replaces it.  MC_E_PARSE for malformed text, MC_E_INVALID for another constraint name. */
+int mc_set_history_prefix(mc_ctx* ctx, const char* constraint, const char* trace_text);
+
 /* Breadth-first model checking on the GPU until completion, violation or error. */
 int mc_run(mc_ctx* ctx);
 

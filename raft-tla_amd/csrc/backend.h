@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "model.h"
+#include "tla_value.h"
 
 namespace rmc {
 
@@ -48,6 +49,11 @@ struct Backend {
   virtual std::string describe_json() const = 0;
   virtual int run(const RunOpts& o, RunResult& r, std::string& err) = 0;
   virtual int dump_states(const std::string& path, std::string& err) = 0;
+  // punctuated-search prefix constraints whose golden history trace is data (tla_value.h)
+  virtual std::vector<std::string> history_prefixes_needed() const { return {}; }
+  virtual int set_history_prefix(const std::string& con, const TVal& trace, std::string& err) {
+    (void)trace; err = "'" + con + "' is not a constraint of this spec"; return -1;
+  }
   // ---- sharded BFS (include/raftmc.h mc_shard_*); rank-local device work only
   virtual int shard_open(const RunOpts& o, int rank, int world, std::string& err) = 0;
   virtual int shard_record_bytes(int what) const = 0;

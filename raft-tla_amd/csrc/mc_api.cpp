@@ -84,6 +84,14 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
     if (fam == "raft_original") c->be.reset(rmc::make_orig_backend(cfg));
     else if (fam == "tlc_membership") c->be.reset(rmc::make_memb_backend(cfg));
     else throw rmc::CfgError(MC_E_UNSUPPORTED, "spec family '" + fam + "' has no GPU backend in this build");
+    // the golden traces of punctuated-search constraints are operator definitions of the module
+    // (or of a module it EXTENDS, next to it); the caller may also pass them (mc_set_history_prefix)
+    for (const auto& con : c->be->history_prefixes_needed()) {
+      const std::string lit = rmc::find_trace_literal(tla_path, con);
+      if (lit.empty()) continue;
+      std::string err;
+      if (int rc = c->be->set_history_prefix(con, rmc::parse_tla_value(lit), err)) throw rmc::CfgError(rc, con + ": " + err);
+    }
   } catch (const rmc::CfgError& e) {
     c->last_error = e.what();
     int code = e.code;
@@ -95,6 +103,20 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
     return MC_E_PARSE;
   }
   *out = c;
+  return MC_OK;
+}
+
+int mc_set_history_prefix(mc_ctx* c, const char* constraint, const char* trace_text) {
+  if (!c || !constraint || !trace_text) return MC_E_INVALID;
+  if (!c->be) return MC_E_STATE;
+  try {
+    std::string err;
+    const int rc = c->be->set_history_prefix(constraint, rmc::parse_tla_value(trace_text), err);
+    if (rc) { c->last_error = err; return rc; }
+  } catch (const rmc::CfgError& e) {
+    c->last_error = e.what();
+    return e.code;
+  }
   return MC_OK;
 }
 

@@ -41,6 +41,7 @@
 
 #include "../../include/raftmc.h"
 #include "backend.h"
+#include "memb_prefix.h"
 #include "memb_spec.h"
 #include "memb_text.h"
 
@@ -426,6 +427,54 @@ class MembGpu : public Backend {
   explicit MembGpu(const MembModel& m) : m_(m), text_(m_) {}
   ~MembGpu() override { release(); }
 
+  // ---- punctuated-search prefixes (memb_prefix.h): region 0 CommitWhenConcurrentLeaders_unique,
+  // region 1 MajorityOfClusterRestarts_constraint
+  std::vector<std::string> history_prefixes_needed() const override {
+    std::vector<std::string> v;
+    for (int r = 0; r < 2; ++r)
+      if ((m_.rt.constraints >> kPrefixCon[r]) & 1u) v.push_back(kMembConNames[kPrefixCon[r]]);
+    return v;
+  }
+  int set_history_prefix(const std::string& con, const TVal& trace, std::string& err) override {
+    int r = -1;
+    for (int q = 0; q < 2; ++q) if (con == kMembConNames[kPrefixCon[q]]) r = q;
+    if (r < 0) { err = "'" + con + "' is not a punctuated-search prefix constraint"; return MC_E_INVALID; }
+    try {
+      const auto& g = trace_global(trace);
+      if (g.size() > 1000) { err = "history prefix longer than the 10-bit history length field"; return MC_E_UNSUPPORTED; }
+      int unmatched = 0;
+      ptab_[r] = encode_prefix_table<S>(m_, g, &unmatched);
+      plen_[r] = (u32)g.size();
+      have_prefix_[r] = true;
+    } catch (const CfgError& e) { err = e.what(); return e.code; }
+    return 0;
+  }
+  // runtime descriptors with the prefix tables: host copies for host-side re-derivation, device
+  // copies for the kernels
+  int prepare_prefixes(std::string& err) {
+    rt_host_ = m_.rt; rt_dev_ = m_.rt;
+    u32 off = S::H_PREFIX;
+    for (int r = 0; r < 2; ++r) {
+      if (!((m_.rt.constraints >> kPrefixCon[r]) & 1u)) continue;
+      if (!have_prefix_[r]) {
+        err = std::string(kMembConNames[kPrefixCon[r]]) + " needs its golden history trace: place the reference's "
+              "raft.tla next to the module, or pass the trace with mc_set_history_prefix";
+        return MC_E_UNSUPPORTED;
+      }
+      if (off + S::NB > 64) { err = "both punctuated-search prefix constraints at once do not fit the history word for this |Server|"; return MC_E_UNSUPPORTED; }
+      if (r == 1) rt_host_.preg1_off = rt_dev_.preg1_off = off;
+      off += S::NB;
+      if (d_ptab_[r]) { (void)hipFree(d_ptab_[r]); d_ptab_[r] = nullptr; }
+      const size_t bytes = std::max<size_t>(16, ptab_[r].size() * 8);
+      HIPCHK(hipMalloc(&d_ptab_[r], bytes));
+      if (!ptab_[r].empty()) HIPCHK(hipMemcpy(d_ptab_[r], ptab_[r].data(), ptab_[r].size() * 8, hipMemcpyHostToDevice));
+      const u32 len = plen_[r] ? plen_[r] : 0;
+      if (r == 0) { rt_host_.ptab0 = ptab_[0].data(); rt_dev_.ptab0 = d_ptab_[0]; rt_host_.plen0 = rt_dev_.plen0 = len; }
+      else { rt_host_.ptab1 = ptab_[1].data(); rt_dev_.ptab1 = d_ptab_[1]; rt_host_.plen1 = rt_dev_.plen1 = len; }
+    }
+    return 0;
+  }
+
   std::string family() const override { return "tlc_membership"; }
 
   std::string describe_json() const override {
@@ -438,7 +487,14 @@ class MembGpu : public Backend {
     for (size_t k = 0; k < m_.constraint_names.size(); ++k) o << (k ? ", " : "") << "\"" << m_.constraint_names[k] << "\"";
     o << "], \"action_constraints\": [";
     for (size_t k = 0; k < m_.action_constraint_names.size(); ++k) o << (k ? ", " : "") << "\"" << m_.action_constraint_names[k] << "\"";
-    o << "], \"invariants\": [";
+    o << "], \"history_prefixes\": {";
+    bool first = true;
+    for (int q = 0; q < 2; ++q)
+      if ((m_.rt.constraints >> kPrefixCon[q]) & 1u) {
+        o << (first ? "" : ", ") << "\"" << kMembConNames[kPrefixCon[q]] << "\": " << (have_prefix_[q] ? (int)plen_[q] : -1);
+        first = false;
+      }
+    o << "}, \"prefix_bindings\": " << S::NB << ", \"invariants\": [";
     for (size_t k = 0; k < m_.inv_names.size(); ++k) o << (k ? ", " : "") << "\"" << m_.inv_names[k] << "\"";
     o << "], \"actions\": [";
     for (int k = 0; k < MA_NACT; ++k) o << (k ? ", " : "") << "\"" << kMembActNames[k] << "\"";
@@ -485,7 +541,14 @@ class MembGpu : public Backend {
   float ms(int a, int b) { float x = 0; (void)hipEventElapsedTime(&x, ev_[a], ev_[b]); return x; }
 
   int run(const RunOpts& o, RunResult& r, std::string& err) override {
+    for (int q = 0; q < 2; ++q)
+      if (((m_.rt.constraints >> kPrefixCon[q]) & 1u) && !have_prefix_[q]) {
+        err = std::string(kMembConNames[kPrefixCon[q]]) + " needs its golden history trace: place the reference's "
+              "raft.tla next to the module, or pass the trace with mc_set_history_prefix";
+        return MC_E_UNSUPPORTED;
+      }
     if (int rc = ensure_alloc(o, err)) return rc;
+    if (int rc = prepare_prefixes(err)) return rc;
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
@@ -496,7 +559,7 @@ class MembGpu : public Backend {
     r.act_generated.assign(MA_NACT, 0); r.act_distinct.assign(MA_NACT, 0);
     r.kernels = {{"memb_expand", 0, 0, 0}, {"memb_fingerprint", 0, 0, 0}, {"memb_dedup", 0, 0, 0},
                  {"memb_select", 0, 0, 0}, {"memb_compact", 0, 0, 0}, {"memb_materialize", 0, 0, 0}};
-    const MembRuntime& rt = m_.rt;
+    const MembRuntime& rt = rt_host_;
 
     // ---- Init (raft.tla:388-393): generated 1; constraints; invariants (TLC checks them on initial states)
     W s0; S::init(s0);
@@ -543,7 +606,7 @@ class MembGpu : public Backend {
         MGenArgs g;
         g.states = d_states_; g.chunk_begin = cb; g.chunk_count = cnt; g.rank0 = rank0; g.cand = d_cand_; g.cells = d_cells_;
         g.cells_oom = d_cells_oom_; g.cell_count = d_cell_count_; g.nsucc = d_nsucc_;
-        g.seed = r.seed; g.rt = rt; g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.deadlock = o.check_deadlock ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_;
+        g.seed = r.seed; g.rt = rt_dev_; g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.deadlock = o.check_deadlock ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_;
         MDedupArgs d;
         d.cand = d_cand_; d.nslots = nslots; d.chunk_count = cnt; d.rank0 = rank0; d.nslot = S::NSLOT; d.level = level + 1;
         d.table = d_table_; d.table_mask = table_mask_; d.ctr = (unsigned long long*)d_ctr_;
@@ -583,7 +646,7 @@ class MembGpu : public Backend {
         if (nnew && next_write + nnew <= cap_) {
           MMatArgs m;
           m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.n_new = nnew; m.dst_base = next_write; m.cap = cap_;
-          m.level_begin = level_begin; m.rt = rt; m.ctr = (unsigned long long*)d_ctr_;
+          m.level_begin = level_begin; m.rt = rt_dev_; m.ctr = (unsigned long long*)d_ctr_;
           HIPCHK(hipEventRecord(ev_[5], stream_));
           hipLaunchKernelGGL((memb_materialize<S>), dim3((unsigned)((nnew + BS - 1) / BS)), dim3(BS), 0, stream_, m);
           HIPCHK(hipGetLastError());
@@ -691,8 +754,8 @@ class MembGpu : public Backend {
       return;
     }
     W t; u32 e2 = 0;
-    const int act = S::apply(s, k, sub, t, e2, m_.rt);
-    const u32 res = S::check_invariants(t, m_.rt);
+    const int act = S::apply(s, k, sub, t, e2, rt_host_);
+    const u32 res = S::check_invariants(t, rt_host_);
     const int id = (int)(res & 255);
     if (kind == EV_INV_ERROR) {
       r.verdict = MC_VERDICT_EVAL_ERROR;
@@ -753,7 +816,14 @@ class MembGpu : public Backend {
   u64 table_mask_ = 0, cap_ = 0, total_ = 0, chunk_ = 0;
   int dev_ = -1; uint64_t req_table_ = 0, req_store_ = 0;
 
+  MembRuntime rt_host_{}, rt_dev_{};
+  std::vector<u64> ptab_[2];
+  u32 plen_[2] = {0, 0};
+  bool have_prefix_[2] = {false, false};
+  u64* d_ptab_[2] = {nullptr, nullptr};
+
   void release() {
+    for (auto& p : d_ptab_) { if (p) (void)hipFree(p); p = nullptr; }
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_cand_, (void*)d_newrec_,
                     (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_, (void*)d_cells_oom_, (void*)d_cell_count_})
       if (p) (void)hipFree(p);

@@ -89,11 +89,7 @@ MembModel resolve_memb_model(const CfgFile& cfg) {
   for (auto& c : cfg.constraints) {
     int id = -1;
     for (int k = 0; k < MC_NCON; ++k) if (c == kMembConNames[k]) id = k;
-    if (id < 0) {
-      if (c == "CommitWhenConcurrentLeaders_unique" || c == "MajorityOfClusterRestarts_constraint")
-        throw CfgError(MC_E_UNSUPPORTED, "punctuated-search prefix constraint '" + c + "' is not compiled yet (DESIGN.md §7)");
-      throw CfgError(MC_E_UNSUPPORTED, "unknown state constraint '" + c + "' for tlc_membership");
-    }
+    if (id < 0) throw CfgError(MC_E_UNSUPPORTED, "unknown state constraint '" + c + "' for tlc_membership");
     m.rt.constraints |= 1u << id;
     m.constraint_names.push_back(c);
   }
@@ -101,6 +97,16 @@ MembModel resolve_memb_model(const CfgFile& cfg) {
     if (c == "CommitWhenConcurrentLeaders_action_constraint") m.rt.action_constraints |= MAC_CommitWhenConcurrentLeaders;
     else throw CfgError(MC_E_UNSUPPORTED, "unknown action constraint '" + c + "'");
     m.action_constraint_names.push_back(c);
+  }
+  // each punctuated-search prefix constraint keeps a dead-binding mask of N(N-1)(N-2) bits in the
+  // history word h1 from bit 36 (memb_spec.h H_PREFIX)
+  {
+    const int nb = m.N >= 3 ? m.N * (m.N - 1) * (m.N - 2) : 0;
+    int regions = 0;
+    for (int r = 0; r < 2; ++r) if ((m.rt.constraints >> kPrefixCon[r]) & 1u) ++regions;
+    if (36 + regions * nb > 64)
+      throw CfgError(MC_E_UNSUPPORTED, "CommitWhenConcurrentLeaders_unique and MajorityOfClusterRestarts_constraint together "
+                                       "need more history bits than compiled for |Server| = " + std::to_string(m.N));
   }
   // the bounds that size the packed fields (raft.tla:22-30) must be in force
   for (int need : {MC_BoundedInFlightMessages, MC_BoundedLogSize, MC_BoundedTerms})

@@ -52,13 +52,17 @@ enum MembCon {
   MC_BoundedInFlightMessages, MC_BoundedRequestVote, MC_BoundedLogSize, MC_BoundedRestarts, MC_BoundedTimeouts,
   MC_BoundedTerms, MC_BoundedClientRequests, MC_BoundedTriedMembershipChanges, MC_BoundedMembershipChanges,
   MC_ElectionsUncontested, MC_CleanStartUntilFirstRequest, MC_CleanStartUntilTwoLeaders,
-  MC_CommitWhenConcurrentLeaders_constraint, MC_NCON
+  MC_CommitWhenConcurrentLeaders_constraint, MC_CommitWhenConcurrentLeaders_unique, MC_MajorityOfClusterRestarts_constraint,
+  MC_NCON
 };
 static const char* const kMembConNames[MC_NCON] = {
     "BoundedInFlightMessages", "BoundedRequestVote", "BoundedLogSize", "BoundedRestarts", "BoundedTimeouts",
     "BoundedTerms", "BoundedClientRequests", "BoundedTriedMembershipChanges", "BoundedMembershipChanges",
     "ElectionsUncontested", "CleanStartUntilFirstRequest", "CleanStartUntilTwoLeaders",
-    "CommitWhenConcurrentLeaders_constraint"};
+    "CommitWhenConcurrentLeaders_constraint", "CommitWhenConcurrentLeaders_unique",
+    "MajorityOfClusterRestarts_constraint"};
+// the punctuated-search prefix constraints (raft.tla:1198-1204, :1228-1234) in prefix-region order
+static const int kPrefixCon[2] = {MC_CommitWhenConcurrentLeaders_unique, MC_MajorityOfClusterRestarts_constraint};
 // action constraints, raft.tla:1207-1210
 enum { MAC_CommitWhenConcurrentLeaders = 1 };
 
@@ -99,6 +103,13 @@ struct MembRuntime {
   u32 n_inv;                // invariants in cfg order
   u64 inv_order[4];         // invariant ids in cfg order, one byte each (read with selects, never a
                             // runtime-indexed array: that would put the kernel argument in scratch)
+  // punctuated-search prefixes (region 0: CommitWhenConcurrentLeaders_unique, 1:
+  // MajorityOfClusterRestarts_constraint): device tables of [position][binding] history-entry
+  // codes (x, y), bindings = injective (s1, s2, s3) -> Server in lexicographic order; 0 length = off
+  const u64* ptab0;
+  const u64* ptab1;
+  u32 plen0, plen1;
+  u32 preg1_off;            // h1 bit offset of region 1's dead-binding mask
 };
 
 // ------------------------------------------------------------------ small constexpr tables
@@ -390,9 +401,12 @@ struct Memb {
   // h0: restarted[i] 2b @2i | timeout[i] 3b @2N+3i | hadNumLeaders 4b | hadNumClientRequests 3b |
   //     hadNumTriedMembershipChanges 3b | hadNumMembershipChanges 3b | Len(history["global"]) 10b
   static constexpr int H_TO = 2 * N, H_HL = 5 * N, H_CR = H_HL + 4, H_TMC = H_CR + 3, H_MC = H_TMC + 3, H_GLEN = H_MC + 3;
-  // h1: flags | k0 (first CommitEntry position after a concurrent BecomeLeader) | last Restart position | added mask
+  // h1: flags | k0 (first CommitEntry position after a concurrent BecomeLeader) | last Restart position | added mask |
+  //     dead-binding masks of the punctuated-search prefix constraints (NB bits per enabled region)
   enum { F_BL = 0, F_CE, F_CONCBL, F_RCLOSE, F_ADD, F_CMC, F_CMC2, F_ADDCOMMITS, F_NEWLEADER, F_PENDADD, F_LCDCC };
-  static constexpr int H_K0 = 11, H_LASTR = 21, H_ADDED = 31;
+  static constexpr int H_K0 = 11, H_LASTR = 21, H_ADDED = 31, H_PREFIX = 36;
+  static constexpr int NB = N >= 3 ? N * (N - 1) * (N - 2) : 0;   // bindings of s1, s2, s3 (raft.tla:1199, :1229)
+  static constexpr u64 NBMASK = lomask(NB);
   RMC_HD static int hget(u64 h, int off, int w) { return (int)((h >> off) & lomask(w)); }
   RMC_HD static void hset(u64& h, int off, int w, int v, u32& err) {
     if (v < 0 || (u64)v > lomask(w)) { err |= ME_CAP; v &= (int)lomask(w); }
@@ -404,55 +418,120 @@ struct Memb {
   RMC_HD static int glen(const Work& s) { return hget(s.h0, H_GLEN, 10); }
   RMC_HD static void h_bump(Work& t, int off, int w, u32& err) { hset(t.h0, off, w, hget(t.h0, off, w) + 1, err); }
   RMC_HD static int h_append(Work& t, int d, u32& err) { const int g = glen(t) + d; hset(t.h0, H_GLEN, 10, g, err); return g; }
+  // History entries as (x, y) codes for the prefix constraints: x = kind | executedOn << 4 |
+  // aux << 8, y = the message code (Send/Receive) or 0.  The host encodes the golden traces the
+  // same way (memb_prefix.h).
+  enum { HE_SEND = 1, HE_RECV, HE_TRYADD, HE_TRYREM, HE_ADD, HE_REM, HE_BL, HE_CE, HE_CMC, HE_RESTART, HE_TIMEOUT };
+  RMC_HD static u64 hx(int kind, int exec, u32 aux) { return (u64)kind | (u64)exec << 4 | (u64)aux << 8; }
   // Bag changes of one successor are recorded as a delta (at most one message added, one
   // removed) and applied once at the end of apply(): one inlined copy of the 33-entry bag
-  // loops instead of one per call site keeps every kernel within short-branch range.
-  struct Delta { u64 add, rem; bool a, r; };
+  // loops instead of one per call site keeps every kernel within short-branch range.  The
+  // history entries it appends are recorded the same way (hk: HK_* | entry x << 4).
+  enum { HK_NONE = 0, HK_SEND, HK_DISCARD, HK_REPLY, HK_DISCARD_MC, HK_ONE };
+  struct Delta { u64 add, rem; u32 hk; bool a, r; };
   // Send (raft.tla:247-263): TryAddServer/TryRemoveServer precede Send for CatchupRequest/CheckOldConfig
   RMC_HD static void send(Work& t, Delta& d, u64 code, u32& err) {
-    d.add = code; d.a = true;
+    d.add = code; d.a = true; d.hk = HK_SEND;
     const int c = mcls(code);
     if (c == K_CRQ7 || c == K_CRQ8 || c == K_COC) { h_bump(t, H_TMC, 3, err); h_append(t, 2, err); }
     else h_append(t, 1, err);
   }
-  RMC_HD static void discard(Work& t, Delta& d, u64 code, u32& err) { d.rem = code; d.r = true; h_append(t, 1, err); }   // :280-283
-  RMC_HD static void reply(Work& t, Delta& d, u64 resp, u64 req, u32& err) {   // :308-314: WithoutMessage(req, WithMessage(resp, .))
-    d.add = resp; d.a = true; d.rem = req; d.r = true; h_append(t, 2, err);
+  RMC_HD static void discard(Work& t, Delta& d, u64 code, u32& err) {   // :280-283
+    d.rem = code; d.r = true; d.hk = HK_DISCARD; h_append(t, 1, err);
   }
-  // DiscardDirectWithMembershipChange (:285-290) with AddServer/RemoveServer
+  RMC_HD static void reply(Work& t, Delta& d, u64 resp, u64 req, u32& err) {   // :308-314: WithoutMessage(req, WithMessage(resp, .))
+    d.add = resp; d.a = true; d.rem = req; d.r = true; d.hk = HK_REPLY; h_append(t, 2, err);
+  }
+  // DiscardDirectWithMembershipChange (:285-290) with AddServer/RemoveServer (:802-803)
   RMC_HD static void discard_mc(Work& t, Delta& d, u64 code, bool add, int srv, u32& err) {
     d.rem = code; d.r = true;
+    d.hk = HK_DISCARD_MC | (u32)(add ? 1 : 0) << 4 | (u32)srv << 5;
     h_bump(t, H_MC, 3, err);
     h_append(t, 2, err);
     if (add) {
       t.h1 |= (1ull << F_ADD) | (1ull << F_PENDADD) | (1ull << (H_ADDED + srv));
     }
   }
-  RMC_HD static void ev_become_leader(Work& t, int i, u32 leaders, u32& err) {   // :479-483
+  RMC_HD static void one_entry(Delta& d, int kind, int exec, u32 aux) { d.hk = HK_ONE | (u32)hx(kind, exec, aux) << 4; }
+  RMC_HD static void ev_become_leader(Work& t, Delta& d, int i, u32 leaders, u32& err) {   // :479-483
     h_bump(t, H_HL, 4, err);
     h_append(t, 1, err);
+    one_entry(d, HE_BL, i, leaders);
     t.h1 |= 1ull << F_BL;
     if (popc32(leaders) >= 2) t.h1 |= 1ull << F_CONCBL;
     if ((t.h1 >> (H_ADDED + i)) & 1ull) t.h1 |= 1ull << F_NEWLEADER;
     if (hflag(t.h1, F_PENDADD)) t.h1 |= 1ull << F_LCDCC;
   }
-  RMC_HD static void ev_commit_entry(Work& t, u32& err) {
+  RMC_HD static void ev_commit_entry(Work& t, Delta& d, int i, u32 entry, u32& err) {   // :537
     const int pos = h_append(t, 1, err);
+    one_entry(d, HE_CE, i, entry);
     t.h1 |= 1ull << F_CE;
     if (hflag(t.h1, F_CONCBL) && hget(t.h1, H_K0, 10) == 0) hset(t.h1, H_K0, 10, pos, err);
   }
-  RMC_HD static void ev_commit_membership(Work& t, u32 cfgmask, u32& err) {
+  RMC_HD static void ev_commit_membership(Work& t, Delta& d, int i, u32 cfgmask, u32& err) {   // :533-534
     h_append(t, 1, err);
+    one_entry(d, HE_CMC, i, cfgmask);
     if (hflag(t.h1, F_CMC)) t.h1 |= 1ull << F_CMC2;
     t.h1 |= 1ull << F_CMC;
     if (((u32)(t.h1 >> H_ADDED) & cfgmask & (u32)lomask(N)) != 0) t.h1 |= 1ull << F_ADDCOMMITS;
     t.h1 &= ~(1ull << F_PENDADD);
   }
-  RMC_HD static void ev_restart(Work& t, int i, u32& err) {
+  RMC_HD static void ev_restart(Work& t, Delta& d, int i, u32& err) {   // :410
     h_bump(t, 2 * i, 2, err);
     const int pos = h_append(t, 1, err), last = hget(t.h1, H_LASTR, 10);
+    one_entry(d, HE_RESTART, i, 0);
     if (last > 0 && pos - last < 6) t.h1 |= 1ull << F_RCLOSE;
     hset(t.h1, H_LASTR, 10, pos, err);
+  }
+  // executedOn of a Send (msource) / Receive (mdest), from the message code
+  RMC_HD static int msg_src(u64 m) { return (int)fld(m, (int)((mdesc_packed(mcls(m)) >> 7) & 127), SB); }
+  RMC_HD static int msg_dst(u64 m) { return (int)fld(m, (int)(mdesc_packed(mcls(m)) & 127), SB); }
+  // One history entry at 0-based position p against one prefix region: clear the bindings whose
+  // golden entry differs (IsPrefix(SubSeq(trace, 1, maxLen), history["global"]), raft.tla:1201-1204).
+  RMC_HD static u64 prefix_match(u64 dead, const u64* tab, u32 plen, int p, u64 x, u64 y) {
+    if (p >= (int)plen) return dead;
+    const u64* row = tab + (u64)p * NB * 2;
+#pragma unroll 1
+    for (int b = 0; b < NB; ++b)
+      if (row[2 * b] != x || row[2 * b + 1] != y) dead |= 1ull << b;
+    return dead;
+  }
+  // The entries this successor appended (Delta.hk), at positions glen(s), glen(s)+1, against
+  // every enabled prefix region.
+  RMC_HD static void prefix_step(const Work& s, Work& t, const Delta& d, const MembRuntime& rt) {
+    const u32 hk = d.hk & 15u;
+    if (hk == HK_NONE) return;
+    u64 x0, y0 = 0, x1 = 0, y1 = 0;
+    int n = 1;
+    if (hk == HK_SEND) {
+      const int c = mcls(d.add), src = msg_src(d.add);
+      x0 = hx(HE_SEND, src, 0); y0 = d.add;
+      if (c == K_CRQ7 || c == K_CRQ8 || c == K_COC) {   // TryAddServer (added = mdest) / TryRemoveServer (removed = mserver)
+        x1 = x0; y1 = y0; n = 2;
+        x0 = c == K_COC ? hx(HE_TRYREM, src, (u32)fld(d.add, O_COC_SRV, SB)) : hx(HE_TRYADD, src, (u32)msg_dst(d.add));
+        y0 = 0;
+      }
+    } else if (hk == HK_ONE) {
+      x0 = d.hk >> 4;
+    } else {
+      x0 = hx(HE_RECV, msg_dst(d.rem), 0); y0 = d.rem;
+      if (hk == HK_REPLY) { x1 = hx(HE_SEND, msg_src(d.add), 0); y1 = d.add; n = 2; }
+      if (hk == HK_DISCARD_MC) { x1 = hx((d.hk >> 4) & 1u ? HE_ADD : HE_REM, msg_dst(d.rem), d.hk >> 5); n = 2; }
+    }
+    const int p = glen(s);
+    if (rt.plen0) {
+      u64 dead = (t.h1 >> H_PREFIX) & NBMASK;
+      dead = prefix_match(dead, rt.ptab0, rt.plen0, p, x0, y0);
+      if (n == 2) dead = prefix_match(dead, rt.ptab0, rt.plen0, p + 1, x1, y1);
+      t.h1 = (t.h1 & ~(NBMASK << H_PREFIX)) | dead << H_PREFIX;
+    }
+    if (rt.plen1) {
+      const int off = (int)rt.preg1_off;
+      u64 dead = (t.h1 >> off) & NBMASK;
+      dead = prefix_match(dead, rt.ptab1, rt.plen1, p, x0, y0);
+      if (n == 2) dead = prefix_match(dead, rt.ptab1, rt.plen1, p + 1, x1, y1);
+      t.h1 = (t.h1 & ~(NBMASK << off)) | dead << off;
+    }
   }
 
   // Opaque redefinition of the parent's registers (no instructions emitted): called at the top
@@ -502,11 +581,12 @@ struct Memb {
   // Returns its MembAct, or -1 when it does not exist.
   RMC_HD static int apply(const Work& s, int k, int sub, Work& t, u32& err, const MembRuntime& rt) {
     t = s;
-    Delta d{0, 0, false, false};
+    Delta d{0, 0, HK_NONE, false, false};
     const int act = apply_inner(s, k, sub, t, d, err, rt);
     if (act >= 0) {
       if (d.a) with_msg(t.bag, d.add, err);
       if (d.r) without_msg(t.bag, d.rem);
+      if (rt.plen0 | rt.plen1) prefix_step(s, t, d, rt);
     }
     return act;
   }
@@ -530,7 +610,7 @@ struct Memb {
       s_st(t, i, L);
 #pragma unroll
       for (int j = 0; j < N; ++j) { s_next(t, i, j, llen(li) + 1, err); s_match(t, i, j, 0, err); }
-      ev_become_leader(t, i, servers_in(s.st, L) | (1u << i), err);
+      ev_become_leader(t, d, i, servers_in(s.st, L) | (1u << i), err);
       return MA_BecomeLeader;
     }
     if (k < G_ACI) {                                                  // ClientRequest(i, v) :488-497
@@ -561,8 +641,8 @@ struct Memb {
       if (nci > ci) {
         const u32 e = lent(li, nci - 1);
         const bool cmc = etype(e) == cfgt && r2m(evalue(e)) != config_of<MAXLOG>(li, nci - 1, rt.init_cfg, cfgt, nullptr);
-        if (cmc) ev_commit_membership(t, r2m(evalue(e)), err);         // G11
-        else ev_commit_entry(t, err);
+        if (cmc) ev_commit_membership(t, d, i, r2m(evalue(e)), err);   // G11
+        else ev_commit_entry(t, d, i, e, err);
       }
       return MA_AdvanceCommitIndex;
     }
@@ -596,6 +676,7 @@ struct Memb {
       fset<N>(t.vr, i, 0u); fset<N>(t.vg, i, 0u);
       h_bump(t, H_TO + 3 * i, 3, err);
       h_append(t, 1, err);
+      one_entry(d, HE_TIMEOUT, i, 0);
       return MA_Timeout;
     }
     if (k < G_DUP) {                                                  // Restart(i) :401-411
@@ -605,7 +686,7 @@ struct Memb {
 #pragma unroll
       for (int j = 0; j < N; ++j) { s_next(t, i, j, 1, err); s_match(t, i, j, 0, err); }
       s_commit(t, i, 0, err);
-      ev_restart(t, i, err);
+      ev_restart(t, d, i, err);
       return MA_Restart;
     }
     if (k < G_DROP) {                                                 // DuplicateMessage(m), messages[m] = 1 :892-896, :926-928
@@ -808,6 +889,9 @@ struct Memb {
       ok &= !(hl < 1 && cr < 1) || (!anyr && sumt <= 1 && cand <= 1);
     if (c & (1u << MC_CleanStartUntilTwoLeaders)) ok &= !(hl < 2) || (sumr <= 1 && sumt <= 2);
     if (c & (1u << MC_CommitWhenConcurrentLeaders_constraint)) ok &= glen(t) < 20 || hflag(t.h1, F_CONCBL);
+    // \E s1, s2, s3 \in Server : distinct /\ the history extends the golden prefix (raft.tla:1198-1204, :1228-1234)
+    if (c & (1u << MC_CommitWhenConcurrentLeaders_unique)) ok &= ((t.h1 >> H_PREFIX) & NBMASK) != NBMASK;
+    if (c & (1u << MC_MajorityOfClusterRestarts_constraint)) ok &= ((t.h1 >> rt.preg1_off) & NBMASK) != NBMASK;
     if (rt.action_constraints & MAC_CommitWhenConcurrentLeaders) ok &= glen(s) < 20 || servers_in(t.st, C) == 0;
     return ok;
   }

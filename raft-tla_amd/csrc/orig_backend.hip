@@ -3,9 +3,9 @@
 // One BFS level is processed in frontier chunks; each chunk runs three
 // kernels on one stream:
 //
-//  1. orig_generate  (compute): one lane per frontier state, the Next
-//     relation's action instances unrolled (every lane of a wave runs the
-//     same action code on a different state); constraint filter, TLC
+//  1. orig_generate  (compute): one lane per frontier state, a wave-uniform
+//     loop over the Next relation's action instances (every lane of a wave
+//     runs the same action code on a different state); constraint filter, TLC
 //     generated counts, out-of-model invariants (TLC semantics, [ext]
 //     switch), canonical pack and FP64 of each in-model successor into the
 //     instance-major slot array cand[k][s] (0 = none): coalesced, no atomics.
@@ -65,11 +65,12 @@ struct GenArgs {
   void* viol;
 };
 
-// One lane per frontier state, the instance loop unrolled (instance indices become
-// compile-time constants); successor, constraints, TLC generated counts, out-of-model
-// invariants, canonical pack and FP64 in one pass; fingerprint slots written coalesced.
-// (A split expand + full-lane fingerprint pipeline measured 51.4 vs 49.4 ms/run on C2:
-// apply, not the pack + hash, dominates this spec, so the split does not pay here.)
+// One lane per frontier state, a wave-uniform loop over the action instances; successor,
+// constraints, TLC generated counts, out-of-model invariants, canonical pack and FP64 in one
+// pass; fingerprint slots written coalesced.  (A split expand + full-lane fingerprint
+// pipeline measured 51.4 vs 49.4 ms/run on C2: apply, not the pack + hash, dominates this
+// spec, so the split does not pay here.  Unrolling the ~50-instance loop is refused by the
+// compiler at this body size.)
 template <class S>
 __global__ void __launch_bounds__(BS) orig_generate(GenArgs a) {
   using W = typename S::Work;
@@ -95,7 +96,7 @@ __global__ void __launch_bounds__(BS) orig_generate(GenArgs a) {
 #pragma unroll
     for (int q = 0; q < S::AW; ++q) al[q] = 0;
   }
-#pragma unroll
+#pragma unroll 1
   for (int k = 0; k < S::NI; ++k) {
     u64 fp = 0;
     if (active) {

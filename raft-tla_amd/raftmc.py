@@ -26,7 +26,8 @@ EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stat
            "mc_trace", "mc_report", "mc_dump_states", "mc_describe", "mc_exit_code", "mc_free",
            "mc_close", "mc_last_error", "mc_shard_open", "mc_shard_record_bytes", "mc_shard_frontier",
            "mc_shard_generate", "mc_shard_fill", "mc_shard_dedup", "mc_shard_materialize", "mc_shard_store",
-           "mc_shard_level_stats", "mc_shard_level_commit", "mc_shard_read_state", "mc_shard_violation"]
+           "mc_shard_level_stats", "mc_shard_level_commit", "mc_shard_read_state", "mc_shard_violation",
+           "mc_set_history_prefix"]
 
 
 class McOpts(ctypes.Structure):
@@ -78,6 +79,7 @@ def load_library(path=LIB_PATH):
     for f in ("mc_trace", "mc_report", "mc_describe"):
         getattr(lib, f).argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.mc_dump_states.argtypes = [P, ctypes.c_char_p]
+    lib.mc_set_history_prefix.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p]
     lib.mc_exit_code.argtypes = [P]
     lib.mc_free.argtypes = [P]
     lib.mc_close.argtypes = [P]
@@ -127,6 +129,13 @@ class ModelChecker:
         s = ctypes.string_at(p, n.value).decode()
         self.lib.mc_free(p)
         return s
+
+    def set_history_prefix(self, constraint, trace_text):
+        """Golden history trace (TLA+ value text) of a punctuated-search constraint
+        (CommitWhenConcurrentLeaders_unique / MajorityOfClusterRestarts_constraint)."""
+        rc = self.lib.mc_set_history_prefix(self.h, constraint.encode(), trace_text.encode())
+        if rc:
+            raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
 
     def describe(self):
         import json

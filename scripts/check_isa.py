@@ -12,6 +12,7 @@ suite runs this check (tests/test_abi.py).
 import json
 import os
 import re
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -27,7 +28,11 @@ def code_objects(lib):
     """The .hip_fatbin section holds one offload bundle per translation unit; unbundle each."""
     d = tempfile.mkdtemp()
     fat = os.path.join(d, "fat.bin")
-    subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=" + fat, lib], check=True)
+    # objcopy without an output operand rewrites its input in place: dump from a copy, never
+    # from the library a running process may have mapped
+    copy = os.path.join(d, "lib.so")
+    shutil.copyfile(lib, copy)
+    subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=" + fat, copy, os.path.join(d, "discard.so")], check=True)
     blob = open(fat, "rb").read()
     starts = [m.start() for m in re.finditer(re.escape(MAGIC), blob)]
     out = []

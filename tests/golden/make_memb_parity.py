@@ -11,6 +11,10 @@ raft-tla_amd/csrc/memb_spec.h).  TLC itself is unavailable offline
 (SURVEY.md §8c): the counts are oracle-pinned; the oracle is pinned by the
 reference's two TLC traces (tests/test_oracle.py).
 
+Punctuated-search cases take the golden history trace of their prefix
+constraint from the committed trace fixtures (tests/golden/*_trace.json, the
+TLC traces of tlc_membership/raft.tla:1201 and :1231).
+
     python tests/golden/make_memb_parity.py [case ...]
 """
 import hashlib
@@ -20,7 +24,11 @@ import sys
 import tempfile
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from oracle_util import CONFIGS, GOLDEN, MEMB_MC, run_oracle  # noqa: E402
+from oracle_util import CONFIGS, GOLDEN, MEMB_MC, golden_file, run_oracle  # noqa: E402
+
+# prefix constraint -> (oracle flag, trace fixture)
+PREFIXES = {"CommitWhenConcurrentLeaders_unique": ("--golden-cwcl", "concurrent_leaders_trace.json"),
+            "MajorityOfClusterRestarts_constraint": ("--golden-morc", "commit_when_concurrent_leaders_trace.json")}
 
 CASES = {
     "membership_shipped@14": ("membership_shipped", 14),
@@ -31,6 +39,10 @@ CASES = {
     "scen_FirstBecomeLeader": ("scen_FirstBecomeLeader", 0),
     "scen_FirstCommit": ("scen_FirstCommit", 0),
     "scen_EntryCommitted": ("scen_EntryCommitted", 0),
+    "punct_CommitWhenConcurrentLeaders@24": ("scen_CommitWhenConcurrentLeaders_punct", 24, "CommitWhenConcurrentLeaders_unique"),
+    "punct_CommitWhenConcurrentLeaders": ("scen_CommitWhenConcurrentLeaders_punct", 0, "CommitWhenConcurrentLeaders_unique"),
+    "punct_MajorityOfClusterRestarts@30": ("scen_MajorityOfClusterRestarts_punct", 30, "MajorityOfClusterRestarts_constraint"),
+    "punct_MajorityOfClusterRestarts": ("scen_MajorityOfClusterRestarts_punct", 0, "MajorityOfClusterRestarts_constraint"),
 }
 OUT = os.path.join(GOLDEN, "memb_parity.json")
 
@@ -43,10 +55,14 @@ def digest_lines(path):
 def main(names):
     doc = json.load(open(OUT)) if os.path.exists(OUT) else {}
     for n in names:
-        cfg, depth = CASES[n]
+        cfg, depth = CASES[n][:2]
+        prefix = CASES[n][2] if len(CASES[n]) > 2 else None
         fd, dump = tempfile.mkstemp(suffix=".txt")
         os.close(fd)
         args = ["--sym", "view", "--dump", dump, "--trace"]
+        if prefix:
+            flag, fixture = PREFIXES[prefix]
+            args += [flag, golden_file(fixture)[0]]
         if depth:
             args += ["--max-depth", depth]
         r = run_oracle("bfs", MEMB_MC, os.path.join(CONFIGS, cfg + ".cfg"), *args, timeout=100000)
@@ -54,6 +70,7 @@ def main(names):
         sha, cnt = digest_lines(dump)
         os.unlink(dump)
         doc[n] = {"cfg": cfg, "max_depth": depth, "verdict": r["verdict"], "violated": r["violated"],
+                  "prefix": [prefix, PREFIXES[prefix][1]] if prefix else None,
                   "generated": r["generated"], "distinct": r["distinct"], "depth": r["depth"],
                   "left_on_queue": r["left_on_queue"], "levels": r["levels"], "actions": r["actions"],
                   "states_sha256": sha, "states_dumped": cnt,

@@ -4,12 +4,14 @@
 // memb_spec.h, the same header the gfx950 kernels compile), so its semantics
 // can be checked against the oracle on CPU before a GPU run.
 // Shape: -DSHAPE_N=.. -DSHAPE_NV=..
-//   memb_host_bfs CFG MAX_DEPTH [DUMP]  -> JSON {generated, distinct, depth, left_on_queue, verdict, actions}
+//   memb_host_bfs CFG MAX_DEPTH [DUMP|-] [--prefix CONSTRAINT TRACE_FILE]...
+//     -> JSON {generated, distinct, depth, left_on_queue, verdict, actions}
 #include <cstdio>
 #include <string>
 #include <unordered_set>
 #include <vector>
 
+#include "../../raft-tla_amd/csrc/memb_prefix.h"
 #include "../../raft-tla_amd/csrc/memb_text.h"
 
 using namespace rmc;
@@ -20,9 +22,22 @@ int main(int argc, char** argv) {
   CfgFile cfg = parse_cfg_text(read_text_file(argv[1]));
   MembModel m = resolve_memb_model(cfg);
   const long long max_depth = argc > 2 ? std::atoll(argv[2]) : 0;
-  FILE* dump = argc > 3 ? std::fopen(argv[3], "w") : nullptr;
+  FILE* dump = argc > 3 && std::string(argv[3]) != "-" ? std::fopen(argv[3], "w") : nullptr;
   MembText<S> text(m);
-  const MembRuntime& rt = m.rt;
+  MembRuntime rt = m.rt;
+  // punctuated-search prefixes, laid out as the GPU backend does (memb_backend.hip prepare_prefixes)
+  std::vector<u64> tabs[2];
+  u32 off = S::H_PREFIX;
+  for (int a = 4; a + 2 < argc; a += 3) {
+    const std::string con = argv[a + 1];
+    const int r = con == kMembConNames[kPrefixCon[0]] ? 0 : 1;
+    tabs[r] = encode_prefix_table<S>(m, trace_global(parse_tla_value(read_text_file(argv[a + 2]))));
+    const u32 len = (u32)(tabs[r].size() / 2 / (S::NB ? S::NB : 1));
+    if (r == 0) { rt.ptab0 = tabs[0].data(); rt.plen0 = len; }
+    else { rt.ptab1 = tabs[1].data(); rt.plen1 = len; }
+  }
+  for (int r = 0; r < 2; ++r)
+    if ((rt.constraints >> kPrefixCon[r]) & 1u) { if (r == 1) rt.preg1_off = off; off += S::NB; }
   const u64 seed = 0x5EED5EED2024ull;
   std::unordered_set<u64> seen;
   std::vector<W> frontier(1);

@@ -70,7 +70,9 @@ def test_describe_membership_four_servers(raftmc):
     ((("    LogMatching\n", "    LogMatching\n    NotAnInvariant\n"),), -4),
     ((("NEXT NextAsyncCrash", "NEXT NextFoo"),), -4),
     ((("    Server = {s1, s2, s3}", "    Server = {s1, s2, s3, s4, s5}"),), -4),   # shape not compiled in
-    ((("    CleanStartUntilTwoLeaders\n", "    CleanStartUntilTwoLeaders\n    MajorityOfClusterRestarts_constraint\n"),), -4),
+    ((("    Server = {s1, s2, s3}", "    Server = {s1, s2, s3, s4}"),     # two prefix masks of 24 bindings
+      ("    CleanStartUntilTwoLeaders\n", "    CleanStartUntilTwoLeaders\n    MajorityOfClusterRestarts_constraint\n"
+                                        "    CommitWhenConcurrentLeaders_unique\n")), -4),
 ])
 def test_membership_open_rejects_unsupported(raftmc, edit, code):
     from oracle_util import MEMB_MC
@@ -103,3 +105,62 @@ def test_kernels_short_branch_and_no_scratch():
     assert len(ks) > 40 and any("memb_fingerprint" in k for k in ks) and any("orig_generate" in k for k in ks)
     bad = {k: v for k, v in ks.items() if v["long_branches"] or v["scratch_bytes"]}
     assert not bad, bad
+
+
+PUNCT_CWCL = os.path.join(CONFIGS, "scen_CommitWhenConcurrentLeaders_punct.cfg")
+
+
+def trace_fixture_text(name):
+    import json
+    from oracle_util import GOLDEN, tla_text
+    return tla_text(json.load(open(os.path.join(GOLDEN, name)))["value"])
+
+
+def test_prefix_constraint_without_trace_is_refused(raftmc):
+    """configs/ holds no raft.tla, so the wrapper's punctuated-search constraint has no
+    golden trace: mc_run refuses before touching a device (no silent 'always true')."""
+    from oracle_util import MEMB_MC
+    with raftmc.ModelChecker(MEMB_MC, PUNCT_CWCL) as mc:
+        assert mc.describe()["history_prefixes"] == {"CommitWhenConcurrentLeaders_unique": -1}
+        with pytest.raises(raftmc.RaftMCError) as e:
+            mc.run()
+    assert e.value.code == -4 and "golden history trace" in str(e.value)
+
+
+def test_set_history_prefix(raftmc):
+    from oracle_util import MEMB_MC
+    with raftmc.ModelChecker(MEMB_MC, PUNCT_CWCL) as mc:
+        with pytest.raises(raftmc.RaftMCError) as e:
+            mc.set_history_prefix("BoundedTerms", "<<>>")
+        assert e.value.code == -1
+        with pytest.raises(raftmc.RaftMCError) as e:
+            mc.set_history_prefix("CommitWhenConcurrentLeaders_unique", '<<[action |-> "Timeout", executedOn |-> s1')
+        assert e.value.code == -3
+        with pytest.raises(raftmc.RaftMCError) as e:
+            mc.set_history_prefix("CommitWhenConcurrentLeaders_unique", "[local |-> <<>>]")
+        assert e.value.code == -3
+        mc.set_history_prefix("CommitWhenConcurrentLeaders_unique", trace_fixture_text("concurrent_leaders_trace.json"))
+        d = mc.describe()
+    assert d["history_prefixes"] == {"CommitWhenConcurrentLeaders_unique": 20} and d["prefix_bindings"] == 6
+
+
+def test_prefix_taken_from_extended_module(raftmc, tmp_path):
+    """As TLC resolves EXTENDS: the wrapper's `EXTENDS raft` finds raft.tla next to it, and
+    the constraint's trace literal comes from the operator's definition there."""
+    from oracle_util import MEMB_MC
+    wrapper = tmp_path / "raft_membership_mc.tla"
+    wrapper.write_text(open(MEMB_MC).read())
+    trace = trace_fixture_text("commit_when_concurrent_leaders_trace.json")
+    (tmp_path / "raft.tla").write_text(
+        "---- MODULE raft ----\n"
+        "MajorityOfClusterRestarts_constraint ==\n"
+        "    \\E s1, s2, s3 \\in Server :\n"
+        "        /\\ Cardinality({s1, s2, s3}) = 3\n"
+        "        /\\ LET  CommitWhenConcurrentLeaders_trace == " + trace + "\n"
+        "                maxLen == Min({Len(CommitWhenConcurrentLeaders_trace[\"global\"]), Len(history[\"global\"])})\n"
+        "            IN IsPrefix(SubSeq(CommitWhenConcurrentLeaders_trace[\"global\"], 1, maxLen), history[\"global\"])\n"
+        "\n"
+        "Next == TRUE\n"
+        "====\n")
+    with raftmc.ModelChecker(str(wrapper), os.path.join(CONFIGS, "scen_MajorityOfClusterRestarts_punct.cfg")) as mc:
+        assert mc.describe()["history_prefixes"] == {"MajorityOfClusterRestarts_constraint": 28}

@@ -6,7 +6,9 @@ Integer work, so the bar is bit-exact.  With TLC's FIFO first-found order
 reproduced on the GPU (memb_backend.hip), even the order-dependent figures
 match: per-action DISTINCT counts, the history counters of every kept state
 (they are part of the dumped text) and the counterexample trace, state by
-state.  The oracle runs SYMMETRY in orbit ("view") mode, which is what the
+state.  The punctuated-search cases (CommitWhenConcurrentLeaders_unique,
+MajorityOfClusterRestarts_constraint) take the reference's golden history
+traces from the committed fixtures.  The oracle runs SYMMETRY in orbit ("view") mode, which is what the
 GPU implements.
 """
 import hashlib
@@ -16,7 +18,7 @@ import tempfile
 
 import pytest
 
-from oracle_util import CONFIGS, GOLDEN, MEMB_MC
+from oracle_util import CONFIGS, GOLDEN, MEMB_MC, tla_text
 
 pytestmark = pytest.mark.gpu
 
@@ -24,6 +26,16 @@ SMALL = dict(fp_table_bytes=1 << 26, state_store_bytes=1 << 29, deadlock=False)
 FIX = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))
 EXHAUSTIVE = sorted(k for k, v in FIX.items() if v["verdict"] == "OK")
 VIOLATIONS = sorted(k for k, v in FIX.items() if v["verdict"] == "INVARIANT_VIOLATION")
+
+
+def open_case(raftmc, g, **kw):
+    """A handle for a fixture case; punctuated-search cases get their golden history trace
+    (the committed TLC trace fixture) through mc_set_history_prefix."""
+    mc = raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), **kw)
+    if g.get("prefix"):
+        con, fixture = g["prefix"]
+        mc.set_history_prefix(con, tla_text(json.load(open(os.path.join(GOLDEN, fixture)))["value"]))
+    return mc
 
 
 def states_sha(mc):
@@ -38,7 +50,7 @@ def states_sha(mc):
 @pytest.mark.parametrize("case", EXHAUSTIVE)
 def test_membership_parity(raftmc, case):
     g = FIX[case]
-    with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), max_depth=g["max_depth"], **SMALL) as mc:
+    with open_case(raftmc, g, max_depth=g["max_depth"], **SMALL) as mc:
         r = mc.run()
         sha, n = states_sha(mc)
     assert r.verdict in ("OK", "DEPTH_LIMIT"), r.error
@@ -51,7 +63,8 @@ def test_membership_parity(raftmc, case):
 @pytest.mark.parametrize("case", VIOLATIONS)
 def test_scenario_shortest_counterexample(raftmc, case):
     g = FIX[case]
-    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), **SMALL)
+    with open_case(raftmc, g, **SMALL) as mc:
+        r = mc.run()
     assert r.verdict == "INVARIANT_VIOLATION" and r.violated == g["violated"] and r.exit_code == 12, (r, r.error)
     assert (r.depth, r.generated, r.distinct, r.left_on_queue) == (g["depth"], g["generated"], g["distinct"], g["left_on_queue"])
     blocks = r.trace_text.strip().split("\n\n")

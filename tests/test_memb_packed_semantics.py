@@ -13,10 +13,11 @@ import tempfile
 
 import pytest
 
-from oracle_util import CONFIGS, GOLDEN, ROOT
+from oracle_util import CONFIGS, GOLDEN, ROOT, golden_file
 
 SHAPES = {"membership_shipped": (3, 2), "memb_dynamic3": (3, 2), "memb_nosym": (3, 2), "memb_two": (2, 1),
-          "memb_four": (4, 2)}
+          "memb_four": (4, 2), "scen_CommitWhenConcurrentLeaders_punct": (3, 2),
+          "scen_MajorityOfClusterRestarts_punct": (3, 2)}
 FIX = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))
 
 
@@ -24,12 +25,20 @@ def build_harness(shape):
     out = os.path.join(tempfile.gettempdir(), "memb_host_bfs_%d%d" % shape)
     csrc = os.path.join(ROOT, "raft-tla_amd", "csrc")
     src = [os.path.join(ROOT, "tests", "native", "memb_host_bfs.cpp"), os.path.join(csrc, "model.cpp"),
-           os.path.join(csrc, "memb_model.cpp")]
-    deps = src + [os.path.join(csrc, f) for f in ("memb_spec.h", "memb_text.h", "common.h")]
+           os.path.join(csrc, "memb_model.cpp"), os.path.join(csrc, "tla_value.cpp")]
+    deps = src + [os.path.join(csrc, f) for f in ("memb_spec.h", "memb_text.h", "memb_prefix.h", "tla_value.h", "common.h")]
     if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(p) for p in deps):
         subprocess.run(["g++", "-O2", "-std=c++17", "-DSHAPE_N=%d" % shape[0], "-DSHAPE_NV=%d" % shape[1], "-o", out, *src],
                        check=True)
     return out
+
+
+def prefix_args(g):
+    """--prefix CONSTRAINT FILE for punctuated-search cases (golden trace from the committed fixture)."""
+    if not g.get("prefix"):
+        return []
+    con, fixture = g["prefix"]
+    return ["--prefix", con, golden_file(fixture)[0]]
 
 
 @pytest.mark.parametrize("case", sorted(k for k, v in FIX.items() if v["verdict"] == "OK"))
@@ -38,7 +47,7 @@ def test_packed_membership_matches_oracle(case):
     exe = build_harness(SHAPES[g["cfg"]])
     fd, dump = tempfile.mkstemp(suffix=".txt")
     os.close(fd)
-    r = json.loads(subprocess.run([exe, os.path.join(CONFIGS, g["cfg"] + ".cfg"), str(g["max_depth"]), dump],
+    r = json.loads(subprocess.run([exe, os.path.join(CONFIGS, g["cfg"] + ".cfg"), str(g["max_depth"]), dump, *prefix_args(g)],
                                   capture_output=True, text=True, check=True).stdout)
     assert r["err"] == 0 and r["verdict"] == "OK"
     assert (r["generated"], r["distinct"], r["depth"], r["left_on_queue"]) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
@@ -48,11 +57,12 @@ def test_packed_membership_matches_oracle(case):
     assert hashlib.sha256("\n".join(lines).encode()).hexdigest() == g["states_sha256"]
 
 
-@pytest.mark.parametrize("case", ["scen_FirstBecomeLeader"])
+@pytest.mark.parametrize("case", ["scen_FirstBecomeLeader", "punct_CommitWhenConcurrentLeaders",
+                                  "punct_MajorityOfClusterRestarts"])
 def test_packed_membership_first_violation(case):
     g = FIX[case]
-    exe = build_harness(SHAPES["membership_shipped"])
-    r = json.loads(subprocess.run([exe, os.path.join(CONFIGS, g["cfg"] + ".cfg"), "0"], capture_output=True, text=True,
-                                  check=True).stdout)
+    exe = build_harness(SHAPES.get(g["cfg"], (3, 2)))
+    r = json.loads(subprocess.run([exe, os.path.join(CONFIGS, g["cfg"] + ".cfg"), "0", "-", *prefix_args(g)],
+                                  capture_output=True, text=True, check=True).stdout)
     assert (r["verdict"], r["violated"], r["depth"], r["generated"], r["distinct"], r["left_on_queue"]) == \
         (g["verdict"], g["violated"], g["depth"], g["generated"], g["distinct"], g["left_on_queue"])

@@ -90,3 +90,16 @@ def test_oracle_check_trace_rejects_a_broken_trace(tmp_path):
     p.write_text("\n".join(lines) + "\n")
     r = run_oracle("check-trace", MEMB_MC, os.path.join(CONFIGS, "memb_four.cfg"), "--golden", str(p))
     assert not r["valid"] and r["bad_step"] == 7
+
+
+def test_punctuated_search_prefix_fixture_reproduces():
+    """MajorityOfClusterRestarts_constraint (raft.tla:1228-1234) with the 28-entry TLC trace of
+    :1231 as its golden prefix: the oracle's bounded search reproduces the committed fixture
+    (the GPU and the packed host harness are checked against the same fixture)."""
+    g = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))["punct_MajorityOfClusterRestarts@30"]
+    path, _ = golden_file("commit_when_concurrent_leaders_trace.json")
+    r = run_oracle("bfs", MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), "--sym", "view", "--golden-morc", path,
+                   "--max-depth", g["max_depth"])
+    assert (r["generated"], r["distinct"], r["depth"], r["left_on_queue"]) == \
+        (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
+    assert r["actions"] == g["actions"]
