@@ -176,6 +176,23 @@ int mc_shard_level_commit(mc_ctx* ctx, const int64_t* global_stats, int32_t* don
 int mc_shard_read_state(const mc_ctx* ctx, uint64_t gid, char** text, size_t* len, uint64_t* meta);
 int mc_shard_violation(const mc_ctx* ctx, uint64_t* parent_gid, char** action, char** text);
 
+/* FIFO-ranked sharding (tlc_membership: VIEW vars makes the kept representative depend on TLC's
+ * single-worker FIFO order).  Keys are global (global parent rank * slots + slot);
+ * the owner's seen-set entry keeps the minimum key of the level, so winners are decided once per
+ * level, not per chunk:
+ *   mc_shard_layout(counts)        every rank's frontier size (global ranks in rank order)
+ *   per chunk: mc_shard_generate -> ROUTE all-to-all -> mc_shard_dedup (no replies yet)
+ *   mc_shard_select(reply_counts)  the owner's winning keys per generating rank -> REPLY all-to-all
+ *   mc_shard_materialize(acks)     the generator sorts its winners and re-derives them in key order
+ *   mc_shard_level_stats, all-reduce; on a stop (stats[4] != 0) mc_shard_event_stats, all-reduce
+ *   (sum), merged into the global stats; mc_shard_level_commit
+ *   rebalance: STATES records of the level's new states (key order, one run per rank) to equal
+ *   contiguous slices of the next level, then mc_shard_store.
+ * The driver is raft-tla_amd/shard.py (fifo_sharded_bfs). */
+int mc_shard_layout(mc_ctx* ctx, const int64_t* frontier_counts);
+int mc_shard_select(mc_ctx* ctx, int64_t* reply_counts);
+int mc_shard_event_stats(mc_ctx* ctx, const int64_t* global_stats, int64_t* stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -68,6 +68,10 @@ struct Backend {
   virtual int shard_read_state(uint64_t gid, std::string& text, uint64_t* meta, std::string& err) const = 0;
   virtual int shard_violation(uint64_t* parent, std::string& action, std::string& text) const = 0;
   virtual const RunResult* shard_result() const = 0;
+  // FIFO first-found specs (VIEW): level layout, per-level winner selection, stop-point counters
+  virtual int shard_layout(const int64_t* counts, std::string& err) { (void)counts; err = "not a FIFO-ranked spec"; return -4; }
+  virtual int shard_select(int64_t* reply_counts, std::string& err) { (void)reply_counts; err = "not a FIFO-ranked spec"; return -4; }
+  virtual int shard_event_stats(const int64_t* g, int64_t* st, std::string& err) { (void)g; (void)st; err = "not a FIFO-ranked spec"; return -4; }
 };
 
 Backend* make_orig_backend(const CfgFile& cfg);   // throws CfgError

@@ -283,6 +283,21 @@ int mc_shard_store(mc_ctx* c, const void* states, int64_t n) {
   SHARD_GUARD();
   SHARD_RC(c->be->shard_store(states, n, err));
 }
+int mc_shard_layout(mc_ctx* c, const int64_t* frontier_counts) {
+  SHARD_GUARD();
+  if (!frontier_counts) return MC_E_INVALID;
+  SHARD_RC(c->be->shard_layout(frontier_counts, err));
+}
+int mc_shard_select(mc_ctx* c, int64_t* reply_counts) {
+  SHARD_GUARD();
+  if (!reply_counts) return MC_E_INVALID;
+  SHARD_RC(c->be->shard_select(reply_counts, err));
+}
+int mc_shard_event_stats(mc_ctx* c, const int64_t* global_stats, int64_t* stats) {
+  SHARD_GUARD();
+  if (!global_stats || !stats) return MC_E_INVALID;
+  SHARD_RC(c->be->shard_event_stats(global_stats, stats, err));
+}
 int mc_shard_level_stats(mc_ctx* c, int64_t* stats) {
   SHARD_GUARD();
   SHARD_RC(c->be->shard_level_stats(stats, err));

@@ -32,6 +32,7 @@
 // 64-bit atomicMin of (key << 2 | kind); the host re-derives that successor
 // with the same spec code to name the invariant and build the trace.
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -50,7 +51,7 @@ namespace rmc {
 namespace {
 enum {
   C_CELLS = 0, C_ERR = 1, C_EVENT = 2, C_NEW = 3, C_ERRGID = 4, C_GEN_IN = 5, C_CELLS_OOM = 6,
-  C_ACT = 8, C_NCTR = C_ACT + 2 * MA_NACT
+  C_ACT = 8, C_SHARD = C_ACT + 2 * MA_NACT, C_NCTR = C_SHARD + 8   // C_SHARD: per-rank bucket counters
 };
 enum { EV_NEXT_ERROR = 0, EV_DEADLOCK = 1, EV_INV_ERROR = 2, EV_VIOLATION = 3 };
 enum { MERR_TABLE_FULL = 0x100, MERR_STORE = 0x200 };
@@ -363,7 +364,8 @@ struct MMatArgs {
   u32* states;
   u64* meta;
   const u64* newrec;
-  u64 n_new, dst_base, cap, level_begin;
+  u64 n_new, dst_base, cap, level_begin;   // level_begin: store index of rank 0 of the level (mod 2^64)
+  u64 gid_tag;                             // sharded: owner rank << 37, or-ed into parent pointers
   MembRuntime rt;
   unsigned long long* ctr;
 };
@@ -398,7 +400,7 @@ __global__ void __launch_bounds__(BS) memb_materialize(MMatArgs a) {
 #pragma unroll
       for (int q = 0; q < NWP / 4; ++q)
         o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
-      a.meta[dst] = (gid << 20) | ((u64)act << 10) | (u64)slot;
+      a.meta[dst] = ((gid | a.gid_tag) << 20) | ((u64)act << 10) | (u64)slot;
       atomicAdd(&lds_cnt[act], 1u);
       const u32 r = S::check_invariants(t, a.rt);
       if (r) ev = ((((gid - a.level_begin) * (u64)S::NSLOT + (u64)slot)) << 2) | ((r >> 8) == IV_BAD ? EV_VIOLATION : EV_INV_ERROR);
@@ -411,6 +413,195 @@ __global__ void __launch_bounds__(BS) memb_materialize(MMatArgs a) {
   __syncthreads();
   for (int t = threadIdx.x; t < MA_NACT; t += BS)
     if (lds_cnt[t]) atomicAdd(&a.ctr[C_ACT + MA_NACT + t], (unsigned long long)lds_cnt[t]);
+}
+
+// ------------------------------------------------------------------ sharded (multi-GPU) kernels
+// FIFO first-found across ranks: keys are global (global parent rank * NSLOT + slot),
+// every fingerprint has one owner ((fp >> 32) mod world) whose seen-set entry keeps the minimum
+// key of the level; after all chunks the owner sends each winning key back to the rank that
+// generated it, which re-derives its winners in key order.
+constexpr int RPER = 16;   // slots / records per thread in the bucketing kernels
+
+struct MRouteArgs {
+  const u64* cand;             // [NSLOT][chunk] fingerprints, 0 = none
+  u64 nslots, chunk_count, rank0, nslot;
+  u32 world;
+  unsigned long long* counts;  // [world]: count pass totals / write pass cursors
+  u64* out;                    // write pass: (fp, key) records, per-owner segments
+};
+RMC_HD inline u32 fp_owner(u64 fp, u32 world) { return (u32)((fp >> 32) % world); }
+
+// per-owner bucketing in two passes (count, then write at reserved cursors); one global atomic
+// per (workgroup, owner)
+template <bool WRITE>
+__global__ void __launch_bounds__(BS) memb_route(MRouteArgs a) {
+  __shared__ unsigned int cnt[8], base[8];
+  if (threadIdx.x < 8) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const u64 tile = (u64)blockIdx.x * (BS * RPER);
+  u64 fp[RPER];
+  unsigned int off[RPER];
+#pragma unroll
+  for (int j = 0; j < RPER; ++j) {
+    const u64 idx = tile + (u64)j * BS + threadIdx.x;
+    fp[j] = idx < a.nslots ? a.cand[idx] : 0ull;
+    off[j] = fp[j] ? atomicAdd(&cnt[fp_owner(fp[j], a.world)], 1u) : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x < a.world) {
+    const unsigned int c = cnt[threadIdx.x];
+    base[threadIdx.x] = c ? (unsigned int)atomicAdd(&a.counts[threadIdx.x], (unsigned long long)c) : 0u;
+  }
+  if (!WRITE) return;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPER; ++j) {
+    if (!fp[j]) continue;
+    const u64 idx = tile + (u64)j * BS + threadIdx.x;
+    const u64 sl = idx / a.chunk_count, st = idx - sl * a.chunk_count;
+    const u64 o = (u64)base[fp_owner(fp[j], a.world)] + off[j];
+    a.out[2 * o] = fp[j];
+    a.out[2 * o + 1] = (a.rank0 + st) * a.nslot + sl;
+  }
+}
+
+struct MDedupShArgs {
+  const u64* recv;             // (fp, key) records
+  u64 n, level;
+  u64* table;
+  u64 table_mask;
+  u64* lvl;                    // level records out: (table position + 1, key)
+  unsigned long long* ctr;
+};
+
+// owner side: insert-if-absent, keep the minimum (level, key); remember (position, key) for select
+__global__ void __launch_bounds__(BS) memb_dedup_sh(MDedupShArgs a) {
+  const u64 tile = (u64)blockIdx.x * (BS * DPER);
+  u64 fp[DPER], key[DPER], cur[DPER], pos[DPER];
+#pragma unroll
+  for (int j = 0; j < DPER; ++j) {
+    const u64 i = tile + (u64)j * BS + threadIdx.x;
+    fp[j] = i < a.n ? a.recv[2 * i] : 0ull;
+    key[j] = i < a.n ? a.recv[2 * i + 1] : 0ull;
+    pos[j] = fp[j] & a.table_mask;
+  }
+#pragma unroll
+  for (int j = 0; j < DPER; ++j) cur[j] = fp[j] ? a.table[2 * pos[j]] : ~0ull;
+#pragma unroll
+  for (int j = 0; j < DPER; ++j)
+    if (fp[j] && cur[j] == 0ull)
+      cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[2 * pos[j]], 0ull, (unsigned long long)fp[j]);
+  u32 err = 0;
+#pragma unroll
+  for (int j = 0; j < DPER; ++j) {
+    if (!fp[j]) continue;
+    if (cur[j] == 0ull || cur[j] == fp[j]) continue;
+    u64 slot = (pos[j] + 1) & a.table_mask;
+    for (int probe = 0;; ++probe) {
+      if (probe >= (1 << 20)) { err |= MERR_TABLE_FULL; break; }
+      const u64 c = a.table[2 * slot];
+      if (c == fp[j]) break;
+      if (c == 0ull) {
+        const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[2 * slot], 0ull, (unsigned long long)fp[j]);
+        if (old == 0ull || old == fp[j]) break;
+      }
+      slot = (slot + 1) & a.table_mask;
+    }
+    pos[j] = slot;
+  }
+#pragma unroll
+  for (int j = 0; j < DPER; ++j) {
+    if (!fp[j]) continue;
+    const u64 i = tile + (u64)j * BS + threadIdx.x;
+    atomicMax((unsigned long long*)&a.table[2 * pos[j] + 1], (unsigned long long)~((a.level << 40) | key[j]));
+    a.lvl[2 * i] = pos[j] + 1;
+    a.lvl[2 * i + 1] = key[j];
+  }
+  if (err) atomicOr(&a.ctr[C_ERR], (unsigned long long)err);
+}
+
+struct MSelShArgs {
+  const u64* lvl;              // (position + 1, key) of the level
+  u64 n, level;
+  const u64* table;
+  u64 kstart[8];               // first key of each generating rank's range (kstart[0] = 0)
+  u32 world;
+  unsigned long long* counts;  // [world]: count pass totals / write pass cursors
+  u64* out;                    // write pass: winning keys, per-generator segments
+};
+
+// owner side, after every chunk of the level: the winners (entry still holds this level's key)
+// bucketed by the rank that generated them
+template <bool WRITE>
+__global__ void __launch_bounds__(BS) memb_select_sh(MSelShArgs a) {
+  __shared__ unsigned int cnt[8], base[8];
+  if (threadIdx.x < 8) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const u64 tile = (u64)blockIdx.x * (BS * RPER);
+  u64 key[RPER];
+  unsigned int off[RPER], gen[RPER];
+  bool win[RPER];
+#pragma unroll
+  for (int j = 0; j < RPER; ++j) {
+    const u64 i = tile + (u64)j * BS + threadIdx.x;
+    win[j] = false; key[j] = 0; gen[j] = 0; off[j] = 0;
+    if (i < a.n) {
+      const u64 p = a.lvl[2 * i] - 1;
+      key[j] = a.lvl[2 * i + 1];
+      win[j] = a.table[2 * p + 1] == ~((a.level << 40) | key[j]);
+      u32 g = 0;
+#pragma unroll
+      for (int q = 1; q < 8; ++q) if ((u32)q < a.world && key[j] >= a.kstart[q]) g = (u32)q;
+      gen[j] = g;
+      if (win[j]) off[j] = atomicAdd(&cnt[g], 1u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < a.world) {
+    const unsigned int c = cnt[threadIdx.x];
+    base[threadIdx.x] = c ? (unsigned int)atomicAdd(&a.counts[threadIdx.x], (unsigned long long)c) : 0u;
+  }
+  if (!WRITE) return;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPER; ++j)
+    if (win[j]) a.out[(u64)base[gen[j]] + off[j]] = key[j];
+}
+
+// generating side: sorted winning keys -> (parent store index << 10 | slot) for memb_materialize
+__global__ void __launch_bounds__(BS) memb_keys_to_newrec(const u64* keys, u64 n, u64 nslot, u64 rank_base, u64 level_begin,
+                                                         u64* newrec) {
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  const u64 k = keys[i], r = k / nslot;
+  newrec[i] = ((r - rank_base + level_begin) << 10) | (k - r * nslot);
+}
+
+// STATES records (packed state words, parent meta) <-> the store
+template <int NWP>
+__global__ void __launch_bounds__(BS) memb_pack_states(const u32* states, const u64* meta, u64 first, u64 n, u32* out) {
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  constexpr int RW = NWP + 2;
+  const uint4* src = reinterpret_cast<const uint4*>(states + (first + i) * NWP);
+#pragma unroll
+  for (int q = 0; q < NWP / 4; ++q) {
+    const uint4 v = src[q];
+    out[i * RW + 4 * q] = v.x; out[i * RW + 4 * q + 1] = v.y; out[i * RW + 4 * q + 2] = v.z; out[i * RW + 4 * q + 3] = v.w;
+  }
+  const u64 m = meta[first + i];
+  out[i * RW + NWP] = (u32)m; out[i * RW + NWP + 1] = (u32)(m >> 32);
+}
+template <int NWP>
+__global__ void __launch_bounds__(BS) memb_unpack_states(const u32* in, u64 n, u64 first, u32* states, u64* meta) {
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  constexpr int RW = NWP + 2;
+  uint4* dst = reinterpret_cast<uint4*>(states + (first + i) * NWP);
+#pragma unroll
+  for (int q = 0; q < NWP / 4; ++q)
+    dst[q] = make_uint4(in[i * RW + 4 * q], in[i * RW + 4 * q + 1], in[i * RW + 4 * q + 2], in[i * RW + 4 * q + 3]);
+  meta[first + i] = (u64)in[i * RW + NWP] | ((u64)in[i * RW + NWP + 1] << 32);
 }
 
 #define HIPCHK(x)                                                                             \
@@ -646,7 +837,7 @@ class MembGpu : public Backend {
         if (nnew && next_write + nnew <= cap_) {
           MMatArgs m;
           m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.n_new = nnew; m.dst_base = next_write; m.cap = cap_;
-          m.level_begin = level_begin; m.rt = rt_dev_; m.ctr = (unsigned long long*)d_ctr_;
+          m.level_begin = level_begin; m.gid_tag = 0; m.rt = rt_dev_; m.ctr = (unsigned long long*)d_ctr_;
           HIPCHK(hipEventRecord(ev_[5], stream_));
           hipLaunchKernelGGL((memb_materialize<S>), dim3((unsigned)((nnew + BS - 1) / BS)), dim3(BS), 0, stream_, m);
           HIPCHK(hipGetLastError());
@@ -786,23 +977,385 @@ class MembGpu : public Backend {
     return 0;
   }
 
-  // ---- sharded mode: not available for this spec yet (FIFO ranking across ranks)
-  int shard_open(const RunOpts&, int, int, std::string& err) override {
-    err = "sharded (multi-GPU) BFS is implemented for raft_original only; tlc_membership runs on one GPU";
-    return MC_E_UNSUPPORTED;
+  // ---- sharded mode: FIFO first-found across ranks.  Per level the driver
+  // (raft-tla_amd/shard.py fifo_sharded_bfs) calls layout, then per chunk generate / fill(ROUTE) /
+  // all-to-all / dedup, then select / fill(REPLY) / all-to-all / materialize, the level
+  // statistics (+ event_stats on a stop), level_commit, and the rebalance fill(STATES) /
+  // all-to-all / store that gives every rank an equal contiguous slice of the next level.
+  int shard_open(const RunOpts& o, int rank, int world, std::string& err) override {
+    if (world < 1 || world > 8 || rank < 0 || rank >= world) { err = "world must be 1..8"; return MC_E_INVALID; }
+    for (int q = 0; q < 2; ++q)
+      if (((m_.rt.constraints >> kPrefixCon[q]) & 1u) && !have_prefix_[q]) {
+        err = std::string(kMembConNames[kPrefixCon[q]]) + " needs its golden history trace (mc_set_history_prefix)";
+        return MC_E_UNSUPPORTED;
+      }
+    RunOpts so = o;
+    if (!so.state_store_bytes) {   // leave room for the level records and the sort (see below)
+      size_t freeb = 0, totalb = 0;
+      if (hipSetDevice(o.device) == hipSuccess && hipMemGetInfo(&freeb, &totalb) == hipSuccess)
+        so.state_store_bytes = std::min<uint64_t>(96ull << 30, freeb / 4);
+    }
+    if (int rc = ensure_alloc(so, err)) return rc;
+    if (int rc = prepare_prefixes(err)) return rc;
+    sopts_ = o; s_rank_ = rank; s_world_ = world; s_finished_ = false; have_viol_ = false; sres_err_ = 0;
+    // level records / sorted winners / newrec: lvl_cap_ entries each, plus the sort's scratch
+    const u64 sb = so.state_store_bytes;
+    const u64 want = std::max<u64>(4096, (sb / 4) / 16);
+    if (!d_lvl_ || lvl_cap_ != want) {
+      for (void* q : {(void*)d_lvl_, (void*)d_sorted_, (void*)d_newrec_lvl_, (void*)d_sort_tmp_, (void*)d_nsucc_lvl_}) if (q) (void)hipFree(q);
+      lvl_cap_ = want;
+      HIPCHK(hipMalloc(&d_lvl_, lvl_cap_ * 16));
+      HIPCHK(hipMalloc(&d_sorted_, lvl_cap_ * 8));
+      HIPCHK(hipMalloc(&d_newrec_lvl_, lvl_cap_ * 8));
+      HIPCHK(hipMalloc(&d_nsucc_lvl_, cap_ * 2));
+      sort_tmp_bytes_ = 0;
+      HIPCHK(rocprim::radix_sort_keys(nullptr, sort_tmp_bytes_, (const u64*)nullptr, (u64*)nullptr, (size_t)lvl_cap_, 0, 48,
+                                      stream_));
+      HIPCHK(hipMalloc(&d_sort_tmp_, std::max<size_t>(sort_tmp_bytes_, 16)));
+    }
+    HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    sres_ = RunResult();
+    sres_.seed = o.seed ? o.seed : 0x5EED5EED2024ull;
+    sres_.state_bytes = NWP * 4;
+    for (int k = 0; k < MA_NACT; ++k) sres_.action_names.push_back(kMembActNames[k]);
+    sres_.act_generated.assign(MA_NACT, 0); sres_.act_distinct.assign(MA_NACT, 0);
+    sres_.kernels = {{"memb_expand", 0, 0, 0}, {"memb_fingerprint", 0, 0, 0}, {"memb_dedup_sh", 0, 0, 0},
+                     {"memb_select_sh", 0, 0, 0}, {"memb_materialize", 0, 0, 0}};
+    t0_ = std::chrono::steady_clock::now();
+    // Init (raft.tla:388-393): every rank evaluates it; rank 0 stores it, its owner seeds the seen-set
+    W s0; S::init(s0);
+    sres_.generated = 1; sres_.depth = 1;
+    sres_.levels.push_back({1, 0, 0.0});
+    s_level_ = 0; s_level_begin_ = 0; s_level_count_ = 0; total_ = 0;
+    if (!S::in_model(s0, s0, rt_host_)) { sres_.distinct = 0; sres_.depth = 0; s_finished_ = true; finish(sres_, t0_); return 0; }
+    const u64 fp0 = S::fingerprint(s0, sres_.seed, rt_host_);
+    if (fp_owner(fp0, (u32)world) == (u32)rank) {
+      const u64 e2[2] = {fp0, ~0ull};
+      HIPCHK(hipMemcpy(d_table_ + 2 * (fp0 & table_mask_), e2, 16, hipMemcpyHostToDevice));
+    }
+    if (rank == 0) {
+      u32 w0[S::NW]; S::pack(s0, w0);
+      u32 wp[NWP] = {0}; for (int q = 0; q < S::NW; ++q) wp[q] = w0[q];
+      HIPCHK(hipMemcpy(d_states_, wp, NWP * 4, hipMemcpyHostToDevice));
+      const u64 nometa = ~0ull;
+      HIPCHK(hipMemcpy(d_meta_, &nometa, 8, hipMemcpyHostToDevice));
+      total_ = 1; s_level_count_ = 1;
+    }
+    sres_.distinct = 1;
+    if (u32 bad = S::check_invariants(s0, rt_host_)) {
+      if ((bad >> 8) == IV_BAD) { sres_.verdict = MC_VERDICT_INVARIANT_VIOLATION; sres_.violated = kMembInvNames[bad & 255]; }
+      else { sres_.verdict = MC_VERDICT_EVAL_ERROR; sres_.error = std::string("TLC evaluation error in invariant ") + kMembInvNames[bad & 255]; }
+      if (rank == 0) { have_viol_ = true; viol_parent_ = ~0ull; viol_act_ = "<Initial predicate>"; viol_text_ = text_.text(s0, true); }
+      s_finished_ = true; s_level_count_ = 0; finish(sres_, t0_);
+    }
+    return 0;
   }
-  int shard_record_bytes(int) const override { return -1; }
-  int shard_frontier(int64_t*, int64_t*) const override { return MC_E_STATE; }
-  int shard_generate(int64_t, int64_t, int64_t*, std::string&) override { return MC_E_STATE; }
-  int shard_fill(int, void*, const int64_t*, std::string&) override { return MC_E_STATE; }
-  int shard_dedup(const void*, const int64_t*, int64_t*, std::string&) override { return MC_E_STATE; }
-  int shard_materialize(const void*, const int64_t*, std::string&) override { return MC_E_STATE; }
-  int shard_store(const void*, int64_t, std::string&) override { return MC_E_STATE; }
-  int shard_level_stats(int64_t*, std::string&) override { return MC_E_STATE; }
-  int shard_level_commit(const int64_t*, int*, std::string&) override { return MC_E_STATE; }
-  int shard_read_state(uint64_t, std::string&, uint64_t*, std::string&) const override { return MC_E_STATE; }
-  int shard_violation(uint64_t*, std::string&, std::string&) const override { return MC_E_STATE; }
-  const RunResult* shard_result() const override { return nullptr; }
+  int shard_record_bytes(int what) const override {
+    return what == MC_SHARD_ROUTE ? 16 : what == MC_SHARD_REPLY ? 8 : what == MC_SHARD_STATES ? NWP * 4 + 8 : -1;
+  }
+  int shard_frontier(int64_t* states, int64_t* chunk) const override {
+    if (states) *states = s_finished_ ? 0 : (int64_t)s_level_count_;
+    if (chunk) *chunk = (int64_t)chunk_;
+    return 0;
+  }
+  // start of a level: every rank's frontier size (global ranks = concatenation in rank order)
+  int shard_layout(const int64_t* counts, std::string& err) override {
+    u64 acc = 0;
+    for (int q = 0; q < 8; ++q) {
+      if (q < s_world_) { if (q == s_rank_) s_B_ = acc; ks_[q] = acc * (u64)S::NSLOT; acc += (u64)counts[q]; }
+      else ks_[q] = ~0ull;
+    }
+    s_F_ = acc;
+    if (s_F_ * (u64)S::NSLOT >= (1ull << 40)) { err = "level too large for 40-bit FIFO keys"; return MC_E_UNSUPPORTED; }
+    HIPCHK(hipMemsetAsync(d_ctr_, 0, C_NCTR * 8, stream_));
+    HIPCHK(hipMemsetAsync(d_ctr_ + C_EVENT, 0xFF, 8, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    lvl_n_ = 0; n_sorted_ = 0; nnew_ = 0; level_ms_ = 0;
+    return 0;
+  }
+  int shard_generate(int64_t begin, int64_t count, int64_t* counts, std::string& err) override {
+    for (int q = 0; q < s_world_; ++q) counts[q] = 0;
+    gen_cnt_ = (u64)std::max<int64_t>(0, count);
+    gen_begin_ = (u64)begin;
+    if (!gen_cnt_) return 0;
+    const u64 cnt = gen_cnt_, nslots = cnt * (u64)S::NSLOT;
+    const u32 nblk = (u32)((cnt + BS - 1) / BS);
+    MGenArgs g;
+    g.states = d_states_; g.chunk_begin = s_level_begin_ + gen_begin_; g.chunk_count = cnt; g.rank0 = s_B_ + gen_begin_;
+    g.cand = d_cand_; g.cells = d_cells_; g.cells_oom = d_cells_oom_; g.cell_count = d_cell_count_; g.nsucc = d_nsucc_;
+    g.seed = sres_.seed; g.rt = rt_dev_; g.inv_oom = sopts_.inv_out_of_model ? 1u : 0u;
+    g.deadlock = sopts_.check_deadlock ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_;
+    HIPCHK(hipEventRecord(ev_[0], stream_));
+    hipLaunchKernelGGL((memb_expand<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+    HIPCHK(hipGetLastError());
+    if (sopts_.inv_out_of_model) hipLaunchKernelGGL((memb_oom_check<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ev_[1], stream_));
+    hipLaunchKernelGGL((memb_fingerprint<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ev_[2], stream_));
+    HIPCHK(hipMemcpyAsync(d_nsucc_lvl_ + gen_begin_, d_nsucc_, cnt * 2, hipMemcpyDeviceToDevice, stream_));
+    route_.cand = d_cand_; route_.nslots = nslots; route_.chunk_count = cnt; route_.rank0 = s_B_ + gen_begin_;
+    route_.nslot = S::NSLOT; route_.world = (u32)s_world_; route_.counts = (unsigned long long*)(d_ctr_ + C_SHARD);
+    route_.out = nullptr;
+    HIPCHK(hipMemsetAsync(d_ctr_ + C_SHARD, 0, 8 * 8, stream_));
+    hipLaunchKernelGGL((memb_route<false>), dim3((unsigned)((nslots + BS * RPER - 1) / (BS * RPER))), dim3(BS), 0, stream_, route_);
+    HIPCHK(hipGetLastError());
+    u64 c[8];
+    HIPCHK(hipMemcpyAsync(c, d_ctr_ + C_SHARD, sizeof c, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    sres_.kernels[0].ms += ms(0, 1); sres_.kernels[0].launches++;
+    sres_.kernels[1].ms += ms(1, 2); sres_.kernels[1].launches++;
+    level_ms_ += ms(0, 2);
+    for (int q = 0; q < s_world_; ++q) counts[q] = (int64_t)c[q];
+    return 0;
+  }
+  int shard_fill(int what, void* dst, const int64_t* offsets, std::string& err) override {
+    if (what == MC_SHARD_ROUTE) {
+      if (!gen_cnt_) return 0;
+      u64 cur[8] = {0};
+      for (int q = 0; q < s_world_; ++q) cur[q] = (u64)offsets[q];
+      HIPCHK(hipMemcpyAsync(d_ctr_ + C_SHARD, cur, sizeof cur, hipMemcpyHostToDevice, stream_));
+      route_.out = (u64*)dst;
+      hipLaunchKernelGGL((memb_route<true>), dim3((unsigned)((route_.nslots + BS * RPER - 1) / (BS * RPER))), dim3(BS), 0, stream_, route_);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(stream_));
+      return 0;
+    }
+    if (what == MC_SHARD_REPLY) {
+      if (!lvl_n_) return 0;
+      u64 cur[8] = {0};
+      for (int q = 0; q < s_world_; ++q) cur[q] = (u64)offsets[q];
+      HIPCHK(hipMemcpyAsync(d_ctr_ + C_SHARD, cur, sizeof cur, hipMemcpyHostToDevice, stream_));
+      sel_.out = (u64*)dst;
+      hipLaunchKernelGGL((memb_select_sh<true>), dim3((unsigned)((lvl_n_ + BS * RPER - 1) / (BS * RPER))), dim3(BS), 0, stream_, sel_);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(stream_));
+      return 0;
+    }
+    if (what == MC_SHARD_STATES) {   // this rank's new states, in key order (one contiguous run)
+      if (!nnew_) return 0;
+      hipLaunchKernelGGL((memb_pack_states<NWP>), dim3((unsigned)((nnew_ + BS - 1) / BS)), dim3(BS), 0, stream_,
+                         (const u32*)d_states_, (const u64*)d_meta_, total_, nnew_, (u32*)dst);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(stream_));
+      return 0;
+    }
+    err = "unknown record kind";
+    return MC_E_INVALID;
+  }
+  int shard_dedup(const void* recv, const int64_t* counts, int64_t* reply_counts, std::string& err) override {
+    u64 n = 0;
+    for (int q = 0; q < s_world_; ++q) { n += (u64)counts[q]; reply_counts[q] = 0; }   // winners are decided per level
+    if (!n) return 0;
+    if (lvl_n_ + n > lvl_cap_) { sres_err_ |= MERR_STORE; return 0; }
+    MDedupShArgs d;
+    d.recv = (const u64*)recv; d.n = n; d.level = s_level_ + 1; d.table = d_table_; d.table_mask = table_mask_;
+    d.lvl = d_lvl_ + 2 * lvl_n_; d.ctr = (unsigned long long*)d_ctr_;
+    HIPCHK(hipEventRecord(ev_[3], stream_));
+    hipLaunchKernelGGL(memb_dedup_sh, dim3((unsigned)((n + BS * DPER - 1) / (BS * DPER))), dim3(BS), 0, stream_, d);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ev_[4], stream_));
+    HIPCHK(hipEventSynchronize(ev_[4]));
+    sres_.kernels[2].ms += ms(3, 4); sres_.kernels[2].launches++; sres_.kernels[2].algo_bytes += (double)n * 48;
+    level_ms_ += ms(3, 4);
+    lvl_n_ += n;
+    return 0;
+  }
+  // owner side, after the level's last chunk: winning keys per generating rank
+  int shard_select(int64_t* reply_counts, std::string& err) override {
+    for (int q = 0; q < s_world_; ++q) reply_counts[q] = 0;
+    if (!lvl_n_) return 0;
+    sel_.lvl = d_lvl_; sel_.n = lvl_n_; sel_.level = s_level_ + 1; sel_.table = d_table_;
+    for (int q = 0; q < 8; ++q) sel_.kstart[q] = ks_[q];
+    sel_.world = (u32)s_world_; sel_.counts = (unsigned long long*)(d_ctr_ + C_SHARD); sel_.out = nullptr;
+    HIPCHK(hipMemsetAsync(d_ctr_ + C_SHARD, 0, 8 * 8, stream_));
+    HIPCHK(hipEventRecord(ev_[3], stream_));
+    hipLaunchKernelGGL((memb_select_sh<false>), dim3((unsigned)((lvl_n_ + BS * RPER - 1) / (BS * RPER))), dim3(BS), 0, stream_, sel_);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ev_[4], stream_));
+    u64 c[8];
+    HIPCHK(hipMemcpyAsync(c, d_ctr_ + C_SHARD, sizeof c, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    sres_.kernels[3].ms += ms(3, 4); sres_.kernels[3].launches++; sres_.kernels[3].algo_bytes += (double)lvl_n_ * 24;
+    level_ms_ += ms(3, 4);
+    for (int q = 0; q < s_world_; ++q) reply_counts[q] = (int64_t)c[q];
+    return 0;
+  }
+  // generating side: sort the winning keys, re-derive them in key order at the store's end
+  int shard_materialize(const void* acks, const int64_t* counts, std::string& err) override {
+    u64 n = 0;
+    for (int q = 0; q < s_world_; ++q) n += (u64)counts[q];
+    n_sorted_ = n; nnew_ = 0;
+    if (!n) return 0;
+    if (n > lvl_cap_) { sres_err_ |= MERR_STORE; n_sorted_ = 0; return 0; }
+    if (total_ + n > cap_) { sres_err_ |= MERR_STORE; n_sorted_ = 0; return 0; }
+    size_t tb = sort_tmp_bytes_;
+    HIPCHK(hipEventRecord(ev_[5], stream_));
+    HIPCHK(rocprim::radix_sort_keys(d_sort_tmp_, tb, (const u64*)acks, d_sorted_, (size_t)n, 0, 48, stream_));
+    hipLaunchKernelGGL(memb_keys_to_newrec, dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, (const u64*)d_sorted_, n,
+                       (u64)S::NSLOT, s_B_, s_level_begin_, d_newrec_lvl_);
+    HIPCHK(hipGetLastError());
+    MMatArgs m;
+    m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_lvl_; m.n_new = n; m.dst_base = total_; m.cap = cap_;
+    m.level_begin = s_level_begin_ - s_B_;   // gid - level_begin = global rank (mod 2^64)
+    m.gid_tag = (u64)s_rank_ << 37; m.rt = rt_dev_; m.ctr = (unsigned long long*)d_ctr_;
+    hipLaunchKernelGGL((memb_materialize<S>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, m);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ev_[6], stream_));
+    HIPCHK(hipEventSynchronize(ev_[6]));
+    sres_.kernels[4].ms += ms(5, 6); sres_.kernels[4].launches++; sres_.kernels[4].algo_bytes += (double)n * (8 + 2 * NWP * 4 + 8);
+    level_ms_ += ms(5, 6);
+    nnew_ = n;
+    return 0;
+  }
+  // the received slice of the next level, appended to the store (replacing the staged new states)
+  int shard_store(const void* states, int64_t n, std::string& err) override {
+    if (total_ + (u64)n > cap_) { err = "state store full (raise state_store_bytes)"; return MC_E_OOM; }
+    if (n > 0) {
+      hipLaunchKernelGGL((memb_unpack_states<NWP>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, (const u32*)states,
+                         (u64)n, total_, d_states_, d_meta_);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(stream_));
+    }
+    s_level_begin_ = total_;
+    s_level_count_ = (u64)n;
+    total_ += (u64)n;
+    nnew_ = 0;
+    return 0;
+  }
+  // stats layout (MC_SHARD_NSTAT): [0] winners materialised here, [1] generated, [2] in-model
+  // generated, [3] error flags, [4] (1 << 62) - first event (0 = none; max-reduced = min event),
+  // [6] frontier, [8..28) per-action generated, [40..60) per-action distinct, [30] / [31] the stop
+  // point's generated / new-state counts and [32] 1 + the violated invariant's id (event_stats)
+  int shard_level_stats(int64_t* st, std::string& err) override {
+    u64 c[C_NCTR];
+    HIPCHK(hipMemcpy(c, d_ctr_, sizeof c, hipMemcpyDeviceToHost));
+    std::memset(st, 0, MC_SHARD_NSTAT * sizeof(int64_t));
+    int64_t gen = 0;
+    for (int k = 0; k < MA_NACT; ++k) { st[8 + k] = (int64_t)c[C_ACT + k]; st[40 + k] = (int64_t)c[C_ACT + MA_NACT + k]; gen += (int64_t)c[C_ACT + k]; }
+    st[0] = (int64_t)nnew_; st[1] = gen; st[2] = (int64_t)c[C_GEN_IN];
+    st[3] = (int64_t)(c[C_ERR] | sres_err_);
+    st[4] = c[C_EVENT] == ~0ull ? 0 : (int64_t)((1ull << 62) - c[C_EVENT]);
+    st[6] = (int64_t)s_level_count_;
+    return 0;
+  }
+  // the global first event K: this rank's share of TLC's counters at the stop point; the rank
+  // that generated K records the counterexample head
+  int shard_event_stats(const int64_t* g, int64_t* st, std::string& err) override {
+    std::memset(st, 0, MC_SHARD_NSTAT * sizeof(int64_t));
+    if (!g[4]) return 0;
+    const u64 ev = (1ull << 62) - (u64)g[4], key = ev >> 2;
+    const int kind = (int)(ev & 3);
+    const u64 R = key / S::NSLOT, slot = key % S::NSLOT;
+    // generated: whole successor lists of the parents before R (and R's, unless next() failed)
+    std::vector<unsigned short> ns(s_level_count_);
+    if (s_level_count_) HIPCHK(hipMemcpy(ns.data(), d_nsucc_lvl_, s_level_count_ * 2, hipMemcpyDeviceToHost));
+    int64_t gen = 0;
+    for (u64 q = 0; q < s_level_count_; ++q) {
+      const u64 r = s_B_ + q;
+      if (r < R || (r == R && kind != EV_NEXT_ERROR)) gen += ns[q];
+    }
+    // distinct: this rank's winners with key < K (<= K when the event state itself may be new)
+    std::vector<u64> ks(n_sorted_);
+    if (n_sorted_) HIPCHK(hipMemcpy(ks.data(), d_sorted_, n_sorted_ * 8, hipMemcpyDeviceToHost));
+    int64_t before = 0;
+    for (u64 k : ks) if (k < key || (k == key && kind >= EV_INV_ERROR)) ++before;
+    st[30] = gen; st[31] = before;
+    if (R >= s_B_ && R < s_B_ + s_level_count_) {   // the event's parent is ours: the counterexample head
+      const u64 gid = s_level_begin_ + (R - s_B_);
+      W s; read_state(gid, s);
+      u64 meta = 0;
+      HIPCHK(hipMemcpy(&meta, d_meta_ + gid, 8, hipMemcpyDeviceToHost));
+      have_viol_ = true;
+      if (kind == EV_DEADLOCK || kind == EV_NEXT_ERROR) {   // the trace ends at the parent itself
+        viol_parent_ = meta == ~0ull ? ~0ull : (meta >> 20);
+        viol_act_ = meta == ~0ull ? "<Initial predicate>" : kMembActNames[(meta >> 10) & 1023];
+        viol_text_ = text_.text(s, true);
+      } else {
+        int k, sub;
+        S::inst_of_slot((int)slot, k, sub);
+        W t; u32 e2 = 0;
+        const int act = S::apply(s, k, sub, t, e2, rt_host_);
+        viol_parent_ = gid | ((u64)s_rank_ << 37);
+        viol_act_ = act >= 0 ? kMembActNames[act] : "?";
+        viol_text_ = text_.text(t, true);
+        st[32] = 1 + (int64_t)(S::check_invariants(t, rt_host_) & 255);   // the invariant's id, for every rank
+      }
+    }
+    return 0;
+  }
+  int shard_level_commit(const int64_t* g, int* done, std::string& err) override {
+    *done = 0;
+    if (s_finished_) { *done = 1; return 0; }
+    sres_.seconds_kernels += level_ms_ / 1000.0;
+    sres_.n_launches += 1;
+    if (g[4]) {   // the level's first event in key order stops the search (single-GPU handle_event)
+      const u64 ev = (1ull << 62) - (u64)g[4], key = ev >> 2;
+      const int kind = (int)(ev & 3);
+      const u64 R = key / S::NSLOT;
+      sres_.generated += g[30];
+      sres_.distinct += g[31];
+      if (kind == EV_DEADLOCK) sres_.verdict = MC_VERDICT_DEADLOCK;
+      else if (kind == EV_NEXT_ERROR) {
+        sres_.verdict = MC_VERDICT_EVAL_ERROR;
+        sres_.error = "TLC evaluation error while computing the successors of a state (SubSeq index out of domain, raft.tla:551/764)";
+      } else if (kind == EV_INV_ERROR) {
+        sres_.verdict = MC_VERDICT_EVAL_ERROR;
+        sres_.error = std::string("TLC evaluation error while checking invariant ") + (g[32] ? kMembInvNames[g[32] - 1] : "?") +
+                      " (Committed(i) = SubSeq(log[i], 1, commitIndex[i]) or log[l][idx] outside its domain)";
+      } else {
+        sres_.verdict = MC_VERDICT_INVARIANT_VIOLATION;
+        sres_.violated = g[32] ? kMembInvNames[g[32] - 1] : "?";
+        sres_.depth = (int64_t)s_level_ + 2;
+        sres_.left_on_queue = (int64_t)(s_F_ - R - 1) + g[31];
+      }
+      s_finished_ = true; *done = 1;
+      finish(sres_, t0_);
+      return 0;
+    }
+    if (g[3]) {
+      sres_.verdict = MC_VERDICT_CAPACITY_OVERFLOW;
+      std::ostringstream os; os << "error flags 0x" << std::hex << g[3] << " raised on some rank"; sres_.error = os.str();
+      s_finished_ = true; *done = 1;
+      finish(sres_, t0_);
+      return 0;
+    }
+    sres_.generated += g[1];
+    sres_.generated_in_model += g[2];
+    for (int k = 0; k < MA_NACT; ++k) { sres_.act_generated[k] += g[8 + k]; sres_.act_distinct[k] += g[40 + k]; }
+    sres_.levels.back().generated = g[1];
+    sres_.levels.back().kernel_ms = level_ms_;
+    sres_.distinct += g[0];
+    if (g[0] > 0) { sres_.levels.push_back({g[0], 0, 0.0}); sres_.depth += 1; }
+    ++s_level_;
+    if (g[0] == 0) *done = 1;
+    else if (sopts_.max_depth && sres_.depth >= sopts_.max_depth) { sres_.verdict = MC_VERDICT_DEPTH_LIMIT; sres_.left_on_queue = g[0]; *done = 1; }
+    if (*done) {   // the last level stays where it was generated (no rebalance follows)
+      total_ += nnew_; nnew_ = 0;
+      s_finished_ = true; finish(sres_, t0_);
+    }
+    return 0;
+  }
+  int shard_read_state(uint64_t gid, std::string& text, uint64_t* meta, std::string& err) const override {
+    const u64 local = gid & ((1ull << 37) - 1);
+    if (local >= total_) { err = "state id out of range"; return MC_E_INVALID; }
+    W s; read_state(local, s);
+    u64 m = 0;
+    if (hipMemcpy(&m, d_meta_ + local, 8, hipMemcpyDeviceToHost) != hipSuccess) { err = "hipMemcpy failed"; return MC_E_NO_DEVICE; }
+    text = text_.text(s, true);
+    // normalised as the raft_original records: parent gid << 24 | action << 16
+    if (meta) *meta = m == ~0ull ? ~0ull : ((m >> 20) << 24) | (((m >> 10) & 1023) << 16);
+    return 0;
+  }
+  int shard_violation(uint64_t* parent, std::string& action, std::string& text) const override {
+    if (!have_viol_) return MC_E_STATE;
+    if (parent) *parent = viol_parent_;
+    action = viol_act_; text = viol_text_;
+    return 0;
+  }
+  const RunResult* shard_result() const override { return &sres_; }
 
  private:
   MembModel m_;
@@ -816,6 +1369,23 @@ class MembGpu : public Backend {
   u64 table_mask_ = 0, cap_ = 0, total_ = 0, chunk_ = 0;
   int dev_ = -1; uint64_t req_table_ = 0, req_store_ = 0;
 
+  // sharded mode
+  RunOpts sopts_;
+  RunResult sres_;
+  std::chrono::steady_clock::time_point t0_;
+  int s_rank_ = 0, s_world_ = 1;
+  bool s_finished_ = false, have_viol_ = false;
+  u32 s_level_ = 0;
+  u64 s_level_begin_ = 0, s_level_count_ = 0, s_B_ = 0, s_F_ = 0, ks_[8] = {0};
+  u64 gen_begin_ = 0, gen_cnt_ = 0, lvl_n_ = 0, lvl_cap_ = 0, n_sorted_ = 0, nnew_ = 0, sres_err_ = 0;
+  double level_ms_ = 0;
+  u64* d_lvl_ = nullptr; u64* d_sorted_ = nullptr; u64* d_newrec_lvl_ = nullptr; void* d_sort_tmp_ = nullptr;
+  unsigned short* d_nsucc_lvl_ = nullptr;
+  size_t sort_tmp_bytes_ = 0;
+  MRouteArgs route_{};
+  MSelShArgs sel_{};
+  u64 viol_parent_ = 0; std::string viol_act_, viol_text_;
+
   MembRuntime rt_host_{}, rt_dev_{};
   std::vector<u64> ptab_[2];
   u32 plen_[2] = {0, 0};
@@ -824,6 +1394,8 @@ class MembGpu : public Backend {
 
   void release() {
     for (auto& p : d_ptab_) { if (p) (void)hipFree(p); p = nullptr; }
+    for (void* q : {(void*)d_lvl_, (void*)d_sorted_, (void*)d_newrec_lvl_, (void*)d_sort_tmp_, (void*)d_nsucc_lvl_}) if (q) (void)hipFree(q);
+    d_lvl_ = nullptr; d_sorted_ = nullptr; d_newrec_lvl_ = nullptr; d_sort_tmp_ = nullptr; d_nsucc_lvl_ = nullptr; lvl_cap_ = 0;
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_cand_, (void*)d_newrec_,
                     (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_, (void*)d_cells_oom_, (void*)d_cell_count_})
       if (p) (void)hipFree(p);

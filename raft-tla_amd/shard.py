@@ -12,7 +12,17 @@ Per BFS level and frontier chunk every rank runs (include/raftmc.h mc_shard_*):
   store      the owner appends them to its part of the next level
 
 then one all-reduce of the level counters (sum; max for the error, violation
-and deadlock flags).  All payloads are device tensors moved with
+and deadlock flags).
+
+tlc_membership (VIEW vars) needs TLC's single-worker FIFO first-found order,
+so its driver (fifo_sharded_bfs) decides winners once per level: keys are
+global (global parent rank * slots + slot), the owner keeps the minimum key per
+fingerprint over all chunks, then sends each winning key back to the rank
+that generated it (select + one all-to-all); the generator sorts and
+re-derives its winners in key order, and a rebalancing all-to-all gives every
+rank an equal contiguous slice of the next level.  The result (counts,
+per-action distinct counts, the kept representatives, counterexamples) is the
+single-GPU result.  All payloads are device tensors moved with
 torch.distributed (backend "nccl" = RCCL over xGMI on MI355X); with the "gloo"
 backend they are staged through host memory (used by the CPU tests and to
 run several ranks on one GPU).  Parent pointers carry the owner rank, so a
@@ -51,6 +61,9 @@ class LibShard:
         lib.mc_shard_read_state.argtypes = [P, ctypes.c_uint64, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t),
                                             ctypes.POINTER(ctypes.c_uint64)]
         lib.mc_shard_violation.argtypes = [P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(P), ctypes.POINTER(P)]
+        lib.mc_shard_layout.argtypes = [P, I64P]
+        lib.mc_shard_select.argtypes = [P, I64P]
+        lib.mc_shard_event_stats.argtypes = [P, I64P, I64P]
         self._check(lib.mc_shard_open(self.h, rank, world))
         self.rec_bytes = {w: lib.mc_shard_record_bytes(self.h, w) for w in (ROUTE, REPLY, STATES)}
 
@@ -92,6 +105,20 @@ class LibShard:
 
     def store(self, states, n):
         self._check(self.lib.mc_shard_store(self.h, self._ptr(states), n))
+
+    def layout(self, counts):
+        self._check(self.lib.mc_shard_layout(self.h, self._arr(counts)))
+
+    def select(self):
+        out = self._arr()
+        self._check(self.lib.mc_shard_select(self.h, out))
+        return list(out)
+
+    def event_stats(self, g):
+        a = (ctypes.c_int64 * NSTAT)(*[int(x) for x in g])
+        out = (ctypes.c_int64 * NSTAT)()
+        self._check(self.lib.mc_shard_event_stats(self.h, a, out))
+        return list(out)
 
     def level_stats(self):
         a = (ctypes.c_int64 * NSTAT)()
@@ -164,6 +191,23 @@ class Exchanger:
         t[FLAG_SLICE] = m
         return t.tolist()
 
+    def allreduce_sum(self, st):
+        if self.world == 1:
+            return list(st)
+        dev = "cpu" if self.host_staged else self.device
+        t = torch.tensor(st, dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t.tolist()
+
+    def allgather(self, x):
+        if self.world == 1:
+            return [int(x)]
+        dev = "cpu" if self.host_staged else self.device
+        t = torch.tensor([int(x)], dtype=torch.int64, device=dev)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return [int(o.item()) for o in out]
+
     def allreduce_max(self, x):
         if self.world == 1:
             return x
@@ -221,6 +265,65 @@ def sharded_bfs(shard, ex, rank, device):
     return _trace(shard, ex, rank, world)
 
 
+def _overlap(a0, a1, b0, b1):
+    return max(0, min(a1, b1) - max(a0, b0))
+
+
+def rebalance_counts(news, rank, world):
+    """The level's new states are one key-ordered run per rank (news[g] states at global offset
+    sum(news[:g])); the next level gives rank k the slice [k*D//W, (k+1)*D//W).  Returns
+    (send_counts, recv_counts) of this rank, per peer in rank order."""
+    total = sum(news)
+    off = _offsets(news)
+    tgt = [(k * total // world, (k + 1) * total // world) for k in range(world)]
+    mine = (off[rank], off[rank] + news[rank])
+    send = [_overlap(mine[0], mine[1], t0, t1) for t0, t1 in tgt]
+    recv = [_overlap(off[g], off[g] + news[g], tgt[rank][0], tgt[rank][1]) for g in range(world)]
+    return send, recv
+
+
+def fifo_sharded_bfs(shard, ex, rank, device):
+    """Level loop for FIFO-ranked specs (tlc_membership); returns the trace on a stop."""
+    world = ex.world
+    while True:
+        front, chunk = shard.frontier()
+        counts = ex.allgather(front)
+        shard.layout(counts)
+        nchunks = max((c + chunk - 1) // chunk for c in counts) if chunk else 0
+        for c in range(nchunks):
+            begin = c * chunk
+            count = max(0, min(chunk, front - begin))
+            send_counts = shard.generate(min(begin, front), count)
+            recv_counts = ex.counts(send_counts)
+            rb = shard.rec_bytes[ROUTE]
+            send = torch.empty(sum(send_counts) * rb, dtype=torch.uint8, device=device)
+            shard.fill(ROUTE, send, _offsets(send_counts))
+            recv = ex.payload(send, send_counts, recv_counts, rb)
+            shard.dedup(recv, recv_counts)
+        reply_counts = shard.select()                              # winners generated by rank r go to r
+        ack_counts = ex.counts(reply_counts)
+        rb = shard.rec_bytes[REPLY]
+        send = torch.empty(sum(reply_counts) * rb, dtype=torch.uint8, device=device)
+        shard.fill(REPLY, send, _offsets(reply_counts))
+        acks = ex.payload(send, reply_counts, ack_counts, rb)
+        shard.materialize(acks, ack_counts)
+        st = shard.level_stats()
+        news = ex.allgather(st[0])
+        g = ex.allreduce_stats(st)
+        if g[4]:                                                   # the level's first event stops the search
+            e = ex.allreduce_sum(shard.event_stats(g))
+            g[30], g[31], g[32] = e[30], e[31], e[32]
+        if shard.level_commit(g):
+            break
+        send_counts, recv_counts = rebalance_counts(news, rank, world)
+        rb = shard.rec_bytes[STATES]
+        send = torch.empty(sum(send_counts) * rb, dtype=torch.uint8, device=device)
+        shard.fill(STATES, send, _offsets(send_counts))
+        states = ex.payload(send, send_counts, recv_counts, rb)
+        shard.store(states, sum(recv_counts))
+    return _trace(shard, ex, rank, world)
+
+
 def _trace(shard, ex, rank, world):
     v = shard.violation()
     # the lowest rank that recorded a violation reports it
@@ -232,6 +335,8 @@ def _trace(shard, ex, rank, world):
     if head is None:
         return None
     parent, act, text = head
+    if parent == (1 << 64) - 1:                  # the stop is at the initial state itself
+        return [("<Initial predicate>", text)]
     trace = [(act, text)]
     gid = parent
     for _ in range(1 << 20):
@@ -259,15 +364,18 @@ class ShardedChecker:
     """One rank of a sharded model-checking job; run() may be called repeatedly
     (device buffers are kept, the seen-set is re-zeroed by mc_shard_open)."""
 
-    def __init__(self, spec, config, rank, world, device_index=0, group=None, **kw):
+    def __init__(self, spec, config, rank, world, device_index=0, group=None, history_prefixes=None, **kw):
         self.rank, self.world = rank, world
         self.device = torch.device("cuda", device_index)
         self.mc = _rm.ModelChecker(spec, config, device=device_index, **kw)
+        for con, text in (history_prefixes or {}).items():   # punctuated-search golden traces
+            self.mc.set_history_prefix(con, text)
         self.ex = Exchanger(world, self.device, group)
 
     def run(self):
         shard = LibShard(self.mc, self.rank, self.world)
-        trace = sharded_bfs(shard, self.ex, self.rank, self.device)
+        fifo = self.mc.describe()["spec"] == "tlc_membership"
+        trace = (fifo_sharded_bfs if fifo else sharded_bfs)(shard, self.ex, self.rank, self.device)
         res = self.mc.summary()
         if trace:
             res.trace_text = trace_text(trace)

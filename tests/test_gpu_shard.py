@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from oracle_util import CONFIGS, GOLDEN, ORIG_MC
+from oracle_util import CONFIGS, GOLDEN, MEMB_MC, ORIG_MC, tla_text
 
 pytestmark = pytest.mark.gpu
 
@@ -83,3 +83,82 @@ def test_sharded_violation_trace():
     assert len(states) == 10                     # same shortest length as the single-GPU / oracle run
     assert states[0].startswith("State 1: <Initial predicate>")
     assert "<BecomeLeader>" in states[-1].split("\n")[0]
+
+
+# ---------------------------------------------------------------- tlc_membership (FIFO-ranked sharding)
+MEMB_FIX = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))
+MSMALL = dict(fp_table_bytes=1 << 26, state_store_bytes=1 << 29, deadlock=False)
+
+
+def _memb_worker(rank, world, port, case, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shard = importlib.import_module("raft-tla_amd.shard")
+    g = MEMB_FIX[case]
+    prefixes = {}
+    if g.get("prefix"):
+        con, fixture = g["prefix"]
+        prefixes[con] = tla_text(json.load(open(os.path.join(GOLDEN, fixture)))["value"])
+    try:
+        sc = shard.ShardedChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), rank, world, device_index=0,
+                                  history_prefixes=prefixes, max_depth=g["max_depth"], **MSMALL)
+        r = sc.run()
+        dump = "%s.rank%d" % (os.environ["RAFTMC_DUMP"], rank)
+        sc.mc.dump_states(dump)
+        sc.close()
+        q.put((rank, r.verdict, r.generated, r.distinct, r.depth, r.left_on_queue, r.actions, r.violated,
+               getattr(r, "trace_text", ""), [lv[0] for lv in r.levels]))
+    except Exception as e:
+        q.put((rank, "ERROR: %r" % e, 0, 0, 0, 0, {}, "", "", []))
+    dist.destroy_process_group()
+
+
+def run_memb_sharded(case, world, tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    os.environ["RAFTMC_DUMP"] = str(tmp_path / "dump")
+    ps = [ctx.Process(target=_memb_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    lines = []
+    for r in range(world):
+        lines += [l.rstrip("\n") for l in open(str(tmp_path / "dump") + ".rank%d" % r)]
+    return out, lines
+
+
+@pytest.mark.parametrize("case,world", [("membership_shipped@14", 2), ("memb_dynamic3@14", 3), ("memb_four@10", 2),
+                                        ("punct_MajorityOfClusterRestarts@30", 2)])
+def test_membership_sharded_equals_fifo_fixture(case, world, tmp_path):
+    """Sharded BFS with FIFO ranking across ranks: identical counts, per-action generated AND
+    distinct counts, level sizes and set of kept states (first-found representatives) as the
+    oracle's single-worker fixture."""
+    import hashlib
+    g = MEMB_FIX[case]
+    out, lines = run_memb_sharded(case, world, tmp_path)
+    for rank, verdict, gen, dist_, depth, left, acts, _, _, levels in out:
+        assert verdict in ("OK", "DEPTH_LIMIT"), verdict
+        assert (gen, dist_, depth, left) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
+        assert acts == g["actions"]
+        assert levels == g["levels"]
+    assert len(lines) == g["distinct"]
+    assert hashlib.sha256("\n".join(sorted(lines)).encode()).hexdigest() == g["states_sha256"]
+
+
+@pytest.mark.parametrize("case,world", [("scen_FirstCommit", 2), ("punct_CommitWhenConcurrentLeaders", 3)])
+def test_membership_sharded_counterexample(case, world, tmp_path):
+    g = MEMB_FIX[case]
+    out, _ = run_memb_sharded(case, world, tmp_path)
+    for rank, verdict, gen, dist_, depth, left, acts, violated, trace, _ in out:
+        assert verdict == "INVARIANT_VIOLATION" and violated == g["violated"], verdict
+        assert (gen, dist_, depth, left) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
+    blocks = out[0][8].strip().split("\n\n")
+    assert len(blocks) == len(g["trace"]) == g["depth"]
+    for k, (blk, ref) in enumerate(zip(blocks, g["trace"])):
+        head, *body = blk.split("\n")
+        assert " ".join(body) == ref["state"], "trace state %d differs" % (k + 1)
+        if k:
+            assert head == "State %d: <%s>" % (k + 1, ref["action"])
