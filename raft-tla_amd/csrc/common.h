@@ -66,21 +66,18 @@ RMC_HD int popc32(u32 x) {
 constexpr u64 P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full, P3 = 0x165667B19E3779F9ull,
               P4 = 0x85EBCA77C2B2AE63ull, P5 = 0x27D4EB2F165667C5ull;
 RMC_HD u64 rotl64(u64 x, int r) { return (x << r) | (x >> (64 - r)); }
+RMC_HD u64 fmix64(u64 h) { h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32; return h; }
 template <int NW32>
 RMC_HD u64 fp64(const u32 (&w)[NW32], u64 seed) {
-  u64 h = seed + P5 + (u64)NW32 * 4;
+  // per 64-bit word a bijective mix keyed by its position, summed, then a final mix: equal
+  // fingerprints need equal words or a 2^-64 coincidence of mixes
+  u64 acc = 0;
 #pragma unroll
-  for (int k = 0; k + 1 < NW32; k += 2) {
-    u64 v = (u64)w[k] | ((u64)w[k + 1] << 32);
-    u64 acc = rotl64(v * P2, 31) * P1;
-    h ^= acc;
-    h = rotl64(h, 27) * P1 + P4;
+  for (int k = 0; k < NW32; k += 2) {
+    const u64 v = (u64)w[k] | (k + 1 < NW32 ? (u64)w[k + 1] << 32 : 0ull);
+    acc += fmix64(v ^ (seed + (u64)(k / 2 + 1) * P1));
   }
-  if (NW32 & 1) {
-    h ^= (u64)w[NW32 - 1] * P1;
-    h = rotl64(h, 23) * P2 + P3;
-  }
-  h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+  const u64 h = fmix64(acc ^ seed ^ ((u64)NW32 * P4));
   return h ? h : 1ull;
 }
 

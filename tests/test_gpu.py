@@ -74,7 +74,8 @@ def test_seed_independence_c1(raftmc):
 def test_c2_full_size_properties(raftmc):
     """BASELINE configs[1] at full size: order-independent counts (no VIEW in
     raft_original) must not depend on the fingerprint seed or on re-use of
-    the handle; the level sizes sum to the distinct count."""
+    the handle, and must equal the exact (collision-free) host count; the level
+    sizes sum to the distinct count."""
     cfg = os.path.join(CONFIGS, "c2.cfg")
     with raftmc.ModelChecker(ORIG_MC, cfg, seed=7) as mc:
         a = mc.run()
@@ -82,6 +83,11 @@ def test_c2_full_size_properties(raftmc):
     c = raftmc.check(ORIG_MC, cfg, seed=0x1234567)
     assert a.verdict == "OK", a.error
     assert (a.generated, a.distinct, a.depth) == (b.generated, b.distinct, b.depth) == (c.generated, c.distinct, c.depth)
+    # the exact state space (host BFS over full packed states, tests/golden/make_c2_exact.py): a
+    # fingerprint collision would show here as missing states, whatever the seed
+    exact = json.load(open(os.path.join(GOLDEN, "c2_exact.json")))
+    assert (a.generated, a.distinct, a.depth) == (exact["generated"], exact["distinct"], exact["depth"])
+    assert {k: v[0] for k, v in a.actions.items()} == exact["actions_generated"]
     assert sum(lv[0] for lv in a.levels) == a.distinct
     assert sum(v[1] for v in a.actions.values()) + 1 == a.distinct
     assert sum(v[0] for v in a.actions.values()) + 1 == a.generated
