@@ -1269,41 +1269,49 @@ struct Memb {
     }
     return acc;
   }
-  // Permutation-invariant signature of server i (partition refinement): its own scalars, vote
-  // counts and self-relations, the multiset of its nextIndex/matchIndex row, its log with config
-  // values reduced to (cardinality, self-membership), and the multiset of (class, term, count,
-  // role) of the messages it sends or receives.  sig(pi(s), pi(i)) = sig(s, i) for every pi.
-  RMC_HD static u64 server_sig(const Work& t, int i, u32 cfgt) {
-    const int vo = g_voted(t, i);
-    const u32 vr = g_vr(t, i), vg = g_vg(t, i);
-    const u64 w = (u64)g_term(t, i) | (u64)g_st(t, i) << 3 | (u64)g_commit(t, i) << 5 | (u64)(vo == N) << 8 | (u64)(vo == i) << 9 |
-                  (u64)popc32(vr) << 10 | (u64)popc32(vg) << 13 | (u64)((vr >> i) & 1u) << 16 | (u64)((vg >> i) & 1u) << 17 |
-                  (u64)g_next(t, i, i) << 18 | (u64)g_match(t, i, i) << 21;
-    u64 rows = 0;
+  // Permutation-invariant signature of every server (sig_i(pi(t)) = sig_pi(i)(t)): its own fields,
+  // its nextIndex/matchIndex rows as a multiset, its log with config values reduced to
+  // (cardinality, membership of i), and the multiset of the messages it sends / receives.  The
+  // bag is walked once; each message is credited to its destination and its source.
+  RMC_HD static void server_sigs(const Work& t, u32 cfgt, u64 (&sig)[N]) {
+    u64 ms[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j)
-      if (j != i) rows += fmix((u64)g_next(t, i, j) | (u64)g_match(t, i, j) << 3 | 0x5151ull << 8);
-    const LogV l = getlog(t, i);
-    u64 lh = (u64)llen(l);
-#pragma unroll
-    for (int p = 0; p < MAXLOG; ++p) {
-      if (p >= llen(l)) continue;
-      u32 e = lent(l, p);
-      if (etype(e) == cfgt) { const u32 m = r2m(evalue(e)); e = (e & ~(u32)lomask(VW)) | (u32)popc32(m) << 1 | ((m >> i) & 1u); }
-      lh = lh * P1 + (u64)e + 1;
-    }
-    u64 ms = 0;
+    for (int i = 0; i < N; ++i) ms[i] = 0;
 #pragma unroll 1
     for (int q = 0; q < MK; ++q) {
       const u64 e = sel(t.bag, q);
       if (e == EMPTY) break;
       const u64 c = mcode(e), dp = mdesc_packed(mcls(c));
       const int d = (int)fld(c, (int)(dp & 127), SB), sr = (int)fld(c, (int)((dp >> 7) & 127), SB);
-      if (d == i || sr == i)
-        ms += fmix((u64)mcls(c) | (u64)fld(c, (int)((dp >> 14) & 127), TB) << 3 | (u64)mcount(e) << 6 | (u64)(d == i) << 13 |
-                   (u64)(sr == i) << 14 | (u64)(d == sr) << 15 | 0xA5ull << 16);
+      const u64 base = (u64)mcls(c) | (u64)fld(c, (int)((dp >> 14) & 127), TB) << 3 | (u64)mcount(e) << 6 | 0xA5ull << 16;
+      const bool self = d == sr;
+      const u64 hd = fmix(base | 1ull << 13 | (self ? (1ull << 14 | 1ull << 15) : 0ull));   // the destination's view
+      const u64 hs = self ? 0ull : fmix(base | 1ull << 14);                                 // the source's view
+#pragma unroll
+      for (int i = 0; i < N; ++i) ms[i] += (d == i ? hd : 0ull) + (sr == i ? hs : 0ull);
     }
-    return fmix(w ^ fmix(rows ^ 0x9E37ull) ^ rotl64(fmix(lh), 17) ^ rotl64(ms, 31));
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int vo = g_voted(t, i);
+      const u32 vr = g_vr(t, i), vg = g_vg(t, i);
+      const u64 w = (u64)g_term(t, i) | (u64)g_st(t, i) << 3 | (u64)g_commit(t, i) << 5 | (u64)(vo == N) << 8 | (u64)(vo == i) << 9 |
+                    (u64)popc32(vr) << 10 | (u64)popc32(vg) << 13 | (u64)((vr >> i) & 1u) << 16 | (u64)((vg >> i) & 1u) << 17 |
+                    (u64)g_next(t, i, i) << 18 | (u64)g_match(t, i, i) << 21;
+      u64 rows = 0;
+#pragma unroll
+      for (int j = 0; j < N; ++j)
+        if (j != i) rows += fmix((u64)g_next(t, i, j) | (u64)g_match(t, i, j) << 3 | 0x5151ull << 8);
+      const LogV l = getlog(t, i);
+      u64 lh = (u64)llen(l);
+#pragma unroll
+      for (int p = 0; p < MAXLOG; ++p) {
+        if (p >= llen(l)) continue;
+        u32 en = lent(l, p);
+        if (etype(en) == cfgt) { const u32 m = r2m(evalue(en)); en = (en & ~(u32)lomask(VW)) | (u32)popc32(m) << 1 | ((m >> i) & 1u); }
+        lh = lh * P1 + (u64)en + 1;
+      }
+      sig[i] = fmix(w ^ fmix(rows ^ 0x9E37ull) ^ rotl64(fmix(lh), 17) ^ rotl64(ms[i], 31));
+    }
   }
   // FP64 of raftmc for this spec.  With SYMMETRY: min over the permutations that respect the
   // order of the server signatures (ties permuted among themselves).  For pi(s) in the orbit of
@@ -1320,15 +1328,22 @@ struct Memb {
       best = acc[0];
     } else {
       u64 sig[N];
-#pragma unroll
-      for (int i = 0; i < N; ++i) sig[i] = server_sig(t, i, rt.cfg_type);
-      u32 lo = 0, hi = 0;                                              // packed 3-bit bounds per server
+      server_sigs(t, rt.cfg_type, sig);
+      u32 lo = 0, hi = 0, rank_pi = 0;                                 // packed 3-bit bounds per server
+      bool distinct = true;
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         u32 l = 0, e = 0;
 #pragma unroll
         for (int j = 0; j < N; ++j) { l += sig[j] < sig[i]; e += sig[j] == sig[i]; }
         lo |= l << (3 * i); hi |= (l + e) << (3 * i);
+        rank_pi |= l << (2 * i);
+        distinct &= e == 1;
+      }
+      if (distinct) {   // the one signature-respecting permutation: every server to its rank
+        best = ce ? view_hash1<true>(t, rank_pi, seed, rt.cfg_type) : view_hash1<false>(t, rank_pi, seed, rt.cfg_type);
+        const u64 fp = fmix(best ^ seed);
+        return fp ? fp : 1ull;
       }
       auto valid = [&](u32 pi) {
         bool ok = true;
