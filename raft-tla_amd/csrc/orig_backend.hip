@@ -5,16 +5,18 @@
 //
 //  1. orig_generate  (compute): one lane per frontier state, a wave-uniform
 //     loop over the Next relation's action instances (every lane of a wave
-//     runs the same action code on a different state); constraint filter, TLC
-//     generated counts, out-of-model invariants (TLC semantics, [ext]
+//     runs the same action code on a different state); constraint filter,
+//     TLC generated counts, out-of-model invariants (TLC semantics, [ext]
 //     switch), canonical pack and FP64 of each in-model successor into the
-//     instance-major slot array cand[k][s] (0 = none): coalesced, no atomics.
-//  2. orig_dedup     (HBM random access): each thread takes 16 slots, issues
-//     their 16 independent seen-set loads together, then the atomicCAS
-//     inserts of the empty ones together (lock-free open addressing over u64
-//     fingerprints, linear probing); the new slots of a 4096-slot tile are
-//     compacted with one global atomic per tile into (parent, instance)
-//     records.
+//     slot array cand[block][instance][lane] (0 = none): coalesced, no atomics.
+//  2. orig_dedup_blk (HBM random access): workgroup b takes generate
+//     workgroup b's 256 parents, one per thread: coalesced slot loads, a
+//     workgroup-local LDS fingerprint set drops the successors the 256
+//     parents produce more than once (diamonds of commuting actions), the
+//     rest probe the seen-set 16 at a time (lock-free open addressing over u64
+//     fingerprints, linear probing, CAS insert); new states are numbered in
+//     (parent, instance) order with one global atomic per workgroup, so the
+//     next level is parent-major and its diamonds land in one workgroup again.
 //  3. orig_materialize: one lane per new state re-derives it from
 //     (parent, instance), stores the packed state + parent pointer into the
 //     HBM-resident state store and checks the invariants.
@@ -71,7 +73,31 @@ struct GenArgs {
 // pipeline measured 51.4 vs 49.4 ms/run on C2: apply, not the pack + hash, dominates this
 // spec, so the split does not pay here.  Unrolling the ~50-instance loop is refused by the
 // compiler at this body size.)
-template <class S>
+// PM (single-GPU pipeline): slots laid out per workgroup, cand[(block * NI + instance) * BS +
+// lane] (coalesced stores), consumed by orig_dedup_blk one parent per thread, so the next level
+// comes out parent-major (siblings adjacent) and the dedup workgroup can drop the successors its
+// 256 parents produce more than once before they cost a seen-set probe.
+//
+// Workgroup-local fingerprint set (LDS): answers only "certainly produced here before"; when
+// its probe window is full the successor goes to the global seen-set as usual.  A lane's
+// "produced before" answer is only ever about an fp it reads back equal, so races (plain loads
+// and stores, no atomics) can cost a probe but never lose a state.
+constexpr int LDS_FP_SLOTS = 4096;   // 32 KB per workgroup
+RMC_HD inline bool lds_first(unsigned long long* set, u64 fp) {
+  // plain LDS loads and stores, no atomics: a race between two lanes can only make the set
+  // forget an entry or let a duplicate through to the seen-set, never drop a new state
+  u32 h = (u32)(fp >> 20) & (LDS_FP_SLOTS - 1);
+#pragma unroll 1
+  for (int p = 0; p < 8; ++p) {
+    const unsigned long long cur = set[h];
+    if (cur == fp) return false;            // produced here before
+    if (cur == 0ull) { set[h] = fp; return true; }
+    h = (h + 1) & (LDS_FP_SLOTS - 1);
+  }
+  return true;                              // window full: let the seen-set decide
+}
+
+template <class S, bool PM>
 __global__ void __launch_bounds__(BS) orig_generate(GenArgs a) {
   using W = typename S::Work;
   constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
@@ -120,7 +146,7 @@ __global__ void __launch_bounds__(BS) orig_generate(GenArgs a) {
           }
         }
       }
-      a.cand[(u64)k * a.chunk_count + tid] = fp;
+      a.cand[PM ? ((u64)blockIdx.x * S::NI + (u64)k) * BS + threadIdx.x : (u64)k * a.chunk_count + tid] = fp;
     }
   }
   if (active && nsucc == 0) atomicCAS(&a.ctr[K_DEADLOCK], 0ull, (unsigned long long)(gid + 1));
@@ -138,54 +164,65 @@ __global__ void __launch_bounds__(BS) orig_generate(GenArgs a) {
 
 struct DedupArgs {
   const u64* cand;
-  u64 nslots, chunk_begin, chunk_count;
+  u64 nslots, chunk_begin, chunk_count, ni;   // ni: instances per state (parent-major slot layout)
   u64* table;
   u64 table_mask;
   u64* newrec;                 // (parent gid << 8 | instance), compacted
   unsigned long long* ctr;
 };
 
-__global__ void __launch_bounds__(BS) orig_dedup(DedupArgs a) {
+// Seen-set insertion for the PM layout: workgroup b takes generate-workgroup b's slots, one
+// parent per thread; its NI slot loads are coalesced across the wave, its probes go out in
+// groups of 16, and its new states are numbered in (parent, instance) order by a workgroup scan
+// and one global atomic, so the next level is parent-major.
+template <int NI>
+__global__ void __launch_bounds__(BS) orig_dedup_blk(DedupArgs a) {
+  static_assert(NI <= 64, "new-state bits are one u64 per parent");
   __shared__ unsigned int wave_tot[BS / 64];
   __shared__ unsigned long long base_sh;
-  const u64 tile = (u64)blockIdx.x * (BS * DEDUP_PER);
+  __shared__ unsigned long long lds_fp[LDS_FP_SLOTS];
+  for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lds_fp[t] = 0ull;
+  __syncthreads();
   const int lane = __lane_id(), wave = threadIdx.x >> 6;
-  u64 fp[DEDUP_PER], cur[DEDUP_PER];
-  // 1. slot loads (coalesced), then all seen-set loads back to back
+  const u64 st = (u64)blockIdx.x * BS + threadIdx.x;
+  const u64* row = a.cand + (u64)blockIdx.x * NI * BS + threadIdx.x;
+  u64 isnew = 0;
+  u32 err = 0;
+  constexpr int G = 16;
+#pragma unroll 1
+  for (int k0 = 0; k0 < NI; k0 += G) {
+    u64 fp[G], cur[G];
 #pragma unroll
-  for (int j = 0; j < DEDUP_PER; ++j) {
-    const u64 idx = tile + (u64)j * BS + threadIdx.x;
-    fp[j] = idx < a.nslots ? a.cand[idx] : 0ull;
-  }
+    for (int j = 0; j < G; ++j) fp[j] = (st < a.chunk_count && k0 + j < NI) ? row[(u64)(k0 + j) * BS] : 0ull;
 #pragma unroll
-  for (int j = 0; j < DEDUP_PER; ++j) cur[j] = fp[j] ? a.table[fp[j] & a.table_mask] : ~0ull;
-  // 2. CAS the empty home slots together
+    for (int j = 0; j < G; ++j)   // diamonds of commuting actions: ~half of C2's successors within 256 parents
+      if (fp[j] && !lds_first(lds_fp, fp[j])) fp[j] = 0;
 #pragma unroll
-  for (int j = 0; j < DEDUP_PER; ++j)
-    if (fp[j] && cur[j] == 0ull)
-      cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[fp[j] & a.table_mask], 0ull, (unsigned long long)fp[j]);
-  // 3. resolve; a home slot owned by another fingerprint continues linear probing
-  u32 isnew = 0, err = 0;
+    for (int j = 0; j < G; ++j) cur[j] = fp[j] ? a.table[fp[j] & a.table_mask] : ~0ull;
 #pragma unroll
-  for (int j = 0; j < DEDUP_PER; ++j) {
-    if (!fp[j]) continue;
-    if (cur[j] == 0ull) { isnew |= 1u << j; continue; }       // our CAS won on an empty home slot
-    if (cur[j] == fp[j]) continue;                            // seen (or lost the CAS race to an equal fp)
-    u64 slot = (fp[j] + 1) & a.table_mask;
-    for (int probe = 0;; ++probe) {
-      if (probe >= (1 << 20)) { err |= OE_TABLE_FULL; break; }
-      const u64 c = a.table[slot];
-      if (c == fp[j]) break;
-      if (c == 0ull) {
-        const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[slot], 0ull, (unsigned long long)fp[j]);
-        if (old == 0ull) { isnew |= 1u << j; break; }
-        if (old == fp[j]) break;
+    for (int j = 0; j < G; ++j)
+      if (fp[j] && cur[j] == 0ull)
+        cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[fp[j] & a.table_mask], 0ull, (unsigned long long)fp[j]);
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      if (!fp[j]) continue;
+      if (cur[j] == 0ull) { isnew |= 1ull << (k0 + j); continue; }
+      if (cur[j] == fp[j]) continue;
+      u64 slot = (fp[j] + 1) & a.table_mask;
+      for (int probe = 0;; ++probe) {
+        if (probe >= (1 << 20)) { err |= OE_TABLE_FULL; break; }
+        const u64 c = a.table[slot];
+        if (c == fp[j]) break;
+        if (c == 0ull) {
+          const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[slot], 0ull, (unsigned long long)fp[j]);
+          if (old == 0ull) { isnew |= 1ull << (k0 + j); break; }
+          if (old == fp[j]) break;
+        }
+        slot = (slot + 1) & a.table_mask;
       }
-      slot = (slot + 1) & a.table_mask;
     }
   }
-  // 4. tile compaction: wave prefix sums, one global atomic per tile
-  const unsigned int mine = (unsigned int)__popc(isnew);
+  const unsigned int mine = (unsigned int)__popcll(isnew);
   unsigned int incl = mine;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) { const unsigned int v = __shfl_up(incl, d); if (lane >= d) incl += v; }
@@ -198,11 +235,10 @@ __global__ void __launch_bounds__(BS) orig_dedup(DedupArgs a) {
   }
   __syncthreads();
   u64 pos = base_sh + wave_tot[wave] + (incl - mine);
-  for (int j = 0; j < DEDUP_PER; ++j) {
-    if (!((isnew >> j) & 1u)) continue;
-    const u64 idx = tile + (u64)j * BS + threadIdx.x;
-    const u64 k = idx / a.chunk_count, st = idx - k * a.chunk_count;
-    a.newrec[pos++] = ((a.chunk_begin + st) << 8) | k;
+  while (isnew) {
+    const int k = __ffsll((unsigned long long)isnew) - 1;
+    isnew &= isnew - 1;
+    a.newrec[pos++] = ((a.chunk_begin + st) << 8) | (u64)k;
   }
   if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
 }
@@ -511,6 +547,7 @@ class OrigGpu : public Backend {
     // sharded mode also needs world route regions of 16-B records per slot
     chunk_states_ = std::max<u64>(4096, std::min<u64>(cap_, (sb / 8) / (16 * (u64)S::NI)));
     if (world > 1) chunk_states_ = std::max<u64>(4096, chunk_states_ / (u64)world);
+    chunk_states_ = (chunk_states_ / BS) * BS;   // whole workgroups: the PM slot layout is [block][instance][lane]
     table_mask_ = slots - 1;
     HIPCHK(hipMalloc(&d_table_, slots * 8));
     HIPCHK(hipMalloc(&d_states_, cap_ * NWP * 4));
@@ -529,10 +566,11 @@ class OrigGpu : public Backend {
     return 0;
   }
 
-  int run_generate(GenArgs& g, u64 cnt, float& ms_g, std::string& err) {
+  int run_generate(GenArgs& g, u64 cnt, float& ms_g, std::string& err, bool pm = false) {
     const unsigned nblk = (unsigned)((cnt + BS - 1) / BS);
     HIPCHK(hipEventRecord(ev_[5], stream_));
-    hipLaunchKernelGGL((orig_generate<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+    if (pm) hipLaunchKernelGGL((orig_generate<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
+    else hipLaunchKernelGGL((orig_generate<S, false>), dim3(nblk), dim3(BS), 0, stream_, g);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev_[6], stream_));
     HIPCHK(hipEventSynchronize(ev_[6]));
@@ -551,7 +589,7 @@ class OrigGpu : public Backend {
     r.state_bytes = NWP * 4;
     for (int k = 0; k < OA_NACT; ++k) r.action_names.push_back(kOrigActNames[k]);
     r.act_generated.assign(OA_NACT, 0); r.act_distinct.assign(OA_NACT, 0);
-    r.kernels = {{"orig_generate", 0, 0, 0}, {"orig_dedup", 0, 0, 0}, {"orig_materialize", 0, 0, 0}};
+    r.kernels = {{"orig_generate", 0, 0, 0}, {"orig_dedup_blk", 0, 0, 0}, {"orig_materialize", 0, 0, 0}};
 
     // ---- Init (raft_original.tla:139-159): one state, generated and distinct
     W s0; S::init(s0);
@@ -590,9 +628,10 @@ class OrigGpu : public Backend {
         d.cand = d_cand_; d.nslots = nslots; d.chunk_begin = cb; d.chunk_count = cnt; d.table = d_table_;
         d.table_mask = table_mask_; d.newrec = d_newrec_; d.ctr = (unsigned long long*)d_ctr_;
         float ms_x = 0;
-        if (int rc = run_generate(g, cnt, ms_x, err)) return rc;
+        if (int rc = run_generate(g, cnt, ms_x, err, true)) return rc;
         HIPCHK(hipEventRecord(ev_[1], stream_));
-        hipLaunchKernelGGL(orig_dedup, dim3((unsigned)((nslots + BS * DEDUP_PER - 1) / (BS * DEDUP_PER))), dim3(BS), 0, stream_, d);
+        d.ni = S::NI;
+        hipLaunchKernelGGL((orig_dedup_blk<S::NI>), dim3((unsigned)((cnt + BS - 1) / BS)), dim3(BS), 0, stream_, d);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ev_[2], stream_));
         u64 nnew = 0;
