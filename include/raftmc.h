@@ -130,6 +130,12 @@ int mc_kernel_stats(const mc_ctx* ctx, int32_t k, const char** name, double* ms,
 /* Counterexample (TLC "State k:" blocks) as text; caller frees with mc_free. */
 int mc_trace(const mc_ctx* ctx, char** text, size_t* len);
 
+/* TLC's second collision estimate, "based on the actual fingerprints": 1 / (minimum distance
+ * between two fingerprints of the seen-set) after a single-GPU mc_run (a sort of the seen-set on
+ * the device, outside mc_run's time).  Also fills mc_summary_t.collision_prob_observed and the
+ * report's estimate line. */
+int mc_collision_observed(mc_ctx* ctx, double* val);
+
 /* Full TLC-style report (summary + trace) as text; caller frees with mc_free. */
 int mc_report(const mc_ctx* ctx, char** text, size_t* len);
 

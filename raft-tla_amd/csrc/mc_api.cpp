@@ -201,15 +201,34 @@ int mc_report(const mc_ctx* c, char** text, size_t* len) {
     o << "Error: " << r.error << "\n";
   } else if (r.verdict == MC_VERDICT_OK) {
     o << "Model checking completed. No error has been found.\n";
+    o << "  Estimates of the probability that TLC did not check all reachable states\n";
+    o << "  because two distinct states had the same fingerprint:\n";
     char buf[160];
-    std::snprintf(buf, sizeof buf, "  The probability of a fingerprint collision is calculated (optimistic): val = %.1E\n", r.collision_optimistic);
+    std::snprintf(buf, sizeof buf, "  calculated (optimistic):  val = %.1E\n", r.collision_optimistic);
     o << buf;
+    if (r.collision_observed >= 0) {
+      std::snprintf(buf, sizeof buf, "  based on the actual fingerprints:  val = %.1E\n", r.collision_observed);
+      o << buf;
+    }
   }
   o << r.generated << " states generated, " << r.distinct << " distinct states found, " << r.left_on_queue << " states left on queue.\n";
   o << "The depth of the complete state graph search is " << r.depth << ".\n";
+  o << "Finished in " << (long long)(r.seconds_total * 1000.0 + 0.5) << "ms\n";
   o << "Verdict: " << verdict_name(r.verdict) << "\n";
   *text = dup_text(o.str(), len);
   return *text ? MC_OK : MC_E_OOM;
+}
+
+int mc_collision_observed(mc_ctx* c, double* val) {
+  if (!c || !val) return MC_E_INVALID;
+  if (!c->ran) return MC_E_STATE;
+  std::string err;
+  double v = -1;
+  const int rc = c->be->observed_collision(v, err);
+  if (rc) { c->last_error = err; return rc; }
+  c->res.collision_observed = v;
+  *val = v;
+  return MC_OK;
 }
 
 int mc_dump_states(const mc_ctx* c, const char* path) {

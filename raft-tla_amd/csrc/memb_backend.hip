@@ -42,6 +42,7 @@
 
 #include "../../include/raftmc.h"
 #include "backend.h"
+#include "fp_gap.h"
 #include "memb_prefix.h"
 #include "memb_spec.h"
 #include "memb_text.h"
@@ -429,7 +430,7 @@ struct MRouteArgs {
   unsigned long long* counts;  // [world]: count pass totals / write pass cursors
   u64* out;                    // write pass: (fp, key) records, per-owner segments
 };
-RMC_HD inline u32 fp_owner(u64 fp, u32 world) { return (u32)((fp >> 32) % world); }
+RMC_HD u32 fp_owner(u64 fp, u32 world) { return (u32)((fp >> 32) % world); }
 
 // per-owner bucketing in two passes (count, then write at reserved cursors); one global atomic
 // per (workgroup, owner)
@@ -668,6 +669,11 @@ class MembGpu : public Backend {
 
   std::string family() const override { return "tlc_membership"; }
 
+  int observed_collision(double& v, std::string& err) override {
+    if (!d_table_ || sharded_) { err = "after a single-GPU mc_run only"; return MC_E_STATE; }
+    return fpgap::observed(d_table_, table_mask_ + 1, 2, stream_, v, err);
+  }
+
   std::string describe_json() const override {
     std::ostringstream o;
     o << "{\"spec\": \"tlc_membership\", \"N\": " << S::N << ", \"NV\": " << S::NV << ", \"MK\": " << S::MK
@@ -732,6 +738,7 @@ class MembGpu : public Backend {
   float ms(int a, int b) { float x = 0; (void)hipEventElapsedTime(&x, ev_[a], ev_[b]); return x; }
 
   int run(const RunOpts& o, RunResult& r, std::string& err) override {
+    sharded_ = false;
     for (int q = 0; q < 2; ++q)
       if (((m_.rt.constraints >> kPrefixCon[q]) & 1u) && !have_prefix_[q]) {
         err = std::string(kMembConNames[kPrefixCon[q]]) + " needs its golden history trace: place the reference's "
@@ -997,7 +1004,7 @@ class MembGpu : public Backend {
     }
     if (int rc = ensure_alloc(so, err)) return rc;
     if (int rc = prepare_prefixes(err)) return rc;
-    sopts_ = o; s_rank_ = rank; s_world_ = world; s_finished_ = false; have_viol_ = false; sres_err_ = 0;
+    sopts_ = o; s_rank_ = rank; s_world_ = world; s_finished_ = false; have_viol_ = false; sres_err_ = 0; sharded_ = true;
     // level records / sorted winners / newrec: lvl_cap_ entries each, plus the sort's scratch
     const u64 sb = so.state_store_bytes;
     const u64 want = std::max<u64>(4096, (sb / 4) / 16);
@@ -1374,7 +1381,7 @@ class MembGpu : public Backend {
   RunResult sres_;
   std::chrono::steady_clock::time_point t0_;
   int s_rank_ = 0, s_world_ = 1;
-  bool s_finished_ = false, have_viol_ = false;
+  bool s_finished_ = false, have_viol_ = false, sharded_ = false;
   u32 s_level_ = 0;
   u64 s_level_begin_ = 0, s_level_count_ = 0, s_B_ = 0, s_F_ = 0, ks_[8] = {0};
   u64 gen_begin_ = 0, gen_cnt_ = 0, lvl_n_ = 0, lvl_cap_ = 0, n_sorted_ = 0, nnew_ = 0, sres_err_ = 0;

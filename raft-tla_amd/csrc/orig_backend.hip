@@ -36,6 +36,7 @@
 
 #include "../../include/raftmc.h"
 #include "backend.h"
+#include "fp_gap.h"
 #include "orig_spec.h"
 #include "orig_text.h"
 
@@ -83,7 +84,7 @@ struct GenArgs {
 // "produced before" answer is only ever about an fp it reads back equal, so races (plain loads
 // and stores, no atomics) can cost a probe but never lose a state.
 constexpr int LDS_FP_SLOTS = 4096;   // 32 KB per workgroup
-RMC_HD inline bool lds_first(unsigned long long* set, u64 fp) {
+RMC_HD bool lds_first(unsigned long long* set, u64 fp) {
   // plain LDS loads and stores, no atomics: a race between two lanes can only make the set
   // forget an entry or let a duplicate through to the seen-set, never drop a new state
   u32 h = (u32)(fp >> 20) & (LDS_FP_SLOTS - 1);
@@ -509,6 +510,11 @@ class OrigGpu : public Backend {
   ~OrigGpu() override { release(); }
 
   std::string family() const override { return "raft_original"; }
+
+  int observed_collision(double& v, std::string& err) override {
+    if (!d_table_ || alloc_world_ != 0) { err = "after a single-GPU mc_run only"; return MC_E_STATE; }
+    return fpgap::observed(d_table_, table_mask_ + 1, 1, stream_, v, err);
+  }
 
   std::string describe_json() const override {
     std::ostringstream o;

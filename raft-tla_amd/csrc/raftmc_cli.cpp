@@ -41,6 +41,11 @@ int main(int argc, char** argv) {
   int rc = mc_open(tla.c_str(), cfg.c_str(), &o, &c);
   if (rc) { std::fprintf(stderr, "raftmc: %s (code %d)\n", c ? mc_last_error(c) : "open failed", rc); mc_close(c); return 75; }
   rc = mc_run(c);
+  if (rc == 0) {   // TLC prints its fingerprint-based estimate after a completed search
+    mc_summary_t s;
+    double v = 0;
+    if (mc_summary(c, &s) == 0 && s.verdict == MC_VERDICT_OK) (void)mc_collision_observed(c, &v);
+  }
   if (rc) { std::fprintf(stderr, "raftmc: %s (code %d)\n", mc_last_error(c), rc); mc_close(c); return 75; }
   char* text = nullptr; size_t len = 0;
   mc_report(c, &text, &len);

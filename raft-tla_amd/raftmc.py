@@ -27,7 +27,8 @@ EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stat
            "mc_close", "mc_last_error", "mc_shard_open", "mc_shard_record_bytes", "mc_shard_frontier",
            "mc_shard_generate", "mc_shard_fill", "mc_shard_dedup", "mc_shard_materialize", "mc_shard_store",
            "mc_shard_level_stats", "mc_shard_level_commit", "mc_shard_read_state", "mc_shard_violation",
-           "mc_set_history_prefix", "mc_shard_layout", "mc_shard_select", "mc_shard_event_stats"]
+           "mc_set_history_prefix", "mc_shard_layout", "mc_shard_select", "mc_shard_event_stats",
+           "mc_collision_observed"]
 
 
 class McOpts(ctypes.Structure):
@@ -80,6 +81,7 @@ def load_library(path=LIB_PATH):
         getattr(lib, f).argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.mc_dump_states.argtypes = [P, ctypes.c_char_p]
     lib.mc_set_history_prefix.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p]
+    lib.mc_collision_observed.argtypes = [P, ctypes.POINTER(ctypes.c_double)]
     lib.mc_exit_code.argtypes = [P]
     lib.mc_free.argtypes = [P]
     lib.mc_close.argtypes = [P]
@@ -137,6 +139,14 @@ class ModelChecker:
         if rc:
             raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
 
+    def collision_observed(self):
+        """TLC's "based on the actual fingerprints" estimate (1 / min fingerprint gap); GPU sort."""
+        v = ctypes.c_double()
+        rc = self.lib.mc_collision_observed(self.h, ctypes.byref(v))
+        if rc:
+            raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
+        return v.value
+
     def describe(self):
         import json
         return json.loads(self._text(self.lib.mc_describe))
@@ -172,6 +182,7 @@ class ModelChecker:
                       left_on_queue=s.left_on_queue, depth=s.depth, violated=s.violated.decode(),
                       spec=s.spec.decode(), actions=actions, levels=levels,
                       collision_prob_optimistic=s.collision_prob_optimistic,
+                      collision_prob_observed=s.collision_prob_observed,
                       seconds=s.seconds_total, kernel_seconds=s.seconds_kernels, fp_seed=s.fp_seed,
                       algo_bytes=s.algo_bytes, generated_in_model=s.generated_in_model,
                       state_bytes=s.state_bytes, n_launches=s.n_launches,

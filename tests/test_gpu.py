@@ -10,7 +10,7 @@ import tempfile
 
 import pytest
 
-from oracle_util import CONFIGS, GOLDEN, ORIG_MC
+from oracle_util import CONFIGS, GOLDEN, MEMB_MC, ORIG_MC
 
 pytestmark = pytest.mark.gpu
 
@@ -93,3 +93,23 @@ def test_c2_full_size_properties(raftmc):
     assert sum(v[0] for v in a.actions.values()) + 1 == a.generated
     # TLC's "calculated (optimistic)" collision estimate: M * (N - M) / 2^64
     assert a.collision_prob_optimistic == pytest.approx(a.distinct * (a.generated - a.distinct) / 2.0 ** 64)
+
+
+def test_collision_estimates_and_tlc_summary_lines(raftmc):
+    """TLC's two collision estimates: the optimistic M*(N-M)/2^64 and the one "based on the
+    actual fingerprints" (1 / minimum distance between two fingerprints of the seen-set, from a
+    device sort after the run); the report carries TLC's summary lines."""
+    with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c2.cfg")) as mc:
+        r = mc.run()
+        v = mc.collision_observed()
+        r2 = mc.summary()
+    # 54.4M uniform 64-bit fingerprints: expected minimum gap ~ 2^64 / M^2 (~6e3)
+    assert 1e-7 < v < 1e-1
+    assert r2.collision_prob_observed == v
+    assert "Model checking completed. No error has been found." in r2.report
+    assert "calculated (optimistic):  val = " in r2.report and "based on the actual fingerprints:  val = " in r2.report
+    assert "%d states generated, %d distinct states found, 0 states left on queue." % (r.generated, r.distinct) in r2.report
+    assert "The depth of the complete state graph search is %d." % r.depth in r2.report
+    with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, "memb_two.cfg"), max_depth=14, deadlock=False) as mc:
+        mc.run()
+        assert 0 < mc.collision_observed() < 1
