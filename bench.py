@@ -19,7 +19,10 @@ The JSON line adds:
   roofline      dominant kernel (orig_generate): algorithmic bytes F*S + G_in*8 +
                 D*(16+S) / summed HIP-event kernel time,
                 against the 8 TB/s HBM peak; traffic from rocprofv3 PMC passes
-                when --traffic-json points at their summary (else null)
+                when --traffic-json points at their summary (else null); the
+                dominant kernel is integer-VALU bound, so valu_issue_frac = its
+                PMC VALU wave-instructions per launch (--valu-json) / (live
+                launch time x 256 CUs x 2.4 GHz) is reported beside it
   cpu_baseline  the CPU oracle (oracle/, test infrastructure: "port") on a
                 bounded sample of the same model (first --cpu-states distinct
                 states of its BFS), single thread
@@ -63,6 +66,7 @@ def main():
     ap.add_argument("--cpu-states", type=int, default=400000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_r01.json"))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,6 +151,16 @@ def main():
             "kernels": {k: {"ms": v["ms"], "launches": v["launches"],
                             "algo_GBps": v["algo_bytes"] / max(v["ms"], 1e-9) / 1e6} for k, v in res.kernels.items()},
         }
+        # the dominant kernel is integer-VALU bound: its VALU issue fraction (PMC instruction count per
+        # launch from profiles/, live launch time) next to the HBM roofline
+        if os.path.exists(args.valu_json):
+            try:
+                vj = json.load(open(args.valu_json))
+                if vj.get("kernel_name") == kname:
+                    avg_s = kst["ms"] / max(1, kst["launches"]) / 1e3
+                    line["roofline"]["valu_issue_frac"] = vj["valu_insts_per_launch"] / (avg_s * vj["peak_valu_insts_per_s"])
+            except Exception:
+                pass
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_states)
         print(json.dumps(line), flush=True)

@@ -3,6 +3,7 @@
     python scripts/rocpd_summary.py stats  RUN_DB OUT.csv          # per-kernel calls / total / avg (us)
     python scripts/rocpd_summary.py pmc    RUN_DB COUNTER OUT.csv  # per-kernel mean counter value per dispatch
     python scripts/rocpd_summary.py traffic FETCH_DB WRITE_DB KERNEL_SUBSTR OUT.json
+    python scripts/rocpd_summary.py valu   PMC_DB KERNEL_SUBSTR OUT.json   # VALU/SALU wave-instructions per dispatch
 
 `traffic` follows /opt/skills/guides/MI355X_MICROARCH.md (HBM/rocprofv3 section):
 FETCH_SIZE and WRITE_SIZE come from separate --pmc passes, both in KiB per
@@ -61,6 +62,18 @@ def main():
                          "--warmup 0`; KiB*1024 averaged over the kernel's dispatches; FETCH_SIZE doubled per "
                          "MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B), WRITE_SIZE as is"}
         json.dump(doc, open(sys.argv[5], "w"), indent=1)
+        print(json.dumps(doc, indent=1))
+    elif mode == "valu":
+        valu = {r[0]: r for r in pmc(sys.argv[2], "SQ_INSTS_VALU")}
+        salu = {r[0]: r for r in pmc(sys.argv[2], "SQ_INSTS_SALU")}
+        name = next(k for k in valu if sys.argv[3] in k)
+        doc = {"kernel_name": sys.argv[3], "kernel_symbol": name, "dispatches": valu[name][1],
+               "valu_insts_per_launch": valu[name][2], "salu_insts_per_launch": salu[name][2] if name in salu else None,
+               "peak_valu_insts_per_s": 256 * 2.4e9,
+               "method": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU over `bench.py --steps 1 --warmup 0`; wave-instructions "
+                         "per dispatch (a wave64 VALU instruction holds a SIMD16 for 4 cycles: 1 per CU per cycle, 256 CUs "
+                         "at 2.4 GHz peak)"}
+        json.dump(doc, open(sys.argv[4], "w"), indent=1)
         print(json.dumps(doc, indent=1))
 
 
