@@ -315,33 +315,45 @@ struct RouteArgs {
   unsigned long long* rcnt;    // [world]
 };
 
-// bucket the chunk's in-model fingerprints by owner: LDS histogram per 4096-slot
-// tile, one global atomic per (tile, owner)
-__global__ void __launch_bounds__(BS) orig_route(RouteArgs a) {
-  __shared__ unsigned int hist[8], cur[8];
+// Sharded route over the PM slot layout: workgroup b takes generate-workgroup b's 256
+// parents, drops the successors they produce more than once (the LDS set of orig_dedup_blk),
+// and buckets the rest by owner, 16 instances at a time: LDS histogram, one global atomic per
+// (workgroup, group, owner).  Records are (fp, state << 8 | instance).
+template <int NI>
+__global__ void __launch_bounds__(BS) orig_route_blk(RouteArgs a) {
+  static_assert(NI <= 255, "instance in 8 bits");
+  __shared__ unsigned long long lds_fp[LDS_FP_SLOTS];
+  __shared__ unsigned int hist[8];
   __shared__ unsigned long long base[8];
-  if (threadIdx.x < 8) { hist[threadIdx.x] = 0; cur[threadIdx.x] = 0; }
-  __syncthreads();
-  const u64 tile = (u64)blockIdx.x * (BS * DEDUP_PER);
-  u64 fp[DEDUP_PER];
-  int own[DEDUP_PER];
+  for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lds_fp[t] = 0ull;
+  const u64 st = (u64)blockIdx.x * BS + threadIdx.x;
+  const u64* row = a.cand + (u64)blockIdx.x * NI * BS + threadIdx.x;
+  constexpr int G = 16;
+#pragma unroll 1
+  for (int k0 = 0; k0 < NI; k0 += G) {
+    if (threadIdx.x < 8) hist[threadIdx.x] = 0;
+    __syncthreads();   // also orders the set's clearing before its first use
+    u64 fp[G];
+    unsigned int off[G];
+    int own[G];
 #pragma unroll
-  for (int j = 0; j < DEDUP_PER; ++j) {
-    const u64 idx = tile + (u64)j * BS + threadIdx.x;
-    fp[j] = idx < a.nslots ? a.cand[idx] : 0ull;
-    own[j] = fp[j] ? (int)fp_owner(fp[j], a.world) : -1;
-    if (own[j] >= 0) atomicAdd(&hist[own[j]], 1u);
-  }
-  __syncthreads();
-  if (threadIdx.x < a.world) base[threadIdx.x] = hist[threadIdx.x] ? atomicAdd(&a.rcnt[threadIdx.x], (unsigned long long)hist[threadIdx.x]) : 0ull;
-  __syncthreads();
+    for (int j = 0; j < G; ++j) {
+      fp[j] = (st < a.nslots / NI && k0 + j < NI) ? row[(u64)(k0 + j) * BS] : 0ull;
+      if (fp[j] && !lds_first(lds_fp, fp[j])) fp[j] = 0;
+      own[j] = fp[j] ? (int)fp_owner(fp[j], a.world) : -1;
+      off[j] = own[j] >= 0 ? atomicAdd(&hist[own[j]], 1u) : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < a.world) base[threadIdx.x] = hist[threadIdx.x] ? atomicAdd(&a.rcnt[threadIdx.x], (unsigned long long)hist[threadIdx.x]) : 0ull;
+    __syncthreads();
 #pragma unroll
-  for (int j = 0; j < DEDUP_PER; ++j) {
-    if (own[j] < 0) continue;
-    const u64 pos = base[own[j]] + atomicAdd(&cur[own[j]], 1u);
-    u64* r = a.route + ((u64)own[j] * a.route_cap + pos) * 2;
-    r[0] = fp[j];
-    r[1] = tile + (u64)j * BS + threadIdx.x;
+    for (int j = 0; j < G; ++j) {
+      if (own[j] < 0) continue;
+      u64* r = a.route + ((u64)own[j] * a.route_cap + base[own[j]] + off[j]) * 2;
+      r[0] = fp[j];
+      r[1] = (st << 8) | (u64)(k0 + j);
+    }
+    __syncthreads();   // hist / base reused by the next group
   }
 }
 
@@ -434,8 +446,8 @@ __global__ void __launch_bounds__(BS) orig_materialize_sh(MatShArgs a) {
   const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
   u32 err = 0;
   if (i < a.n) {
-    const u64 slot = a.acks[i];
-    const u64 k = slot / a.chunk_count, gid = a.chunk_begin + (slot - k * a.chunk_count);
+    const u64 slot = a.acks[i];   // state in chunk << 8 | instance (orig_route_blk)
+    const u64 k = slot & 255ull, gid = a.chunk_begin + (slot >> 8);
     u32 w[NWP];
     const uint4* src = reinterpret_cast<const uint4*>(a.states + gid * NWP);
 #pragma unroll
@@ -750,7 +762,7 @@ class OrigGpu : public Backend {
     sres_.state_bytes = NWP * 4;
     for (int k = 0; k < OA_NACT; ++k) sres_.action_names.push_back(kOrigActNames[k]);
     sres_.act_generated.assign(OA_NACT, 0); sres_.act_distinct.assign(OA_NACT, 0);
-    sres_.kernels = {{"orig_generate", 0, 0, 0}, {"orig_route", 0, 0, 0}, {"orig_dedup_sh", 0, 0, 0},
+    sres_.kernels = {{"orig_generate", 0, 0, 0}, {"orig_route_blk", 0, 0, 0}, {"orig_dedup_sh", 0, 0, 0},
                      {"orig_materialize_sh", 0, 0, 0}, {"orig_store", 0, 0, 0}};
     st0_ = std::chrono::steady_clock::now();
     // Init: one state, stored and inserted by the owner of its fingerprint
@@ -796,10 +808,10 @@ class OrigGpu : public Backend {
       ra.cand = d_cand_; ra.nslots = nslots; ra.route = d_route_; ra.route_cap = chunk_states_ * S::NI; ra.world = (u32)world_;
       ra.rcnt = (unsigned long long*)d_rcnt_;
       float ms_x = 0;
-      if (int rc = run_generate(g, (u64)count, ms_x, err)) return rc;
+      if (int rc = run_generate(g, (u64)count, ms_x, err, true)) return rc;
       auto& ke = sres_.kernels[0]; ke.ms += ms_x; ke.launches++; ke.algo_bytes += (double)count * NWP * 4 + (double)nslots * 8;
       HIPCHK(hipEventRecord(ev_[1], stream_));
-      hipLaunchKernelGGL(orig_route, dim3((unsigned)((nslots + BS * DEDUP_PER - 1) / (BS * DEDUP_PER))), dim3(BS), 0, stream_, ra);
+      hipLaunchKernelGGL((orig_route_blk<S::NI>), dim3((unsigned)((count + BS - 1) / BS)), dim3(BS), 0, stream_, ra);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(ev_[2], stream_));
     }
