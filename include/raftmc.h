@@ -195,6 +195,20 @@ int mc_shard_violation(const mc_ctx* ctx, uint64_t* parent_gid, char** action, c
  *   rebalance: STATES records of the level's new states (key order, one run per rank) to equal
  *   contiguous slices of the next level, then mc_shard_store.
  * The driver is raft-tla_amd/shard.py (fifo_sharded_bfs). */
+/* Native sharded BFS over RCCL (raft_original).  The same protocol as the caller-driven
+ * mc_shard_* loop above, run entirely inside the library on one HIP stream with grouped
+ * ncclSend/ncclRecv between the kernels' own buffers: two host synchronisations per chunk (the
+ * record counts) and one per level (all-reduce of the level statistics).  Replaces, like the
+ * whole sharded path, TLC's multi-worker BFS (one JVM, shared FPSet).
+ *   mc_rccl_unique_id   rank 0 creates the communicator id (ncclGetUniqueId, 128 B) which
+ *                       the caller broadcasts (torch.distributed in raft-tla_amd/shard.py)
+ *   mc_shard_run_rccl   every rank: shard_open + ncclCommInitRank (cached on the handle for
+ *                       repeated runs with the same id) + the whole level loop; afterwards
+ *                       mc_summary / mc_shard_violation / mc_shard_read_state as usual.
+ * RCCL is dlopen()ed (librccl.so.1) on first use; MC_E_UNSUPPORTED if it cannot be loaded or
+ * the spec has no native loop (tlc_membership uses the FIFO protocol above). */
+int mc_rccl_unique_id(mc_ctx* ctx, void* out, size_t len);
+int mc_shard_run_rccl(mc_ctx* ctx, int32_t rank, int32_t world, const void* unique_id, size_t len);
 int mc_shard_layout(mc_ctx* ctx, const int64_t* frontier_counts);
 int mc_shard_select(mc_ctx* ctx, int64_t* reply_counts);
 int mc_shard_event_stats(mc_ctx* ctx, const int64_t* global_stats, int64_t* stats);

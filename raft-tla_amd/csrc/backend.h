@@ -71,6 +71,8 @@ struct Backend {
   virtual int shard_violation(uint64_t* parent, std::string& action, std::string& text) const = 0;
   virtual const RunResult* shard_result() const = 0;
   // FIFO first-found specs (VIEW): level layout, per-level winner selection, stop-point counters
+  // the whole sharded level loop natively over an RCCL communicator (after shard_open)
+  virtual int shard_run_native(void* comm, std::string& err) { (void)comm; err = "no native sharded loop for this spec"; return -4; }
   virtual int shard_layout(const int64_t* counts, std::string& err) { (void)counts; err = "not a FIFO-ranked spec"; return -4; }
   virtual int shard_select(int64_t* reply_counts, std::string& err) { (void)reply_counts; err = "not a FIFO-ranked spec"; return -4; }
   virtual int shard_event_stats(const int64_t* g, int64_t* st, std::string& err) { (void)g; (void)st; err = "not a FIFO-ranked spec"; return -4; }

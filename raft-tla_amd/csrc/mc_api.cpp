@@ -10,6 +10,7 @@
 #include "../../include/raftmc.h"
 #include "backend.h"
 #include "model.h"
+#include "rccl_api.h"
 
 struct mc_ctx {
   std::unique_ptr<rmc::Backend> be;
@@ -17,6 +18,14 @@ struct mc_ctx {
   rmc::RunResult res;
   bool ran = false;
   std::string last_error, tla_path, cfg_path;
+  // RCCL communicator of the native sharded loop, kept across runs of the same job
+  ncclComm_t comm = nullptr;
+  int comm_rank = -1, comm_world = 0;
+  char comm_id[sizeof(ncclUniqueId)] = {0};
+  ~mc_ctx() {
+    be.reset();
+    if (comm) (void)rmc::rccl().CommDestroy(comm);
+  }
 };
 
 namespace {
@@ -346,6 +355,42 @@ int mc_shard_violation(const mc_ctx* c, uint64_t* parent, char** action, char** 
   if (rc) return rc;
   *action = dup_text(a, nullptr);
   *text = dup_text(t, nullptr);
+  return MC_OK;
+}
+
+int mc_rccl_unique_id(mc_ctx* c, void* out, size_t len) {
+  if (!c || !out || len < sizeof(ncclUniqueId)) return MC_E_INVALID;
+  std::string err;
+  if (rmc::rccl().load(err)) { c->last_error = err; return MC_E_UNSUPPORTED; }
+  ncclUniqueId id;
+  ncclResult_t r = rmc::rccl().GetUniqueId(&id);
+  if (r != ncclSuccess) { c->last_error = std::string("ncclGetUniqueId: ") + rmc::rccl().GetErrorString(r); return MC_E_NO_DEVICE; }
+  std::memcpy(out, &id, sizeof id);
+  return MC_OK;
+}
+int mc_shard_run_rccl(mc_ctx* c, int32_t rank, int32_t world, const void* unique_id, size_t len) {
+  SHARD_GUARD();
+  if (!unique_id || len < sizeof(ncclUniqueId)) return MC_E_INVALID;
+  std::string err;
+  if (rmc::rccl().load(err)) { c->last_error = err; return MC_E_UNSUPPORTED; }
+  c->ran = false;
+  // shard_open selects the device and allocates; the communicator binds to that device
+  int rc = c->be->shard_open(c->ro, rank, world, err);
+  if (rc) { c->last_error = err; return rc; }
+  if (!c->comm || c->comm_rank != rank || c->comm_world != world || std::memcmp(c->comm_id, unique_id, sizeof(ncclUniqueId))) {
+    if (c->comm) { (void)rmc::rccl().CommDestroy(c->comm); c->comm = nullptr; }
+    ncclUniqueId id;
+    std::memcpy(&id, unique_id, sizeof id);
+    ncclResult_t r = rmc::rccl().CommInitRank(&c->comm, world, id, rank);
+    if (r != ncclSuccess) { c->comm = nullptr; c->last_error = std::string("ncclCommInitRank: ") + rmc::rccl().GetErrorString(r); return MC_E_NO_DEVICE; }
+    c->comm_rank = rank; c->comm_world = world;
+    std::memcpy(c->comm_id, unique_id, sizeof(ncclUniqueId));
+  }
+  rc = c->be->shard_run_native(c->comm, err);
+  if (rc) { c->last_error = err; return rc; }
+  c->res = *c->be->shard_result();
+  c->ran = true;
+  c->last_error = c->res.error;
   return MC_OK;
 }
 

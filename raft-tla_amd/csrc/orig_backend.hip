@@ -39,6 +39,7 @@
 #include "fp_gap.h"
 #include "orig_spec.h"
 #include "orig_text.h"
+#include "rccl_api.h"
 
 namespace rmc {
 
@@ -178,7 +179,7 @@ struct DedupArgs {
 // and one global atomic, so the next level is parent-major.
 template <int NI>
 __global__ void __launch_bounds__(BS) orig_dedup_blk(DedupArgs a) {
-  static_assert(NI <= 64, "new-state bits are one u64 per parent");
+  static_assert(NI <= 128, "new-state bits are two u64 per parent");
   __shared__ unsigned int wave_tot[BS / 64];
   __shared__ unsigned long long base_sh;
   __shared__ unsigned long long lds_fp[LDS_FP_SLOTS];
@@ -187,7 +188,8 @@ __global__ void __launch_bounds__(BS) orig_dedup_blk(DedupArgs a) {
   const int lane = __lane_id(), wave = threadIdx.x >> 6;
   const u64 st = (u64)blockIdx.x * BS + threadIdx.x;
   const u64* row = a.cand + (u64)blockIdx.x * NI * BS + threadIdx.x;
-  u64 isnew = 0;
+  u64 isnew = 0, isnew_hi = 0;   // instances 0..63 / 64..127 (the latter only for NI > 64, e.g. N = 5)
+  auto mark = [&](int k) { if (NI <= 64 || k < 64) isnew |= 1ull << (k & 63); else isnew_hi |= 1ull << (k & 63); };
   u32 err = 0;
   constexpr int G = 16;
 #pragma unroll 1
@@ -207,7 +209,7 @@ __global__ void __launch_bounds__(BS) orig_dedup_blk(DedupArgs a) {
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       if (!fp[j]) continue;
-      if (cur[j] == 0ull) { isnew |= 1ull << (k0 + j); continue; }
+      if (cur[j] == 0ull) { mark(k0 + j); continue; }
       if (cur[j] == fp[j]) continue;
       u64 slot = (fp[j] + 1) & a.table_mask;
       for (int probe = 0;; ++probe) {
@@ -216,14 +218,14 @@ __global__ void __launch_bounds__(BS) orig_dedup_blk(DedupArgs a) {
         if (c == fp[j]) break;
         if (c == 0ull) {
           const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[slot], 0ull, (unsigned long long)fp[j]);
-          if (old == 0ull) { isnew |= 1ull << (k0 + j); break; }
+          if (old == 0ull) { mark(k0 + j); break; }
           if (old == fp[j]) break;
         }
         slot = (slot + 1) & a.table_mask;
       }
     }
   }
-  const unsigned int mine = (unsigned int)__popcll(isnew);
+  const unsigned int mine = (unsigned int)(__popcll(isnew) + __popcll(isnew_hi));
   unsigned int incl = mine;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) { const unsigned int v = __shfl_up(incl, d); if (lane >= d) incl += v; }
@@ -239,6 +241,11 @@ __global__ void __launch_bounds__(BS) orig_dedup_blk(DedupArgs a) {
   while (isnew) {
     const int k = __ffsll((unsigned long long)isnew) - 1;
     isnew &= isnew - 1;
+    a.newrec[pos++] = ((a.chunk_begin + st) << 8) | (u64)k;
+  }
+  while (isnew_hi) {
+    const int k = 64 + __ffsll((unsigned long long)isnew_hi) - 1;
+    isnew_hi &= isnew_hi - 1;
     a.newrec[pos++] = ((a.chunk_begin + st) << 8) | (u64)k;
   }
   if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
@@ -980,6 +987,236 @@ class OrigGpu : public Backend {
   }
   const RunResult* shard_result() const override { return &sres_; }
 
+  // ---------------------------------------------------------------- native level loop over RCCL
+  // The whole sharded BFS of raft-tla_amd/shard.py (sharded_bfs) in C++ on one HIP stream:
+  // per chunk generate+route -> counts exchange -> ROUTE payload -> dedup -> counts exchange ->
+  // REPLY payload -> materialize -> STATES payload -> store, with grouped ncclSend/ncclRecv
+  // straight from the kernels' buffers (no staging copies) and two host synchronisations per
+  // chunk (the counts) plus one per level (the all-reduce of the level statistics).
+  int shard_run_native(void* comm_v, std::string& err) override {
+    RcclApi& R = rccl();
+    if (!R.ok) { err = "RCCL not loaded"; return MC_E_STATE; }
+    ncclComm_t comm = (ncclComm_t)comm_v;
+#define NCCLCHK(x)                                                                                   \
+  do {                                                                                               \
+    ncclResult_t r_ = (x);                                                                           \
+    if (r_ != ncclSuccess) { err = std::string(#x) + ": " + R.GetErrorString(r_); return MC_E_NO_DEVICE; } \
+  } while (0)
+    const int W = world_, me = rank_;
+    const u64 SBW = (u64)(NWP + 4) * 4;          // STATES record bytes
+    if (!d_nat_) HIPCHK(hipMalloc(&d_nat_, (32 + 2 * MC_SHARD_NSTAT) * 8));
+    if (!h_nat_) HIPCHK(hipHostMalloc(&h_nat_, (32 + 2 * MC_SHARD_NSTAT) * 8));
+    u64* d_xs = d_nat_;        // [0,8) counts I send  (copied from d_rcnt_)
+    u64* d_xr = d_nat_ + 8;    // [8,16) counts I receive
+    int64_t* d_sum = (int64_t*)(d_nat_ + 32);
+    int64_t* d_max = d_sum + MC_SHARD_NSTAT;
+    u64* h_xs = h_nat_; u64* h_xr = h_nat_ + 8;
+    int64_t* h_sum = (int64_t*)(h_nat_ + 32);
+    int64_t* h_max = h_sum + MC_SHARD_NSTAT;
+    // grow-only device buffer
+    auto grow = [&](void*& p, u64& cap, u64 need) -> int {
+      if (need <= cap) return 0;
+      if (p) { HIPCHK(hipStreamSynchronize(stream_)); HIPCHK(hipFree(p)); p = nullptr; }
+      cap = std::max<u64>(need + need / 4, 1 << 20);
+      HIPCHK(hipMalloc(&p, cap));
+      return 0;
+    };
+    // counts exchange: send[r] from d_send (device), received into d_xr; both land on the host
+    auto xcounts = [&](const u64* d_send) -> int {
+      HIPCHK(hipMemcpyAsync(d_xs, d_send, 8 * (u64)W, hipMemcpyDeviceToDevice, stream_));
+      HIPCHK(hipMemcpyAsync(d_xr + me, d_send + me, 8, hipMemcpyDeviceToDevice, stream_));
+      if (W > 1) {
+        NCCLCHK(R.GroupStart());
+        for (int r = 0; r < W; ++r) {
+          if (r == me) continue;
+          NCCLCHK(R.Send(d_xs + r, 1, ncclUint64, r, comm, stream_));
+          NCCLCHK(R.Recv(d_xr + r, 1, ncclUint64, r, comm, stream_));
+        }
+        NCCLCHK(R.GroupEnd());
+      }
+      HIPCHK(hipMemcpyAsync(h_xs, d_xs, 16 * 8, hipMemcpyDeviceToHost, stream_));
+      HIPCHK(hipStreamSynchronize(stream_));
+      return 0;
+    };
+    // payload exchange: segment r of the send side (bytes) goes to rank r, the receive side is
+    // packed in source-rank order
+    auto xpay = [&](const char* const* src, const u64* sbytes, char* dst, const u64* rbytes) -> int {
+      u64 roff[8]; u64 acc = 0;
+      for (int r = 0; r < W; ++r) { roff[r] = acc; acc += rbytes[r]; }
+      if (sbytes[me] != rbytes[me]) { err = "sharded exchange: self segment size mismatch"; return MC_E_STATE; }
+      if (sbytes[me]) HIPCHK(hipMemcpyAsync(dst + roff[me], src[me], sbytes[me], hipMemcpyDeviceToDevice, stream_));
+      if (W > 1) {
+        NCCLCHK(R.GroupStart());
+        for (int r = 0; r < W; ++r) {
+          if (r == me) continue;
+          if (sbytes[r]) NCCLCHK(R.Send(src[r], sbytes[r], ncclUint8, r, comm, stream_));
+          if (rbytes[r]) NCCLCHK(R.Recv(dst + roff[r], rbytes[r], ncclUint8, r, comm, stream_));
+        }
+        NCCLCHK(R.GroupEnd());
+      }
+      return 0;
+    };
+    // HIP-event timing, read back at the level's synchronisation points
+    std::vector<std::pair<int, int>> pending;   // (kernel index, event pair index)
+    auto ev_pair = [&](int k) -> int {
+      const int i = (int)pending.size();
+      while ((int)nat_ev_.size() < 2 * (i + 1)) { hipEvent_t e; if (hipEventCreate(&e) != hipSuccess) return -1; nat_ev_.push_back(e); }
+      pending.push_back({k, i});
+      return i;
+    };
+    auto harvest = [&]() {
+      for (auto& pr : pending) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, nat_ev_[2 * pr.second], nat_ev_[2 * pr.second + 1]);
+        sres_.kernels[pr.first].ms += ms;
+      }
+      pending.clear();
+    };
+#define NAT_TIMED(k, launch)                                                   \
+  do {                                                                         \
+    const int ep_ = ev_pair(k);                                                \
+    if (ep_ < 0) { err = "hipEventCreate failed"; return MC_E_NO_DEVICE; }     \
+    HIPCHK(hipEventRecord(nat_ev_[2 * ep_], stream_));                         \
+    launch;                                                                    \
+    HIPCHK(hipGetLastError());                                                 \
+    HIPCHK(hipEventRecord(nat_ev_[2 * ep_ + 1], stream_));                     \
+    sres_.kernels[k].launches++;                                               \
+  } while (0)
+    auto allreduce_level = [&](int64_t* g, int64_t next_chunks, int64_t& chunks_out) -> int {
+      // g: local stats in, global stats out; MAX slots: [3,6) flags, [6] chunk rounds of the next level
+      for (int k = 0; k < MC_SHARD_NSTAT; ++k) h_sum[k] = g[k];
+      for (int k = 0; k < MC_SHARD_NSTAT; ++k) h_max[k] = 0;
+      h_max[3] = g[3]; h_max[4] = g[4]; h_max[5] = g[5]; h_max[6] = next_chunks;
+      HIPCHK(hipMemcpyAsync(d_sum, h_sum, 2 * MC_SHARD_NSTAT * 8, hipMemcpyHostToDevice, stream_));
+      if (W > 1) {
+        NCCLCHK(R.GroupStart());
+        NCCLCHK(R.AllReduce(d_sum, d_sum, MC_SHARD_NSTAT, ncclInt64, ncclSum, comm, stream_));
+        NCCLCHK(R.AllReduce(d_max, d_max, 8, ncclInt64, ncclMax, comm, stream_));
+        NCCLCHK(R.GroupEnd());
+      }
+      HIPCHK(hipMemcpyAsync(h_sum, d_sum, 2 * MC_SHARD_NSTAT * 8, hipMemcpyDeviceToHost, stream_));
+      HIPCHK(hipStreamSynchronize(stream_));
+      for (int k = 0; k < MC_SHARD_NSTAT; ++k) g[k] = h_sum[k];
+      g[3] = h_max[3]; g[4] = h_max[4]; g[5] = h_max[5];
+      chunks_out = h_max[6];
+      return 0;
+    };
+
+    const u64 chunk = chunk_states_;
+    auto rounds = [&](u64 n) -> int64_t { return (int64_t)((n + chunk - 1) / chunk); };
+    int64_t nchunks = 0;
+    {   // agree on the first level's chunk rounds (only the owner of Init holds a state)
+      int64_t z[MC_SHARD_NSTAT] = {0};
+      if (int rc = allreduce_level(z, rounds(sh_level_count_), nchunks)) return rc;
+    }
+    const u64 route_cap = chunk_states_ * S::NI;
+    for (;;) {
+      const u64 front = sh_level_count_;
+      for (int64_t c = 0; c < nchunks; ++c) {
+        const u64 begin = std::min<u64>((u64)c * chunk, front);
+        const u64 count = std::min<u64>(chunk, front - begin);
+        sh_chunk_begin_ = sh_level_begin_ + begin; sh_chunk_count_ = count;
+        HIPCHK(hipMemsetAsync(d_rcnt_, 0, 16 * 8, stream_));
+        if (count > 0) {
+          const u64 nslots = count * (u64)S::NI;
+          GenArgs g;
+          g.states = d_states_; g.chunk_begin = sh_chunk_begin_; g.chunk_count = count; g.cand = d_cand_; g.seed = sres_.seed;
+          g.rt = m_.rt; g.inv_oom = sopts_.inv_out_of_model ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_; g.viol = d_viol_;
+          const unsigned nblk = (unsigned)((count + BS - 1) / BS);
+          NAT_TIMED(0, hipLaunchKernelGGL((orig_generate<S, true>), dim3(nblk), dim3(BS), 0, stream_, g));
+          sres_.kernels[0].algo_bytes += (double)count * NWP * 4 + (double)nslots * 8;
+          RouteArgs ra;
+          ra.cand = d_cand_; ra.nslots = nslots; ra.route = d_route_; ra.route_cap = route_cap; ra.world = (u32)W;
+          ra.rcnt = (unsigned long long*)d_rcnt_;
+          NAT_TIMED(1, hipLaunchKernelGGL((orig_route_blk<S::NI>), dim3(nblk), dim3(BS), 0, stream_, ra));
+          sres_.kernels[1].algo_bytes += (double)nslots * 8;
+        }
+        // ---- ROUTE: (fp, slot) records to the fingerprints' owners
+        if (int rc = xcounts(d_rcnt_)) return rc;
+        u64 scnt[8], rcnt[8], sb[8], rb[8], rtot = 0;
+        const char* src[8];
+        for (int r = 0; r < W; ++r) {
+          scnt[r] = h_xs[r]; rcnt[r] = h_xr[r]; rtot += rcnt[r];
+          sb[r] = scnt[r] * 16; rb[r] = rcnt[r] * 16;
+          src[r] = (const char*)(d_route_ + (u64)r * route_cap * 2);
+          sres_.kernels[1].algo_bytes += (double)scnt[r] * 16;
+        }
+        if (rtot > route_cap) { err = "shard: received more ROUTE records than one chunk holds"; return MC_E_STATE; }
+        if (int rc = grow(nat_recv_, nat_recv_cap_, rtot * 16)) return rc;
+        if (int rc = xpay(src, sb, (char*)nat_recv_, rb)) return rc;
+        // ---- owner-side dedup, one launch per source rank
+        {
+          u64 off = 0;
+          for (int r = 0; r < W; ++r) {
+            seg_off_[r] = off;
+            const u64 n = rcnt[r];
+            if (n) {
+              DedupShArgs d;
+              d.recv = (const u64*)nat_recv_ + 2 * off; d.n = n; d.table = d_table_; d.table_mask = table_mask_;
+              d.reply = d_newrec_ + off; d.counter = (unsigned long long*)(d_rcnt_ + 8 + r); d.ctr = (unsigned long long*)d_ctr_;
+              NAT_TIMED(2, hipLaunchKernelGGL(orig_dedup_sh, dim3((unsigned)((n + BS * DEDUP_PER - 1) / (BS * DEDUP_PER))), dim3(BS), 0, stream_, d));
+            }
+            off += n;
+          }
+        }
+        // ---- REPLY: the new ones' slots back to the generating ranks
+        if (int rc = xcounts(d_rcnt_ + 8)) return rc;
+        u64 rep[8], ack[8], atot = 0, ntot = 0;
+        for (int r = 0; r < W; ++r) {
+          rep[r] = h_xs[r]; ack[r] = h_xr[r]; atot += ack[r]; ntot += rep[r];
+          sb[r] = rep[r] * 8; rb[r] = ack[r] * 8;
+          src[r] = (const char*)(d_newrec_ + seg_off_[r]);
+        }
+        sres_.kernels[2].algo_bytes += (double)rtot * 24 + (double)ntot * 16;
+        if (int rc = grow(nat_acks_, nat_acks_cap_, atot * 8)) return rc;
+        if (int rc = xpay(src, sb, (char*)nat_acks_, rb)) return rc;
+        // ---- generator re-derives the acknowledged states
+        {
+          u64 off = 0;
+          for (int r = 0; r < W; ++r) { seg_off_ack_[r] = off; off += ack[r]; }
+          void* so = d_stout_;
+          u64 socap = stout_cap_ * SBW;
+          if (int rc = grow(so, socap, atot * SBW)) return rc;
+          d_stout_ = (u32*)so; stout_cap_ = socap / SBW;
+          for (int r = 0; r < W; ++r) {
+            if (!ack[r]) continue;
+            MatShArgs m;
+            m.states = d_states_; m.acks = (const u64*)nat_acks_ + seg_off_ack_[r]; m.n = ack[r]; m.chunk_begin = sh_chunk_begin_;
+            m.chunk_count = sh_chunk_count_; m.out = d_stout_ + seg_off_ack_[r] * (NWP + 4); m.rank_bits = (u64)me << 37;
+            m.seed = sres_.seed; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.viol = d_viol_;
+            NAT_TIMED(3, hipLaunchKernelGGL((orig_materialize_sh<S>), dim3((unsigned)((ack[r] + BS - 1) / BS)), dim3(BS), 0, stream_, m));
+          }
+          sres_.kernels[3].algo_bytes += (double)atot * (8 + NWP * 4 + SBW);
+        }
+        // ---- STATES: packed states + parent pointers to their owners (sizes known: no sync)
+        for (int r = 0; r < W; ++r) { sb[r] = ack[r] * SBW; rb[r] = rep[r] * SBW; src[r] = (const char*)(d_stout_ + seg_off_ack_[r] * (NWP + 4)); }
+        if (int rc = grow(nat_stin_, nat_stin_cap_, ntot * SBW)) return rc;
+        if (int rc = xpay(src, sb, (char*)nat_stin_, rb)) return rc;
+        if (ntot) {
+          StoreArgs a;
+          a.in = (const u32*)nat_stin_; a.n = ntot; a.dst = sh_next_write_; a.cap = cap_; a.states = d_states_; a.meta = d_meta_;
+          a.ctr = (unsigned long long*)d_ctr_;
+          NAT_TIMED(4, hipLaunchKernelGGL((orig_store<NWP>), dim3((unsigned)((ntot + BS - 1) / BS)), dim3(BS), 0, stream_, a));
+          sres_.kernels[4].algo_bytes += (double)ntot * (SBW + NWP * 4 + 8);
+          sh_next_write_ += ntot; sh_new_ += ntot;
+        }
+      }
+      HIPCHK(hipStreamSynchronize(stream_));
+      harvest();
+      int64_t g[MC_SHARD_NSTAT];
+      if (int rc = shard_level_stats(g, err)) return rc;
+      int64_t next_chunks = 0;
+      if (int rc = allreduce_level(g, rounds(sh_new_), next_chunks)) return rc;
+      int done = 0;
+      if (int rc = shard_level_commit(g, &done, err)) return rc;
+      if (done) break;
+      nchunks = next_chunks;
+    }
+#undef NAT_TIMED
+#undef NCCLCHK
+    return 0;
+  }
+
  private:
   OrigModel m_;
   u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr; void* d_viol_ = nullptr;
@@ -998,11 +1235,23 @@ class OrigGpu : public Backend {
   u64 seg_off_[8] = {0}, seg_off_ack_[8] = {0}, fill_counts_reply_[8] = {0}, fill_counts_states_[8] = {0};
   u64 fill_counts_route_[8] = {0};
   u64 sviol_parent_ = 0; u32 sviol_bad_ = 0; std::string sviol_act_, sviol_text_;
+  // native (RCCL) level loop buffers
+  u64* d_nat_ = nullptr; u64* h_nat_ = nullptr;
+  void* nat_recv_ = nullptr; void* nat_acks_ = nullptr; void* nat_stin_ = nullptr;
+  u64 nat_recv_cap_ = 0, nat_acks_cap_ = 0, nat_stin_cap_ = 0;
+  std::vector<hipEvent_t> nat_ev_;
 
   void release() {
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, d_viol_, (void*)d_cand_, (void*)d_newrec_,
                     (void*)d_route_, (void*)d_rcnt_, (void*)d_stout_})
       if (p) (void)hipFree(p);
+    for (void* p : {(void*)d_nat_, nat_recv_, nat_acks_, nat_stin_})
+      if (p) (void)hipFree(p);
+    if (h_nat_) (void)hipHostFree(h_nat_);
+    d_nat_ = nullptr; h_nat_ = nullptr; nat_recv_ = nat_acks_ = nat_stin_ = nullptr;
+    nat_recv_cap_ = nat_acks_cap_ = nat_stin_cap_ = 0;
+    for (auto& e : nat_ev_) (void)hipEventDestroy(e);
+    nat_ev_.clear();
     for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
     if (stream_) (void)hipStreamDestroy(stream_);
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_viol_ = nullptr;
@@ -1061,7 +1310,8 @@ class OrigGpu : public Backend {
   X(2, 1, 2, 1, 5)          \
   X(2, 1, 2, 1, 6)          \
   X(2, 1, 3, 2, 5)          \
-  X(2, 2, 3, 2, 6)
+  X(2, 2, 3, 2, 6)          \
+  X(5, 1, 3, 3, 4) /* C5 */
 #endif
 
 static Backend* orig_factory(const OrigModel& m) {

@@ -36,6 +36,7 @@ import torch.distributed as dist
 from . import raftmc as _rm
 
 ROUTE, REPLY, STATES = 0, 1, 2
+RCCL_ID_BYTES = 128    # sizeof(ncclUniqueId)
 NSTAT = 72
 FLAG_SLICE = slice(3, 6)   # error flags, violation, deadlock: reduced with MAX
 
@@ -43,7 +44,7 @@ FLAG_SLICE = slice(3, 6)   # error flags, violation, deadlock: reduced with MAX
 class LibShard:
     """ctypes view of the mc_shard_* entry points of one raftmc handle."""
 
-    def __init__(self, checker, rank, world):
+    def __init__(self, checker, rank, world, open_shard=True):
         self.mc, self.lib, self.h = checker, checker.lib, checker.h
         self.world = world
         lib = self.lib
@@ -64,7 +65,10 @@ class LibShard:
         lib.mc_shard_layout.argtypes = [P, I64P]
         lib.mc_shard_select.argtypes = [P, I64P]
         lib.mc_shard_event_stats.argtypes = [P, I64P, I64P]
-        self._check(lib.mc_shard_open(self.h, rank, world))
+        lib.mc_rccl_unique_id.argtypes = [P, P, ctypes.c_size_t]
+        lib.mc_shard_run_rccl.argtypes = [P, ctypes.c_int32, ctypes.c_int32, P, ctypes.c_size_t]
+        if open_shard:
+            self._check(lib.mc_shard_open(self.h, rank, world))
         self.rec_bytes = {w: lib.mc_shard_record_bytes(self.h, w) for w in (ROUTE, REPLY, STATES)}
 
     def _check(self, rc):
@@ -81,6 +85,15 @@ class LibShard:
     @staticmethod
     def _ptr(t):
         return ctypes.c_void_p(t.data_ptr() if t.numel() else 0)
+
+    def rccl_unique_id(self):
+        buf = ctypes.create_string_buffer(RCCL_ID_BYTES)
+        self._check(self.lib.mc_rccl_unique_id(self.h, buf, RCCL_ID_BYTES))
+        return buf.raw
+
+    def run_rccl(self, rank, world, uid):
+        buf = ctypes.create_string_buffer(uid, RCCL_ID_BYTES)
+        self._check(self.lib.mc_shard_run_rccl(self.h, rank, world, buf, RCCL_ID_BYTES))
 
     def frontier(self):
         s, c = ctypes.c_int64(), ctypes.c_int64()
@@ -364,18 +377,40 @@ class ShardedChecker:
     """One rank of a sharded model-checking job; run() may be called repeatedly
     (device buffers are kept, the seen-set is re-zeroed by mc_shard_open)."""
 
-    def __init__(self, spec, config, rank, world, device_index=0, group=None, history_prefixes=None, **kw):
+    def __init__(self, spec, config, rank, world, device_index=0, group=None, history_prefixes=None,
+                 transport="auto", **kw):
+        """transport: "rccl" = the library's native level loop over its own RCCL communicator
+        (mc_shard_run_rccl; raft_original only), "torch" = this module's level loop with
+        torch.distributed collectives, "auto" = rccl for raft_original when the process group's
+        backend is nccl (RCCL), else torch."""
         self.rank, self.world = rank, world
         self.device = torch.device("cuda", device_index)
         self.mc = _rm.ModelChecker(spec, config, device=device_index, **kw)
         for con, text in (history_prefixes or {}).items():   # punctuated-search golden traces
             self.mc.set_history_prefix(con, text)
         self.ex = Exchanger(world, self.device, group)
+        self.fifo = self.mc.describe()["spec"] == "tlc_membership"
+        if transport == "auto":
+            backend = dist.get_backend(group) if dist.is_initialized() else "none"
+            transport = "rccl" if (not self.fifo and backend == "nccl") else "torch"
+        if transport == "rccl" and self.fifo:
+            raise ValueError("the native RCCL loop covers raft_original; tlc_membership needs transport='torch'")
+        self.transport = transport
+        self._uid = None
 
     def run(self):
+        if self.transport == "rccl":
+            shard = LibShard(self.mc, self.rank, self.world, open_shard=False)
+            if self._uid is None:   # one communicator per job, cached by the library across runs
+                self._uid = self.ex.broadcast_obj(shard.rccl_unique_id() if self.rank == 0 else None, 0)
+            shard.run_rccl(self.rank, self.world, self._uid)
+            trace = _trace(shard, self.ex, self.rank, self.world)
+            res = self.mc.summary()
+            if trace:
+                res.trace_text = trace_text(trace)
+            return res
         shard = LibShard(self.mc, self.rank, self.world)
-        fifo = self.mc.describe()["spec"] == "tlc_membership"
-        trace = (fifo_sharded_bfs if fifo else sharded_bfs)(shard, self.ex, self.rank, self.device)
+        trace = (fifo_sharded_bfs if self.fifo else sharded_bfs)(shard, self.ex, self.rank, self.device)
         res = self.mc.summary()
         if trace:
             res.trace_text = trace_text(trace)
@@ -386,6 +421,7 @@ class ShardedChecker:
 
 
 def check_sharded(spec, config, rank, world, device_index=0, group=None, **kw):
+    # kw may carry transport= (see ShardedChecker)
     """Run one sharded BFS on this rank (call on every rank of the group).
 
     Returns the raftmc Result (identical on every rank) with .trace_text

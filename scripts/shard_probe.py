@@ -1,5 +1,7 @@
-"""Time the sharded raft_original pipeline at world 1 (no communication) against the single-GPU
-pipeline on C2: the per-rank cost of the sharded kernels.  A development tool (C ABI only).
+"""Time the sharded raft_original pipeline at world 1 against the single-GPU pipeline on C2: the
+per-rank cost of the sharded kernels, with the Python level loop (torch transport, no
+communication at world 1) and with the library's native RCCL loop (a one-rank communicator:
+self-exchanges are device copies).  A development tool.
 
     python scripts/shard_probe.py [CFG]
 """
@@ -22,6 +24,21 @@ r = sc.run()
 ms = (time.perf_counter() - t0) * 1e3
 sc.close()
 print(json.dumps({"mode": "sharded_w1", "distinct": r.distinct, "generated": r.generated, "ms": ms,
+                  "kernels_ms": {k: round(v["ms"], 2) for k, v in r.kernels.items()}}), flush=True)
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+os.environ.setdefault("MASTER_PORT", "29533")
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+sc = shard.ShardedChecker(tla, cfg, 0, 1, seed=0x5EED, transport="rccl")
+sc.run()
+t0 = time.perf_counter()
+r = sc.run()
+ms = (time.perf_counter() - t0) * 1e3
+sc.close()
+dist.destroy_process_group()
+print(json.dumps({"mode": "sharded_w1_rccl_native", "distinct": r.distinct, "generated": r.generated, "ms": ms,
                   "kernels_ms": {k: round(v["ms"], 2) for k, v in r.kernels.items()}}), flush=True)
 with raftmc.ModelChecker(tla, cfg, seed=0x5EED) as mc:
     mc.run()

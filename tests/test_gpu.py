@@ -95,6 +95,35 @@ def test_c2_full_size_properties(raftmc):
     assert a.collision_prob_optimistic == pytest.approx(a.distinct * (a.generated - a.distinct) / 2.0 ** 64)
 
 
+def test_c5_prefix_parity(raftmc):
+    """BASELINE configs[4] (C5: 5 servers, term <= 3, log <= 3; 87 action instances per
+    state, 96-B packed states) to the oracle's depth limit: identical counts, per-level
+    sizes, per-action generated counts, left-on-queue and the set of states found."""
+    g = json.load(open(os.path.join(GOLDEN, "c5_prefix.json")))
+    with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c5.cfg"), max_depth=g["max_depth"], **SMALL) as mc:
+        r = mc.run()
+        sha, n = states_sha(mc)
+    assert r.verdict == "DEPTH_LIMIT", r.error
+    assert (r.generated, r.distinct, r.depth, r.left_on_queue) == (g["generated"], g["distinct"], g["depth"],
+                                                                   g["left_on_queue"])
+    assert [lv[0] for lv in r.levels] == g["levels"]
+    assert {k: v[0] for k, v in r.actions.items()} == {k: v[0] for k, v in g["actions"].items()}
+    assert n == g["distinct"] and sha == g["states_sha256"]
+
+
+def test_c5_deep_properties(raftmc):
+    """C5 five levels past the oracle's reach (~1e8 distinct states): seed-independent
+    counts, levels summing to the distinct count, TLC's generated bookkeeping."""
+    cfg = os.path.join(CONFIGS, "c5.cfg")
+    a = raftmc.check(ORIG_MC, cfg, max_depth=11, seed=3)
+    b = raftmc.check(ORIG_MC, cfg, max_depth=11, seed=0xC5C5C5)
+    assert a.verdict == b.verdict == "DEPTH_LIMIT", (a.error, b.error)
+    assert (a.generated, a.distinct, a.left_on_queue) == (b.generated, b.distinct, b.left_on_queue)
+    assert [lv[0] for lv in a.levels] == [lv[0] for lv in b.levels]
+    assert sum(lv[0] for lv in a.levels) == a.distinct and a.left_on_queue == a.levels[-1][0]
+    assert sum(v[0] for v in a.actions.values()) + 1 == a.generated
+
+
 def test_collision_estimates_and_tlc_summary_lines(raftmc):
     """TLC's two collision estimates: the optimistic M*(N-M)/2^64 and the one "based on the
     actual fingerprints" (1 / minimum distance between two fingerprints of the seen-set, from a

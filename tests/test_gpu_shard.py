@@ -85,6 +85,51 @@ def test_sharded_violation_trace():
     assert "<BecomeLeader>" in states[-1].split("\n")[0]
 
 
+def _native_worker(port, q):
+    """One rank with the nccl (RCCL) backend: the library's native level loop (mc_shard_run_rccl)
+    over a one-rank communicator; RCCL refuses two ranks on one GPU, so N>1 runs only on a node."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    shard = importlib.import_module("raft-tla_amd.shard")
+    out = {}
+    try:
+        for name, kw in (("parity_pair", SMALL), ("scenario_first_leader", SMALL), ("c2", {})):
+            sc = shard.ShardedChecker(ORIG_MC, os.path.join(CONFIGS, name + ".cfg"), 0, 1, **kw)
+            assert sc.transport == "rccl"
+            runs = [sc.run() for _ in range(2)]      # the second run reuses the cached communicator
+            sc.close()
+            out[name] = [(r.verdict, r.generated, r.distinct, r.depth, {k: v[0] for k, v in r.actions.items()},
+                          r.violated, getattr(r, "trace_text", "")) for r in runs]
+    except Exception as e:
+        out["error"] = repr(e)
+    q.put(out)
+    dist.destroy_process_group()
+
+
+def test_native_rccl_loop_world1():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_native_worker, args=(_port(), q))
+    p.start()
+    out = q.get(timeout=240)
+    p.join(timeout=60)
+    assert "error" not in out, out.get("error")
+    g = json.load(open(os.path.join(GOLDEN, "orig_parity.json")))["parity_pair"]
+    for verdict, gen, dist_, depth, acts, _, _ in out["parity_pair"]:
+        assert (verdict, gen, dist_, depth) == ("OK", g["generated"], g["distinct"], g["depth"])
+        assert acts == {k: v[0] for k, v in g["actions"].items()}
+    exact = json.load(open(os.path.join(GOLDEN, "c2_exact.json")))
+    for verdict, gen, dist_, depth, acts, _, _ in out["c2"]:
+        assert (verdict, gen, dist_, depth) == ("OK", exact["generated"], exact["distinct"], exact["depth"])
+        assert acts == exact["actions_generated"]
+    for verdict, _, _, _, _, violated, trace in out["scenario_first_leader"]:
+        assert verdict == "INVARIANT_VIOLATION" and violated == "NoLeader"
+        states = trace.strip().split("\n\n")
+        assert len(states) == 10 and states[0].startswith("State 1: <Initial predicate>")
+        assert "<BecomeLeader>" in states[-1].split("\n")[0]
+
+
 # ---------------------------------------------------------------- tlc_membership (FIFO-ranked sharding)
 MEMB_FIX = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))
 MSMALL = dict(fp_table_bytes=1 << 26, state_store_bytes=1 << 29, deadlock=False)
