@@ -81,6 +81,37 @@ RMC_HD u64 fp64(const u32 (&w)[NW32], u64 seed) {
   return h ? h : 1ull;
 }
 
+// The same fingerprint, incrementally: fp64 is a sum of per-word terms, so a successor's
+// accumulator is its parent's minus the terms of the words it changed plus their new terms
+// (identical value, mod 2^64).  FpBase holds one parent's terms; successors that change few
+// words skip most of the multiplies.
+template <int NW32>
+struct FpBase {
+  static constexpr int NW64 = (NW32 + 1) / 2;
+  u64 term[NW64];
+  u64 sum;
+  RMC_HD static u64 word(const u32 (&w)[NW32], int k) {
+    return (u64)w[2 * k] | (2 * k + 1 < NW32 ? (u64)w[2 * k + 1] << 32 : 0ull);
+  }
+  RMC_HD static u64 key(u64 seed, int k) { return seed + (u64)(k + 1) * P1; }
+  RMC_HD void init(const u32 (&w)[NW32], u64 seed) {
+    sum = 0;
+#pragma unroll
+    for (int k = 0; k < NW64; ++k) { term[k] = fmix64(word(w, k) ^ key(seed, k)); sum += term[k]; }
+  }
+  // fp64(w, seed) given the parent's words `base` (from which init() was computed)
+  RMC_HD u64 fp(const u32 (&w)[NW32], const u32 (&base)[NW32], u64 seed) const {
+    u64 acc = sum;
+#pragma unroll
+    for (int k = 0; k < NW64; ++k) {
+      const u64 v = word(w, k);
+      if (v != word(base, k)) acc += fmix64(v ^ key(seed, k)) - term[k];
+    }
+    const u64 h = fmix64(acc ^ seed ^ ((u64)NW32 * P4));
+    return h ? h : 1ull;
+  }
+};
+
 // Compile-time bit-stream writer/reader over a u32 word array (offsets are
 // template-constant after unrolling, so every access is a shift/or pair).
 template <int NW32>

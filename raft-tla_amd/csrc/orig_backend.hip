@@ -44,7 +44,7 @@
 namespace rmc {
 
 enum {
-  K_NEW = 0, K_GEN_IN = 1, K_ERR = 2, K_VIOL = 3, K_ERRGID = 4, K_DEADLOCK = 5, K_CHUNK_NEW = 6,
+  K_NEW = 0, K_GEN_IN = 1, K_ERR = 2, K_VIOL = 3, K_ERRGID = 4, K_DEADLOCK = 5, K_CHUNK_NEW = 6, K_LEVEL_NEW = 7,
   K_ACT = 8, K_NCTR = K_ACT + 2 * OA_NACT
 };
 enum { OE_CAP_STORE = 0x100, OE_TABLE_FULL = 0x200 };
@@ -100,7 +100,10 @@ RMC_HD bool lds_first(unsigned long long* set, u64 fp) {
 }
 
 template <class S, bool PM>
-__global__ void __launch_bounds__(BS) orig_generate(GenArgs a) {
+// 3 waves per SIMD (<= 168 VGPRs) measured fastest for C2's expand (19.9 vs 22.3 ms without the
+// hint, 26.6 ms at the 2 waves the incremental fingerprint would otherwise get); larger states
+// (C5: 24 words) would spill at 3 and get no hint.
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 16 ? 3 : 1))) orig_generate(GenArgs a) {
   using W = typename S::Work;
   constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
   __shared__ unsigned int lds_cnt[OA_NACT + 1];
@@ -112,6 +115,13 @@ __global__ void __launch_bounds__(BS) orig_generate(GenArgs a) {
   W s;
   u64 al[S::AW];
   u32 err = 0, nsucc = 0, nin = 0;
+  // the parent's packed words with allLogs' (every successor carries allLogs \cup {log[i]},
+  // raft_original.tla:464) and their fingerprint terms: successors re-hash changed words only
+  // (C5-sized states keep the plain hash: the base terms would cost them occupancy, measured
+  // 45 vs 38 ms of expand time for C5 to depth 12)
+  constexpr bool INC = NW <= 16;
+  u32 bw[INC ? NW : 1];
+  FpBase<INC ? NW : 2> fb;
   if (active) {
     u32 w[NWP];
     const uint4* src = reinterpret_cast<const uint4*>(a.states + gid * NWP);
@@ -123,6 +133,13 @@ __global__ void __launch_bounds__(BS) orig_generate(GenArgs a) {
     S::init(s);
 #pragma unroll
     for (int q = 0; q < S::AW; ++q) al[q] = 0;
+  }
+  if constexpr (INC) {
+    W b = s;
+#pragma unroll
+    for (int q = 0; q < S::AW; ++q) b.allLogs[q] = al[q];
+    S::pack(b, bw);
+    fb.init(bw, a.seed);
   }
 #pragma unroll 1
   for (int k = 0; k < S::NI; ++k) {
@@ -139,7 +156,8 @@ __global__ void __launch_bounds__(BS) orig_generate(GenArgs a) {
           ++nin;
           u32 pw[NW];
           S::pack(t, pw);
-          fp = fp64(pw, a.seed);
+          if constexpr (INC) fp = fb.fp(pw, bw, a.seed);
+          else fp = fp64(pw, a.seed);
         } else if (a.inv_oom) {
           const u32 bad = S::violated(t, a.rt.invariants);
           if (bad && atomicCAS(&a.ctr[K_VIOL], 0ull, 1ull) == 0ull) {
@@ -255,12 +273,14 @@ struct MatArgs {
   u32* states;
   u64* meta;
   const u64* newrec;
-  u64 n_new, dst_base, cap;
+  u64 dst_base, cap;           // new state i of the chunk goes to dst_base + ctr[K_LEVEL_NEW] + i
   OrigRuntime rt;
-  unsigned long long* ctr;
+  unsigned long long* ctr;     // ctr[K_CHUNK_NEW] = the chunk's new states (set by orig_dedup_blk)
   void* viol;
 };
 
+// Grid-stride over the chunk's new states, whose number stays on the device: the host does
+// not wait for the dedup kernel to size this launch (one host synchronisation per level).
 template <class S>
 __global__ void __launch_bounds__(BS) orig_materialize(MatArgs a) {
   using W = typename S::Work;
@@ -268,9 +288,10 @@ __global__ void __launch_bounds__(BS) orig_materialize(MatArgs a) {
   __shared__ unsigned int lds_cnt[OA_NACT];
   for (int t = threadIdx.x; t < OA_NACT; t += BS) lds_cnt[t] = 0;
   __syncthreads();
-  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  const u64 n_new = a.ctr[K_CHUNK_NEW];
+  const u64 base = a.dst_base + a.ctr[K_LEVEL_NEW];
   u32 err = 0;
-  if (i < a.n_new) {
+  for (u64 i = (u64)blockIdx.x * BS + threadIdx.x; i < n_new; i += (u64)gridDim.x * BS) {
     const u64 rec = a.newrec[i], gid = rec >> 8;
     const int k = (int)(rec & 0xff);
     u32 w[NWP];
@@ -286,7 +307,7 @@ __global__ void __launch_bounds__(BS) orig_materialize(MatArgs a) {
     for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
     u32 pw[NW];
     S::pack(t, pw);
-    const u64 dst = a.dst_base + i;
+    const u64 dst = base + i;
     if (act >= 0 && dst < a.cap) {
       uint4* o = reinterpret_cast<uint4*>(a.states + dst * NWP);
 #pragma unroll
@@ -307,6 +328,11 @@ __global__ void __launch_bounds__(BS) orig_materialize(MatArgs a) {
   __syncthreads();
   for (int t = threadIdx.x; t < OA_NACT; t += BS)
     if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + OA_NACT + t], (unsigned long long)lds_cnt[t]);
+}
+
+// after a chunk's materialize: the level's running count of new states
+__global__ void orig_advance(unsigned long long* ctr) {
+  if (threadIdx.x == 0) ctr[K_LEVEL_NEW] += ctr[K_CHUNK_NEW];
 }
 
 // ------------------------------------------------------------------ sharded (multi-GPU) kernels
@@ -591,6 +617,16 @@ class OrigGpu : public Backend {
     return 0;
   }
 
+  // event pairs (generate, dedup, materialize) of chunk q of the current level: lvl_ev_[6q .. 6q+6)
+  int lvl_events(int q) {
+    while ((int)lvl_ev_.size() < 6 * (q + 1)) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return MC_E_NO_DEVICE;
+      lvl_ev_.push_back(e);
+    }
+    return 0;
+  }
+
   int run_generate(GenArgs& g, u64 cnt, float& ms_g, std::string& err, bool pm = false) {
     const unsigned nblk = (unsigned)((cnt + BS - 1) / BS);
     HIPCHK(hipEventRecord(ev_[5], stream_));
@@ -640,54 +676,59 @@ class OrigGpu : public Backend {
     while (level_count > 0) {
       if (o.max_depth && r.depth >= o.max_depth) { r.left_on_queue = (int64_t)level_count; r.verdict = MC_VERDICT_DEPTH_LIMIT; break; }
       HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
-      u64 next_write = level_begin + level_count;
-      double level_ms = 0;
-      for (u64 cb = level_begin; cb < level_begin + level_count; cb += chunk_states_) {
-        const u64 cnt = std::min<u64>(chunk_states_, level_begin + level_count - cb);
+      const u64 level_end = level_begin + level_count;
+      // every chunk's kernels are queued without waiting: the dedup kernel numbers the new
+      // states on the device and the materialize kernel reads that count (grid-stride), so the
+      // host synchronises once per level, for the counters
+      int nch = 0;
+      for (u64 cb = level_begin; cb < level_end; cb += chunk_states_, ++nch) {
+        const u64 cnt = std::min<u64>(chunk_states_, level_end - cb);
         const u64 nslots = cnt * (u64)S::NI;
+        const unsigned nblk = (unsigned)((cnt + BS - 1) / BS);
+        if (int rc = lvl_events(nch)) { err = "hipEventCreate failed"; return rc; }
+        hipEvent_t* e = &lvl_ev_[6 * nch];
         HIPCHK(hipMemsetAsync(d_ctr_ + K_CHUNK_NEW, 0, 8, stream_));
         GenArgs g;
         g.states = d_states_; g.chunk_begin = cb; g.chunk_count = cnt; g.cand = d_cand_; g.seed = r.seed; g.rt = m_.rt;
         g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_; g.viol = d_viol_;
+        HIPCHK(hipEventRecord(e[0], stream_));
+        hipLaunchKernelGGL((orig_generate<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(e[1], stream_));
         DedupArgs d;
         d.cand = d_cand_; d.nslots = nslots; d.chunk_begin = cb; d.chunk_count = cnt; d.table = d_table_;
-        d.table_mask = table_mask_; d.newrec = d_newrec_; d.ctr = (unsigned long long*)d_ctr_;
-        float ms_x = 0;
-        if (int rc = run_generate(g, cnt, ms_x, err, true)) return rc;
-        HIPCHK(hipEventRecord(ev_[1], stream_));
-        d.ni = S::NI;
-        hipLaunchKernelGGL((orig_dedup_blk<S::NI>), dim3((unsigned)((cnt + BS - 1) / BS)), dim3(BS), 0, stream_, d);
+        d.table_mask = table_mask_; d.newrec = d_newrec_; d.ctr = (unsigned long long*)d_ctr_; d.ni = S::NI;
+        HIPCHK(hipEventRecord(e[2], stream_));
+        hipLaunchKernelGGL((orig_dedup_blk<S::NI>), dim3(nblk), dim3(BS), 0, stream_, d);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(ev_[2], stream_));
-        u64 nnew = 0;
-        HIPCHK(hipMemcpyAsync(&nnew, d_ctr_ + K_CHUNK_NEW, 8, hipMemcpyDeviceToHost, stream_));
-        HIPCHK(hipStreamSynchronize(stream_));
-        float ms_d = 0, ms_m = 0;
-        HIPCHK(hipEventElapsedTime(&ms_d, ev_[1], ev_[2]));
-        if (nnew) {
-          MatArgs m;
-          m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.n_new = nnew; m.dst_base = next_write; m.cap = cap_;
-          m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.viol = d_viol_;
-          HIPCHK(hipEventRecord(ev_[3], stream_));
-          hipLaunchKernelGGL((orig_materialize<S>), dim3((unsigned)((nnew + BS - 1) / BS)), dim3(BS), 0, stream_, m);
-          HIPCHK(hipGetLastError());
-          HIPCHK(hipEventRecord(ev_[4], stream_));
-          HIPCHK(hipEventSynchronize(ev_[4]));
-          HIPCHK(hipEventElapsedTime(&ms_m, ev_[3], ev_[4]));
-          r.kernels[2].ms += ms_m; r.kernels[2].launches += 1;
-          r.kernels[2].algo_bytes += (double)nnew * (8 + S_B + S_B + 8);
-        }
-        next_write += nnew;
-        level_ms += ms_x + ms_d + ms_m;
-        r.kernels[0].ms += ms_x; r.kernels[0].launches += 1;
+        HIPCHK(hipEventRecord(e[3], stream_));
+        MatArgs m;
+        m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.dst_base = level_end; m.cap = cap_;
+        m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.viol = d_viol_;
+        const unsigned mblk = (unsigned)std::min<u64>(4096, (nslots + BS - 1) / BS);
+        HIPCHK(hipEventRecord(e[4], stream_));
+        hipLaunchKernelGGL((orig_materialize<S>), dim3(mblk), dim3(BS), 0, stream_, m);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(e[5], stream_));
+        hipLaunchKernelGGL(orig_advance, dim3(1), dim3(64), 0, stream_, (unsigned long long*)d_ctr_);
+        HIPCHK(hipGetLastError());
+        r.kernels[0].launches += 1; r.kernels[1].launches += 1; r.kernels[2].launches += 1;
         r.kernels[0].algo_bytes += (double)cnt * S_B + (double)nslots * 8;
-        r.kernels[1].ms += ms_d; r.kernels[1].launches += 1;
-        r.kernels[1].algo_bytes += (double)nslots * 8 + (double)nnew * 16;   // + G_in*8 probe bytes added per level below
-        if (next_write > cap_) break;
+        r.kernels[1].algo_bytes += (double)nslots * 8;   // + G_in*8 probe bytes and D*16 per level below
       }
       u64 c[K_NCTR];
       HIPCHK(hipMemcpyAsync(c, d_ctr_, sizeof c, hipMemcpyDeviceToHost, stream_));
       HIPCHK(hipStreamSynchronize(stream_));
+      double level_ms = 0;
+      for (int q = 0; q < nch; ++q)
+        for (int k = 0; k < 3; ++k) {
+          float ms = 0;
+          (void)hipEventElapsedTime(&ms, lvl_ev_[6 * q + 2 * k], lvl_ev_[6 * q + 2 * k + 1]);
+          r.kernels[k].ms += ms; level_ms += ms;
+        }
+      const u64 next_write = level_end + c[K_LEVEL_NEW];
+      r.kernels[1].algo_bytes += (double)c[K_LEVEL_NEW] * 16;
+      r.kernels[2].algo_bytes += (double)c[K_LEVEL_NEW] * (8 + S_B + S_B + 8);
       int64_t gen = 0;
       for (int k = 0; k < OA_NACT; ++k) { r.act_generated[k] += (int64_t)c[K_ACT + k]; r.act_distinct[k] += (int64_t)c[K_ACT + OA_NACT + k]; gen += (int64_t)c[K_ACT + k]; }
       r.generated += gen;
@@ -1240,6 +1281,7 @@ class OrigGpu : public Backend {
   void* nat_recv_ = nullptr; void* nat_acks_ = nullptr; void* nat_stin_ = nullptr;
   u64 nat_recv_cap_ = 0, nat_acks_cap_ = 0, nat_stin_cap_ = 0;
   std::vector<hipEvent_t> nat_ev_;
+  std::vector<hipEvent_t> lvl_ev_;
 
   void release() {
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, d_viol_, (void*)d_cand_, (void*)d_newrec_,
@@ -1252,6 +1294,8 @@ class OrigGpu : public Backend {
     nat_recv_cap_ = nat_acks_cap_ = nat_stin_cap_ = 0;
     for (auto& e : nat_ev_) (void)hipEventDestroy(e);
     nat_ev_.clear();
+    for (auto& e : lvl_ev_) (void)hipEventDestroy(e);
+    lvl_ev_.clear();
     for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
     if (stream_) (void)hipStreamDestroy(stream_);
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_viol_ = nullptr;

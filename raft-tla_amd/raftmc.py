@@ -15,7 +15,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libraftmc.so")
+LIB_PATH = os.environ.get("RAFTMC_LIB") or os.path.join(_HERE, "_build", "libraftmc.so")   # RAFTMC_LIB: experiment builds only
 ABI_VERSION = 1
 
 VERDICTS = {0: "OK", 1: "INVARIANT_VIOLATION", 2: "EVAL_ERROR", 3: "CAPACITY_OVERFLOW", 4: "DEADLOCK", 5: "DEPTH_LIMIT"}
