@@ -382,9 +382,9 @@ __global__ void __launch_bounds__(BS) orig_route_blk(RouteArgs a) {
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       if (own[j] < 0) continue;
-      u64* r = a.route + ((u64)own[j] * a.route_cap + base[own[j]] + off[j]) * 2;
-      r[0] = fp[j];
-      r[1] = (st << 8) | (u64)(k0 + j);
+      // one 16-B store per record
+      *reinterpret_cast<ulonglong2*>(a.route + ((u64)own[j] * a.route_cap + base[own[j]] + off[j]) * 2) =
+          make_ulonglong2((unsigned long long)fp[j], (unsigned long long)((st << 8) | (u64)(k0 + j)));
     }
     __syncthreads();   // hist / base reused by the next group
   }

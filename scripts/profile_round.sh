@@ -14,4 +14,7 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run -- pyt
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc_write.log" 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU -d "$OUT/pmc_valu" -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/pmc_valu.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_memb" -o run -- python3 scripts/memb_probe.py memb_four 0 > "$OUT/prof_memb.log" 2>&1
-echo "exit $?"
+rc=$?
+[ $rc -eq 0 ] && timeout -k 10 200 python3 scripts/shard_probe.py > "$OUT/shard_probe.jsonl" 2> "$OUT/shard_probe.err"
+rc2=$?
+echo "exit $rc $rc2"
