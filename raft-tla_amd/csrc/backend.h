@@ -19,6 +19,10 @@ struct RunOpts {
   bool inv_out_of_model = true;
   bool check_deadlock = false;
   int block_size = 256;
+  // TLC -checkpoint / -recover analogues (raft_original): write the BFS state every
+  // checkpoint_every levels to checkpoint_path; resume the next run from recover_path
+  std::string checkpoint_path, recover_path;
+  int checkpoint_every = 0;
 };
 
 struct LevelStat { int64_t states = 0, generated = 0; double kernel_ms = 0; };

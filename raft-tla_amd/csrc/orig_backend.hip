@@ -540,6 +540,32 @@ __global__ void __launch_bounds__(BS) orig_store(StoreArgs a) {
   a.meta[dst] = (u64)m.x | ((u64)m.y << 32);
 }
 
+// Recovery from a checkpoint: re-insert the fingerprints of every stored state into the
+// zeroed seen-set (the checkpoint holds states, not the table; FP64 is a function of the
+// packed words, so the rebuilt set is the saved one).
+template <class S>
+__global__ void __launch_bounds__(BS) orig_reinsert(const u32* states, u64 n, u64* table, u64 mask, u64 seed,
+                                                    unsigned long long* ctr) {
+  constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  u32 w[NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) w[q] = states[i * NWP + q];
+  const u64 fp = fp64(w, seed);
+  u64 slot = fp & mask;
+  for (int probe = 0; probe < (1 << 20); ++probe) {
+    const u64 c = table[slot];
+    if (c == fp) return;
+    if (c == 0ull) {
+      const u64 old = (u64)atomicCAS((unsigned long long*)&table[slot], 0ull, (unsigned long long)fp);
+      if (old == 0ull || old == fp) return;
+    }
+    slot = (slot + 1) & mask;
+  }
+  atomicOr(&ctr[K_ERR], (unsigned long long)OE_TABLE_FULL);
+}
+
 #define HIPCHK(x)                                                                             \
   do {                                                                                        \
     hipError_t e_ = (x);                                                                      \
@@ -652,8 +678,13 @@ class OrigGpu : public Backend {
     r.act_generated.assign(OA_NACT, 0); r.act_distinct.assign(OA_NACT, 0);
     r.kernels = {{"orig_generate", 0, 0, 0}, {"orig_dedup_blk", 0, 0, 0}, {"orig_materialize", 0, 0, 0}};
 
-    // ---- Init (raft_original.tla:139-159): one state, generated and distinct
     W s0; S::init(s0);
+    const u64 S_B = NWP * 4;
+    u64 level_begin = 0, level_count = 1;
+    if (!o.recover_path.empty()) {   // TLC -recover: continue the BFS saved by a checkpoint
+      if (int rc = load_checkpoint(o.recover_path, r, level_begin, level_count, err)) return rc;
+    } else {
+    // ---- Init (raft_original.tla:139-159): one state, generated and distinct
     u32 w0[S::NW]; S::pack(s0, w0);
     u32 wp[NWP] = {0}; for (int q = 0; q < S::NW; ++q) wp[q] = w0[q];
     const u64 fp0 = fp64(w0, r.seed);
@@ -670,9 +701,8 @@ class OrigGpu : public Backend {
       r.trace.push_back({"<Initial predicate>", state_text(s0, true)});
       finish(r, t0); return 0;
     }
+    }
 
-    const u64 S_B = NWP * 4;
-    u64 level_begin = 0, level_count = 1;
     while (level_count > 0) {
       if (o.max_depth && r.depth >= o.max_depth) { r.left_on_queue = (int64_t)level_count; r.verdict = MC_VERDICT_DEPTH_LIMIT; break; }
       HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
@@ -776,8 +806,84 @@ class OrigGpu : public Backend {
       }
       level_begin += level_count;
       level_count = nnew;
+      if (o.checkpoint_every > 0 && !o.checkpoint_path.empty() && r.depth % o.checkpoint_every == 0 && level_count > 0)
+        if (int rc = save_checkpoint(o.checkpoint_path, r, level_begin, level_count, err)) return rc;
     }
     finish(r, t0);
+    return 0;
+  }
+
+  // ---------------------------------------------------------------- checkpoint / recover
+  // File: magic, the model's describe_json (a checkpoint only resumes the same model), the BFS
+  // position (level_begin/count, stored states) and TLC's counters, then the stored states and
+  // parent pointers [0, total).  The seen-set is rebuilt from the states on recovery.
+  struct CkptHead {
+    char magic[8];
+    u64 nwp, total, level_begin, level_count, seed;
+    int64_t generated, distinct, depth, generated_in_model, n_act, n_levels, desc_len;
+  };
+  int save_checkpoint(const std::string& path, const RunResult& r, u64 level_begin, u64 level_count, std::string& err) {
+    const std::string desc = describe_json();
+    CkptHead h;
+    std::memcpy(h.magic, "RAFTMCK1", 8);
+    h.nwp = NWP; h.total = total_; h.level_begin = level_begin; h.level_count = level_count; h.seed = r.seed;
+    h.generated = r.generated; h.distinct = r.distinct; h.depth = r.depth; h.generated_in_model = r.generated_in_model;
+    h.n_act = OA_NACT; h.n_levels = (int64_t)r.levels.size(); h.desc_len = (int64_t)desc.size();
+    std::vector<u32> st(total_ * NWP);
+    std::vector<u64> me(total_);
+    HIPCHK(hipMemcpy(st.data(), d_states_, st.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(me.data(), d_meta_, me.size() * 8, hipMemcpyDeviceToHost));
+    const std::string tmp = path + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) { err = "cannot write checkpoint " + tmp; return MC_E_IO; }
+    bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(desc.data(), 1, desc.size(), f) == desc.size() &&
+              std::fwrite(r.act_generated.data(), 8, OA_NACT, f) == (size_t)OA_NACT &&
+              std::fwrite(r.act_distinct.data(), 8, OA_NACT, f) == (size_t)OA_NACT;
+    for (const auto& lv : r.levels) ok = ok && std::fwrite(&lv.states, 8, 1, f) == 1 && std::fwrite(&lv.generated, 8, 1, f) == 1;
+    ok = ok && std::fwrite(st.data(), 4, st.size(), f) == st.size() && std::fwrite(me.data(), 8, me.size(), f) == me.size();
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) { err = "writing checkpoint " + path + " failed"; return MC_E_IO; }
+    return 0;
+  }
+  int load_checkpoint(const std::string& path, RunResult& r, u64& level_begin, u64& level_count, std::string& err) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) { err = "cannot read checkpoint " + path; return MC_E_IO; }
+    CkptHead h;
+    const std::string desc = describe_json();
+    std::string fdesc;
+    bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, "RAFTMCK1", 8) == 0 && h.nwp == (u64)NWP &&
+              h.n_act == OA_NACT && h.desc_len >= 0 && h.desc_len < (1 << 20) && h.n_levels > 0 && h.n_levels < (1 << 20);
+    if (ok) { fdesc.resize((size_t)h.desc_len); ok = std::fread(&fdesc[0], 1, fdesc.size(), f) == fdesc.size(); }
+    if (!ok || fdesc != desc) { std::fclose(f); err = "checkpoint " + path + " is not a checkpoint of this model"; return MC_E_INVALID; }
+    if (h.total > cap_) { std::fclose(f); err = "checkpoint holds more states than the state store (raise state_store_bytes)"; return MC_E_OOM; }
+    ok = std::fread(r.act_generated.data(), 8, OA_NACT, f) == (size_t)OA_NACT &&
+         std::fread(r.act_distinct.data(), 8, OA_NACT, f) == (size_t)OA_NACT;
+    r.levels.clear();
+    for (int64_t k = 0; ok && k < h.n_levels; ++k) {
+      LevelStat lv;
+      ok = std::fread(&lv.states, 8, 1, f) == 1 && std::fread(&lv.generated, 8, 1, f) == 1;
+      r.levels.push_back(lv);
+    }
+    std::vector<u32> st(h.total * NWP);
+    std::vector<u64> me(h.total);
+    ok = ok && std::fread(st.data(), 4, st.size(), f) == st.size() && std::fread(me.data(), 8, me.size(), f) == me.size();
+    std::fclose(f);
+    if (!ok) { err = "checkpoint " + path + " is truncated"; return MC_E_IO; }
+    HIPCHK(hipMemcpy(d_states_, st.data(), st.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_meta_, me.data(), me.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
+    if (h.total) {
+      hipLaunchKernelGGL((orig_reinsert<S>), dim3((unsigned)((h.total + BS - 1) / BS)), dim3(BS), 0, stream_,
+                         (const u32*)d_states_, (u64)h.total, d_table_, table_mask_, (u64)h.seed, (unsigned long long*)d_ctr_);
+      HIPCHK(hipGetLastError());
+    }
+    u64 e = 0;
+    HIPCHK(hipMemcpyAsync(&e, d_ctr_ + K_ERR, 8, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    if (e) { err = "fingerprint table too small for the checkpoint (raise fp_table_bytes)"; return MC_E_OOM; }
+    r.seed = h.seed; r.generated = h.generated; r.distinct = h.distinct; r.depth = h.depth;
+    r.generated_in_model = h.generated_in_model;
+    total_ = h.total; level_begin = h.level_begin; level_count = h.level_count;
     return 0;
   }
 

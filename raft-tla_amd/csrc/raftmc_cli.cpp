@@ -1,6 +1,8 @@
 // raftmc — command-line front end mirroring TLC's flags:
 //   raftmc [-config F.cfg] [-workers N] [-deadlock] [-depth D] [-device K]
-//          [-fptable BYTES] [-store BYTES] [-seed S] [-no-inv-oom] [-dump FILE] [-json] F.tla
+//          [-fptable BYTES] [-store BYTES] [-seed S] [-no-inv-oom] [-dump FILE] [-json]
+//          [-checkpoint LEVELS] [-checkpoint-file FILE] [-recover FILE] F.tla
+// (-checkpoint counts BFS levels where TLC counts minutes; the file defaults to states/raftmc.ckpt)
 // Prints TLC-style lines and exits with TLC-like codes (0 ok, 12 safety
 // violation, 11 deadlock, 75 error).
 #include <cstdio>
@@ -8,12 +10,15 @@
 #include <cstring>
 #include <string>
 
+#include <sys/stat.h>
+
 #include "../../include/raftmc.h"
 
 int main(int argc, char** argv) {
   mc_opts o;
   mc_default_opts(&o);
-  std::string tla, cfg, dump;
+  std::string tla, cfg, dump, ckpt_file = "states/raftmc.ckpt", recover;
+  int ckpt_every = 0;
   bool json = false;
   for (int a = 1; a < argc; ++a) {
     std::string k = argv[a];
@@ -32,6 +37,9 @@ int main(int argc, char** argv) {
     else if (k == "-no-inv-oom") o.tlc_compat_flags &= ~MC_COMPAT_INV_OUT_OF_MODEL;
     else if (k == "-dump") dump = val();
     else if (k == "-json") json = true;
+    else if (k == "-checkpoint") ckpt_every = std::atoi(val());
+    else if (k == "-checkpoint-file") ckpt_file = val();
+    else if (k == "-recover") recover = val();
     else if (!k.empty() && k[0] == '-') { std::fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
     else tla = k;
   }
@@ -40,6 +48,12 @@ int main(int argc, char** argv) {
   mc_ctx* c = nullptr;
   int rc = mc_open(tla.c_str(), cfg.c_str(), &o, &c);
   if (rc) { std::fprintf(stderr, "raftmc: %s (code %d)\n", c ? mc_last_error(c) : "open failed", rc); mc_close(c); return 75; }
+  if (!rc && ckpt_every > 0) {
+    if (ckpt_file == "states/raftmc.ckpt") (void)::mkdir("states", 0755);
+    rc = mc_set_checkpoint(c, ckpt_file.c_str(), ckpt_every);
+  }
+  if (!rc && !recover.empty()) rc = mc_set_recover(c, recover.c_str());
+  if (rc) { std::fprintf(stderr, "raftmc: %s (code %d)\n", mc_last_error(c), rc); mc_close(c); return 75; }
   rc = mc_run(c);
   if (rc == 0) {   // TLC prints its fingerprint-based estimate after a completed search
     mc_summary_t s;

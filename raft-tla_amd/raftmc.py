@@ -28,7 +28,8 @@ EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stat
            "mc_shard_generate", "mc_shard_fill", "mc_shard_dedup", "mc_shard_materialize", "mc_shard_store",
            "mc_shard_level_stats", "mc_shard_level_commit", "mc_shard_read_state", "mc_shard_violation",
            "mc_set_history_prefix", "mc_shard_layout", "mc_shard_select", "mc_shard_event_stats",
-           "mc_collision_observed", "mc_rccl_unique_id", "mc_shard_run_rccl"]
+           "mc_collision_observed", "mc_rccl_unique_id", "mc_shard_run_rccl",
+           "mc_set_checkpoint", "mc_set_recover"]
 
 
 class McOpts(ctypes.Structure):
@@ -82,6 +83,8 @@ def load_library(path=LIB_PATH):
     lib.mc_dump_states.argtypes = [P, ctypes.c_char_p]
     lib.mc_set_history_prefix.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p]
     lib.mc_collision_observed.argtypes = [P, ctypes.POINTER(ctypes.c_double)]
+    lib.mc_set_checkpoint.argtypes = [P, ctypes.c_char_p, ctypes.c_int32]
+    lib.mc_set_recover.argtypes = [P, ctypes.c_char_p]
     lib.mc_exit_code.argtypes = [P]
     lib.mc_free.argtypes = [P]
     lib.mc_close.argtypes = [P]
@@ -136,6 +139,18 @@ class ModelChecker:
         """Golden history trace (TLA+ value text) of a punctuated-search constraint
         (CommitWhenConcurrentLeaders_unique / MajorityOfClusterRestarts_constraint)."""
         rc = self.lib.mc_set_history_prefix(self.h, constraint.encode(), trace_text.encode())
+        if rc:
+            raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
+
+    def set_checkpoint(self, path, every_levels=1):
+        """TLC -checkpoint: write the BFS state to `path` every `every_levels` levels (None: off)."""
+        rc = self.lib.mc_set_checkpoint(self.h, path.encode() if path else None, every_levels if path else 0)
+        if rc:
+            raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
+
+    def set_recover(self, path):
+        """TLC -recover: the next run() resumes the search saved in `path`."""
+        rc = self.lib.mc_set_recover(self.h, path.encode() if path else None)
         if rc:
             raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
 
@@ -216,10 +231,15 @@ def check(spec, config=None, **kw):
 def tlc_main(argv):
     """TLC-compatible argv entry point; prints the report, returns TLC's exit code."""
     spec, config, kw = None, None, {}
+    checkpoint, recover = None, None
     it = iter(argv)
     for a in it:
         if a == "-config":
             config = next(it)
+        elif a == "-checkpoint":                 # raftmc: levels between checkpoints (TLC: minutes)
+            checkpoint = int(next(it))
+        elif a == "-recover":
+            recover = next(it)
         elif a == "-workers":
             kw["workers"] = int(next(it))
         elif a == "-deadlock":
@@ -228,6 +248,13 @@ def tlc_main(argv):
             kw["max_depth"] = int(next(it))
         else:
             spec = a
-    res = check(spec, config, **kw)
+    with ModelChecker(spec, config, **kw) as mc:
+        if checkpoint:   # TLC keeps its checkpoints under states/ next to the spec
+            path = recover or os.path.join(os.path.dirname(os.path.abspath(spec)), "states", "raftmc.ckpt")
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            mc.set_checkpoint(path, checkpoint)
+        if recover:
+            mc.set_recover(recover)
+        res = mc.run()
     print(res.report, end="")
     return res.exit_code

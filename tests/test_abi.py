@@ -5,7 +5,7 @@ import re
 
 import pytest
 
-from oracle_util import CONFIGS, ORIG_MC, ROOT, cfg_variant
+from oracle_util import CONFIGS, MEMB_MC, ORIG_MC, ROOT, cfg_variant
 
 HEADER = os.path.join(ROOT, "include", "raftmc.h")
 
@@ -164,3 +164,16 @@ def test_prefix_taken_from_extended_module(raftmc, tmp_path):
         "====\n")
     with raftmc.ModelChecker(str(wrapper), os.path.join(CONFIGS, "scen_MajorityOfClusterRestarts_punct.cfg")) as mc:
         assert mc.describe()["history_prefixes"] == {"MajorityOfClusterRestarts_constraint": 28}
+
+
+def test_checkpoint_api_scope(raftmc):
+    """Checkpoints are a raft_original feature; tlc_membership handles refuse them."""
+    lib = raftmc.load_library()
+    with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, "membership_shipped.cfg")) as mc:
+        assert lib.mc_set_checkpoint(mc.h, b"/tmp/x.ckpt", 1) == -4
+        assert lib.mc_set_recover(mc.h, b"/tmp/x.ckpt") == -4
+    with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c1.cfg")) as mc:
+        assert lib.mc_set_checkpoint(mc.h, b"/tmp/x.ckpt", -1) == -1
+        mc.set_checkpoint("/tmp/x.ckpt", 2)
+        mc.set_checkpoint(None)
+        mc.set_recover(None)

@@ -124,6 +124,50 @@ def test_c5_deep_properties(raftmc):
     assert sum(v[0] for v in a.actions.values()) + 1 == a.generated
 
 
+def test_checkpoint_recover_c1(raftmc, tmp_path):
+    """TLC -checkpoint / -recover: a search stopped at depth 6 with a checkpoint per level,
+    resumed by a fresh handle, ends exactly like the uninterrupted search (counts, levels,
+    per-action generated counts, the set of states)."""
+    g = FIXTURES["c1"]
+    cfg = os.path.join(CONFIGS, "c1.cfg")
+    ck = str(tmp_path / "c1.ckpt")
+    with raftmc.ModelChecker(ORIG_MC, cfg, max_depth=6, **SMALL) as mc:
+        mc.set_checkpoint(ck, 1)
+        a = mc.run()
+    assert a.verdict == "DEPTH_LIMIT" and os.path.exists(ck)
+    with raftmc.ModelChecker(ORIG_MC, cfg, **SMALL) as mc:
+        mc.set_recover(ck)
+        b = mc.run()
+        sha, n = states_sha(mc)
+    assert (b.verdict, b.generated, b.distinct, b.depth) == ("OK", g["generated"], g["distinct"], g["depth"])
+    assert {k: v[0] for k, v in b.actions.items()} == {k: v[0] for k, v in g["actions"].items()}
+    assert [lv[0] for lv in b.levels] == g["levels"]
+    assert n == g["distinct"] and sha == g["states_sha256"]
+    # a checkpoint only resumes its own model
+    with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "parity_pair.cfg"), **SMALL) as mc:
+        mc.set_recover(ck)
+        with pytest.raises(raftmc.RaftMCError) as e:
+            mc.run()
+    assert e.value.code == -1
+
+
+def test_checkpoint_recover_c2(raftmc, tmp_path):
+    """BASELINE configs[1]: checkpoint at depth 20 of a full run, resume to the exact count."""
+    cfg = os.path.join(CONFIGS, "c2.cfg")
+    ck = str(tmp_path / "c2.ckpt")
+    with raftmc.ModelChecker(ORIG_MC, cfg) as mc:
+        mc.set_checkpoint(ck, 20)
+        a = mc.run()
+    with raftmc.ModelChecker(ORIG_MC, cfg, seed=99) as mc:   # the checkpoint's seed wins
+        mc.set_recover(ck)
+        b = mc.run()
+    exact = json.load(open(os.path.join(GOLDEN, "c2_exact.json")))
+    for r in (a, b):
+        assert (r.verdict, r.generated, r.distinct, r.depth) == ("OK", exact["generated"], exact["distinct"], exact["depth"])
+        assert {k: v[0] for k, v in r.actions.items()} == exact["actions_generated"]
+    assert [lv[0] for lv in a.levels] == [lv[0] for lv in b.levels]
+
+
 def test_collision_estimates_and_tlc_summary_lines(raftmc):
     """TLC's two collision estimates: the optimistic M*(N-M)/2^64 and the one "based on the
     actual fingerprints" (1 / minimum distance between two fingerprints of the seen-set, from a
