@@ -274,6 +274,7 @@ struct MatArgs {
   u64* meta;
   const u64* newrec;
   u64 dst_base, cap;           // new state i of the chunk goes to dst_base + ctr[K_LEVEL_NEW] + i
+  u64 base;                    // global id of device slot 0 (completed levels spilled to the host)
   OrigRuntime rt;
   unsigned long long* ctr;     // ctr[K_CHUNK_NEW] = the chunk's new states (set by orig_dedup_blk)
   void* viol;
@@ -313,7 +314,7 @@ __global__ void __launch_bounds__(BS) orig_materialize(MatArgs a) {
 #pragma unroll
       for (int q = 0; q < NWP / 4; ++q)
         o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
-      a.meta[dst] = (gid << 24) | ((u64)act << 16) | (u64)k;
+      a.meta[dst] = ((gid + a.base) << 24) | ((u64)act << 16) | (u64)k;
       atomicAdd(&lds_cnt[act], 1u);
       const u32 bad = S::violated(t, a.rt.invariants);
       if (bad && atomicCAS(&a.ctr[K_VIOL], 0ull, 1ull) == 0ull) {
@@ -677,6 +678,7 @@ class OrigGpu : public Backend {
     for (int k = 0; k < OA_NACT; ++k) r.action_names.push_back(kOrigActNames[k]);
     r.act_generated.assign(OA_NACT, 0); r.act_distinct.assign(OA_NACT, 0);
     r.kernels = {{"orig_generate", 0, 0, 0}, {"orig_dedup_blk", 0, 0, 0}, {"orig_materialize", 0, 0, 0}};
+    base_ = 0; host_states_.clear(); host_meta_.clear();
 
     W s0; S::init(s0);
     const u64 S_B = NWP * 4;
@@ -705,6 +707,15 @@ class OrigGpu : public Backend {
 
     while (level_count > 0) {
       if (o.max_depth && r.depth >= o.max_depth) { r.left_on_queue = (int64_t)level_count; r.verdict = MC_VERDICT_DEPTH_LIMIT; break; }
+      // the device keeps what the search still reads (the frontier) and writes (the next
+      // level); when the next level, predicted from the last growth ratio with a 1.5x margin,
+      // might not fit behind what is stored, the completed levels move to host memory
+      if (level_begin > base_) {
+        const double prev = r.levels.size() >= 2 ? (double)r.levels[r.levels.size() - 2].states : 1.0;
+        const double pred = (double)level_count * std::max(1.0, (double)level_count / std::max(prev, 1.0)) * 1.5;
+        if ((double)(total_ - base_) + pred > (double)cap_)
+          if (int rc = spill(level_begin, level_count, err)) return rc;
+      }
       HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
       const u64 level_end = level_begin + level_count;
       // every chunk's kernels are queued without waiting: the dedup kernel numbers the new
@@ -719,22 +730,23 @@ class OrigGpu : public Backend {
         hipEvent_t* e = &lvl_ev_[6 * nch];
         HIPCHK(hipMemsetAsync(d_ctr_ + K_CHUNK_NEW, 0, 8, stream_));
         GenArgs g;
-        g.states = d_states_; g.chunk_begin = cb; g.chunk_count = cnt; g.cand = d_cand_; g.seed = r.seed; g.rt = m_.rt;
+        // kernels index the device store (global id - base_); parent pointers are global
+        g.states = d_states_; g.chunk_begin = cb - base_; g.chunk_count = cnt; g.cand = d_cand_; g.seed = r.seed; g.rt = m_.rt;
         g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_; g.viol = d_viol_;
         HIPCHK(hipEventRecord(e[0], stream_));
         hipLaunchKernelGGL((orig_generate<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e[1], stream_));
         DedupArgs d;
-        d.cand = d_cand_; d.nslots = nslots; d.chunk_begin = cb; d.chunk_count = cnt; d.table = d_table_;
+        d.cand = d_cand_; d.nslots = nslots; d.chunk_begin = cb - base_; d.chunk_count = cnt; d.table = d_table_;
         d.table_mask = table_mask_; d.newrec = d_newrec_; d.ctr = (unsigned long long*)d_ctr_; d.ni = S::NI;
         HIPCHK(hipEventRecord(e[2], stream_));
         hipLaunchKernelGGL((orig_dedup_blk<S::NI>), dim3(nblk), dim3(BS), 0, stream_, d);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e[3], stream_));
         MatArgs m;
-        m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.dst_base = level_end; m.cap = cap_;
-        m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.viol = d_viol_;
+        m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.dst_base = level_end - base_; m.cap = cap_;
+        m.base = base_; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.viol = d_viol_;
         const unsigned mblk = (unsigned)std::min<u64>(4096, (nslots + BS - 1) / BS);
         HIPCHK(hipEventRecord(e[4], stream_));
         hipLaunchKernelGGL((orig_materialize<S>), dim3(mblk), dim3(BS), 0, stream_, m);
@@ -768,19 +780,19 @@ class OrigGpu : public Backend {
       r.n_launches += 1;
       const u64 nnew = next_write - (level_begin + level_count);
       r.algo_bytes += (double)level_count * S_B + (double)c[K_GEN_IN] * 8 + (double)nnew * (16 + S_B);
-      if (next_write > cap_) c[K_ERR] |= OE_CAP_STORE;
+      if (next_write - base_ > cap_) c[K_ERR] |= OE_CAP_STORE;
       if (c[K_ERR]) {
         const u64 e = c[K_ERR];
         r.verdict = (e & (OE_CAP_STORE | OE_TABLE_FULL | OE_CAP_ELECTIONS | OE_CAP_COUNT)) ? MC_VERDICT_CAPACITY_OVERFLOW : MC_VERDICT_EVAL_ERROR;
         std::ostringstream os;
-        os << "error flags 0x" << std::hex << e << std::dec << " while expanding state " << (c[K_ERRGID] ? (int64_t)c[K_ERRGID] - 1 : -1) << ":";
+        os << "error flags 0x" << std::hex << e << std::dec << " while expanding state " << (c[K_ERRGID] ? (int64_t)(c[K_ERRGID] - 1 + base_) : -1) << ":";
         if (e & OE_EVAL_LOG_INDEX) os << " log[i][prevLogIndex] applied outside its domain (raft_original.tla:207-210);";
         if (e & OE_CAP_ELECTIONS) os << " elections set exceeds the compiled capacity;";
         if (e & OE_CAP_COUNT) os << " message count / bag capacity exceeded;";
         if (e & OE_CAP_STORE) os << " state store full (raise state_store_bytes);";
         if (e & OE_TABLE_FULL) os << " fingerprint table full (raise fp_table_bytes);";
         r.error = os.str();
-        total_ = std::min<u64>(next_write, cap_);
+        total_ = std::min<u64>(next_write, base_ + cap_);
         r.distinct = (int64_t)total_;
         break;
       }
@@ -794,13 +806,13 @@ class OrigGpu : public Backend {
         HIPCHK(hipMemcpy(&v, d_viol_, sizeof v, hipMemcpyDeviceToHost));
         r.verdict = MC_VERDICT_INVARIANT_VIOLATION;
         r.violated = first_violated(v.bad);
-        build_trace(v.parent, kOrigActNames[v.act], v.w, r, err);
+        build_trace(v.parent + base_, kOrigActNames[v.act], v.w, r, err);
         r.left_on_queue = (int64_t)nnew;
         break;
       }
       if (o.check_deadlock && c[K_DEADLOCK]) {
         r.verdict = MC_VERDICT_DEADLOCK;
-        build_trace(c[K_DEADLOCK] - 1, nullptr, s0, r, err);
+        build_trace(c[K_DEADLOCK] - 1 + base_, nullptr, s0, r, err);
         r.left_on_queue = (int64_t)nnew;
         break;
       }
@@ -831,8 +843,10 @@ class OrigGpu : public Backend {
     h.n_act = OA_NACT; h.n_levels = (int64_t)r.levels.size(); h.desc_len = (int64_t)desc.size();
     std::vector<u32> st(total_ * NWP);
     std::vector<u64> me(total_);
-    HIPCHK(hipMemcpy(st.data(), d_states_, st.size() * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(me.data(), d_meta_, me.size() * 8, hipMemcpyDeviceToHost));
+    std::memcpy(st.data(), host_states_.data(), base_ * NWP * 4);
+    std::memcpy(me.data(), host_meta_.data(), base_ * 8);
+    HIPCHK(hipMemcpy(st.data() + base_ * NWP, d_states_, (total_ - base_) * NWP * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(me.data() + base_, d_meta_, (total_ - base_) * 8, hipMemcpyDeviceToHost));
     const std::string tmp = path + ".tmp";
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) { err = "cannot write checkpoint " + tmp; return MC_E_IO; }
@@ -855,7 +869,9 @@ class OrigGpu : public Backend {
               h.n_act == OA_NACT && h.desc_len >= 0 && h.desc_len < (1 << 20) && h.n_levels > 0 && h.n_levels < (1 << 20);
     if (ok) { fdesc.resize((size_t)h.desc_len); ok = std::fread(&fdesc[0], 1, fdesc.size(), f) == fdesc.size(); }
     if (!ok || fdesc != desc) { std::fclose(f); err = "checkpoint " + path + " is not a checkpoint of this model"; return MC_E_INVALID; }
-    if (h.total > cap_) { std::fclose(f); err = "checkpoint holds more states than the state store (raise state_store_bytes)"; return MC_E_OOM; }
+    // completed levels that do not fit the device store stay in host memory (spilled)
+    const u64 lb = h.total > cap_ ? h.level_begin : 0;
+    if (h.total - lb > cap_ || h.level_begin > h.total) { std::fclose(f); err = "checkpoint frontier exceeds the state store (raise state_store_bytes)"; return MC_E_OOM; }
     ok = std::fread(r.act_generated.data(), 8, OA_NACT, f) == (size_t)OA_NACT &&
          std::fread(r.act_distinct.data(), 8, OA_NACT, f) == (size_t)OA_NACT;
     r.levels.clear();
@@ -869,14 +885,27 @@ class OrigGpu : public Backend {
     ok = ok && std::fread(st.data(), 4, st.size(), f) == st.size() && std::fread(me.data(), 8, me.size(), f) == me.size();
     std::fclose(f);
     if (!ok) { err = "checkpoint " + path + " is truncated"; return MC_E_IO; }
-    HIPCHK(hipMemcpy(d_states_, st.data(), st.size() * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d_meta_, me.data(), me.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
-    if (h.total) {
-      hipLaunchKernelGGL((orig_reinsert<S>), dim3((unsigned)((h.total + BS - 1) / BS)), dim3(BS), 0, stream_,
-                         (const u32*)d_states_, (u64)h.total, d_table_, table_mask_, (u64)h.seed, (unsigned long long*)d_ctr_);
+    // the host part's fingerprints go in through the (idle) candidate buffer, chunk by chunk
+    const u64 stage = std::max<u64>(1, chunk_states_ * S::NI * 8 / (NWP * 4));
+    for (u64 b = 0; b < lb; b += stage) {
+      const u64 n = std::min<u64>(stage, lb - b);
+      HIPCHK(hipMemcpy(d_cand_, st.data() + b * NWP, n * NWP * 4, hipMemcpyHostToDevice));
+      hipLaunchKernelGGL((orig_reinsert<S>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_,
+                         (const u32*)d_cand_, n, d_table_, table_mask_, (u64)h.seed, (unsigned long long*)d_ctr_);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(stream_));
+    }
+    HIPCHK(hipMemcpy(d_states_, st.data() + lb * NWP, (h.total - lb) * NWP * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_meta_, me.data() + lb, (h.total - lb) * 8, hipMemcpyHostToDevice));
+    if (h.total > lb) {
+      hipLaunchKernelGGL((orig_reinsert<S>), dim3((unsigned)((h.total - lb + BS - 1) / BS)), dim3(BS), 0, stream_,
+                         (const u32*)d_states_, (u64)(h.total - lb), d_table_, table_mask_, (u64)h.seed, (unsigned long long*)d_ctr_);
       HIPCHK(hipGetLastError());
     }
+    host_states_.assign(st.begin(), st.begin() + lb * NWP);
+    host_meta_.assign(me.begin(), me.begin() + lb);
+    base_ = lb;
     u64 e = 0;
     HIPCHK(hipMemcpyAsync(&e, d_ctr_ + K_ERR, 8, hipMemcpyDeviceToHost, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
@@ -890,7 +919,8 @@ class OrigGpu : public Backend {
   int dump_states(const std::string& path, std::string& err) override {
     if (!d_states_) { err = "mc_dump_states before mc_run"; return MC_E_STATE; }
     std::vector<u32> h(total_ * NWP);
-    HIPCHK(hipMemcpy(h.data(), d_states_, h.size() * 4, hipMemcpyDeviceToHost));
+    std::memcpy(h.data(), host_states_.data(), base_ * NWP * 4);
+    HIPCHK(hipMemcpy(h.data() + base_ * NWP, d_states_, (total_ - base_) * NWP * 4, hipMemcpyDeviceToHost));
     FILE* f = std::fopen(path.c_str(), "w");
     if (!f) { err = "cannot write " + path; return MC_E_IO; }
     for (u64 g = 0; g < total_; ++g) {
@@ -924,6 +954,7 @@ class OrigGpu : public Backend {
     u32 w0[S::NW]; S::pack(s0, w0);
     const u64 fp0 = fp64(w0, sres_.seed);
     total_ = 0; sh_level_begin_ = 0; sh_level_count_ = 0; sh_new_ = 0;
+    base_ = 0; host_states_.clear(); host_meta_.clear();
     if ((int)fp_owner(fp0, (u32)world) == rank) {
       u32 wp[NWP] = {0}; for (int q = 0; q < S::NW; ++q) wp[q] = w0[q];
       HIPCHK(hipMemcpy(d_table_ + (fp0 & table_mask_), &fp0, 8, hipMemcpyHostToDevice));
@@ -1388,6 +1419,10 @@ class OrigGpu : public Backend {
   u64 nat_recv_cap_ = 0, nat_acks_cap_ = 0, nat_stin_cap_ = 0;
   std::vector<hipEvent_t> nat_ev_;
   std::vector<hipEvent_t> lvl_ev_;
+  // completed levels moved to host memory: global ids [0, base_) live in host_states_/host_meta_
+  u64 base_ = 0;
+  std::vector<u32> host_states_;
+  std::vector<u64> host_meta_;
 
   void release() {
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, d_viol_, (void*)d_cand_, (void*)d_newrec_,
@@ -1423,6 +1458,39 @@ class OrigGpu : public Backend {
     r.seconds_total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 
+  // stored state `gid` (global id) and its parent pointer, from the host part or the device
+  bool stored_state(u64 gid, u32 (&w)[NWP], u64& meta) const {
+    if (gid < base_) {
+      std::memcpy(w, host_states_.data() + gid * NWP, NWP * 4);
+      meta = host_meta_[gid];
+      return true;
+    }
+    const u64 d = gid - base_;
+    return hipMemcpy(w, d_states_ + d * NWP, NWP * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+           hipMemcpy(&meta, d_meta_ + d, 8, hipMemcpyDeviceToHost) == hipSuccess;
+  }
+
+  // move the completed levels [base_, level_begin) to host memory and the frontier to the
+  // front of the device store (left shift by d in blocks of <= d slots: each block's target
+  // only overlaps blocks already moved)
+  int spill(u64 level_begin, u64 level_count, std::string& err) {
+    const u64 d = level_begin - base_;
+    const u64 h0 = host_meta_.size();
+    host_states_.resize((h0 + d) * NWP);
+    host_meta_.resize(h0 + d);
+    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(hipMemcpy(host_states_.data() + h0 * NWP, d_states_, d * NWP * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(host_meta_.data() + h0, d_meta_, d * 8, hipMemcpyDeviceToHost));
+    for (u64 off = 0; off < level_count; off += d) {
+      const u64 n = std::min<u64>(d, level_count - off);
+      HIPCHK(hipMemcpyAsync(d_states_ + off * NWP, d_states_ + (d + off) * NWP, n * NWP * 4, hipMemcpyDeviceToDevice, stream_));
+      HIPCHK(hipMemcpyAsync(d_meta_ + off, d_meta_ + d + off, n * 8, hipMemcpyDeviceToDevice, stream_));
+      HIPCHK(hipStreamSynchronize(stream_));
+    }
+    base_ = level_begin;
+    return 0;
+  }
+
   // parent-pointer chase on the host (<= depth device reads of one state each)
   void build_trace(u64 parent, const char* last_act, const W& last, RunResult& r, std::string& err) {
     std::vector<std::pair<std::string, std::string>> tr;
@@ -1430,8 +1498,7 @@ class OrigGpu : public Backend {
     u64 g = parent;
     while (true) {
       u32 w[NWP]; u64 meta = 0;
-      if (hipMemcpy(w, d_states_ + g * NWP, NWP * 4, hipMemcpyDeviceToHost) != hipSuccess ||
-          hipMemcpy(&meta, d_meta_ + g, 8, hipMemcpyDeviceToHost) != hipSuccess) { err = "trace readback failed"; break; }
+      if (!stored_state(g, w, meta)) { err = "trace readback failed"; break; }
       W s; S::unpack(w, s);
       if (meta == ~0ull) { tr.push_back({"<Initial predicate>", state_text(s, true)}); break; }
       tr.push_back({kOrigActNames[(meta >> 16) & 0xff], state_text(s, true)});

@@ -168,6 +168,68 @@ def test_checkpoint_recover_c2(raftmc, tmp_path):
     assert [lv[0] for lv in a.levels] == [lv[0] for lv in b.levels]
 
 
+def _slot_bytes(raftmc, cfg):
+    """device bytes per stored state: packed state + parent pointer"""
+    with raftmc.ModelChecker(ORIG_MC, cfg) as mc:
+        return mc.describe()["state_bytes_stored"] + 8
+
+
+def test_spill_completed_levels_c2(raftmc, tmp_path):
+    """A state store too small for the whole search but large enough for two consecutive
+    levels: completed levels move to host memory and the search ends exactly like the
+    in-HBM one (counts, levels, per-action counts); a checkpoint taken after spills and the
+    trace-visible parent pointers keep working."""
+    cfg = os.path.join(CONFIGS, "c2.cfg")
+    a = raftmc.check(ORIG_MC, cfg)
+    sizes = [lv[0] for lv in a.levels]
+    cap = int(max(x + y for x, y in zip(sizes, sizes[1:])) * 1.6)
+    assert cap < a.distinct                          # the store cannot hold the search
+    ck = str(tmp_path / "c2s.ckpt")
+    with raftmc.ModelChecker(ORIG_MC, cfg, state_store_bytes=cap * _slot_bytes(raftmc, cfg)) as mc:
+        mc.set_checkpoint(ck, 22)
+        b = mc.run()
+    assert (b.verdict, b.generated, b.distinct, b.depth) == ("OK", a.generated, a.distinct, a.depth), b.error
+    assert [lv[0] for lv in b.levels] == sizes
+    assert {k: v[0] for k, v in b.actions.items()} == {k: v[0] for k, v in a.actions.items()}
+    with raftmc.ModelChecker(ORIG_MC, cfg, state_store_bytes=cap * _slot_bytes(raftmc, cfg)) as mc:   # resume: spilled part on the host
+        mc.set_recover(ck)
+        c = mc.run()
+    assert (c.generated, c.distinct, c.depth) == (a.generated, a.distinct, a.depth), c.error
+
+
+def test_spill_state_set_c1(raftmc):
+    """The host-spilled and device parts together are exactly the oracle's state set."""
+    g = FIXTURES["c1"]
+    cap = int(max(x + y for x, y in zip(g["levels"], g["levels"][1:])) * 1.3)
+    assert cap < g["distinct"]
+    cfg = os.path.join(CONFIGS, "c1.cfg")
+    with raftmc.ModelChecker(ORIG_MC, cfg, fp_table_bytes=1 << 26, state_store_bytes=cap * _slot_bytes(raftmc, cfg)) as mc:
+        r = mc.run()
+        sha, n = states_sha(mc)
+    assert (r.verdict, r.generated, r.distinct, r.depth) == ("OK", g["generated"], g["distinct"], g["depth"]), r.error
+    assert n == g["distinct"] and sha == g["states_sha256"]
+
+
+def test_spill_violation_trace(raftmc, tmp_path):
+    """Trace reconstruction across the host/device split: with a store that forces spills,
+    NoLeader's witness has the in-HBM (shortest) length and the oracle replays it step by step
+    (which shortest witness is kept depends on thread timing, as with TLC's workers)."""
+    from oracle_util import run_oracle
+    cfg = os.path.join(CONFIGS, "scenario_first_leader.cfg")
+    a = raftmc.check(ORIG_MC, cfg, **SMALL)
+    sizes = [lv[0] for lv in a.levels]
+    cap = max(64, int(max(x + y for x, y in zip(sizes, sizes[1:])) * 1.6))
+    b = raftmc.check(ORIG_MC, cfg, fp_table_bytes=1 << 26, state_store_bytes=cap * _slot_bytes(raftmc, cfg))
+    assert b.verdict == a.verdict == "INVARIANT_VIOLATION"
+    assert (b.distinct, b.generated) == (a.distinct, a.generated)
+    states = b.trace_text.strip().split("\n\n")
+    assert len(states) == len(a.trace_text.strip().split("\n\n")) == 10
+    p = tmp_path / "trace.txt"
+    p.write_text("\n".join(" ".join(st.split("\n")[1:]) for st in states) + "\n")
+    r = run_oracle("check-trace", ORIG_MC, cfg, "--golden", str(p))
+    assert r["valid"] and r["length"] == 10 and r["violated"] == "NoLeader", r
+
+
 def test_collision_estimates_and_tlc_summary_lines(raftmc):
     """TLC's two collision estimates: the optimistic M*(N-M)/2^64 and the one "based on the
     actual fingerprints" (1 / minimum distance between two fingerprints of the seen-set, from a
