@@ -1217,12 +1217,12 @@ class OrigGpu : public Backend {
       return 0;
     };
     // payload exchange: segment r of the send side (bytes) goes to rank r, the receive side is
-    // packed in source-rank order
+    // packed in source-rank order; the self segment is not copied (its consumer reads it in
+    // place), so dst + roff[me] stays unused
     auto xpay = [&](const char* const* src, const u64* sbytes, char* dst, const u64* rbytes) -> int {
       u64 roff[8]; u64 acc = 0;
       for (int r = 0; r < W; ++r) { roff[r] = acc; acc += rbytes[r]; }
       if (sbytes[me] != rbytes[me]) { err = "sharded exchange: self segment size mismatch"; return MC_E_STATE; }
-      if (sbytes[me]) HIPCHK(hipMemcpyAsync(dst + roff[me], src[me], sbytes[me], hipMemcpyDeviceToDevice, stream_));
       if (W > 1) {
         NCCLCHK(R.GroupStart());
         for (int r = 0; r < W; ++r) {
@@ -1330,7 +1330,8 @@ class OrigGpu : public Backend {
             const u64 n = rcnt[r];
             if (n) {
               DedupShArgs d;
-              d.recv = (const u64*)nat_recv_ + 2 * off; d.n = n; d.table = d_table_; d.table_mask = table_mask_;
+              d.recv = r == me ? d_route_ + (u64)me * route_cap * 2 : (const u64*)nat_recv_ + 2 * off;
+              d.n = n; d.table = d_table_; d.table_mask = table_mask_;
               d.reply = d_newrec_ + off; d.counter = (unsigned long long*)(d_rcnt_ + 8 + r); d.ctr = (unsigned long long*)d_ctr_;
               NAT_TIMED(2, hipLaunchKernelGGL(orig_dedup_sh, dim3((unsigned)((n + BS * DEDUP_PER - 1) / (BS * DEDUP_PER))), dim3(BS), 0, stream_, d));
             }
@@ -1359,7 +1360,8 @@ class OrigGpu : public Backend {
           for (int r = 0; r < W; ++r) {
             if (!ack[r]) continue;
             MatShArgs m;
-            m.states = d_states_; m.acks = (const u64*)nat_acks_ + seg_off_ack_[r]; m.n = ack[r]; m.chunk_begin = sh_chunk_begin_;
+            m.states = d_states_; m.acks = r == me ? d_newrec_ + seg_off_[me] : (const u64*)nat_acks_ + seg_off_ack_[r];
+            m.n = ack[r]; m.chunk_begin = sh_chunk_begin_;
             m.chunk_count = sh_chunk_count_; m.out = d_stout_ + seg_off_ack_[r] * (NWP + 4); m.rank_bits = (u64)me << 37;
             m.seed = sres_.seed; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.viol = d_viol_;
             NAT_TIMED(3, hipLaunchKernelGGL((orig_materialize_sh<S>), dim3((unsigned)((ack[r] + BS - 1) / BS)), dim3(BS), 0, stream_, m));
@@ -1370,13 +1372,21 @@ class OrigGpu : public Backend {
         for (int r = 0; r < W; ++r) { sb[r] = ack[r] * SBW; rb[r] = rep[r] * SBW; src[r] = (const char*)(d_stout_ + seg_off_ack_[r] * (NWP + 4)); }
         if (int rc = grow(nat_stin_, nat_stin_cap_, ntot * SBW)) return rc;
         if (int rc = xpay(src, sb, (char*)nat_stin_, rb)) return rc;
-        if (ntot) {
-          StoreArgs a;
-          a.in = (const u32*)nat_stin_; a.n = ntot; a.dst = sh_next_write_; a.cap = cap_; a.states = d_states_; a.meta = d_meta_;
-          a.ctr = (unsigned long long*)d_ctr_;
-          NAT_TIMED(4, hipLaunchKernelGGL((orig_store<NWP>), dim3((unsigned)((ntot + BS - 1) / BS)), dim3(BS), 0, stream_, a));
-          sres_.kernels[4].algo_bytes += (double)ntot * (SBW + NWP * 4 + 8);
-          sh_next_write_ += ntot; sh_new_ += ntot;
+        {   // the owner stores the states in source-rank order (its own ones straight from d_stout_)
+          u64 in_off = 0;
+          for (int r = 0; r < W; ++r) {
+            const u64 n = rep[r];
+            if (n) {
+              StoreArgs a;
+              a.in = r == me ? d_stout_ + seg_off_ack_[me] * (NWP + 4) : (const u32*)((const char*)nat_stin_ + in_off * SBW);
+              a.n = n; a.dst = sh_next_write_; a.cap = cap_; a.states = d_states_; a.meta = d_meta_;
+              a.ctr = (unsigned long long*)d_ctr_;
+              NAT_TIMED(4, hipLaunchKernelGGL((orig_store<NWP>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, a));
+              sres_.kernels[4].algo_bytes += (double)n * (SBW + NWP * 4 + 8);
+              sh_next_write_ += n; sh_new_ += n;
+            }
+            in_off += n;
+          }
         }
       }
       HIPCHK(hipStreamSynchronize(stream_));
