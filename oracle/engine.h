@@ -14,7 +14,9 @@
 //   FIFO order         (v)   single worker, level order, TLC action order
 // ============================================================================
 #pragma once
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <fstream>
 #include <sstream>
 #include <unordered_map>
@@ -159,6 +161,9 @@ struct Options {
   bool check_deadlock = false;
   std::string dump_states;          // write canonical text of every distinct state
   bool store_text_keys = true;      // seen-set keyed by full canonical text (exact)
+  int workers = 1;                  // >1: successors, constraints, keys and invariants of a batch
+                                    // of parents are computed by this many threads, merged in
+                                    // frontier order (results identical to workers = 1)
 };
 
 struct Result {
@@ -279,6 +284,84 @@ inline Result bfs(const Spec& sp, const Cfg& cfg, const Options& o) {
     while (!frontier.empty()) {
       if (o.max_depth && level >= o.max_depth) { r.left_on_queue = (int64_t)frontier.size(); break; }
       std::vector<int64_t> nextf;
+      if (o.workers > 1) {
+        // ---- parallel expansion, sequential merge in frontier order (the FIFO order of the
+        // single-worker search, so every count, kept representative and trace is the same)
+        struct SRec { int action; bool im; std::string key, bad, bad_err; State s; };
+        struct PRec { std::vector<SRec> succ; bool err = false; std::string errmsg; };
+        const size_t B = 4096;
+        for (size_t b0 = 0; b0 < frontier.size(); b0 += B) {
+          const size_t b1 = std::min(frontier.size(), b0 + B);
+          std::vector<PRec> recs(b1 - b0);
+          std::atomic<size_t> next_i{b0};
+          auto work = [&]() {
+            std::vector<Succ> ss;
+            for (size_t i; (i = next_i.fetch_add(1)) < b1;) {
+              PRec& pr = recs[i - b0];
+              const State& cur = store[frontier[i]];
+              try {
+                ss.clear();
+                sp.next(cur, ss);
+                for (auto& su : ss) {
+                  SRec sr;
+                  sr.action = su.action;
+                  sr.im = in_model(su.s) && in_actions(cur, su.s);
+                  if (sr.im) sr.key = canon_key(sp, cfg, o, su.s, perms, vv);
+                  if (sr.im || o.inv_out_of_model) {
+                    try { sr.bad = check_inv(su.s); } catch (const EvalError& e) { sr.bad_err = e.what(); }
+                  }
+                  sr.s = su.s;
+                  pr.succ.push_back(std::move(sr));
+                }
+              } catch (const EvalError& e) { pr.err = true; pr.errmsg = e.what(); }
+            }
+          };
+          std::vector<std::thread> th;
+          for (int t = 1; t < o.workers; ++t) th.emplace_back(work);
+          work();
+          for (auto& t : th) t.join();
+          for (size_t fi = b0; fi < b1; ++fi) {
+            PRec& pr = recs[fi - b0];
+            const int64_t idx = frontier[fi];
+            if (pr.err) throw EvalError(pr.errmsg);
+            r.generated += (int64_t)pr.succ.size();
+            if (pr.succ.empty() && o.check_deadlock) {
+              r.verdict = "DEADLOCK"; build_trace(idx, -1, nullptr); goto finish;
+            }
+            for (auto& su : pr.succ) {
+              r.act_generated[su.action]++;
+              bool isnew = false;
+              if (su.im) {
+                isnew = seen.insert(su.key).second;
+                if (isnew) {
+                  store.push_back(su.s); nodes.push_back({idx, su.action, level + 1});
+                  nextf.push_back((int64_t)store.size() - 1);
+                  r.act_distinct[su.action]++;
+                  if (dump) std::fprintf(dump, "%s\n", sp.dump_line(su.s).c_str());
+                }
+              }
+              if (isnew || (!su.im && o.inv_out_of_model)) {
+                if (!su.bad_err.empty()) throw EvalError(su.bad_err);
+                if (!su.bad.empty()) {
+                  r.verdict = "INVARIANT_VIOLATION"; r.violated = su.bad;
+                  if (isnew) build_trace((int64_t)store.size() - 1, -1, nullptr);
+                  else build_trace(idx, su.action, &su.s);
+                  r.depth = level + 1;
+                  r.left_on_queue = (int64_t)(frontier.size() - fi - 1 + nextf.size());
+                  goto finish;
+                }
+              }
+              if (o.max_states && (int64_t)seen.size() >= o.max_states) {
+                r.verdict = "SAMPLE_LIMIT"; r.left_on_queue = (int64_t)(frontier.size() - fi - 1 + nextf.size());
+                goto finish;
+              }
+            }
+          }
+        }
+        if (!nextf.empty()) { level++; r.depth = level; r.level_sizes.push_back((int64_t)nextf.size()); }
+        frontier.swap(nextf);
+        continue;
+      }
       for (size_t fi = 0; fi < frontier.size(); ++fi) {
         int64_t idx = frontier[fi];
         State cur = store[idx];

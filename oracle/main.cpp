@@ -56,6 +56,7 @@ int main(int argc, char** argv) {
     else if (k == "--cfg") cfgp = nxt();
     else if (k == "--max-depth") o.max_depth = std::stoll(nxt());
     else if (k == "--max-states") o.max_states = std::stoll(nxt());
+    else if (k == "--workers") o.workers = std::max(1, std::stoi(nxt()));
     else if (k == "--dump") o.dump_states = nxt();
     else if (k == "--sym") o.sym_mode = nxt();
     else if (k == "--no-inv-oom") o.inv_out_of_model = false;

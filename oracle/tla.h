@@ -25,6 +25,8 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <shared_mutex>
+#include <mutex>
 #include <unordered_map>
 #include <vector>
 
@@ -40,19 +42,39 @@ struct EvalError : std::runtime_error {
 };
 
 // ---- interning of strings and model values (ids are stable per process) ----
+// Thread-safe for the parallel BFS (engine.h, --workers): lookups take a shared lock,
+// insertions an exclusive one, and the name vectors are reserved up front so an
+// insertion never moves the strings other threads are reading by id.
 struct Names {
   std::vector<std::string> str, mv;
   std::unordered_map<std::string, int> str_id, mv_id;
+  std::shared_mutex mu;
+  Names() { str.reserve(1 << 16); mv.reserve(1 << 12); }
   static Names& get() { static Names n; return n; }
+  int intern(std::vector<std::string>& names, std::unordered_map<std::string, int>& ids, const std::string& s) {
+    {
+      std::shared_lock<std::shared_mutex> lk(mu);
+      auto it = ids.find(s);
+      if (it != ids.end()) return it->second;
+    }
+    std::unique_lock<std::shared_mutex> lk(mu);
+    auto it = ids.find(s);
+    if (it != ids.end()) return it->second;
+    if (names.size() == names.capacity()) throw EvalError("too many distinct names");
+    int id = (int)names.size(); names.push_back(s); ids[s] = id; return id;
+  }
+  // per-thread memo in front of the shared table: no shared cache line on the hot path
   int intern_str(const std::string& s) {
-    auto it = str_id.find(s);
-    if (it != str_id.end()) return it->second;
-    int id = (int)str.size(); str.push_back(s); str_id[s] = id; return id;
+    thread_local std::unordered_map<std::string, int> memo;
+    auto it = memo.find(s);
+    if (it != memo.end()) return it->second;
+    return memo[s] = intern(str, str_id, s);
   }
   int intern_mv(const std::string& s) {
-    auto it = mv_id.find(s);
-    if (it != mv_id.end()) return it->second;
-    int id = (int)mv.size(); mv.push_back(s); mv_id[s] = id; return id;
+    thread_local std::unordered_map<std::string, int> memo;
+    auto it = memo.find(s);
+    if (it != memo.end()) return it->second;
+    return memo[s] = intern(mv, mv_id, s);
   }
 };
 

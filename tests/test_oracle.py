@@ -8,6 +8,8 @@ are unpinned against TLC (not runnable offline).
 import json
 import os
 
+import pytest
+
 from oracle_util import CONFIGS, GOLDEN, MEMB_MC, ORIG_MC, golden_file, run_oracle
 
 
@@ -103,3 +105,18 @@ def test_punctuated_search_prefix_fixture_reproduces():
     assert (r["generated"], r["distinct"], r["depth"], r["left_on_queue"]) == \
         (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
     assert r["actions"] == g["actions"]
+
+
+@pytest.mark.parametrize("tla,cfg,extra", [
+    ("orig", "c1.cfg", ()), ("orig", "scenario_first_leader.cfg", ("--trace",)),
+    ("memb", "memb_two.cfg", ("--max-depth", "11", "--trace")),
+])
+def test_oracle_parallel_expansion_is_identical(tla, cfg, extra):
+    """--workers N (the bench's CPU baseline) expands a batch of parents on N threads and merges
+    in frontier order: the result (counts, per-action counts, levels, traces) equals 1 thread."""
+    from oracle_util import MEMB_MC, ORIG_MC, run_oracle
+    spec = ORIG_MC if tla == "orig" else MEMB_MC
+    a = run_oracle("bfs", spec, os.path.join(CONFIGS, cfg), *extra)
+    b = run_oracle("bfs", spec, os.path.join(CONFIGS, cfg), *extra, "--workers", "4")
+    a.pop("seconds"), b.pop("seconds")
+    assert a == b
