@@ -127,8 +127,16 @@ int mc_level_stats(const mc_ctx* ctx, int32_t level, int64_t* states, int64_t* g
  * bytes per SURVEY.md §8d), 0 <= k < number of kernels; MC_E_INVALID past the last one. */
 int mc_kernel_stats(const mc_ctx* ctx, int32_t k, const char** name, double* ms, double* algo_bytes, int64_t* launches);
 
-/* Counterexample (TLC "State k:" blocks) as text; caller frees with mc_free. */
+/* Counterexample (TLC "State k:" blocks) as text; caller frees with mc_free.  Each header is
+ * "State k: <Action line L1, col C1 to line L2, col C2 of module M>" when the action's
+ * definition is found in the spec module or a module it EXTENDS (else "<Action>"). */
 int mc_trace(const mc_ctx* ctx, char** text, size_t* len);
+
+/* TLC's trace-header location of an action (the span of the body of `Action(params) == body`
+ * in the spec module, or in a module it EXTENDS found next to it — the part of TLC's
+ * "State k: <...>" line after the name, e.g. "line 177, col 15 to line 186, col 58 of module raft").
+ * Needs no run.  MC_E_INVALID when no definition is found; caller frees with mc_free. */
+int mc_action_location(const mc_ctx* ctx, const char* action, char** text, size_t* len);
 
 /* TLC's second collision estimate, "based on the actual fingerprints": 1 / (minimum distance
  * between two fingerprints of the seen-set) after a single-GPU mc_run (a sort of the seen-set on

@@ -3,6 +3,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <sstream>
 #include <string>
@@ -11,6 +12,7 @@
 #include "backend.h"
 #include "model.h"
 #include "rccl_api.h"
+#include "tla_value.h"
 
 struct mc_ctx {
   std::unique_ptr<rmc::Backend> be;
@@ -18,6 +20,12 @@ struct mc_ctx {
   rmc::RunResult res;
   bool ran = false;
   std::string last_error, tla_path, cfg_path;
+  mutable std::map<std::string, std::string> action_loc;   // action name -> TLC location text ("" if none)
+  const std::string& location_of(const std::string& act) const {
+    auto it = action_loc.find(act);
+    if (it == action_loc.end()) it = action_loc.emplace(act, rmc::action_location(tla_path, act)).first;
+    return it->second;
+  }
   // RCCL communicator of the native sharded loop, kept across runs of the same job
   ncclComm_t comm = nullptr;
   int comm_rank = -1, comm_world = 0;
@@ -47,10 +55,18 @@ const char* verdict_name(int v) {
   }
   return "?";
 }
-std::string trace_text(const rmc::RunResult& r) {
+// TLC's header: "State k: <Action line L1, col C1 to line L2, col C2 of module M>" when the
+// action's definition is found in the spec module (or a module it EXTENDS), else "<Action>"
+std::string trace_text(const mc_ctx* c, const rmc::RunResult& r) {
   std::ostringstream o;
   for (size_t k = 0; k < r.trace.size(); ++k) {
-    o << "State " << (k + 1) << ": " << (k == 0 ? "<Initial predicate>" : "<" + r.trace[k].first + ">") << "\n";
+    o << "State " << (k + 1) << ": ";
+    if (k == 0) o << "<Initial predicate>";
+    else {
+      const std::string& loc = c->location_of(r.trace[k].first);
+      o << "<" << r.trace[k].first << (loc.empty() ? "" : " " + loc) << ">";
+    }
+    o << "\n";
     o << r.trace[k].second << "\n\n";
   }
   return o.str();
@@ -208,7 +224,7 @@ int mc_kernel_stats(const mc_ctx* c, int32_t k, const char** name, double* ms, d
 int mc_trace(const mc_ctx* c, char** text, size_t* len) {
   if (!c || !text) return MC_E_INVALID;
   if (!c->ran) return MC_E_STATE;
-  *text = dup_text(trace_text(c->res), len);
+  *text = dup_text(trace_text(c, c->res), len);
   return *text ? MC_OK : MC_E_OOM;
 }
 
@@ -220,9 +236,9 @@ int mc_report(const mc_ctx* c, char** text, size_t* len) {
   o << "raftmc (MI355X/gfx950) checking " << c->tla_path << " with " << c->cfg_path << "\n";
   if (r.verdict == MC_VERDICT_INVARIANT_VIOLATION) {
     o << "Error: Invariant " << r.violated << " is violated.\n";
-    o << "Error: The behavior up to this point is:\n" << trace_text(r);
+    o << "Error: The behavior up to this point is:\n" << trace_text(c, r);
   } else if (r.verdict == MC_VERDICT_DEADLOCK) {
-    o << "Error: Deadlock reached.\nError: The behavior up to this point is:\n" << trace_text(r);
+    o << "Error: Deadlock reached.\nError: The behavior up to this point is:\n" << trace_text(c, r);
   } else if (r.verdict == MC_VERDICT_EVAL_ERROR || r.verdict == MC_VERDICT_CAPACITY_OVERFLOW) {
     o << "Error: " << r.error << "\n";
   } else if (r.verdict == MC_VERDICT_OK) {
@@ -242,6 +258,17 @@ int mc_report(const mc_ctx* c, char** text, size_t* len) {
   o << "Finished in " << (long long)(r.seconds_total * 1000.0 + 0.5) << "ms\n";
   o << "Verdict: " << verdict_name(r.verdict) << "\n";
   *text = dup_text(o.str(), len);
+  return *text ? MC_OK : MC_E_OOM;
+}
+
+int mc_action_location(const mc_ctx* c, const char* action, char** text, size_t* len) {
+  if (!c || !action || !text) return MC_E_INVALID;
+  const std::string& loc = c->location_of(action);
+  if (loc.empty()) {
+    const_cast<mc_ctx*>(c)->last_error = std::string("no definition of action ") + action + " in " + c->tla_path + " or the modules it EXTENDS";
+    return MC_E_INVALID;
+  }
+  *text = dup_text(loc, len);
   return *text ? MC_OK : MC_E_OOM;
 }
 

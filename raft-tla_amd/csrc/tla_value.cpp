@@ -224,6 +224,107 @@ std::string find_trace_literal(const std::string& module_path, const std::string
   return "";
 }
 
+namespace {
+
+// offset of the first significant character at or after p (skips blanks, `\*` and nested `(* *)` comments)
+size_t skip_blank(const std::string& t, size_t p) {
+  while (p < t.size()) {
+    if (isspace((unsigned char)t[p])) { ++p; continue; }
+    if (t.compare(p, 2, "\\*") == 0) { p = t.find('\n', p); if (p == std::string::npos) return t.size(); continue; }
+    if (t.compare(p, 2, "(*") == 0) {
+      int depth = 0;
+      while (p < t.size()) {
+        if (t.compare(p, 2, "(*") == 0) { ++depth; p += 2; }
+        else if (t.compare(p, 2, "*)") == 0) { p += 2; if (--depth == 0) break; }
+        else ++p;
+      }
+      continue;
+    }
+    break;
+  }
+  return p;
+}
+
+// offset just past `op` or `op(params)` followed by `==`, for a definition that starts a line
+size_t definition_body(const std::string& t, const std::string& op, size_t& head) {
+  for (size_t at = t.find(op); at != std::string::npos; at = t.find(op, at + 1)) {
+    if (at != 0 && t[at - 1] != '\n') continue;
+    size_t q = at + op.size();
+    if (q < t.size() && (isalnum((unsigned char)t[q]) || t[q] == '_')) continue;
+    while (q < t.size() && (t[q] == ' ' || t[q] == '\t')) ++q;
+    if (q < t.size() && t[q] == '(') {
+      const size_t close = t.find(')', q);
+      if (close == std::string::npos) continue;
+      q = close + 1;
+      while (q < t.size() && (t[q] == ' ' || t[q] == '\t')) ++q;
+    }
+    if (t.compare(q, 2, "==") != 0) continue;
+    head = at;
+    return q + 2;
+  }
+  return std::string::npos;
+}
+
+void line_col(const std::string& t, size_t off, int& line, int& col) {
+  line = 1;
+  size_t ls = 0;
+  for (size_t k = 0; k < off; ++k)
+    if (t[k] == '\n') { ++line; ls = k + 1; }
+  col = (int)(off - ls) + 1;
+}
+
+std::string module_name(const std::string& t) {
+  const size_t at = t.find("MODULE");
+  if (at == std::string::npos) return "";
+  Reader r(t, at + 6);
+  try { return r.ident(); } catch (const CfgError&) { return ""; }
+}
+
+}  // namespace
+
+std::string action_location(const std::string& module_path, const std::string& op, int depth) {
+  std::string t;
+  try { t = read_text_file(module_path); } catch (const CfgError&) { return ""; }
+  size_t head = 0;
+  const size_t eq = definition_body(t, op, head);
+  if (eq == std::string::npos) {
+    if (depth >= 4) return "";
+    for (const auto& m : extends_of(t)) {
+      const std::string loc = action_location(dir_of(module_path) + "/" + m + ".tla", op, depth + 1);
+      if (!loc.empty()) return loc;
+    }
+    return "";
+  }
+  // the unit ends at the next line that starts a definition or a separator
+  size_t unit_end = t.size();
+  for (size_t nl = t.find('\n', head); nl != std::string::npos; nl = t.find('\n', nl + 1)) {
+    const size_t ls = nl + 1;
+    if (ls >= t.size()) break;
+    if (isalpha((unsigned char)t[ls]) || t.compare(ls, 4, "----") == 0 || t.compare(ls, 4, "====") == 0) { unit_end = ls; break; }
+  }
+  const size_t begin = skip_blank(t, eq);
+  if (begin >= unit_end) return "";
+  size_t last = begin;   // last significant character of the body
+  for (size_t p = begin; p < unit_end;) {
+    const size_t q = skip_blank(t, p);
+    if (q >= unit_end) break;
+    if (t[q] == '"') {
+      size_t e = q + 1;
+      while (e < unit_end && t[e] != '"') e += t[e] == '\\' ? 2 : 1;
+      last = std::min(e, unit_end - 1);
+      p = e + 1;
+      continue;
+    }
+    last = q;
+    p = q + 1;
+  }
+  int l0, c0, l1, c1;
+  line_col(t, begin, l0, c0);
+  line_col(t, last, l1, c1);
+  return "line " + std::to_string(l0) + ", col " + std::to_string(c0) + " to line " + std::to_string(l1) + ", col " +
+         std::to_string(c1) + " of module " + module_name(t);
+}
+
 const std::vector<TVal>& trace_global(const TVal& v) {
   if (v.kind == TVal::Seq) return v.elems;
   if (v.kind == TVal::Rec) {

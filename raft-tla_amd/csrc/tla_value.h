@@ -34,6 +34,12 @@ TVal parse_tla_value(const std::string& text);
 // text, or in a module it EXTENDS (looked up as <dir>/<name>.tla, one level); "" if absent.
 std::string find_trace_literal(const std::string& module_path, const std::string& op);
 
+// TLC's trace-header location of action `op`: the span of the body of its definition
+// `op == body` / `op(params) == body`, as "line L1, col C1 to line L2, col C2 of module M"
+// (1-based, end inclusive; comments after the last token excluded).  Looked up in the module,
+// then in the modules it EXTENDS (<dir>/<name>.tla, as TLC resolves them); "" if absent.
+std::string action_location(const std::string& module_path, const std::string& op, int depth = 0);
+
 // The history sequence of a trace value: the value itself if it is a sequence, else its
 // `global` field (throws CfgError(MC_E_PARSE) otherwise).
 const std::vector<TVal>& trace_global(const TVal& v);

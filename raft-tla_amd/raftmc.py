@@ -29,7 +29,7 @@ EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stat
            "mc_shard_level_stats", "mc_shard_level_commit", "mc_shard_read_state", "mc_shard_violation",
            "mc_set_history_prefix", "mc_shard_layout", "mc_shard_select", "mc_shard_event_stats",
            "mc_collision_observed", "mc_rccl_unique_id", "mc_shard_run_rccl",
-           "mc_set_checkpoint", "mc_set_recover"]
+           "mc_set_checkpoint", "mc_set_recover", "mc_action_location"]
 
 
 class McOpts(ctypes.Structure):
@@ -81,6 +81,7 @@ def load_library(path=LIB_PATH):
     for f in ("mc_trace", "mc_report", "mc_describe"):
         getattr(lib, f).argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.mc_dump_states.argtypes = [P, ctypes.c_char_p]
+    lib.mc_action_location.argtypes = [P, ctypes.c_char_p, ctypes.POINTER(P), ctypes.POINTER(ctypes.c_size_t)]
     lib.mc_set_history_prefix.argtypes = [P, ctypes.c_char_p, ctypes.c_char_p]
     lib.mc_collision_observed.argtypes = [P, ctypes.POINTER(ctypes.c_double)]
     lib.mc_set_checkpoint.argtypes = [P, ctypes.c_char_p, ctypes.c_int32]
@@ -161,6 +162,16 @@ class ModelChecker:
         if rc:
             raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
         return v.value
+
+    def action_location(self, action):
+        """TLC's trace-header location of `action` ("line L1, col C1 to line L2, col C2 of module M"),
+        or None when the spec module (and the modules it EXTENDS) holds no definition of it."""
+        p, n = ctypes.c_void_p(), ctypes.c_size_t()
+        if self.lib.mc_action_location(self.h, action.encode(), ctypes.byref(p), ctypes.byref(n)):
+            return None
+        s = ctypes.string_at(p, n.value).decode()
+        self.lib.mc_free(p)
+        return s
 
     def describe(self):
         import json

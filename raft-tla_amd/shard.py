@@ -366,10 +366,14 @@ def _trace(shard, ex, rank, world):
     return trace
 
 
-def trace_text(trace):
+def trace_text(trace, locate=None):
+    """TLC's "State k: <Action line .. of module M>" blocks; `locate(action)` gives the location
+    text (ModelChecker.action_location) or None, which leaves the header as "<Action>"."""
     out = []
     for k, (act, text) in enumerate(trace):
-        out.append("State %d: %s\n%s\n" % (k + 1, "<Initial predicate>" if k == 0 else "<%s>" % act, text))
+        loc = locate(act) if (locate and k) else None
+        head = "<Initial predicate>" if k == 0 else ("<%s %s>" % (act, loc) if loc else "<%s>" % act)
+        out.append("State %d: %s\n%s\n" % (k + 1, head, text))
     return "\n".join(out) + ("\n" if out else "")
 
 
@@ -407,13 +411,13 @@ class ShardedChecker:
             trace = _trace(shard, self.ex, self.rank, self.world)
             res = self.mc.summary()
             if trace:
-                res.trace_text = trace_text(trace)
+                res.trace_text = trace_text(trace, self.mc.action_location)
             return res
         shard = LibShard(self.mc, self.rank, self.world)
         trace = (fifo_sharded_bfs if self.fifo else sharded_bfs)(shard, self.ex, self.rank, self.device)
         res = self.mc.summary()
         if trace:
-            res.trace_text = trace_text(trace)
+            res.trace_text = trace_text(trace, self.mc.action_location)
         return res
 
     def close(self):

@@ -177,3 +177,39 @@ def test_checkpoint_api_scope(raftmc):
         mc.set_checkpoint("/tmp/x.ckpt", 2)
         mc.set_checkpoint(None)
         mc.set_recover(None)
+
+
+def test_action_location_in_extended_module(raftmc, tmp_path):
+    """TLC's trace header names the action and the span of its definition body
+    ("line L1, col C1 to line L2, col C2 of module M"): found through the wrapper's
+    `EXTENDS raft`, parameters and `==` skipped, comments after the last token excluded."""
+    wrapper = tmp_path / "raft_original_mc.tla"
+    wrapper.write_text(open(ORIG_MC).read())
+    (tmp_path / "raft.tla").write_text(
+        "------ MODULE raft ------\n"                                  # 1
+        "\\* Server i times out.\n"                                     # 2
+        "Timeout(i) == /\\ state[i] = Follower\n"                       # 3
+        "              \\* a comment inside the body\n"                 # 4
+        "              /\\ UNCHANGED <<log>> \\* trailing comment\n"    # 5
+        "\n"                                                            # 6
+        "\\* next unit\n"                                               # 7
+        "Restart(i) ==\n"                                               # 8
+        "    /\\ state' = [state EXCEPT ![i] = Follower]\n"             # 9
+        "    (* block\n"                                                # 10
+        "       comment *)\n"                                           # 11
+        "----\n"                                                        # 12
+        "RestartAll == \\A i \\in Server : Restart(i)\n"                # 13
+        "====\n")
+    with raftmc.ModelChecker(str(wrapper), os.path.join(CONFIGS, "c1.cfg")) as mc:
+        assert mc.action_location("Timeout") == "line 3, col 15 to line 5, col 34 of module raft"
+        assert mc.action_location("Restart") == "line 9, col 5 to line 9, col 46 of module raft"
+        assert mc.action_location("RestartAll") == "line 13, col 15 to line 13, col 42 of module raft"
+        assert mc.action_location("Rest") is None            # a prefix of a defined name is not a definition
+        assert mc.action_location("BoundedTerms") == "line 17, col 17 to line 17, col 59 of module raft_original_mc"
+
+
+def test_action_location_without_module(raftmc):
+    """configs/ holds no raft.tla: headers stay "<Action>" and the lookup reports absence."""
+    with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c1.cfg")) as mc:
+        assert mc.action_location("Timeout") is None
+        assert "Timeout" in mc.lib.mc_last_error(mc.h).decode()

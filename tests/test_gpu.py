@@ -64,6 +64,33 @@ def test_violation_shortest_trace(raftmc):
     assert "<BecomeLeader>" in states[-1].split("\n")[0] and "Leader" in states[-1]
 
 
+def test_trace_headers_carry_action_locations(raftmc, tmp_path):
+    """TLC's "State k: <Action line L1, col C1 to line L2, col C2 of module M>" headers: with the
+    spec module next to the wrapper (as TLC resolves EXTENDS), every step names the span of its
+    action's definition body; the action sequence is that of the run without the module."""
+    wrapper = tmp_path / "raft_original_mc.tla"
+    wrapper.write_text(open(ORIG_MC).read())
+    with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c1.cfg")) as mc:
+        names = mc.describe()["actions"]
+    body = ["------ MODULE raft ------"]
+    for a in names:                                   # action a's body is the whole of line 2k+2
+        body += ["\\* %s" % a, "%s(i) == TRUE" % a]
+    (tmp_path / "raft.tla").write_text("\n".join(body + ["===="]) + "\n")
+    cfg = os.path.join(CONFIGS, "scenario_first_leader.cfg")
+    plain = raftmc.check(ORIG_MC, cfg, **SMALL)
+    r = raftmc.check(str(wrapper), cfg, **SMALL)
+    heads = [b.split("\n")[0] for b in r.trace_text.strip().split("\n\n")]
+    plain_heads = [b.split("\n")[0] for b in plain.trace_text.strip().split("\n\n")]
+    assert len(heads) == len(plain_heads) == 10 and heads[0] == plain_heads[0]
+    for k, (h, p) in enumerate(zip(heads[1:], plain_heads[1:])):
+        act = p[len("State %d: <" % (k + 2)):-1]
+        line = 2 * names.index(act) + 3
+        col = len(act) + 8                            # after "Act(i) == "
+        assert h == "State %d: <%s line %d, col %d to line %d, col %d of module raft>" % (
+            k + 2, act, line, col, line, col + 3)
+    assert heads[-1] in r.report
+
+
 def test_seed_independence_c1(raftmc):
     cfg = os.path.join(CONFIGS, "c1.cfg")
     a = raftmc.check(ORIG_MC, cfg, seed=1, **SMALL)
