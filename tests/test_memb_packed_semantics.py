@@ -28,8 +28,10 @@ def build_harness(shape):
            os.path.join(csrc, "memb_model.cpp"), os.path.join(csrc, "tla_value.cpp")]
     deps = src + [os.path.join(csrc, f) for f in ("memb_spec.h", "memb_text.h", "memb_prefix.h", "tla_value.h", "common.h")]
     if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(p) for p in deps):
-        subprocess.run(["g++", "-O2", "-std=c++17", "-DSHAPE_N=%d" % shape[0], "-DSHAPE_NV=%d" % shape[1], "-o", out, *src],
+        tmp = "%s.%d" % (out, os.getpid())    # build aside and rename: parallel workers never run a partial file
+        subprocess.run(["g++", "-O2", "-std=c++17", "-DSHAPE_N=%d" % shape[0], "-DSHAPE_NV=%d" % shape[1], "-o", tmp, *src],
                        check=True)
+        os.replace(tmp, out)
     return out
 
 

@@ -25,7 +25,9 @@ def build_harness(shape):
     if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(p) for p in src + [
             os.path.join(ROOT, "raft-tla_amd", "csrc", "orig_spec.h")]):
         defs = ["-DSHAPE_%s=%d" % (k, v) for k, v in zip(("N", "NV", "MT", "ML", "MK"), shape)]
-        subprocess.run(["g++", "-O2", "-std=c++17", *defs, "-o", out, *src], check=True)
+        tmp = "%s.%d" % (out, os.getpid())    # build aside and rename: parallel workers never run a partial file
+        subprocess.run(["g++", "-O2", "-std=c++17", *defs, "-o", tmp, *src], check=True)
+        os.replace(tmp, out)
     return out
 
 
