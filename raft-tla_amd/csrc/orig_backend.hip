@@ -332,8 +332,13 @@ __global__ void __launch_bounds__(BS) orig_materialize(MatArgs a) {
 }
 
 // after a chunk's materialize: the level's running count of new states
+// after a chunk's materialize: fold its new-state count into the level's and re-arm the chunk
+// counter for the next chunk (the level's first chunk starts from the per-level counter reset)
 __global__ void orig_advance(unsigned long long* ctr) {
-  if (threadIdx.x == 0) ctr[K_LEVEL_NEW] += ctr[K_CHUNK_NEW];
+  if (threadIdx.x == 0) {
+    ctr[K_LEVEL_NEW] += ctr[K_CHUNK_NEW];
+    ctr[K_CHUNK_NEW] = 0;
+  }
 }
 
 // ------------------------------------------------------------------ sharded (multi-GPU) kernels
@@ -728,7 +733,6 @@ class OrigGpu : public Backend {
         const unsigned nblk = (unsigned)((cnt + BS - 1) / BS);
         if (int rc = lvl_events(nch)) { err = "hipEventCreate failed"; return rc; }
         hipEvent_t* e = &lvl_ev_[6 * nch];
-        HIPCHK(hipMemsetAsync(d_ctr_ + K_CHUNK_NEW, 0, 8, stream_));
         GenArgs g;
         // kernels index the device store (global id - base_); parent pointers are global
         g.states = d_states_; g.chunk_begin = cb - base_; g.chunk_count = cnt; g.cand = d_cand_; g.seed = r.seed; g.rt = m_.rt;
