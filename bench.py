@@ -70,6 +70,8 @@ def main():
     # 25.2k distinct/s vs 1 thread 35.6k distinct/s); the fastest configuration is reported
     ap.add_argument("--cpu-workers", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fp-table-bytes", type=int, default=0, help="seen-set bytes (0 = library default)")
+    ap.add_argument("--state-store-bytes", type=int, default=0, help="state store bytes (0 = library default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_r01.json"))
     args = ap.parse_args()
@@ -90,7 +92,8 @@ def main():
         shard = importlib.import_module("raft-tla_amd.shard")
         mc = shard.ShardedChecker(TLA, args.config, rank, world, device_index=local, seed=0x5EED)
     else:
-        mc = mod.ModelChecker(TLA, args.config, device=local, seed=0x5EED)
+        mc = mod.ModelChecker(TLA, args.config, device=local, seed=0x5EED, fp_table_bytes=args.fp_table_bytes,
+                              state_store_bytes=args.state_store_bytes)
 
     def barrier_sync():
         if dist is not None:

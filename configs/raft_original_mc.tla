@@ -36,4 +36,10 @@ LogMatching ==
 
 \* Test-only scenario invariant (a reachable "violation"): no leader ever.
 NoLeader == ~ \E i \in Server : state[i] = Leader
+
+\* Test-only scenario invariant reached only after a full replication round trip
+\* (AppendEntries, HandleAppendEntriesRequest, HandleAppendEntriesResponse,
+\* AdvanceCommitIndex): no server ever commits.  Its counterexamples exercise the
+\* TLC order of every message type.
+NoCommit == \A i \in Server : commitIndex[i] = 0
 ===============================================================================

@@ -323,10 +323,16 @@ inline Result bfs(const Spec& sp, const Cfg& cfg, const Options& o) {
           for (size_t fi = b0; fi < b1; ++fi) {
             PRec& pr = recs[fi - b0];
             const int64_t idx = frontier[fi];
-            if (pr.err) throw EvalError(pr.errmsg);
+            if (pr.err) {
+              r.verdict = "EVAL_ERROR"; r.error = pr.errmsg; build_trace(idx, -1, nullptr);
+              r.left_on_queue = (int64_t)(frontier.size() - fi - 1 + nextf.size());
+              goto finish;
+            }
             r.generated += (int64_t)pr.succ.size();
             if (pr.succ.empty() && o.check_deadlock) {
-              r.verdict = "DEADLOCK"; build_trace(idx, -1, nullptr); goto finish;
+              r.verdict = "DEADLOCK"; build_trace(idx, -1, nullptr);
+              r.left_on_queue = (int64_t)(frontier.size() - fi - 1 + nextf.size());
+              goto finish;
             }
             for (auto& su : pr.succ) {
               r.act_generated[su.action]++;
@@ -341,7 +347,14 @@ inline Result bfs(const Spec& sp, const Cfg& cfg, const Options& o) {
                 }
               }
               if (isnew || (!su.im && o.inv_out_of_model)) {
-                if (!su.bad_err.empty()) throw EvalError(su.bad_err);
+                if (!su.bad_err.empty()) {
+                  r.verdict = "EVAL_ERROR"; r.error = su.bad_err;
+                  if (isnew) build_trace((int64_t)store.size() - 1, -1, nullptr);
+                  else build_trace(idx, su.action, &su.s);
+                  r.depth = level + 1;
+                  r.left_on_queue = (int64_t)(frontier.size() - fi - 1 + nextf.size());
+                  goto finish;
+                }
                 if (!su.bad.empty()) {
                   r.verdict = "INVARIANT_VIOLATION"; r.violated = su.bad;
                   if (isnew) build_trace((int64_t)store.size() - 1, -1, nullptr);
@@ -366,10 +379,19 @@ inline Result bfs(const Spec& sp, const Cfg& cfg, const Options& o) {
         int64_t idx = frontier[fi];
         State cur = store[idx];
         succs.clear();
-        sp.next(cur, succs);
+        // TLC evaluation error while computing the successors: the search stops at this parent,
+        // with the behaviour up to it as the trace ([ext]: TLC prints "The behavior up to this
+        // point is:" and the summary lines)
+        try { sp.next(cur, succs); } catch (const EvalError& e) {
+          r.verdict = "EVAL_ERROR"; r.error = e.what(); build_trace(idx, -1, nullptr);
+          r.left_on_queue = (int64_t)(frontier.size() - fi - 1 + nextf.size());
+          goto finish;
+        }
         r.generated += (int64_t)succs.size();
         if (succs.empty() && o.check_deadlock) {
-          r.verdict = "DEADLOCK"; build_trace(idx, -1, nullptr); goto finish;
+          r.verdict = "DEADLOCK"; build_trace(idx, -1, nullptr);
+          r.left_on_queue = (int64_t)(frontier.size() - fi - 1 + nextf.size());
+          goto finish;
         }
         for (auto& su : succs) {
           r.act_generated[su.action]++;
@@ -386,7 +408,15 @@ inline Result bfs(const Spec& sp, const Cfg& cfg, const Options& o) {
             }
           }
           if (isnew || (!im && o.inv_out_of_model)) {
-            auto bad = check_inv(su.s);
+            std::string bad;
+            try { bad = check_inv(su.s); } catch (const EvalError& e) {   // error evaluating an invariant
+              r.verdict = "EVAL_ERROR"; r.error = e.what();
+              if (isnew) build_trace((int64_t)store.size() - 1, -1, nullptr);
+              else build_trace(idx, su.action, &su.s);
+              r.depth = level + 1;
+              r.left_on_queue = (int64_t)(frontier.size() - fi - 1 + nextf.size());
+              goto finish;
+            }
             if (!bad.empty()) {
               r.verdict = "INVARIANT_VIOLATION"; r.violated = bad;
               if (isnew) build_trace((int64_t)store.size() - 1, -1, nullptr);

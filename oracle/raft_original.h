@@ -327,6 +327,10 @@ struct RaftOriginal : Spec {
       for (auto& i : Server->a) if (eq(ap(s[state], i), Leader)) return false;
       return true;
     }
+    if (n == "NoCommit") {            // test-only scenario invariant: \A i : commitIndex[i] = 0
+      for (auto& i : Server->a) if (as_int(ap(s[commitIndex], i)) != 0) return false;
+      return true;
+    }
     throw EvalError("unknown invariant " + n);
   }
 };

@@ -1,28 +1,41 @@
 // raftmc — gfx950 BFS backend for thirdparty/raft_original.tla.
 //
-// One BFS level is processed in frontier chunks; each chunk runs three
-// kernels on one stream:
+// TLC's single-worker FIFO order, reproduced on a data-parallel GPU.  Every successor has the
+// key  (global id of its parent) << 8 | instance,  where the instance index is its position in
+// TLC's enumeration of the Next disjuncts (raft_original.tla:453-462; the order-preserving
+// message codes of orig_spec.h make bag slot order the order of `\E m \in DOMAIN messages`).
+// States are stored level by level in key order, so parent ids increase in FIFO order and the
+// key is globally monotone over the whole search: the seen-set keeps the MINIMUM key per
+// fingerprint (16-B entries {fp, ~key}, atomicMax on the complement), i.e. TLC's first-found
+// parent, and every count, parent pointer, counterexample and stop point is TLC's.
 //
-//  1. orig_generate  (compute): one lane per frontier state, a wave-uniform
-//     loop over the Next relation's action instances (every lane of a wave
-//     runs the same action code on a different state); constraint filter,
-//     TLC generated counts, out-of-model invariants (TLC semantics, [ext]
-//     switch), canonical pack and FP64 of each in-model successor into the
-//     slot array cand[block][instance][lane] (0 = none): coalesced, no atomics.
-//  2. orig_dedup_blk (HBM random access): workgroup b takes generate
-//     workgroup b's 256 parents, one per thread: coalesced slot loads, a
-//     workgroup-local LDS fingerprint set drops the successors the 256
-//     parents produce more than once (diamonds of commuting actions), the
-//     rest probe the seen-set 16 at a time (lock-free open addressing over u64
-//     fingerprints, linear probing, CAS insert); new states are numbered in
-//     (parent, instance) order with one global atomic per workgroup, so the
-//     next level is parent-major and its diamonds land in one workgroup again.
-//  3. orig_materialize: one lane per new state re-derives it from
-//     (parent, instance), stores the packed state + parent pointer into the
-//     HBM-resident state store and checks the invariants.
+// One BFS level is processed in frontier chunks; each chunk runs on one stream:
 //
-// All distinct states stay resident in HBM; counterexamples are read back by
-// chasing parent pointers (no host replay).
+//  1. orig_generate  (compute): one lane per frontier state, a wave-uniform loop over the
+//     action instances; constraint filter, TLC generated counts, out-of-model invariants (TLC
+//     semantics, [ext] switch), canonical pack and FP64 of each in-model successor.  The
+//     workgroup's in-model successors are compacted (wave ballot + one LDS atomic per wave and
+//     instance) into its own record region: fp (8 B) + local key lane << 8 | instance (2 B).
+//  2. orig_dedup     (HBM random access): workgroup b takes generate-workgroup b's records; a
+//     workgroup-local LDS set {fp, min local key} merges the successors its 256 parents produce
+//     more than once (diamonds of commuting actions, ~half of C2's), then every distinct fp of
+//     the set probes the seen-set, 16 in flight per thread (lock-free linear probing over 16-B
+//     entries, CAS insert of the fp, atomicMax of ~key).  Inserted entries' positions are
+//     appended (one global atomic per workgroup).
+//  3. orig_mark      lane per inserted entry: its final key names TLC's first-found producer;
+//     set that (parent, instance) bit of the winner mask, count per workgroup of parents.
+//  4. orig_scan      exclusive scan of the per-workgroup winner counts (one workgroup).
+//  5. orig_materialize workgroup per 256 parents: winners in key order (parent-major, instance
+//     order), re-derived from (parent, instance), stored with their parent pointers at their
+//     FIFO position; invariants of the new states.
+//  6. orig_advance   the level's running count of new states.
+//
+// The first *event* of a level in key order — a TLC evaluation error while computing a
+// parent's successors, a deadlock, an invariant violation (new or out-of-model successor) — is
+// a 64-bit atomicMin of key << 2 | kind; the host re-derives that successor with the same
+// spec code and reproduces TLC's stop point (generated / distinct / per-action counts /
+// left-on-queue) and counterexample.  All distinct states stay resident in HBM (completed
+// levels spill to host memory when the store fills); traces chase parent pointers.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -44,77 +57,67 @@
 namespace rmc {
 
 enum {
-  K_NEW = 0, K_GEN_IN = 1, K_ERR = 2, K_VIOL = 3, K_ERRGID = 4, K_DEADLOCK = 5, K_CHUNK_NEW = 6, K_LEVEL_NEW = 7,
-  K_ACT = 8, K_NCTR = K_ACT + 2 * OA_NACT
+  K_NEW = 0, K_GEN_IN = 1, K_ERR = 2, K_EVENT = 3, K_ERRGID = 4, K_INS = 5, K_CHUNK_NEW = 6, K_LEVEL_NEW = 7,
+  K_ACT = 8, K_PROF = K_ACT + 2 * OA_NACT, K_NCTR = K_PROF + 8   // K_PROF: phase timers (RAFTMC_PROF)
 };
+enum { EV_NEXT_ERROR = 0, EV_DEADLOCK = 1, EV_INV_ERROR = 2, EV_VIOLATION = 3 };
 enum { OE_CAP_STORE = 0x100, OE_TABLE_FULL = 0x200 };
-constexpr int DEDUP_PER = 16;      // slots per dedup thread (independent probes in flight)
-constexpr int BS = 256;            // workgroup size of every kernel (4 waves)
+#ifndef RMC_DEDUP_PER
+#define RMC_DEDUP_PER 8
+#endif
+#ifndef RMC_LDS_SLOTS
+#define RMC_LDS_SLOTS 4096
+#endif
+constexpr int DEDUP_PER = RMC_DEDUP_PER;      // probes in flight per dedup thread
+constexpr int BS = 256;                       // workgroup size of every kernel (4 waves)
+constexpr int LDS_FP_SLOTS = RMC_LDS_SLOTS;   // workgroup-local fingerprint set (8 B fp + 4 B key per slot)
+constexpr int MAT_CAP = 2048;      // winners staged in LDS per materialize round
+constexpr int SCAN_BS = 1024;      // orig_scan workgroup
 
-template <class S>
-struct ViolRec {
-  u64 parent;
-  u32 act, inst, bad, inmodel;
-  typename S::Work w;
-};
+// 64-bit event word: key << 2 | kind, key = parent gid << 8 | instance (gid < 2^40)
+RMC_HD u64 ev_word(u64 gid, u32 inst, u32 kind) { return (((gid << 8) | (u64)inst) << 2) | (u64)kind; }
 
 struct GenArgs {
-  const u32* states;           // [cap][NWP]
-  u64 chunk_begin, chunk_count;
-  u64* cand;                   // [NI][chunk_count] fingerprints, 0 = none
+  const u32* states;           // device store [cap][NWP]
+  u64 chunk_begin, chunk_count;   // device index of the chunk's first parent, parents
+  u64 gid0;                    // global id of the chunk's first parent
+  u64* rfp;                    // [nblk][BS * NI] fingerprints of in-model successors (per-workgroup region)
+  unsigned short* rkey;        // [nblk][BS * NI] local key: lane << 8 | instance
+  u32* rcnt;                   // [nblk] records per workgroup
   u64 seed;
   OrigRuntime rt;
-  u32 inv_oom;
+  u32 inv_oom, deadlock;
   unsigned long long* ctr;
-  void* viol;
 };
 
 // One lane per frontier state, a wave-uniform loop over the action instances; successor,
 // constraints, TLC generated counts, out-of-model invariants, canonical pack and FP64 in one
-// pass; fingerprint slots written coalesced.  (A split expand + full-lane fingerprint
-// pipeline measured 51.4 vs 49.4 ms/run on C2: apply, not the pack + hash, dominates this
-// spec, so the split does not pay here.  Unrolling the ~50-instance loop is refused by the
-// compiler at this body size.)
-// PM (single-GPU pipeline): slots laid out per workgroup, cand[(block * NI + instance) * BS +
-// lane] (coalesced stores), consumed by orig_dedup_blk one parent per thread, so the next level
-// comes out parent-major (siblings adjacent) and the dedup workgroup can drop the successors its
-// 256 parents produce more than once before they cost a seen-set probe.
-//
-// Workgroup-local fingerprint set (LDS): answers only "certainly produced here before"; when
-// its probe window is full the successor goes to the global seen-set as usual.  A lane's
-// "produced before" answer is only ever about an fp it reads back equal, so races (plain loads
-// and stores, no atomics) can cost a probe but never lose a state.
-constexpr int LDS_FP_SLOTS = 4096;   // 32 KB per workgroup
-RMC_HD bool lds_first(unsigned long long* set, u64 fp) {
-  // plain LDS loads and stores, no atomics: a race between two lanes can only make the set
-  // forget an entry or let a duplicate through to the seen-set, never drop a new state
-  u32 h = (u32)(fp >> 20) & (LDS_FP_SLOTS - 1);
-#pragma unroll 1
-  for (int p = 0; p < 8; ++p) {
-    const unsigned long long cur = set[h];
-    if (cur == fp) return false;            // produced here before
-    if (cur == 0ull) { set[h] = fp; return true; }
-    h = (h + 1) & (LDS_FP_SLOTS - 1);
-  }
-  return true;                              // window full: let the seen-set decide
-}
-
-template <class S, bool PM>
+// pass.  (A split expand + full-lane fingerprint pipeline measured 51.4 vs 49.4 ms/run on C2:
+// apply, not the pack + hash, dominates this spec.  Unrolling the ~50-instance loop is refused
+// by the compiler at this body size.)  In-model successors leave as compacted records: per
+// instance a wave ballot, one LDS atomic per wave for the base, and consecutive stores
+// (only ~21% of C2's instance slots carry an in-model successor).
+template <class S>
 // 3 waves per SIMD (<= 168 VGPRs) measured fastest for C2's expand (19.9 vs 22.3 ms without the
 // hint, 26.6 ms at the 2 waves the incremental fingerprint would otherwise get); larger states
 // (C5: 24 words) would spill at 3 and get no hint.
-__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 16 ? 3 : 1))) orig_generate(GenArgs a) {
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 15 ? 3 : 1))) orig_generate(GenArgs a) {
   using W = typename S::Work;
   constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
-  __shared__ unsigned int lds_cnt[OA_NACT + 1];
-  for (int t = threadIdx.x; t < OA_NACT + 1; t += BS) lds_cnt[t] = 0;
+  __shared__ unsigned int lds_cnt[OA_NACT + 2];   // per-action generated, in-model total, record count
+  for (int t = threadIdx.x; t < OA_NACT + 2; t += BS) lds_cnt[t] = 0;
   __syncthreads();
   const u64 tid = (u64)blockIdx.x * BS + threadIdx.x;
   const bool active = tid < a.chunk_count;
-  const u64 gid = a.chunk_begin + tid;
+  const u64 gid = a.gid0 + tid;
+  const int lane = __lane_id();
+  const u64 lanes_below = (1ull << lane) - 1ull;
+  u64* rfp = a.rfp + (u64)blockIdx.x * (BS * S::NI);
+  unsigned short* rkey = a.rkey + (u64)blockIdx.x * (BS * S::NI);
   W s;
   u64 al[S::AW];
   u32 err = 0, nsucc = 0, nin = 0;
+  unsigned long long ev = ~0ull;
   // the parent's packed words with allLogs' (every successor carries allLogs \cup {log[i]},
   // raft_original.tla:464) and their fingerprint terms: successors re-hash changed words only
   // (C5-sized states keep the plain hash: the base terms would cost them occupancy, measured
@@ -124,7 +127,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
   FpBase<INC ? NW : 2> fb;
   if (active) {
     u32 w[NWP];
-    const uint4* src = reinterpret_cast<const uint4*>(a.states + gid * NWP);
+    const uint4* src = reinterpret_cast<const uint4*>(a.states + (a.chunk_begin + tid) * NWP);
 #pragma unroll
     for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
     S::unpack(w, s);
@@ -144,6 +147,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
 #pragma unroll 1
   for (int k = 0; k < S::NI; ++k) {
     u64 fp = 0;
+    bool have = false;
     if (active) {
       W t;
       const int act = S::apply(s, k, t, err);
@@ -154,191 +158,460 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
         atomicAdd(&lds_cnt[act], 1u);
         if (S::in_model(t, a.rt)) {
           ++nin;
+          have = true;
           u32 pw[NW];
           S::pack(t, pw);
           if constexpr (INC) fp = fb.fp(pw, bw, a.seed);
           else fp = fp64(pw, a.seed);
-        } else if (a.inv_oom) {
-          const u32 bad = S::violated(t, a.rt.invariants);
-          if (bad && atomicCAS(&a.ctr[K_VIOL], 0ull, 1ull) == 0ull) {
-            ViolRec<S>* v = reinterpret_cast<ViolRec<S>*>(a.viol);
-            v->parent = gid; v->act = (u32)act; v->inst = (u32)k; v->bad = bad; v->inmodel = 0; v->w = t;
-          }
+        } else if (a.inv_oom && S::violated(t, a.rt.invariants)) {
+          // TLC checks invariants on out-of-model successors ([ext] switch (ii)); first in key order wins
+          const u64 e = ev_word(gid, (u32)k, EV_VIOLATION);
+          ev = e < ev ? e : ev;
         }
       }
-      a.cand[PM ? ((u64)blockIdx.x * S::NI + (u64)k) * BS + threadIdx.x : (u64)k * a.chunk_count + tid] = fp;
+    }
+    const u64 mask = __ballot(have);
+    if (mask) {
+      const int leader = __ffsll((unsigned long long)mask) - 1;
+      unsigned int base = 0;
+      if (lane == leader) base = atomicAdd(&lds_cnt[OA_NACT + 1], (unsigned int)__popcll(mask));   // LDS: no global contention
+      base = __shfl(base, leader);
+      if (have) {
+        const unsigned int idx = base + (unsigned int)__popcll(mask & lanes_below);
+        rfp[idx] = fp;
+        rkey[idx] = (unsigned short)((threadIdx.x << 8) | (unsigned)k);
+      }
     }
   }
-  if (active && nsucc == 0) atomicCAS(&a.ctr[K_DEADLOCK], 0ull, (unsigned long long)(gid + 1));
-  if (err) {
-    atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+  if (active) {
+    if (err & OE_EVAL_LOG_INDEX) { const u64 e = ev_word(gid, 0, EV_NEXT_ERROR); ev = e < ev ? e : ev; }
+    if (nsucc == 0 && a.deadlock) { const u64 e = ev_word(gid, 0, EV_DEADLOCK); ev = e < ev ? e : ev; }
+  }
+  const u32 cap_err = err & ~(u32)OE_EVAL_LOG_INDEX;   // compiled-capacity limits, not TLC semantics
+  if (cap_err) {
+    atomicOr(&a.ctr[K_ERR], (unsigned long long)cap_err);
     atomicCAS(&a.ctr[K_ERRGID], 0ull, (unsigned long long)(gid + 1));
   }
+  if (ev != ~0ull) atomicMin(&a.ctr[K_EVENT], ev);
   if (nin) atomicAdd(&lds_cnt[OA_NACT], nin);
   __syncthreads();
   for (int t = threadIdx.x; t < OA_NACT; t += BS)
     if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + t], (unsigned long long)lds_cnt[t]);
-  if (threadIdx.x == 0 && lds_cnt[OA_NACT]) atomicAdd(&a.ctr[K_GEN_IN], (unsigned long long)lds_cnt[OA_NACT]);
+  if (threadIdx.x == 0) {
+    if (lds_cnt[OA_NACT]) atomicAdd(&a.ctr[K_GEN_IN], (unsigned long long)lds_cnt[OA_NACT]);
+    a.rcnt[blockIdx.x] = lds_cnt[OA_NACT + 1];
+  }
 }
 
-
-struct DedupArgs {
-  const u64* cand;
-  u64 nslots, chunk_begin, chunk_count, ni;   // ni: instances per state (parent-major slot layout)
-  u64* table;
-  u64 table_mask;
-  u64* newrec;                 // (parent gid << 8 | instance), compacted
-  unsigned long long* ctr;
-};
-
-// Seen-set insertion for the PM layout: workgroup b takes generate-workgroup b's slots, one
-// parent per thread; its NI slot loads are coalesced across the wave, its probes go out in
-// groups of 16, and its new states are numbered in (parent, instance) order by a workgroup scan
-// and one global atomic, so the next level is parent-major.
-template <int NI>
-__global__ void __launch_bounds__(BS) orig_dedup_blk(DedupArgs a) {
-  static_assert(NI <= 128, "new-state bits are two u64 per parent");
-  __shared__ unsigned int wave_tot[BS / 64];
-  __shared__ unsigned long long base_sh;
-  __shared__ unsigned long long lds_fp[LDS_FP_SLOTS];
-  for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lds_fp[t] = 0ull;
-  __syncthreads();
-  const int lane = __lane_id(), wave = threadIdx.x >> 6;
-  const u64 st = (u64)blockIdx.x * BS + threadIdx.x;
-  const u64* row = a.cand + (u64)blockIdx.x * NI * BS + threadIdx.x;
-  u64 isnew = 0, isnew_hi = 0;   // instances 0..63 / 64..127 (the latter only for NI > 64, e.g. N = 5)
-  auto mark = [&](int k) { if (NI <= 64 || k < 64) isnew |= 1ull << (k & 63); else isnew_hi |= 1ull << (k & 63); };
-  u32 err = 0;
-  constexpr int G = 16;
-#pragma unroll 1
-  for (int k0 = 0; k0 < NI; k0 += G) {
-    u64 fp[G], cur[G];
+// ------------------------------------------------------------------ seen-set probing
+// The seen-set: 2^k entries of 16 B {fp, ~key} (0 = empty), linear probing.  probe_batch inserts
+// or finds G fingerprints at once (independent probes in flight), then lowers each entry's key
+// to the given one (atomicMax of the complement; a key only ever decreases, so an entry that
+// already holds a smaller key needs no atomic: the common case, a duplicate of an older state).
+// ins bit j = this call inserted fp[j]; pos[j] = its entry index.
+template <int G, bool KEYED = true>
+__device__ __forceinline__ u32 probe_batch(u64* table, u64 mask, const u64 (&fp)[G], const u64 (&nk)[G], u64 (&pos)[G], u32& err) {
+  u64 cur[G], cnk[G];
 #pragma unroll
-    for (int j = 0; j < G; ++j) fp[j] = (st < a.chunk_count && k0 + j < NI) ? row[(u64)(k0 + j) * BS] : 0ull;
+  for (int j = 0; j < G; ++j) {
+    pos[j] = fp[j] & mask;
+    if (fp[j]) {
+      const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(table + 2 * pos[j]);
+      cur[j] = e.x; cnk[j] = e.y;
+    } else {
+      cur[j] = ~0ull; cnk[j] = ~0ull;
+    }
+  }
+  u32 ins = 0, lower = 0;
 #pragma unroll
-    for (int j = 0; j < G; ++j)   // diamonds of commuting actions: ~half of C2's successors within 256 parents
-      if (fp[j] && !lds_first(lds_fp, fp[j])) fp[j] = 0;
+  for (int j = 0; j < G; ++j)
+    if (fp[j] && cur[j] == 0ull) {
+      cur[j] = (u64)atomicCAS((unsigned long long*)&table[2 * pos[j]], 0ull, (unsigned long long)fp[j]);
+      if (cur[j] == 0ull) { ins |= 1u << j; lower |= 1u << j; }
+      else if (cur[j] == fp[j]) lower |= 1u << j;     // raced with another inserter of the same fp
+    }
 #pragma unroll
-    for (int j = 0; j < G; ++j) cur[j] = fp[j] ? a.table[fp[j] & a.table_mask] : ~0ull;
-#pragma unroll
-    for (int j = 0; j < G; ++j)
-      if (fp[j] && cur[j] == 0ull)
-        cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[fp[j] & a.table_mask], 0ull, (unsigned long long)fp[j]);
+  for (int j = 0; j < G; ++j) {
+    if (!fp[j] || ((lower >> j) & 1u)) continue;
+    if (cur[j] == fp[j]) { if (KEYED && cnk[j] < nk[j]) lower |= 1u << j; continue; }
+    u64 slot = (pos[j] + 1) & mask;
+    for (u64 probe = 0;; ++probe) {
+      if (probe > mask || probe >= (1u << 20)) { err |= OE_TABLE_FULL; break; }   // visited every entry
+      const u64 c = table[2 * slot];
+      if (c == fp[j]) { lower |= 1u << j; break; }
+      if (c == 0ull) {
+        const u64 old = (u64)atomicCAS((unsigned long long*)&table[2 * slot], 0ull, (unsigned long long)fp[j]);
+        if (old == 0ull) { ins |= 1u << j; lower |= 1u << j; break; }
+        if (old == fp[j]) { lower |= 1u << j; break; }
+      }
+      slot = (slot + 1) & mask;
+    }
+    pos[j] = slot;
+  }
+  if (KEYED) {
+#if defined(RMC_EXP_NOKEY)
+    (void)lower;
+#elif defined(RMC_EXP_PLAINKEY)
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-      if (!fp[j]) continue;
-      if (cur[j] == 0ull) { mark(k0 + j); continue; }
-      if (cur[j] == fp[j]) continue;
-      u64 slot = (fp[j] + 1) & a.table_mask;
-      for (int probe = 0;; ++probe) {
-        if (probe >= (1 << 20)) { err |= OE_TABLE_FULL; break; }
-        const u64 c = a.table[slot];
-        if (c == fp[j]) break;
-        if (c == 0ull) {
-          const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[slot], 0ull, (unsigned long long)fp[j]);
-          if (old == 0ull) { mark(k0 + j); break; }
-          if (old == fp[j]) break;
-        }
-        slot = (slot + 1) & a.table_mask;
+      if ((ins >> j) & 1u) table[2 * pos[j] + 1] = nk[j];
+      else if ((lower >> j) & 1u) atomicMax((unsigned long long*)&table[2 * pos[j] + 1], (unsigned long long)nk[j]);
+    }
+#else
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+      if ((lower >> j) & 1u) atomicMax((unsigned long long*)&table[2 * pos[j] + 1], (unsigned long long)nk[j]);
+#endif
+  }
+  return ins;
+}
+
+// one workgroup-wide exclusive scan of per-thread counts; returns this thread's offset, *total
+__device__ __forceinline__ u32 block_excl_scan(u32 mine, u32* wave_tot, u32* total) {
+  const int lane = __lane_id(), wave = threadIdx.x >> 6;
+  u32 incl = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) { const u32 v = __shfl_up(incl, d); if (lane >= d) incl += v; }
+  if (lane == 63) wave_tot[wave] = incl;
+  __syncthreads();
+  u32 base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < BS / 64; ++w) { const u32 x = wave_tot[w]; if (w < wave) base += x; tot += x; }
+  *total = tot;
+  __syncthreads();   // wave_tot may be reused
+  return base + incl - mine;
+}
+
+struct DedupArgs {
+  const u64* rfp;
+  const unsigned short* rkey;
+  const u32* rcnt;
+  u64 region;                  // records per workgroup region (BS * NI)
+  u64 gid0;                    // global id of the chunk's first parent
+  ulonglong2* urec;            // [nblk][region] distinct (fp, ~key) of each workgroup's records
+  u32* ucnt;                   // [nblk]
+  u64* table;
+  u64 table_mask;
+  u64* newpos;                 // entry indices inserted by this chunk (ctr[K_INS] of them)
+  unsigned long long* ctr;
+  u32 prof;                    // accumulate per-workgroup wall-clock ticks into ctr[K_PROF..]
+};
+
+RMC_HD u64 nkey_of(u64 gid0, u32 blk, u32 lk) {   // ~(global key) of a local record key
+  return ~(((gid0 + (u64)blk * BS + (lk >> 8)) << 8) | (u64)(lk & 255u));
+}
+
+// insert-or-find fp in the workgroup's LDS set and lower its slot's key to lk; false = window full
+__device__ __forceinline__ bool lds_merge(unsigned long long* lfp, unsigned int* lkey, u64 fp, u32 lk) {
+  u32 h = (u32)(fp >> 20) & (LDS_FP_SLOTS - 1);
+#pragma unroll 1
+  for (int p = 0; p < 8; ++p) {
+    unsigned long long c = lfp[h];                                   // plain read first: most hits need no CAS
+    if (c == 0ull) c = atomicCAS(&lfp[h], 0ull, (unsigned long long)fp);
+    if (c == 0ull || c == fp) { atomicMin(&lkey[h], lk); return true; }
+    h = (h + 1) & (LDS_FP_SLOTS - 1);
+  }
+  return false;
+}
+
+// Seen-set insertion, part 1 (LDS): workgroup b takes generate-workgroup b's records and merges
+// them in an LDS set {fp, min local key} (exact: LDS CAS + LDS atomicMin; ~half of C2's
+// successors repeat another successor of the same 256 parents).  The distinct (fp, ~global key)
+// pairs are written compacted to the workgroup's region (a record whose probe window is full
+// goes there with its own key: the seen-set keeps the minimum key anyway).  Splitting the merge
+// from the probes lets the probe kernel run at the occupancy its registers allow, instead of
+// the 3 workgroups per CU the 48-KB set allows (measured: fused merge + probes 17-21 ms of C2).
+__global__ void __launch_bounds__(BS) orig_merge(DedupArgs a) {
+  __shared__ unsigned long long lfp[LDS_FP_SLOTS];
+  __shared__ unsigned int lkey[LDS_FP_SLOTS];
+  __shared__ u32 wave_tot[BS / 64];
+  __shared__ u32 ovf_cnt;
+  for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) { lfp[t] = 0ull; lkey[t] = ~0u; }
+  if (threadIdx.x == 0) ovf_cnt = 0;
+  __syncthreads();
+  const u32 n = a.rcnt[blockIdx.x];
+  const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
+  const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
+  ulonglong2* out = a.urec + (u64)blockIdx.x * a.region;
+  // overflow records (probe window full) go to the END of the region, growing down
+  constexpr int P1 = 8;
+#pragma unroll 1
+  for (u32 i0 = 0; i0 < n; i0 += P1 * BS) {
+    u64 fp[P1];
+    u32 lk[P1];
+#pragma unroll
+    for (int j = 0; j < P1; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      fp[j] = i < n ? fps[i] : 0ull;
+      lk[j] = i < n ? (u32)keys[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < P1; ++j) {
+      if (fp[j] && !lds_merge(lfp, lkey, fp[j], lk[j])) {   // window full (rare): the record keeps its own key
+        const u32 at = atomicAdd(&ovf_cnt, 1u);
+        out[a.region - 1 - at] = make_ulonglong2((unsigned long long)fp[j], (unsigned long long)nkey_of(a.gid0, blockIdx.x, lk[j]));
       }
     }
   }
-  const unsigned int mine = (unsigned int)(__popcll(isnew) + __popcll(isnew_hi));
-  unsigned int incl = mine;
+  __syncthreads();
+  // compact the set's occupied slots to the front of the region
+  constexpr int PER = LDS_FP_SLOTS / BS;
+  u32 mine = 0;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) { const unsigned int v = __shfl_up(incl, d); if (lane >= d) incl += v; }
-  if (lane == 63) wave_tot[wave] = incl;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned int tot = 0;
-    for (int w = 0; w < BS / 64; ++w) { const unsigned int x = wave_tot[w]; wave_tot[w] = tot; tot += x; }
-    base_sh = tot ? atomicAdd(&a.ctr[K_CHUNK_NEW], (unsigned long long)tot) : 0ull;
+  for (int j = 0; j < PER; ++j) mine += lfp[threadIdx.x * PER + j] ? 1u : 0u;
+  u32 total = 0;
+  u32 o = block_excl_scan(mine, wave_tot, &total);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int sl = threadIdx.x * PER + j;
+    const u64 fp = lfp[sl];
+    if (fp) out[o++] = make_ulonglong2((unsigned long long)fp, (unsigned long long)nkey_of(a.gid0, blockIdx.x, lkey[sl]));
   }
+  const u32 nov = ovf_cnt;   // (read after the scan's barriers)
   __syncthreads();
-  u64 pos = base_sh + wave_tot[wave] + (incl - mine);
-  while (isnew) {
-    const int k = __ffsll((unsigned long long)isnew) - 1;
-    isnew &= isnew - 1;
-    a.newrec[pos++] = ((a.chunk_begin + st) << 8) | (u64)k;
-  }
-  while (isnew_hi) {
-    const int k = 64 + __ffsll((unsigned long long)isnew_hi) - 1;
-    isnew_hi &= isnew_hi - 1;
-    a.newrec[pos++] = ((a.chunk_begin + st) << 8) | (u64)k;
+  // move the overflow records (end of the region) behind the set's
+  for (u32 q = threadIdx.x; q < nov; q += BS) out[total + q] = out[a.region - 1 - q];
+  if (threadIdx.x == 0) a.ucnt[blockIdx.x] = total + nov;
+}
+
+// Seen-set insertion, part 2 (HBM random access): workgroup b probes the seen-set once per
+// distinct fingerprint of region b, DEDUP_PER probes in flight per thread (insert-if-absent by CAS
+// of the fp, then atomicMax of ~key: the entry keeps the minimum key), and appends the inserted
+// entries' positions (one global atomic per workgroup and round).
+__global__ void __launch_bounds__(BS) orig_probe(DedupArgs a) {
+  __shared__ u32 wave_tot[BS / 64];
+  __shared__ unsigned long long base_sh;
+  const u32 n = a.ucnt[blockIdx.x];
+  const ulonglong2* in = a.urec + (u64)blockIdx.x * a.region;
+  u32 err = 0;
+  const u64 t0 = a.prof ? wall_clock64() : 0;
+#pragma unroll 1
+  for (u32 i0 = 0; i0 < n; i0 += DEDUP_PER * BS) {
+    u64 fp[DEDUP_PER], nk[DEDUP_PER], pos[DEDUP_PER];
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      const ulonglong2 r = i < n ? in[i] : make_ulonglong2(0ull, 0ull);
+      fp[j] = r.x; nk[j] = r.y;
+    }
+    const u32 ins = probe_batch<DEDUP_PER>(a.table, a.table_mask, fp, nk, pos, err);
+    u32 total = 0;
+    const u32 off = block_excl_scan((u32)__popc(ins), wave_tot, &total);
+    if (threadIdx.x == 0) base_sh = total ? atomicAdd(&a.ctr[K_INS], (unsigned long long)total) : 0ull;
+    __syncthreads();
+    u64 o = base_sh + off;
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j)
+      if ((ins >> j) & 1u) a.newpos[o++] = pos[j];
+    __syncthreads();   // base_sh reused
   }
   if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+  if (a.prof && threadIdx.x == 0) {
+    const u64 t3 = wall_clock64();
+    atomicAdd(&a.ctr[K_PROF + 1], (unsigned long long)(t3 - t0));
+    atomicAdd(&a.ctr[K_PROF + 3], 1ull);
+  }
+}
+
+// Winners: an entry inserted by this chunk holds, after the chunk's dedup, the minimum key over
+// all its producers (later chunks have larger keys), i.e. TLC's first-found (parent, instance).
+// orig_mark sets that (parent, instance) bit; orig_count counts each workgroup's winners.
+struct MarkArgs {
+  const u64* newpos;
+  const u64* table;
+  u64 gid0, chunk_count;
+  u64* winmask;                // [chunk][WW] instance bits of each parent's winning successors
+  u32 ww;
+  unsigned long long* ctr;
+};
+
+__global__ void __launch_bounds__(BS) orig_mark(MarkArgs a) {
+  const u64 n = a.ctr[K_INS];
+  for (u64 i = (u64)blockIdx.x * BS + threadIdx.x; i < n; i += (u64)gridDim.x * BS) {
+    const u64 key = ~a.table[2 * a.newpos[i] + 1];
+    const u64 p = (key >> 8) - a.gid0;
+    const u32 k = (u32)(key & 255);
+    if (p >= a.chunk_count) { atomicOr(&a.ctr[K_ERR], (unsigned long long)OE_TABLE_FULL); continue; }   // cannot happen
+    atomicOr((unsigned long long*)&a.winmask[p * a.ww + (k >> 6)], 1ull << (k & 63));
+  }
+}
+
+// winners per workgroup of 256 parents (popcount of their masks; coalesced, no atomics)
+template <int WW>
+__global__ void __launch_bounds__(BS) orig_count(const u64* winmask, u64 chunk_count, u32* wcnt) {
+  __shared__ u32 wave_tot[BS / 64];
+  const u64 p = (u64)blockIdx.x * BS + threadIdx.x;
+  u32 mine = 0;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) mine += p < chunk_count ? (u32)__popcll(winmask[p * WW + q]) : 0u;
+  u32 total = 0;
+  (void)block_excl_scan(mine, wave_tot, &total);
+  if (threadIdx.x == 0) wcnt[blockIdx.x] = total;
+}
+
+// exclusive scan of the per-workgroup winner counts -> woff; the chunk's total -> ctr[K_CHUNK_NEW]
+__global__ void __launch_bounds__(SCAN_BS) orig_scan(const u32* wcnt, u64* woff, u32 nblk, unsigned long long* ctr) {
+  __shared__ unsigned long long part[SCAN_BS];
+  const u32 per = (nblk + SCAN_BS - 1) / SCAN_BS, b0 = threadIdx.x * per;
+  unsigned long long s = 0;
+  for (u32 j = 0; j < per; ++j) if (b0 + j < nblk) s += wcnt[b0 + j];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int d = 1; d < SCAN_BS; d <<= 1) {
+    const unsigned long long x = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0ull;
+    __syncthreads();
+    part[threadIdx.x] += x;
+    __syncthreads();
+  }
+  unsigned long long run = part[threadIdx.x] - s;
+  for (u32 j = 0; j < per; ++j) if (b0 + j < nblk) { woff[b0 + j] = run; run += wcnt[b0 + j]; }
+  if (threadIdx.x == SCAN_BS - 1) ctr[K_CHUNK_NEW] = part[SCAN_BS - 1];
 }
 
 struct MatArgs {
   u32* states;
   u64* meta;
-  const u64* newrec;
-  u64 dst_base, cap;           // new state i of the chunk goes to dst_base + ctr[K_LEVEL_NEW] + i
-  u64 base;                    // global id of device slot 0 (completed levels spilled to the host)
+  u64 chunk_begin, chunk_count, gid0;   // parents: device index, count, global id of the first
+  u64* winmask;                // read and re-zeroed
+  const u64* woff;
+  u32 ww;
+  u64 dst_base, cap;           // new state i of the chunk goes to dst_base + ctr[K_LEVEL_NEW] + i (device index)
   OrigRuntime rt;
-  unsigned long long* ctr;     // ctr[K_CHUNK_NEW] = the chunk's new states (set by orig_dedup_blk)
-  void* viol;
+  unsigned long long* ctr;
 };
 
-// Grid-stride over the chunk's new states, whose number stays on the device: the host does
-// not wait for the dedup kernel to size this launch (one host synchronisation per level).
+// Workgroup per 256 parents (the generate workgroup's): the winners in key order — parent
+// order, then instance order — are numbered by a workgroup scan plus the chunk offset, staged
+// in LDS and spread over the workgroup's lanes; each is re-derived from (parent, instance) and
+// stored at its FIFO position with its parent pointer; invariants of the new state.
 template <class S>
 __global__ void __launch_bounds__(BS) orig_materialize(MatArgs a) {
   using W = typename S::Work;
-  constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
+  constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3, WW = (S::NI + 63) / 64;
   __shared__ unsigned int lds_cnt[OA_NACT];
+  __shared__ unsigned short items[MAT_CAP];
+  __shared__ u32 wave_tot[BS / 64];
   for (int t = threadIdx.x; t < OA_NACT; t += BS) lds_cnt[t] = 0;
-  __syncthreads();
-  const u64 n_new = a.ctr[K_CHUNK_NEW];
-  const u64 base = a.dst_base + a.ctr[K_LEVEL_NEW];
+  const u64 p = (u64)blockIdx.x * BS + threadIdx.x;
+  u64 wm[WW];
+  u32 mine = 0;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) {
+    wm[q] = p < a.chunk_count ? a.winmask[p * WW + q] : 0ull;
+    mine += (u32)__popcll(wm[q]);
+  }
+  if (p < a.chunk_count && mine) {
+#pragma unroll
+    for (int q = 0; q < WW; ++q) a.winmask[p * WW + q] = 0ull;   // ready for the next chunk
+  }
+  u32 total = 0;
+  const u32 off = block_excl_scan(mine, wave_tot, &total);   // (also orders lds_cnt's clearing)
+  const u64 base = a.dst_base + a.ctr[K_LEVEL_NEW] + a.woff[blockIdx.x];
   u32 err = 0;
-  for (u64 i = (u64)blockIdx.x * BS + threadIdx.x; i < n_new; i += (u64)gridDim.x * BS) {
-    const u64 rec = a.newrec[i], gid = rec >> 8;
-    const int k = (int)(rec & 0xff);
-    u32 w[NWP];
-    const uint4* src = reinterpret_cast<const uint4*>(a.states + gid * NWP);
+  unsigned long long ev = ~0ull;
+  for (u32 r0 = 0; r0 < total; r0 += MAT_CAP) {
+    {   // stage this round's window [r0, r0 + MAT_CAP) of the workgroup's winners
+      u32 idx = off;
 #pragma unroll
-    for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
-    W s, t;
-    u64 al[S::AW];
-    S::unpack(w, s);
-    S::all_logs_next(s, al);
-    const int act = S::apply(s, k, t, err);
-#pragma unroll
-    for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
-    u32 pw[NW];
-    S::pack(t, pw);
-    const u64 dst = base + i;
-    if (act >= 0 && dst < a.cap) {
-      uint4* o = reinterpret_cast<uint4*>(a.states + dst * NWP);
-#pragma unroll
-      for (int q = 0; q < NWP / 4; ++q)
-        o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
-      a.meta[dst] = ((gid + a.base) << 24) | ((u64)act << 16) | (u64)k;
-      atomicAdd(&lds_cnt[act], 1u);
-      const u32 bad = S::violated(t, a.rt.invariants);
-      if (bad && atomicCAS(&a.ctr[K_VIOL], 0ull, 1ull) == 0ull) {
-        ViolRec<S>* v = reinterpret_cast<ViolRec<S>*>(a.viol);
-        v->parent = gid; v->act = (u32)act; v->inst = (u32)k; v->bad = bad; v->inmodel = 1; v->w = t;
+      for (int q = 0; q < WW; ++q) {
+        u64 m = wm[q];
+        while (m) {
+          const int k = q * 64 + __ffsll((unsigned long long)m) - 1;
+          m &= m - 1;
+          if (idx >= r0 && idx < r0 + MAT_CAP) items[idx - r0] = (unsigned short)((threadIdx.x << 8) | (unsigned)k);
+          ++idx;
+        }
       }
-    } else {
-      err |= dst >= a.cap ? (u32)OE_CAP_STORE : (u32)OE_EVAL_LOG_INDEX;
     }
+    __syncthreads();
+    const u32 nr = total - r0 < (u32)MAT_CAP ? total - r0 : (u32)MAT_CAP;
+    for (u32 i = threadIdx.x; i < nr; i += BS) {
+      const u32 x = items[i];
+      const u64 par = (u64)blockIdx.x * BS + (x >> 8);
+      const int k = (int)(x & 255);
+      u32 w[NWP];
+      const uint4* src = reinterpret_cast<const uint4*>(a.states + (a.chunk_begin + par) * NWP);
+#pragma unroll
+      for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+      W s, t;
+      u64 al[S::AW];
+      S::unpack(w, s);
+      S::all_logs_next(s, al);
+      u32 e2 = 0;
+      const int act = S::apply(s, k, t, e2);
+#pragma unroll
+      for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
+      u32 pw[NW];
+      S::pack(t, pw);
+      const u64 dst = base + r0 + i;
+      if (act >= 0 && dst < a.cap) {
+        uint4* o = reinterpret_cast<uint4*>(a.states + dst * NWP);
+#pragma unroll
+        for (int q = 0; q < NWP / 4; ++q)
+          o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
+        const u64 pgid = a.gid0 + par;
+        a.meta[dst] = (pgid << 24) | ((u64)act << 16) | (u64)k;
+        atomicAdd(&lds_cnt[act], 1u);
+        if (S::violated(t, a.rt.invariants)) {
+          const u64 e = ev_word(pgid, (u32)k, EV_VIOLATION);
+          ev = e < ev ? e : ev;
+        }
+      } else {
+        err |= dst >= a.cap ? (u32)OE_CAP_STORE : (u32)OE_TABLE_FULL;   // a winner always re-derives
+      }
+    }
+    __syncthreads();
   }
   if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+  if (ev != ~0ull) atomicMin(&a.ctr[K_EVENT], ev);
   __syncthreads();
   for (int t = threadIdx.x; t < OA_NACT; t += BS)
     if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + OA_NACT + t], (unsigned long long)lds_cnt[t]);
 }
 
-// after a chunk's materialize: the level's running count of new states
-// after a chunk's materialize: fold its new-state count into the level's and re-arm the chunk
-// counter for the next chunk (the level's first chunk starts from the per-level counter reset)
+// after a chunk's materialize: fold its new-state count into the level's; re-arm the chunk's
+// insert counter (the level's first chunk starts from the per-level counter reset)
 __global__ void orig_advance(unsigned long long* ctr) {
   if (threadIdx.x == 0) {
     ctr[K_LEVEL_NEW] += ctr[K_CHUNK_NEW];
     ctr[K_CHUNK_NEW] = 0;
+    ctr[K_INS] = 0;
   }
+}
+
+// ------------------------------------------------------------------ TLC's stop point
+// On the level's first event (parent gid_stop, instance k_stop, kind): TLC's generated counts
+// are the whole successor lists of the parents before it and of the event's parent (none when
+// computing its successors raised the error), per-action generated counts stop at the event's
+// successor.  out[0] = generated, out[1 + a] = per-action generated.
+template <class S>
+__global__ void __launch_bounds__(BS) orig_stop_generated(const u32* states, u64 first, u64 n, u64 gid0, u64 gid_stop,
+                                                         u32 k_stop, u32 kind, unsigned long long* out) {
+  using W = typename S::Work;
+  constexpr int NWP = (S::NW + 3) & ~3;
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  const u64 gid = gid0 + i;
+  if (gid == gid_stop && kind == EV_NEXT_ERROR) return;
+  u32 w[NWP];
+#pragma unroll
+  for (int q = 0; q < NWP; ++q) w[q] = states[(first + i) * NWP + q];
+  W s, t;
+  S::unpack(w, s);
+  u32 err = 0, tot = 0;
+  for (int k = 0; k < S::NI; ++k) {
+    const int act = S::apply(s, k, t, err);
+    if (act < 0) continue;
+    ++tot;
+    if (gid < gid_stop || (u32)k <= k_stop) atomicAdd(&out[1 + act], 1ull);
+  }
+  if (tot) atomicAdd(&out[0], (unsigned long long)tot);
+}
+
+// per-action distinct counts of the level's first n new states (stored in key order)
+__global__ void __launch_bounds__(BS) orig_stop_distinct(const u64* meta, u64 n, unsigned long long* out) {
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  if (i < n) atomicAdd(&out[(meta[i] >> 16) & 0xff], 1ull);
 }
 
 // ------------------------------------------------------------------ sharded (multi-GPU) kernels
@@ -346,53 +619,66 @@ __global__ void orig_advance(unsigned long long* ctr) {
 __device__ __host__ __forceinline__ u32 fp_owner(u64 fp, u32 world) { return (u32)((fp >> 32) % world); }
 
 struct RouteArgs {
-  const u64* cand;
-  u64 nslots;
+  const u64* rfp;
+  const unsigned short* rkey;
+  const u32* rcnt;
+  u64 region;                  // records per workgroup region (BS * NI)
   u64* route;                  // [world][route_cap][2] (fp, slot)
   u64 route_cap;
   u32 world;
-  unsigned long long* rcnt;    // [world]
+  unsigned long long* rcnt_out;   // [world]
 };
 
-// Sharded route over the PM slot layout: workgroup b takes generate-workgroup b's 256
-// parents, drops the successors they produce more than once (the LDS set of orig_dedup_blk),
-// and buckets the rest by owner, 16 instances at a time: LDS histogram, one global atomic per
-// (workgroup, group, owner).  Records are (fp, state << 8 | instance).
-template <int NI>
+// Sharded route over the compacted records: workgroup b takes generate-workgroup b's records,
+// drops the successors its 256 parents produce more than once (an exact LDS set, LDS CAS), and
+// buckets the rest by owner, 16 records per thread at a time: LDS histogram, one global atomic
+// per (workgroup, round, owner).  Records are (fp, state in chunk << 8 | instance).
 __global__ void __launch_bounds__(BS) orig_route_blk(RouteArgs a) {
-  static_assert(NI <= 255, "instance in 8 bits");
   __shared__ unsigned long long lds_fp[LDS_FP_SLOTS];
   __shared__ unsigned int hist[8];
   __shared__ unsigned long long base[8];
   for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lds_fp[t] = 0ull;
-  const u64 st = (u64)blockIdx.x * BS + threadIdx.x;
-  const u64* row = a.cand + (u64)blockIdx.x * NI * BS + threadIdx.x;
+  const u32 n = a.rcnt[blockIdx.x];
+  const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
+  const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
   constexpr int G = 16;
 #pragma unroll 1
-  for (int k0 = 0; k0 < NI; k0 += G) {
+  for (u32 i0 = 0; i0 < n; i0 += G * BS) {
     if (threadIdx.x < 8) hist[threadIdx.x] = 0;
     __syncthreads();   // also orders the set's clearing before its first use
-    u64 fp[G];
+    u64 fp[G], slot[G];
     unsigned int off[G];
     int own[G];
 #pragma unroll
     for (int j = 0; j < G; ++j) {
-      fp[j] = (st < a.nslots / NI && k0 + j < NI) ? row[(u64)(k0 + j) * BS] : 0ull;
-      if (fp[j] && !lds_first(lds_fp, fp[j])) fp[j] = 0;
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      fp[j] = i < n ? fps[i] : 0ull;
+      const u32 lk = i < n ? keys[i] : 0u;
+      slot[j] = (((u64)blockIdx.x * BS + (lk >> 8)) << 8) | (u64)(lk & 255u);
+      if (fp[j]) {   // produced before by this workgroup's parents?
+        u32 h = (u32)(fp[j] >> 20) & (LDS_FP_SLOTS - 1);
+#pragma unroll 1
+        for (int p = 0; p < 8; ++p) {
+          const unsigned long long cur = atomicCAS(&lds_fp[h], 0ull, (unsigned long long)fp[j]);
+          if (cur == 0ull) break;                    // first here
+          if (cur == fp[j]) { fp[j] = 0; break; }    // duplicate
+          h = (h + 1) & (LDS_FP_SLOTS - 1);
+        }
+      }
       own[j] = fp[j] ? (int)fp_owner(fp[j], a.world) : -1;
       off[j] = own[j] >= 0 ? atomicAdd(&hist[own[j]], 1u) : 0u;
     }
     __syncthreads();
-    if (threadIdx.x < a.world) base[threadIdx.x] = hist[threadIdx.x] ? atomicAdd(&a.rcnt[threadIdx.x], (unsigned long long)hist[threadIdx.x]) : 0ull;
+    if (threadIdx.x < a.world) base[threadIdx.x] = hist[threadIdx.x] ? atomicAdd(&a.rcnt_out[threadIdx.x], (unsigned long long)hist[threadIdx.x]) : 0ull;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       if (own[j] < 0) continue;
       // one 16-B store per record
       *reinterpret_cast<ulonglong2*>(a.route + ((u64)own[j] * a.route_cap + base[own[j]] + off[j]) * 2) =
-          make_ulonglong2((unsigned long long)fp[j], (unsigned long long)((st << 8) | (u64)(k0 + j)));
+          make_ulonglong2((unsigned long long)fp[j], (unsigned long long)slot[j]);
     }
-    __syncthreads();   // hist / base reused by the next group
+    __syncthreads();   // hist / base reused by the next round
   }
 }
 
@@ -406,59 +692,30 @@ struct DedupShArgs {
   unsigned long long* ctr;
 };
 
+// owner-side insertion of one source rank's records (no FIFO keys in sharded raft_original: the
+// entries' key words stay 0)
 __global__ void __launch_bounds__(BS) orig_dedup_sh(DedupShArgs a) {
-  __shared__ unsigned int wave_tot[BS / 64];
+  __shared__ u32 wave_tot[BS / 64];
   __shared__ unsigned long long base_sh;
   const u64 tile = (u64)blockIdx.x * (BS * DEDUP_PER);
-  const int lane = __lane_id(), wave = threadIdx.x >> 6;
-  u64 fp[DEDUP_PER], cur[DEDUP_PER];
+  u64 fp[DEDUP_PER], nk[DEDUP_PER], pos[DEDUP_PER];
 #pragma unroll
   for (int j = 0; j < DEDUP_PER; ++j) {
     const u64 idx = tile + (u64)j * BS + threadIdx.x;
     fp[j] = idx < a.n ? a.recv[2 * idx] : 0ull;
+    nk[j] = 0ull;
   }
-#pragma unroll
-  for (int j = 0; j < DEDUP_PER; ++j) cur[j] = fp[j] ? a.table[fp[j] & a.table_mask] : ~0ull;
-#pragma unroll
-  for (int j = 0; j < DEDUP_PER; ++j)
-    if (fp[j] && cur[j] == 0ull)
-      cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[fp[j] & a.table_mask], 0ull, (unsigned long long)fp[j]);
-  u32 isnew = 0, err = 0;
-#pragma unroll
-  for (int j = 0; j < DEDUP_PER; ++j) {
-    if (!fp[j]) continue;
-    if (cur[j] == 0ull) { isnew |= 1u << j; continue; }
-    if (cur[j] == fp[j]) continue;
-    u64 slot = (fp[j] + 1) & a.table_mask;
-    for (int probe = 0;; ++probe) {
-      if (probe >= (1 << 20)) { err |= OE_TABLE_FULL; break; }
-      const u64 c = a.table[slot];
-      if (c == fp[j]) break;
-      if (c == 0ull) {
-        const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[slot], 0ull, (unsigned long long)fp[j]);
-        if (old == 0ull) { isnew |= 1u << j; break; }
-        if (old == fp[j]) break;
-      }
-      slot = (slot + 1) & a.table_mask;
-    }
-  }
-  const unsigned int mine = (unsigned int)__popc(isnew);
-  unsigned int incl = mine;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) { const unsigned int v = __shfl_up(incl, d); if (lane >= d) incl += v; }
-  if (lane == 63) wave_tot[wave] = incl;
+  u32 err = 0;
+  const u32 isnew = probe_batch<DEDUP_PER, false>(a.table, a.table_mask, fp, nk, pos, err);
+  u32 total = 0;
+  const u32 off = block_excl_scan((u32)__popc(isnew), wave_tot, &total);
+  if (threadIdx.x == 0) base_sh = total ? atomicAdd(a.counter, (unsigned long long)total) : 0ull;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned int tot = 0;
-    for (int w = 0; w < BS / 64; ++w) { const unsigned int x = wave_tot[w]; wave_tot[w] = tot; tot += x; }
-    base_sh = tot ? atomicAdd(a.counter, (unsigned long long)tot) : 0ull;
-  }
-  __syncthreads();
-  u64 pos = base_sh + wave_tot[wave] + (incl - mine);
+  u64 o = base_sh + off;
   for (int j = 0; j < DEDUP_PER; ++j) {
     if (!((isnew >> j) & 1u)) continue;
     const u64 idx = tile + (u64)j * BS + threadIdx.x;
-    a.reply[pos++] = a.recv[2 * idx + 1];
+    a.reply[o++] = a.recv[2 * idx + 1];
   }
   if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
 }
@@ -472,7 +729,6 @@ struct MatShArgs {
   u64 seed;
   OrigRuntime rt;
   unsigned long long* ctr;
-  void* viol;
 };
 
 template <class S>
@@ -484,6 +740,7 @@ __global__ void __launch_bounds__(BS) orig_materialize_sh(MatShArgs a) {
   __syncthreads();
   const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
   u32 err = 0;
+  unsigned long long ev = ~0ull;
   if (i < a.n) {
     const u64 slot = a.acks[i];   // state in chunk << 8 | instance (orig_route_blk)
     const u64 k = slot & 255ull, gid = a.chunk_begin + (slot >> 8);
@@ -495,7 +752,8 @@ __global__ void __launch_bounds__(BS) orig_materialize_sh(MatShArgs a) {
     u64 al[S::AW];
     S::unpack(w, s);
     S::all_logs_next(s, al);
-    const int act = S::apply(s, (int)k, t, err);
+    u32 e2 = 0;
+    const int act = S::apply(s, (int)k, t, e2);
 #pragma unroll
     for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
     u32 pw[NW];
@@ -509,16 +767,13 @@ __global__ void __launch_bounds__(BS) orig_materialize_sh(MatShArgs a) {
     reinterpret_cast<uint4*>(o)[NWP / 4] = make_uint4((u32)meta, (u32)(meta >> 32), (u32)fp, (u32)(fp >> 32));
     if (act >= 0) {
       atomicAdd(&lds_cnt[act], 1u);
-      const u32 bad = S::violated(t, a.rt.invariants);
-      if (bad && atomicCAS(&a.ctr[K_VIOL], 0ull, 1ull) == 0ull) {
-        ViolRec<S>* v = reinterpret_cast<ViolRec<S>*>(a.viol);
-        v->parent = gid; v->act = (u32)act; v->inst = (u32)k; v->bad = bad; v->inmodel = 1; v->w = t;
-      }
+      if (S::violated(t, a.rt.invariants)) ev = ev_word(gid, (u32)k, EV_VIOLATION);
     } else {
-      err |= OE_EVAL_LOG_INDEX;
+      err |= OE_TABLE_FULL;   // an acknowledged slot always re-derives
     }
   }
   if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+  if (ev != ~0ull) atomicMin(&a.ctr[K_EVENT], ev);
   __syncthreads();
   for (int t = threadIdx.x; t < OA_NACT; t += BS)
     if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + OA_NACT + t], (unsigned long long)lds_cnt[t]);
@@ -558,18 +813,12 @@ __global__ void __launch_bounds__(BS) orig_reinsert(const u32* states, u64 n, u6
   u32 w[NW];
 #pragma unroll
   for (int q = 0; q < NW; ++q) w[q] = states[i * NWP + q];
-  const u64 fp = fp64(w, seed);
-  u64 slot = fp & mask;
-  for (int probe = 0; probe < (1 << 20); ++probe) {
-    const u64 c = table[slot];
-    if (c == fp) return;
-    if (c == 0ull) {
-      const u64 old = (u64)atomicCAS((unsigned long long*)&table[slot], 0ull, (unsigned long long)fp);
-      if (old == 0ull || old == fp) return;
-    }
-    slot = (slot + 1) & mask;
-  }
-  atomicOr(&ctr[K_ERR], (unsigned long long)OE_TABLE_FULL);
+  // stored states are older than any successor the search will generate: key 0 (~key = ~0)
+  const u64 fp[1] = {fp64(w, seed)}, nk[1] = {~0ull};
+  u64 pos[1];
+  u32 err = 0;
+  probe_batch<1>(table, mask, fp, nk, pos, err);
+  if (err) atomicOr(&ctr[K_ERR], (unsigned long long)err);
 }
 
 #define HIPCHK(x)                                                                             \
@@ -590,7 +839,7 @@ class OrigGpu : public Backend {
 
   int observed_collision(double& v, std::string& err) override {
     if (!d_table_ || alloc_world_ != 0) { err = "after a single-GPU mc_run only"; return MC_E_STATE; }
-    return fpgap::observed(d_table_, table_mask_ + 1, 1, stream_, v, err);
+    return fpgap::observed(d_table_, table_mask_ + 1, 2, stream_, v, err);
   }
 
   std::string describe_json() const override {
@@ -620,27 +869,37 @@ class OrigGpu : public Backend {
     size_t freeb = 0, totalb = 0;
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
     uint64_t tb = o.fp_table_bytes ? o.fp_table_bytes : std::min<uint64_t>(8ull << 30, freeb / 4);
-    uint64_t slots = 1; while (slots * 2 * 8 <= tb) slots *= 2;
+    uint64_t slots = 1; while (slots * 2 * 16 <= tb) slots *= 2;   // 16-B entries {fp, ~key}
     if (slots < 1024) slots = 1024;
     uint64_t sb = o.state_store_bytes ? o.state_store_bytes : std::min<uint64_t>(32ull << 30, freeb / 3);
     cap_ = sb / (NWP * 4 + 8);
     if (cap_ < 16) cap_ = 16;
-    // frontier chunk: the slot array holds chunk_states * NI fingerprints and
-    // the record array as many (worst case: every slot new): ~1/8 of the store;
-    // sharded mode also needs world route regions of 16-B records per slot
-    chunk_states_ = std::max<u64>(4096, std::min<u64>(cap_, (sb / 8) / (16 * (u64)S::NI)));
+    // frontier chunk: the record regions hold chunk_states * NI records (10 B each), their
+    // distinct pairs (16 B) and the inserted-position list as many 8-B entries (worst case: every
+    // record new): ~1/4 of the store; sharded mode also needs world route regions of 16-B records
+    chunk_states_ = std::max<u64>(4096, std::min<u64>(cap_, (sb / 4) / (34 * (u64)S::NI)));
     if (world > 1) chunk_states_ = std::max<u64>(4096, chunk_states_ / (u64)world);
-    chunk_states_ = (chunk_states_ / BS) * BS;   // whole workgroups: the PM slot layout is [block][instance][lane]
+    chunk_states_ = std::min<u64>(chunk_states_, (u64)SCAN_BS * 64 * BS);   // orig_scan: <= 64 blocks per lane
+    chunk_states_ = (chunk_states_ / BS) * BS;   // whole workgroups: records are grouped per generate workgroup
+    const u64 nblk = chunk_states_ / BS, nrec = chunk_states_ * (u64)S::NI;
     table_mask_ = slots - 1;
-    HIPCHK(hipMalloc(&d_table_, slots * 8));
+    HIPCHK(hipMalloc(&d_table_, slots * 16));
     HIPCHK(hipMalloc(&d_states_, cap_ * NWP * 4));
     HIPCHK(hipMalloc(&d_meta_, cap_ * 8));
-    HIPCHK(hipMalloc(&d_cand_, chunk_states_ * S::NI * 8));
-    HIPCHK(hipMalloc(&d_newrec_, chunk_states_ * S::NI * 8));
+    HIPCHK(hipMalloc(&d_rfp_, nrec * 8));
+    HIPCHK(hipMalloc(&d_rkey_, nrec * 2));
+    HIPCHK(hipMalloc(&d_rcnt_blk_, nblk * 4));
+    HIPCHK(hipMalloc(&d_newrec_, nrec * 8));          // inserted entry positions (single GPU) / replies (sharded)
+    HIPCHK(hipMalloc(&d_urec_, nrec * 16));           // distinct (fp, ~key) per workgroup region
+    HIPCHK(hipMalloc(&d_ucnt_, nblk * 4));
+    HIPCHK(hipMalloc(&d_winmask_, chunk_states_ * WW * 8));
+    HIPCHK(hipMalloc(&d_wcnt_, nblk * 4));
+    HIPCHK(hipMalloc(&d_woff_, nblk * 8));
     HIPCHK(hipMalloc(&d_ctr_, K_NCTR * 8));
-    HIPCHK(hipMalloc(&d_viol_, sizeof(ViolRec<S>)));
+    HIPCHK(hipMalloc(&d_stop_, (1 + OA_NACT) * 8));
+    HIPCHK(hipMemset(d_winmask_, 0, chunk_states_ * WW * 8));
     if (world >= 1) {   // sharded mode
-      HIPCHK(hipMalloc(&d_route_, (u64)world * chunk_states_ * S::NI * 16));
+      HIPCHK(hipMalloc(&d_route_, (u64)world * nrec * 16));
       HIPCHK(hipMalloc(&d_rcnt_, 2 * 8 * 8));
     }
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
@@ -649,9 +908,10 @@ class OrigGpu : public Backend {
     return 0;
   }
 
-  // event pairs (generate, dedup, materialize) of chunk q of the current level: lvl_ev_[6q .. 6q+6)
+  // event pairs (generate, dedup, winners = mark + scan, materialize) of chunk q of the current
+  // level: lvl_ev_[8q .. 8q+8)
   int lvl_events(int q) {
-    while ((int)lvl_ev_.size() < 6 * (q + 1)) {
+    while ((int)lvl_ev_.size() < 8 * (q + 1)) {
       hipEvent_t e;
       if (hipEventCreate(&e) != hipSuccess) return MC_E_NO_DEVICE;
       lvl_ev_.push_back(e);
@@ -659,22 +919,26 @@ class OrigGpu : public Backend {
     return 0;
   }
 
-  int run_generate(GenArgs& g, u64 cnt, float& ms_g, std::string& err, bool pm = false) {
-    const unsigned nblk = (unsigned)((cnt + BS - 1) / BS);
-    HIPCHK(hipEventRecord(ev_[5], stream_));
-    if (pm) hipLaunchKernelGGL((orig_generate<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
-    else hipLaunchKernelGGL((orig_generate<S, false>), dim3(nblk), dim3(BS), 0, stream_, g);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(ev_[6], stream_));
-    HIPCHK(hipEventSynchronize(ev_[6]));
-    ms_g = time_ms(5, 6);
-    return 0;
+  GenArgs gen_args(u64 dev_begin, u64 count, u64 gid0, u64 seed, const RunOpts& o) const {
+    GenArgs g;
+    g.states = d_states_; g.chunk_begin = dev_begin; g.chunk_count = count; g.gid0 = gid0;
+    g.rfp = d_rfp_; g.rkey = d_rkey_; g.rcnt = d_rcnt_blk_; g.seed = seed; g.rt = m_.rt;
+    g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.deadlock = o.check_deadlock ? 1u : 0u;
+    g.ctr = (unsigned long long*)d_ctr_;
+    return g;
+  }
+
+  RouteArgs route_args(u32 world) const {
+    RouteArgs ra;
+    ra.rfp = d_rfp_; ra.rkey = d_rkey_; ra.rcnt = d_rcnt_blk_; ra.region = (u64)BS * S::NI; ra.route = d_route_;
+    ra.route_cap = chunk_states_ * S::NI; ra.world = world; ra.rcnt_out = (unsigned long long*)d_rcnt_;
+    return ra;
   }
 
   int run(const RunOpts& o, RunResult& r, std::string& err) override {
     if (int rc = ensure_alloc(o, 0, err)) return rc;   // world 0 = single-GPU pipeline
     auto t0 = std::chrono::steady_clock::now();
-    HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 8, stream_));
+    HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
 
     r = RunResult();
@@ -682,7 +946,7 @@ class OrigGpu : public Backend {
     r.state_bytes = NWP * 4;
     for (int k = 0; k < OA_NACT; ++k) r.action_names.push_back(kOrigActNames[k]);
     r.act_generated.assign(OA_NACT, 0); r.act_distinct.assign(OA_NACT, 0);
-    r.kernels = {{"orig_generate", 0, 0, 0}, {"orig_dedup_blk", 0, 0, 0}, {"orig_materialize", 0, 0, 0}};
+    r.kernels = {{"orig_generate", 0, 0, 0}, {"orig_merge_probe", 0, 0, 0}, {"orig_mark_scan", 0, 0, 0}, {"orig_materialize", 0, 0, 0}};
     base_ = 0; host_states_.clear(); host_meta_.clear();
 
     W s0; S::init(s0);
@@ -695,7 +959,8 @@ class OrigGpu : public Backend {
     u32 w0[S::NW]; S::pack(s0, w0);
     u32 wp[NWP] = {0}; for (int q = 0; q < S::NW; ++q) wp[q] = w0[q];
     const u64 fp0 = fp64(w0, r.seed);
-    HIPCHK(hipMemcpy(d_table_ + (fp0 & table_mask_), &fp0, 8, hipMemcpyHostToDevice));
+    const u64 e0[2] = {fp0, ~0ull};   // key 0
+    HIPCHK(hipMemcpy(d_table_ + 2 * (fp0 & table_mask_), e0, 16, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d_states_, wp, NWP * 4, hipMemcpyHostToDevice));
     const u64 nometa = ~0ull;
     HIPCHK(hipMemcpy(d_meta_, &nometa, 8, hipMemcpyHostToDevice));
@@ -722,75 +987,99 @@ class OrigGpu : public Backend {
           if (int rc = spill(level_begin, level_count, err)) return rc;
       }
       HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
+      HIPCHK(hipMemsetAsync(d_ctr_ + K_EVENT, 0xFF, 8, stream_));
       const u64 level_end = level_begin + level_count;
-      // every chunk's kernels are queued without waiting: the dedup kernel numbers the new
-      // states on the device and the materialize kernel reads that count (grid-stride), so the
-      // host synchronises once per level, for the counters
+      // every chunk's kernels are queued without waiting: the chunk's insert and winner counts
+      // stay on the device (grid-stride / scanned offsets), so the host synchronises once per
+      // level, for the counters
       int nch = 0;
       for (u64 cb = level_begin; cb < level_end; cb += chunk_states_, ++nch) {
         const u64 cnt = std::min<u64>(chunk_states_, level_end - cb);
-        const u64 nslots = cnt * (u64)S::NI;
         const unsigned nblk = (unsigned)((cnt + BS - 1) / BS);
         if (int rc = lvl_events(nch)) { err = "hipEventCreate failed"; return rc; }
-        hipEvent_t* e = &lvl_ev_[6 * nch];
-        GenArgs g;
-        // kernels index the device store (global id - base_); parent pointers are global
-        g.states = d_states_; g.chunk_begin = cb - base_; g.chunk_count = cnt; g.cand = d_cand_; g.seed = r.seed; g.rt = m_.rt;
-        g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_; g.viol = d_viol_;
+        hipEvent_t* e = &lvl_ev_[8 * nch];
+        // kernels index the device store (global id - base_); keys and parent pointers are global
+        const GenArgs g = gen_args(cb - base_, cnt, cb, r.seed, o);
         HIPCHK(hipEventRecord(e[0], stream_));
-        hipLaunchKernelGGL((orig_generate<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
+        hipLaunchKernelGGL((orig_generate<S>), dim3(nblk), dim3(BS), 0, stream_, g);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e[1], stream_));
         DedupArgs d;
-        d.cand = d_cand_; d.nslots = nslots; d.chunk_begin = cb - base_; d.chunk_count = cnt; d.table = d_table_;
-        d.table_mask = table_mask_; d.newrec = d_newrec_; d.ctr = (unsigned long long*)d_ctr_; d.ni = S::NI;
+        d.rfp = d_rfp_; d.rkey = d_rkey_; d.rcnt = d_rcnt_blk_; d.region = (u64)BS * S::NI; d.gid0 = cb;
+        d.urec = (ulonglong2*)d_urec_; d.ucnt = d_ucnt_;
+        d.table = d_table_; d.table_mask = table_mask_; d.newpos = d_newrec_; d.ctr = (unsigned long long*)d_ctr_;
+        d.prof = prof_ ? 1u : 0u;
         HIPCHK(hipEventRecord(e[2], stream_));
-        hipLaunchKernelGGL((orig_dedup_blk<S::NI>), dim3(nblk), dim3(BS), 0, stream_, d);
+        hipLaunchKernelGGL(orig_merge, dim3(nblk), dim3(BS), 0, stream_, d);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(orig_probe, dim3(nblk), dim3(BS), 0, stream_, d);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e[3], stream_));
-        MatArgs m;
-        m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.dst_base = level_end - base_; m.cap = cap_;
-        m.base = base_; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.viol = d_viol_;
-        const unsigned mblk = (unsigned)std::min<u64>(4096, (nslots + BS - 1) / BS);
+        MarkArgs mk;
+        mk.newpos = d_newrec_; mk.table = d_table_; mk.gid0 = cb; mk.chunk_count = cnt; mk.winmask = d_winmask_;
+        mk.ww = WW; mk.ctr = (unsigned long long*)d_ctr_;
         HIPCHK(hipEventRecord(e[4], stream_));
-        hipLaunchKernelGGL((orig_materialize<S>), dim3(mblk), dim3(BS), 0, stream_, m);
+        hipLaunchKernelGGL(orig_mark, dim3((unsigned)std::min<u64>(2048, (cnt * 2 + BS - 1) / BS)), dim3(BS), 0, stream_, mk);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL((orig_count<WW>), dim3(nblk), dim3(BS), 0, stream_, (const u64*)d_winmask_, cnt, d_wcnt_);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(orig_scan, dim3(1), dim3(SCAN_BS), 0, stream_, (const u32*)d_wcnt_, d_woff_, (u32)nblk, (unsigned long long*)d_ctr_);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e[5], stream_));
+        MatArgs m;
+        m.states = d_states_; m.meta = d_meta_; m.chunk_begin = cb - base_; m.chunk_count = cnt; m.gid0 = cb;
+        m.winmask = d_winmask_; m.woff = d_woff_; m.ww = WW; m.dst_base = level_end - base_; m.cap = cap_;
+        m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_;
+        HIPCHK(hipEventRecord(e[6], stream_));
+        hipLaunchKernelGGL((orig_materialize<S>), dim3(nblk), dim3(BS), 0, stream_, m);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(e[7], stream_));
         hipLaunchKernelGGL(orig_advance, dim3(1), dim3(64), 0, stream_, (unsigned long long*)d_ctr_);
         HIPCHK(hipGetLastError());
-        r.kernels[0].launches += 1; r.kernels[1].launches += 1; r.kernels[2].launches += 1;
-        r.kernels[0].algo_bytes += (double)cnt * S_B + (double)nslots * 8;
-        r.kernels[1].algo_bytes += (double)nslots * 8;   // + G_in*8 probe bytes and D*16 per level below
+        for (auto& ks : r.kernels) ks.launches += 1;
+        r.kernels[0].algo_bytes += (double)cnt * S_B;        // + G_in * 10 record bytes per level below
       }
       u64 c[K_NCTR];
       HIPCHK(hipMemcpyAsync(c, d_ctr_, sizeof c, hipMemcpyDeviceToHost, stream_));
       HIPCHK(hipStreamSynchronize(stream_));
       double level_ms = 0;
       for (int q = 0; q < nch; ++q)
-        for (int k = 0; k < 3; ++k) {
+        for (int k = 0; k < 4; ++k) {
           float ms = 0;
-          (void)hipEventElapsedTime(&ms, lvl_ev_[6 * q + 2 * k], lvl_ev_[6 * q + 2 * k + 1]);
+          (void)hipEventElapsedTime(&ms, lvl_ev_[8 * q + 2 * k], lvl_ev_[8 * q + 2 * k + 1]);
           r.kernels[k].ms += ms; level_ms += ms;
         }
-      const u64 next_write = level_end + c[K_LEVEL_NEW];
-      r.kernels[1].algo_bytes += (double)c[K_LEVEL_NEW] * 16;
-      r.kernels[2].algo_bytes += (double)c[K_LEVEL_NEW] * (8 + S_B + S_B + 8);
-      int64_t gen = 0;
-      for (int k = 0; k < OA_NACT; ++k) { r.act_generated[k] += (int64_t)c[K_ACT + k]; r.act_distinct[k] += (int64_t)c[K_ACT + OA_NACT + k]; gen += (int64_t)c[K_ACT + k]; }
-      r.generated += gen;
-      r.generated_in_model += (int64_t)c[K_GEN_IN];
-      r.kernels[1].algo_bytes += (double)c[K_GEN_IN] * 8;
+      const u64 nnew = c[K_LEVEL_NEW];
+      const u64 next_write = level_end + nnew;
+      if (prof_) {
+        for (int q = 0; q < 4; ++q) prof_acc_[q] += c[K_PROF + q];
+        prof_acc_[4] = std::max<u64>(prof_acc_[4], c[K_PROF + 5]);
+      }
+      const u64 G_in = c[K_GEN_IN];
+      // per-kernel algorithmic bytes: generate writes 10-B records; dedup reads them and probes
+      // (8 B per in-model successor) and writes 16 B per new state; mark reads the
+      // inserted positions + keys and sets winner bits; materialize re-reads the parent and writes
+      // state + parent pointer
+      r.kernels[0].algo_bytes += (double)G_in * 10;
+      r.kernels[1].algo_bytes += (double)G_in * (10 + 8) + (double)nnew * (16 + 8);
+      r.kernels[2].algo_bytes += (double)nnew * (8 + 16 + 8);
+      r.kernels[3].algo_bytes += (double)level_count * WW * 8 + (double)nnew * (S_B + S_B + 8);
       r.seconds_kernels += level_ms / 1000.0;
       r.n_launches += 1;
-      const u64 nnew = next_write - (level_begin + level_count);
-      r.algo_bytes += (double)level_count * S_B + (double)c[K_GEN_IN] * 8 + (double)nnew * (16 + S_B);
       if (next_write - base_ > cap_) c[K_ERR] |= OE_CAP_STORE;
+      if (c[K_EVENT] != ~0ull && (c[K_ERR] & ~(u64)OE_CAP_STORE) == 0) {
+        // the level's first event in TLC's order stops the search; a full state store only
+        // matters when it cut off states that come before the event in key order
+        const u64 stored = std::min<u64>(nnew, cap_ - std::min<u64>(cap_, level_end - base_));
+        bool decided = false;
+        if (int rc = handle_event(c[K_EVENT], level_begin, level_count, nnew, stored, r, decided, err)) return rc;
+        if (decided) { total_ = level_end + stored; break; }
+      }
       if (c[K_ERR]) {
         const u64 e = c[K_ERR];
-        r.verdict = (e & (OE_CAP_STORE | OE_TABLE_FULL | OE_CAP_ELECTIONS | OE_CAP_COUNT)) ? MC_VERDICT_CAPACITY_OVERFLOW : MC_VERDICT_EVAL_ERROR;
+        r.verdict = MC_VERDICT_CAPACITY_OVERFLOW;
         std::ostringstream os;
-        os << "error flags 0x" << std::hex << e << std::dec << " while expanding state " << (c[K_ERRGID] ? (int64_t)(c[K_ERRGID] - 1 + base_) : -1) << ":";
-        if (e & OE_EVAL_LOG_INDEX) os << " log[i][prevLogIndex] applied outside its domain (raft_original.tla:207-210);";
+        os << "error flags 0x" << std::hex << e << std::dec << " while expanding state " << (c[K_ERRGID] ? (int64_t)(c[K_ERRGID] - 1) : -1) << ":";
         if (e & OE_CAP_ELECTIONS) os << " elections set exceeds the compiled capacity;";
         if (e & OE_CAP_COUNT) os << " message count / bag capacity exceeded;";
         if (e & OE_CAP_STORE) os << " state store full (raise state_store_bytes);";
@@ -800,32 +1089,109 @@ class OrigGpu : public Backend {
         r.distinct = (int64_t)total_;
         break;
       }
+      int64_t gen = 0;
+      for (int k = 0; k < OA_NACT; ++k) { r.act_generated[k] += (int64_t)c[K_ACT + k]; r.act_distinct[k] += (int64_t)c[K_ACT + OA_NACT + k]; gen += (int64_t)c[K_ACT + k]; }
+      r.generated += gen;
+      r.generated_in_model += (int64_t)G_in;
+      r.algo_bytes += (double)level_count * S_B + (double)G_in * 8 + (double)nnew * (16 + S_B);
       total_ += nnew;
       r.distinct = (int64_t)total_;
       r.levels.back().generated = gen;
       r.levels.back().kernel_ms = level_ms;
       if (nnew > 0) { r.levels.push_back({(int64_t)nnew, 0, 0.0}); r.depth += 1; }
-      if (c[K_VIOL]) {
-        ViolRec<S> v;
-        HIPCHK(hipMemcpy(&v, d_viol_, sizeof v, hipMemcpyDeviceToHost));
-        r.verdict = MC_VERDICT_INVARIANT_VIOLATION;
-        r.violated = first_violated(v.bad);
-        build_trace(v.parent + base_, kOrigActNames[v.act], v.w, r, err);
-        r.left_on_queue = (int64_t)nnew;
-        break;
-      }
-      if (o.check_deadlock && c[K_DEADLOCK]) {
-        r.verdict = MC_VERDICT_DEADLOCK;
-        build_trace(c[K_DEADLOCK] - 1 + base_, nullptr, s0, r, err);
-        r.left_on_queue = (int64_t)nnew;
-        break;
-      }
       level_begin += level_count;
       level_count = nnew;
       if (o.checkpoint_every > 0 && !o.checkpoint_path.empty() && r.depth % o.checkpoint_every == 0 && level_count > 0)
         if (int rc = save_checkpoint(o.checkpoint_path, r, level_begin, level_count, err)) return rc;
     }
+    if (prof_ && prof_acc_[3])
+      std::fprintf(stderr, "orig_probe per workgroup (us): %.2f  (%llu workgroups)\n",
+                   prof_acc_[1] / 100.0 / prof_acc_[3], (unsigned long long)prof_acc_[3]);
+    if (prof_) std::fprintf(stderr, "max concurrent dedup workgroups %llu\n", (unsigned long long)prof_acc_[4]);
+    for (auto& x : prof_acc_) x = 0;
     finish(r, t0);
+    return 0;
+  }
+
+  // TLC's stop point at the level's first event (key order = TLC's single-worker FIFO order):
+  // generated = whole successor lists of the parents before the event's parent and of the
+  // parent itself (none when computing its successors raised the error); per-action generated
+  // stops at the event's successor; distinct = states inserted before it (the level's new
+  // states are stored in key order: a binary search over their parent pointers); left on queue
+  // = the level's parents after it + the new states found before it.
+  // stored: how many of the level's nnew new states the store holds (a prefix in key order);
+  // decided = false when the event may lie behind states the full store cut off
+  int handle_event(u64 ev, u64 level_begin, u64 level_count, u64 nnew, u64 stored, RunResult& r, bool& decided,
+                   std::string& err) {
+    const int kind = (int)(ev & 3);
+    const u64 key = ev >> 2, pg = key >> 8;
+    const u32 k = (u32)(key & 255);
+    const u64 level_end = level_begin + level_count;
+    // distinct: this level's new states with key < event key (<= for a violation: the violating
+    // state itself is new when it is in the model)
+    auto key_at = [&](u64 i, u64& kk) -> int {
+      u64 mt = 0;
+      HIPCHK(hipMemcpy(&mt, d_meta_ + (level_end - base_) + i, 8, hipMemcpyDeviceToHost));
+      kk = ((mt >> 24) << 8) | (mt & 0xff);
+      return 0;
+    };
+    u64 lo = 0, hi = stored;   // first index whose key is beyond the stop point
+    while (lo < hi) {
+      const u64 mid = (lo + hi) / 2;
+      u64 kk = 0;
+      if (int rc = key_at(mid, kk)) return rc;
+      const bool before = kk < key || (kk == key && kind >= EV_INV_ERROR);
+      if (before) lo = mid + 1; else hi = mid;
+    }
+    const u64 before = lo;
+    decided = before < stored || stored == nnew;
+    if (!decided) return 0;
+    (void)nnew;
+    // generated (device: re-derive the successor lists of the level's parents up to pg)
+    HIPCHK(hipMemsetAsync(d_stop_, 0, (1 + OA_NACT) * 8, stream_));
+    const u64 npar = pg - level_begin + 1;
+    hipLaunchKernelGGL((orig_stop_generated<S>), dim3((unsigned)((npar + BS - 1) / BS)), dim3(BS), 0, stream_,
+                       (const u32*)d_states_, level_begin - base_, npar, level_begin, pg, k, (u32)kind, (unsigned long long*)d_stop_);
+    HIPCHK(hipGetLastError());
+    u64 gs[1 + OA_NACT];
+    HIPCHK(hipMemcpyAsync(gs, d_stop_, sizeof gs, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(hipMemsetAsync(d_stop_, 0, (1 + OA_NACT) * 8, stream_));
+    if (before)
+      hipLaunchKernelGGL(orig_stop_distinct, dim3((unsigned)((before + BS - 1) / BS)), dim3(BS), 0, stream_,
+                         (const u64*)(d_meta_ + (level_end - base_)), before, (unsigned long long*)d_stop_);
+    HIPCHK(hipGetLastError());
+    u64 ds[1 + OA_NACT];
+    HIPCHK(hipMemcpyAsync(ds, d_stop_, sizeof ds, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    r.generated += (int64_t)gs[0];
+    for (int a = 0; a < OA_NACT; ++a) { r.act_generated[a] += (int64_t)gs[1 + a]; r.act_distinct[a] += (int64_t)ds[a]; }
+    r.distinct = (int64_t)(level_end + before);
+    r.left_on_queue = (int64_t)(level_end - pg - 1 + before);
+    // the event's parent and (for a violation) successor, re-derived on the host
+    u32 w[NWP]; u64 meta = 0;
+    if (!stored_state(pg, w, meta)) { err = "event state readback failed"; return MC_E_NO_DEVICE; }
+    W s; S::unpack(w, s);
+    if (kind == EV_NEXT_ERROR) {
+      r.verdict = MC_VERDICT_EVAL_ERROR;
+      r.error = "TLC evaluation error while computing the successors of state " + std::to_string(pg) +
+                ": log[i][prevLogIndex] applied outside its domain (raft_original.tla:207-210)";
+      build_trace(pg, nullptr, s, r, err);
+      return 0;
+    }
+    if (kind == EV_DEADLOCK) {
+      r.verdict = MC_VERDICT_DEADLOCK;
+      build_trace(pg, nullptr, s, r, err);
+      return 0;
+    }
+    u64 al[S::AW]; S::all_logs_next(s, al);
+    W t; u32 e2 = 0;
+    const int act = S::apply(s, (int)k, t, e2);
+    for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
+    r.verdict = MC_VERDICT_INVARIANT_VIOLATION;
+    r.violated = first_violated(S::violated(t, m_.rt.invariants));
+    r.depth += 1;
+    build_trace(pg, act >= 0 ? kOrigActNames[act] : "?", t, r, err);
     return 0;
   }
 
@@ -894,9 +1260,9 @@ class OrigGpu : public Backend {
     const u64 stage = std::max<u64>(1, chunk_states_ * S::NI * 8 / (NWP * 4));
     for (u64 b = 0; b < lb; b += stage) {
       const u64 n = std::min<u64>(stage, lb - b);
-      HIPCHK(hipMemcpy(d_cand_, st.data() + b * NWP, n * NWP * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(d_rfp_, st.data() + b * NWP, n * NWP * 4, hipMemcpyHostToDevice));
       hipLaunchKernelGGL((orig_reinsert<S>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_,
-                         (const u32*)d_cand_, n, d_table_, table_mask_, (u64)h.seed, (unsigned long long*)d_ctr_);
+                         (const u32*)d_rfp_, n, d_table_, table_mask_, (u64)h.seed, (unsigned long long*)d_ctr_);
       HIPCHK(hipGetLastError());
       HIPCHK(hipStreamSynchronize(stream_));
     }
@@ -942,8 +1308,9 @@ class OrigGpu : public Backend {
     if (world < 1 || world > 8 || rank < 0 || rank >= world) { err = "sharded mode supports 1..8 ranks"; return MC_E_INVALID; }
     if (int rc = ensure_alloc(o, world, err)) return rc;
     rank_ = rank; world_ = world; sopts_ = o;
-    HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 8, stream_));
+    HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
     HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
+    HIPCHK(hipMemsetAsync(d_ctr_ + K_EVENT, 0xFF, 8, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
     sres_ = RunResult();
     sres_.seed = o.seed ? o.seed : 0x5EED5EED2024ull;
@@ -961,7 +1328,8 @@ class OrigGpu : public Backend {
     base_ = 0; host_states_.clear(); host_meta_.clear();
     if ((int)fp_owner(fp0, (u32)world) == rank) {
       u32 wp[NWP] = {0}; for (int q = 0; q < S::NW; ++q) wp[q] = w0[q];
-      HIPCHK(hipMemcpy(d_table_ + (fp0 & table_mask_), &fp0, 8, hipMemcpyHostToDevice));
+      const u64 e0[2] = {fp0, ~0ull};
+      HIPCHK(hipMemcpy(d_table_ + 2 * (fp0 & table_mask_), e0, 16, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(d_states_, wp, NWP * 4, hipMemcpyHostToDevice));
       const u64 nometa = ~0ull;
       HIPCHK(hipMemcpy(d_meta_, &nometa, 8, hipMemcpyHostToDevice));
@@ -989,18 +1357,14 @@ class OrigGpu : public Backend {
     sh_chunk_begin_ = sh_level_begin_ + (u64)begin; sh_chunk_count_ = (u64)count;
     HIPCHK(hipMemsetAsync(d_rcnt_, 0, 8 * 8, stream_));
     if (count > 0) {
-      const u64 nslots = (u64)count * S::NI;
-      GenArgs g;
-      g.states = d_states_; g.chunk_begin = sh_chunk_begin_; g.chunk_count = (u64)count; g.cand = d_cand_; g.seed = sres_.seed;
-      g.rt = m_.rt; g.inv_oom = sopts_.inv_out_of_model ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_; g.viol = d_viol_;
-      RouteArgs ra;
-      ra.cand = d_cand_; ra.nslots = nslots; ra.route = d_route_; ra.route_cap = chunk_states_ * S::NI; ra.world = (u32)world_;
-      ra.rcnt = (unsigned long long*)d_rcnt_;
-      float ms_x = 0;
-      if (int rc = run_generate(g, (u64)count, ms_x, err, true)) return rc;
-      auto& ke = sres_.kernels[0]; ke.ms += ms_x; ke.launches++; ke.algo_bytes += (double)count * NWP * 4 + (double)nslots * 8;
-      HIPCHK(hipEventRecord(ev_[1], stream_));
-      hipLaunchKernelGGL((orig_route_blk<S::NI>), dim3((unsigned)((count + BS - 1) / BS)), dim3(BS), 0, stream_, ra);
+      const GenArgs g = gen_args(sh_chunk_begin_, (u64)count, sh_chunk_begin_, sres_.seed, sopts_);
+      const RouteArgs ra = route_args((u32)world_);
+      const unsigned nblk = (unsigned)((count + BS - 1) / BS);
+      HIPCHK(hipEventRecord(ev_[5], stream_));
+      hipLaunchKernelGGL((orig_generate<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(ev_[6], stream_));
+      hipLaunchKernelGGL(orig_route_blk, dim3(nblk), dim3(BS), 0, stream_, ra);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(ev_[2], stream_));
     }
@@ -1008,9 +1372,9 @@ class OrigGpu : public Backend {
     HIPCHK(hipMemcpyAsync(c, d_rcnt_, 8 * 8, hipMemcpyDeviceToHost, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
     if (count > 0) {
-      const u64 nslots = (u64)count * S::NI;
       u64 valid = 0; for (int r = 0; r < world_; ++r) valid += c[r];
-      auto& kr = sres_.kernels[1]; kr.ms += time_ms(1, 2); kr.launches++; kr.algo_bytes += (double)nslots * 8 + (double)valid * 16;
+      auto& ke = sres_.kernels[0]; ke.ms += time_ms(5, 6); ke.launches++; ke.algo_bytes += (double)count * NWP * 4;
+      auto& kr = sres_.kernels[1]; kr.ms += time_ms(6, 2); kr.launches++; kr.algo_bytes += (double)valid * 16;
     }
     for (int r = 0; r < world_; ++r) { counts[r] = (int64_t)c[r]; fill_counts_route_[r] = c[r]; }
     return 0;
@@ -1075,7 +1439,7 @@ class OrigGpu : public Backend {
       MatShArgs m;
       m.states = d_states_; m.acks = (const u64*)acks + seg_off_ack_[r]; m.n = n; m.chunk_begin = sh_chunk_begin_;
       m.chunk_count = sh_chunk_count_; m.out = d_stout_ + seg_off_ack_[r] * (NWP + 4); m.rank_bits = (u64)rank_ << 37;
-      m.seed = sres_.seed; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.viol = d_viol_;
+      m.seed = sres_.seed; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_;
       hipLaunchKernelGGL((orig_materialize_sh<S>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, m);
       HIPCHK(hipGetLastError());
     }
@@ -1108,8 +1472,11 @@ class OrigGpu : public Backend {
     int64_t gen = 0;
     for (int k = 0; k < OA_NACT; ++k) { st[8 + k] = (int64_t)c[K_ACT + k]; st[40 + k] = (int64_t)c[K_ACT + OA_NACT + k]; gen += (int64_t)c[K_ACT + k]; }
     st[1] = gen; st[2] = (int64_t)c[K_GEN_IN];
-    st[3] = (int64_t)(c[K_ERR] | (sh_next_write_ > cap_ ? (u64)OE_CAP_STORE : 0ull));
-    st[4] = (int64_t)c[K_VIOL]; st[5] = (int64_t)c[K_DEADLOCK]; st[6] = (int64_t)sh_level_count_;
+    // the sharded raft_original search is not FIFO-ranked across ranks: any event stops it
+    sh_event_ = c[K_EVENT];
+    const int kind = sh_event_ == ~0ull ? -1 : (int)(sh_event_ & 3);
+    st[3] = (int64_t)(c[K_ERR] | (sh_next_write_ > cap_ ? (u64)OE_CAP_STORE : 0ull) | (kind == EV_NEXT_ERROR ? (u64)OE_EVAL_LOG_INDEX : 0ull));
+    st[4] = kind == EV_VIOLATION ? 1 : 0; st[5] = kind == EV_DEADLOCK ? 1 : 0; st[6] = (int64_t)sh_level_count_;
     return 0;
   }
 
@@ -1121,6 +1488,7 @@ class OrigGpu : public Backend {
     *done = 0;
     if (g[3]) {
       sres_.verdict = (g[3] & (OE_CAP_STORE | OE_TABLE_FULL | OE_CAP_ELECTIONS | OE_CAP_COUNT)) ? MC_VERDICT_CAPACITY_OVERFLOW : MC_VERDICT_EVAL_ERROR;
+      sh_event_ = ~0ull;
       std::ostringstream os; os << "error flags 0x" << std::hex << g[3] << " raised on some rank"; sres_.error = os.str();
       *done = 1;
     }
@@ -1136,14 +1504,27 @@ class OrigGpu : public Backend {
     total_ = sh_next_write_;
     sh_new_ = 0;
     HIPCHK(hipMemset(d_ctr_, 0, K_NCTR * 8));
+    HIPCHK(hipMemset(d_ctr_ + K_EVENT, 0xFF, 8));
     sres_.n_launches += 1;
     if (*done) {
-      if (sres_.verdict == MC_VERDICT_INVARIANT_VIOLATION) {
-        ViolRec<S> v; (void)hipMemcpy(&v, d_viol_, sizeof v, hipMemcpyDeviceToHost);
-        sviol_parent_ = ((u64)rank_ << 37) | v.parent; sviol_act_ = kOrigActNames[v.act]; sviol_text_ = state_text(v.w, true);
-        sviol_bad_ = v.bad;
-        sres_.violated = first_violated(v.bad);
+      sviol_act_.clear();
+      if (sres_.verdict == MC_VERDICT_INVARIANT_VIOLATION && sh_event_ != ~0ull && (sh_event_ & 3) == EV_VIOLATION) {
+        // this rank's violating successor, re-derived from (parent, instance)
+        const u64 key = sh_event_ >> 2, par = key >> 8;
+        const int k = (int)(key & 255);
+        u32 w[NWP];
+        if (hipMemcpy(w, d_states_ + par * NWP, NWP * 4, hipMemcpyDeviceToHost) == hipSuccess) {
+          W s, t; S::unpack(w, s);
+          u64 al[S::AW]; S::all_logs_next(s, al);
+          u32 e2 = 0;
+          const int act = S::apply(s, k, t, e2);
+          for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
+          sviol_bad_ = S::violated(t, m_.rt.invariants);
+          sviol_parent_ = ((u64)rank_ << 37) | par; sviol_act_ = act >= 0 ? kOrigActNames[act] : "?";
+          sviol_text_ = state_text(t, true);
+        }
       }
+      if (sres_.verdict == MC_VERDICT_INVARIANT_VIOLATION) sres_.violated = sviol_act_.empty() ? "" : first_violated(sviol_bad_);
       double secs = 0; for (auto& k : sres_.kernels) secs += k.ms / 1000.0;
       sres_.seconds_kernels = secs;
       finish(sres_, st0_);
@@ -1300,18 +1681,12 @@ class OrigGpu : public Backend {
         sh_chunk_begin_ = sh_level_begin_ + begin; sh_chunk_count_ = count;
         HIPCHK(hipMemsetAsync(d_rcnt_, 0, 16 * 8, stream_));
         if (count > 0) {
-          const u64 nslots = count * (u64)S::NI;
-          GenArgs g;
-          g.states = d_states_; g.chunk_begin = sh_chunk_begin_; g.chunk_count = count; g.cand = d_cand_; g.seed = sres_.seed;
-          g.rt = m_.rt; g.inv_oom = sopts_.inv_out_of_model ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_; g.viol = d_viol_;
+          const GenArgs g = gen_args(sh_chunk_begin_, count, sh_chunk_begin_, sres_.seed, sopts_);
           const unsigned nblk = (unsigned)((count + BS - 1) / BS);
-          NAT_TIMED(0, hipLaunchKernelGGL((orig_generate<S, true>), dim3(nblk), dim3(BS), 0, stream_, g));
-          sres_.kernels[0].algo_bytes += (double)count * NWP * 4 + (double)nslots * 8;
-          RouteArgs ra;
-          ra.cand = d_cand_; ra.nslots = nslots; ra.route = d_route_; ra.route_cap = route_cap; ra.world = (u32)W;
-          ra.rcnt = (unsigned long long*)d_rcnt_;
-          NAT_TIMED(1, hipLaunchKernelGGL((orig_route_blk<S::NI>), dim3(nblk), dim3(BS), 0, stream_, ra));
-          sres_.kernels[1].algo_bytes += (double)nslots * 8;
+          NAT_TIMED(0, hipLaunchKernelGGL((orig_generate<S>), dim3(nblk), dim3(BS), 0, stream_, g));
+          sres_.kernels[0].algo_bytes += (double)count * NWP * 4;
+          const RouteArgs ra = route_args((u32)W);
+          NAT_TIMED(1, hipLaunchKernelGGL(orig_route_blk, dim3(nblk), dim3(BS), 0, stream_, ra));
         }
         // ---- ROUTE: (fp, slot) records to the fingerprints' owners
         if (int rc = xcounts(d_rcnt_)) return rc;
@@ -1367,7 +1742,7 @@ class OrigGpu : public Backend {
             m.states = d_states_; m.acks = r == me ? d_newrec_ + seg_off_[me] : (const u64*)nat_acks_ + seg_off_ack_[r];
             m.n = ack[r]; m.chunk_begin = sh_chunk_begin_;
             m.chunk_count = sh_chunk_count_; m.out = d_stout_ + seg_off_ack_[r] * (NWP + 4); m.rank_bits = (u64)me << 37;
-            m.seed = sres_.seed; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.viol = d_viol_;
+            m.seed = sres_.seed; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_;
             NAT_TIMED(3, hipLaunchKernelGGL((orig_materialize_sh<S>), dim3((unsigned)((ack[r] + BS - 1) / BS)), dim3(BS), 0, stream_, m));
           }
           sres_.kernels[3].algo_bytes += (double)atot * (8 + NWP * 4 + SBW);
@@ -1411,8 +1786,10 @@ class OrigGpu : public Backend {
 
  private:
   OrigModel m_;
-  u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr; void* d_viol_ = nullptr;
-  u64* d_cand_ = nullptr; u64* d_newrec_ = nullptr;
+  static constexpr int WW = (S::NI + 63) / 64;   // winner-mask words per parent
+  u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr; u64* d_stop_ = nullptr;
+  u64* d_rfp_ = nullptr; unsigned short* d_rkey_ = nullptr; u32* d_rcnt_blk_ = nullptr; u64* d_newrec_ = nullptr;
+  u64* d_winmask_ = nullptr; u32* d_wcnt_ = nullptr; u64* d_woff_ = nullptr; u64* d_urec_ = nullptr; u32* d_ucnt_ = nullptr;
   u64* d_route_ = nullptr; u64* d_rcnt_ = nullptr; u32* d_stout_ = nullptr; u64 stout_cap_ = 0;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_[9] = {};
@@ -1427,6 +1804,10 @@ class OrigGpu : public Backend {
   u64 seg_off_[8] = {0}, seg_off_ack_[8] = {0}, fill_counts_reply_[8] = {0}, fill_counts_states_[8] = {0};
   u64 fill_counts_route_[8] = {0};
   u64 sviol_parent_ = 0; u32 sviol_bad_ = 0; std::string sviol_act_, sviol_text_;
+  u64 sh_event_ = ~0ull;
+  // RAFTMC_PROF=1: per-phase wall-clock ticks (100 MHz) of orig_dedup, summed over workgroups
+  const bool prof_ = std::getenv("RAFTMC_PROF") != nullptr;
+  u64 prof_acc_[5] = {0, 0, 0, 0, 0};
   // native (RCCL) level loop buffers
   u64* d_nat_ = nullptr; u64* h_nat_ = nullptr;
   void* nat_recv_ = nullptr; void* nat_acks_ = nullptr; void* nat_stin_ = nullptr;
@@ -1439,7 +1820,8 @@ class OrigGpu : public Backend {
   std::vector<u64> host_meta_;
 
   void release() {
-    for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, d_viol_, (void*)d_cand_, (void*)d_newrec_,
+    for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_stop_, (void*)d_rfp_, (void*)d_rkey_,
+                    (void*)d_rcnt_blk_, (void*)d_newrec_, (void*)d_winmask_, (void*)d_wcnt_, (void*)d_woff_, (void*)d_urec_, (void*)d_ucnt_,
                     (void*)d_route_, (void*)d_rcnt_, (void*)d_stout_})
       if (p) (void)hipFree(p);
     for (void* p : {(void*)d_nat_, nat_recv_, nat_acks_, nat_stin_})
@@ -1453,15 +1835,14 @@ class OrigGpu : public Backend {
     lvl_ev_.clear();
     for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
     if (stream_) (void)hipStreamDestroy(stream_);
-    d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_viol_ = nullptr;
-    d_cand_ = nullptr; d_newrec_ = nullptr; d_route_ = nullptr; d_rcnt_ = nullptr; d_stout_ = nullptr; stout_cap_ = 0;
+    d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_stop_ = nullptr;
+    d_rfp_ = nullptr; d_rkey_ = nullptr; d_rcnt_blk_ = nullptr; d_newrec_ = nullptr; d_winmask_ = nullptr; d_wcnt_ = nullptr; d_woff_ = nullptr; d_urec_ = nullptr; d_ucnt_ = nullptr; d_route_ = nullptr; d_rcnt_ = nullptr; d_stout_ = nullptr; stout_cap_ = 0;
     stream_ = nullptr; alloc_world_ = 0;
   }
 
   std::string first_violated(u32 bad) const {
     for (auto& n : m_.inv_names) {
-      const u32 bit = n == "ElectionSafety" ? OI_ElectionSafety : n == "LogMatching" ? OI_LogMatching : OI_NoLeader;
-      if (bad & bit) return n;
+      if (bad & orig_inv_bit(n.c_str())) return n;
     }
     return "?";
   }

@@ -50,9 +50,7 @@ OrigModel resolve_orig_model(const CfgFile& cfg) {
   if (m.rt.constraints != (OC_BoundedTerms | OC_BoundedLogs | OC_BoundedMessages))
     throw CfgError(MC_E_UNSUPPORTED, "raft_original needs BoundedTerms, BoundedLogs and BoundedMessages (its state space is infinite otherwise, G1)");
   for (auto& n : cfg.invariants) {
-    if (n == "ElectionSafety") m.rt.invariants |= OI_ElectionSafety;
-    else if (n == "LogMatching") m.rt.invariants |= OI_LogMatching;
-    else if (n == "NoLeader") m.rt.invariants |= OI_NoLeader;
+    if (const u32 bit = orig_inv_bit(n.c_str())) m.rt.invariants |= bit;
     else throw CfgError(MC_E_UNSUPPORTED, "unknown invariant '" + n + "' for raft_original");
     m.inv_names.push_back(n);
   }

@@ -36,8 +36,17 @@ static const char* const kOrigActNames[OA_NACT] = {
 
 // constraint / invariant selection bits (resolved from cfg names on the host)
 enum { OC_BoundedTerms = 1, OC_BoundedLogs = 2, OC_BoundedMessages = 4 };
-enum { OI_ElectionSafety = 1, OI_LogMatching = 2, OI_NoLeader = 4 };
-static const char* const kOrigInvNames[3] = {"ElectionSafety", "LogMatching", "NoLeader"};
+enum { OI_ElectionSafety = 1, OI_LogMatching = 2, OI_NoLeader = 4, OI_NoCommit = 8 };
+static const char* const kOrigInvNames[4] = {"ElectionSafety", "LogMatching", "NoLeader", "NoCommit"};
+// OI_* bit of an invariant name (configs/raft_original_mc.tla), 0 if unknown
+inline u32 orig_inv_bit(const char* n) {
+  for (int k = 0; k < 4; ++k) {
+    const char* a = kOrigInvNames[k]; const char* b = n;
+    while (*a && *a == *b) { ++a; ++b; }
+    if (!*a && !*b) return 1u << k;
+  }
+  return 0;
+}
 
 // error flags raised by the successor function (TLC evaluation errors / capacity)
 enum { OE_EVAL_LOG_INDEX = 1, OE_CAP_ELECTIONS = 2, OE_CAP_COUNT = 4 };
@@ -67,11 +76,12 @@ struct Orig {
   static constexpr int EMAX = MT;                   // elections capacity (one per (term, leader))
   static constexpr int VLB = 1 + LIB;               // voterLog cell: present bit + log index
   static constexpr int CNTB = 4;                    // message count field (count + 8)
-  // message code: type(2) term(TB) src(SB) dst(SB) payload
-  static constexpr int MP0 = 2 + TB + 2 * SB;
-  static constexpr int PAY_RVQ = TB + CIB, PAY_RVP = 1 + LIB, PAY_AEQ = CIB + TB + EB + LIB + CIB, PAY_AEP = 1 + CIB;
-  static constexpr int PAYB = PAY_AEQ > PAY_RVP ? (PAY_AEQ > PAY_RVQ ? PAY_AEQ : PAY_RVQ) : (PAY_RVP > PAY_RVQ ? PAY_RVP : PAY_RVQ);
-  static constexpr int MSGB = MP0 + (PAYB > PAY_AEP ? PAYB : PAY_AEP);
+  // message code: class(2) << BODY | body, ORDER PRESERVING (see "messages" below)
+  static constexpr int BODY_RVQ = SB + CIB + TB + SB + TB, BODY_RVP = SB + LIB + SB + TB + 1,
+                       BODY_AEP = SB + CIB + SB + 1 + TB, BODY_AEQ = CIB + SB + EB + LIB + CIB + TB + SB + TB;
+  static constexpr int BODY_A = BODY_RVQ > BODY_RVP ? BODY_RVQ : BODY_RVP, BODY_B = BODY_AEP > BODY_AEQ ? BODY_AEP : BODY_AEQ;
+  static constexpr int BODY = BODY_A > BODY_B ? BODY_A : BODY_B;
+  static constexpr int MSGB = 2 + BODY;
   static constexpr int ENTB = MSGB + CNTB;          // bag entry width
   static constexpr int ELB = TB + SB + LIB + N + N * VLB;   // election record width
   // ---- packed (stored) layout
@@ -136,27 +146,65 @@ struct Orig {
   }
 
   // ---------------------------------------------------------------- messages
-  enum { RVQ = 0, RVP = 1, AEQ = 2, AEP = 3 };
-  RMC_HD static u64 mhdr(int type, int term, int src, int dst) {
-    return (u64)type | ((u64)term << 2) | ((u64)src << (2 + TB)) | ((u64)dst << (2 + TB + SB));
+  // The code is ORDER PRESERVING: numeric order of codes == the order of the message records
+  // as TLA+ values (the oracle's value order, oracle/tla.h cmp: records by field count, then
+  // field names, then field values in field-name order; sequences by length, then elements;
+  // model values by their TLC intern order = the server index).  The bag is kept sorted by
+  // code, so bag slot order is the enumeration order of `\E m \in DOMAIN messages` (Next,
+  // raft_original.tla:460-462) and the instance index of a successor is its position in TLC's
+  // single-worker FIFO order — the key the GPU uses to pick TLC's first-found parent and stop
+  // point.  Field-name order of the four record shapes (raft_original.tla:191-197, 213-223,
+  // 295-301, 352-357/368-373):
+  //   RequestVoteRequest   mdest, mlastLogIndex, mlastLogTerm, msource, mterm, mtype   (6)
+  //   RequestVoteResponse  mdest, mlog, msource, mterm, mtype, mvoteGranted            (6)
+  //   AppendEntriesResp.   mdest, mmatchIndex, msource, msuccess, mterm, mtype         (6)
+  //   AppendEntriesReq.    mcommitIndex, mdest, mentries, mlog, mprevLogIndex,
+  //                        mprevLogTerm, msource, mterm, mtype                          (9)
+  // so the class order is RVQ < RVP < AEP (second field name "mla" < "mlo" < "mma") < AEQ (more
+  // fields); mtype is constant within a class.  Bodies are MSB-first in field-name order.
+  enum { RVQ = 0, RVP = 1, AEP = 2, AEQ = 3 };
+  RMC_HD static int mtype(u64 c) { return (int)(c >> BODY); }
+  RMC_HD static u64 fld(u64 c, int off, int w) { return (c >> off) & lomask(w); }
+  // offsets from bit 0 (the last field of each body is its least significant)
+  RMC_HD static int mterm(u64 c) { return (int)fld(c, mtype(c) == RVP ? 1 : 0, TB); }
+  RMC_HD static int msrc(u64 c) { const int t = mtype(c); return (int)fld(c, TB + ((t == RVP || t == AEP) ? 1 : 0), SB); }
+  RMC_HD static int mdst(u64 c) {
+    const int t = mtype(c);
+    const int off = t == RVQ ? TB + SB + TB + CIB : t == RVP ? 1 + TB + SB + LIB : t == AEP ? TB + 1 + SB + CIB
+                                                                                             : TB + SB + TB + CIB + LIB + EB;
+    return (int)fld(c, off, SB);
   }
-  RMC_HD static int mtype(u64 c) { return (int)(c & 3); }
-  RMC_HD static int mterm(u64 c) { return (int)((c >> 2) & lomask(TB)); }
-  RMC_HD static int msrc(u64 c) { return (int)((c >> (2 + TB)) & lomask(SB)); }
-  RMC_HD static int mdst(u64 c) { return (int)((c >> (2 + TB + SB)) & lomask(SB)); }
-  RMC_HD static u64 mpay(u64 c, int off, int w) { return (c >> (MP0 + off)) & lomask(w); }
+  RMC_HD static int rvq_llt(u64 c) { return (int)fld(c, TB + SB, TB); }
+  RMC_HD static int rvq_lli(u64 c) { return (int)fld(c, TB + SB + TB, CIB); }
+  RMC_HD static int rvp_granted(u64 c) { return (int)fld(c, 0, 1); }
+  RMC_HD static u32 rvp_log(u64 c) { return (u32)fld(c, 1 + TB + SB, LIB); }
+  RMC_HD static int aep_success(u64 c) { return (int)fld(c, TB, 1); }
+  RMC_HD static int aep_mmi(u64 c) { return (int)fld(c, TB + 1 + SB, CIB); }
+  RMC_HD static int aeq_plt(u64 c) { return (int)fld(c, TB + SB, TB); }
+  RMC_HD static int aeq_pli(u64 c) { return (int)fld(c, TB + SB + TB, CIB); }
+  RMC_HD static u32 aeq_log(u64 c) { return (u32)fld(c, TB + SB + TB + CIB, LIB); }
+  RMC_HD static int aeq_ent(u64 c) { return (int)fld(c, TB + SB + TB + CIB + LIB, EB); }
+  RMC_HD static int aeq_mci(u64 c) { return (int)fld(c, TB + SB + TB + CIB + LIB + EB + SB, CIB); }
   RMC_HD static u64 m_rvq(int term, int llt, int lli, int src, int dst) {
-    return mhdr(RVQ, term, src, dst) | ((u64)llt << MP0) | ((u64)lli << (MP0 + TB));
+    u64 b = (u64)dst;
+    b = (b << CIB) | (u64)lli; b = (b << TB) | (u64)llt; b = (b << SB) | (u64)src; b = (b << TB) | (u64)term;
+    return ((u64)RVQ << BODY) | b;
   }
   RMC_HD static u64 m_rvp(int term, bool granted, u32 logidx, int src, int dst) {
-    return mhdr(RVP, term, src, dst) | ((u64)granted << MP0) | ((u64)logidx << (MP0 + 1));
+    u64 b = (u64)dst;
+    b = (b << LIB) | (u64)logidx; b = (b << SB) | (u64)src; b = (b << TB) | (u64)term; b = (b << 1) | (u64)granted;
+    return ((u64)RVP << BODY) | b;
   }
   RMC_HD static u64 m_aeq(int term, int pli, int plt, int entry, u32 logidx, int commit, int src, int dst) {
-    return mhdr(AEQ, term, src, dst) | ((u64)pli << MP0) | ((u64)plt << (MP0 + CIB)) | ((u64)entry << (MP0 + CIB + TB)) |
-           ((u64)logidx << (MP0 + CIB + TB + EB)) | ((u64)commit << (MP0 + CIB + TB + EB + LIB));
+    u64 b = (u64)commit;
+    b = (b << SB) | (u64)dst; b = (b << EB) | (u64)entry; b = (b << LIB) | (u64)logidx; b = (b << CIB) | (u64)pli;
+    b = (b << TB) | (u64)plt; b = (b << SB) | (u64)src; b = (b << TB) | (u64)term;
+    return ((u64)AEQ << BODY) | b;
   }
   RMC_HD static u64 m_aep(int term, bool success, int mmi, int src, int dst) {
-    return mhdr(AEP, term, src, dst) | ((u64)success << MP0) | ((u64)mmi << (MP0 + 1));
+    u64 b = (u64)dst;
+    b = (b << CIB) | (u64)mmi; b = (b << SB) | (u64)src; b = (b << 1) | (u64)success; b = (b << TB) | (u64)term;
+    return ((u64)AEP << BODY) | b;
   }
   // bag entries: code << CNTB | (count + 8); ~0 = empty; kept sorted ascending
   static constexpr u64 EMPTY = ~0ull;
@@ -379,7 +427,7 @@ struct Orig {
     const u32 li = sel(s.log, i);
     const int n = llen(li);
     if (ty == RVQ) {                                               // HandleRequestVoteRequest :283-302
-      const int llt = (int)mpay(m, 0, TB), lli = (int)mpay(m, TB, CIB), lt = last_term(li);
+      const int llt = rvq_llt(m), lli = rvq_lli(m), lt = last_term(li);
       const bool logOk = llt > lt || (llt == lt && lli >= n);
       const int vf = g_voted(s, i);
       const bool grant = mt == ct && logOk && (vf == N || vf == j);
@@ -391,19 +439,19 @@ struct Orig {
     if (ty == RVP) {
       if (mt < ct) { without_msg(t.bag, m, err); return OA_DropStaleResponse; }   // :414-417
       set_row_bits(t.vresp, i, row_bits(s.vresp, i) | (1u << j));                 // HandleRequestVoteResponse :306-320
-      if (mpay(m, 0, 1)) {
+      if (rvp_granted(m)) {
         set_row_bits(t.vgrant, i, row_bits(s.vgrant, i) | (1u << j));
         u64 row = sel(s.vl, i);
         if (!((row >> (j * VLB)) & 1ull))                                         // voterLog[i] @@ (j :> m.mlog): left-biased
-          row |= ((mpay(m, 1, LIB) << 1) | 1ull) << (j * VLB);
+          row |= (((u64)rvp_log(m) << 1) | 1ull) << (j * VLB);
         put(t.vl, i, row);
       }
       without_msg(t.bag, m, err);
       return OA_HandleRequestVoteResponse;
     }
     if (ty == AEQ) {                                               // HandleAppendEntriesRequest :326-388
-      const int pli = (int)mpay(m, 0, CIB), plt = (int)mpay(m, CIB, TB), ment = (int)mpay(m, CIB + TB, EB);
-      const int mci = (int)mpay(m, CIB + TB + EB + LIB, CIB);
+      const int pli = aeq_pli(m), plt = aeq_plt(m), ment = aeq_ent(m);
+      const int mci = aeq_mci(m);
       const int st = g_st(s, i);
       const bool logOk = pli == 0 || (pli > 0 && pli <= n && plt == eterm(lent(li, pli - 1)));
       if (mt < ct || (st == F && !logOk)) {                        // reject request
@@ -428,8 +476,8 @@ struct Orig {
     // AppendEntriesResponse
     if (mt < ct) { without_msg(t.bag, m, err); return OA_DropStaleResponse; }
     {                                                              // HandleAppendEntriesResponse :392-402
-      const int mmi = (int)mpay(m, 1, CIB);
-      if (mpay(m, 0, 1)) { s_ni(t, i, j, mmi + 1); s_mi(t, i, j, mmi); }
+      const int mmi = aep_mmi(m);
+      if (aep_success(m)) { s_ni(t, i, j, mmi + 1); s_mi(t, i, j, mmi); }
       else { const int ni = g_ni(s, i, j); s_ni(t, i, j, ni - 1 > 1 ? ni - 1 : 1); }
       without_msg(t.bag, m, err);
       return OA_HandleAppendEntriesResponse;
@@ -498,6 +546,9 @@ struct Orig {
 #pragma unroll
       for (int i = 0; i < N; ++i) ok &= g_st(t, i) != L;
       if (!ok) bad |= OI_NoLeader;
+    }
+    if (invs & OI_NoCommit) {         // \A i \in Server : commitIndex[i] = 0 (test-only scenario invariant)
+      if (t.commit != 0u) bad |= OI_NoCommit;
     }
     return bad;
   }

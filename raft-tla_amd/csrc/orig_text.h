@@ -75,23 +75,23 @@ struct OrigText {
     const std::string src = sv(S::msrc(c)), dst = sv(S::mdst(c)), term = std::to_string(S::mterm(c));
     switch (S::mtype(c)) {
       case S::RVQ:
-        return record({{"mtype", m_.t_rvq}, {"mterm", term}, {"mlastLogTerm", std::to_string(S::mpay(c, 0, S::TB))},
-                       {"mlastLogIndex", std::to_string(S::mpay(c, S::TB, S::CIB))}, {"msource", src}, {"mdest", dst}});
+        return record({{"mtype", m_.t_rvq}, {"mterm", term}, {"mlastLogTerm", std::to_string(S::rvq_llt(c))},
+                       {"mlastLogIndex", std::to_string(S::rvq_lli(c))}, {"msource", src}, {"mdest", dst}});
       case S::RVP:
-        return record({{"mtype", m_.t_rvp}, {"mterm", term}, {"mvoteGranted", S::mpay(c, 0, 1) ? "TRUE" : "FALSE"},
-                       {"mlog", log_text(S::lfrom_idx((u32)S::mpay(c, 1, S::LIB)))}, {"msource", src}, {"mdest", dst}});
+        return record({{"mtype", m_.t_rvp}, {"mterm", term}, {"mvoteGranted", S::rvp_granted(c) ? "TRUE" : "FALSE"},
+                       {"mlog", log_text(S::lfrom_idx(S::rvp_log(c)))}, {"msource", src}, {"mdest", dst}});
       case S::AEQ: {
-        const int ent = (int)S::mpay(c, S::CIB + S::TB, S::EB);
-        return record({{"mtype", m_.t_aeq}, {"mterm", term}, {"mprevLogIndex", std::to_string(S::mpay(c, 0, S::CIB))},
-                       {"mprevLogTerm", std::to_string(S::mpay(c, S::CIB, S::TB))},
+        const int ent = S::aeq_ent(c);
+        return record({{"mtype", m_.t_aeq}, {"mterm", term}, {"mprevLogIndex", std::to_string(S::aeq_pli(c))},
+                       {"mprevLogTerm", std::to_string(S::aeq_plt(c))},
                        {"mentries", ent ? "<<" + entry_text(ent) + ">>" : "<<>>"},
-                       {"mlog", log_text(S::lfrom_idx((u32)S::mpay(c, S::CIB + S::TB + S::EB, S::LIB)))},
-                       {"mcommitIndex", std::to_string(S::mpay(c, S::CIB + S::TB + S::EB + S::LIB, S::CIB))},
+                       {"mlog", log_text(S::lfrom_idx(S::aeq_log(c)))},
+                       {"mcommitIndex", std::to_string(S::aeq_mci(c))},
                        {"msource", src}, {"mdest", dst}});
       }
       default:
-        return record({{"mtype", m_.t_aep}, {"mterm", term}, {"msuccess", S::mpay(c, 0, 1) ? "TRUE" : "FALSE"},
-                       {"mmatchIndex", std::to_string(S::mpay(c, 1, S::CIB))}, {"msource", src}, {"mdest", dst}});
+        return record({{"mtype", m_.t_aep}, {"mterm", term}, {"msuccess", S::aep_success(c) ? "TRUE" : "FALSE"},
+                       {"mmatchIndex", std::to_string(S::aep_mmi(c))}, {"msource", src}, {"mdest", dst}});
     }
   }
   std::string state_text(const W& s, bool multiline) const {

@@ -64,9 +64,15 @@ def kernels(co):
     # amdhsa metadata: a list of kernel maps (keys sorted): private segment size, then symbol
     priv = re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)
     syms = re.findall(r"\.symbol:\s+(\S+)\.kd", notes)
-    for s, p in zip(syms, priv):
+    lds = re.findall(r"\.group_segment_fixed_size:\s+(\d+)", notes)
+    vgpr = re.findall(r"\.vgpr_count:\s+(\d+)", notes)
+    agpr = re.findall(r"\.agpr_count:\s+(\d+)", notes)
+    for k, (s, p) in enumerate(zip(syms, priv)):
         if s in out:
             out[s]["scratch_bytes"] = int(p)
+            if k < len(lds): out[s]["lds_bytes"] = int(lds[k])
+            if k < len(vgpr): out[s]["vgprs"] = int(vgpr[k])
+            if k < len(agpr): out[s]["agprs"] = int(agpr[k])
     return {k: v for k, v in out.items() if "scratch_bytes" in v}
 
 

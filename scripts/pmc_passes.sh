@@ -1,0 +1,9 @@
+# PMC passes (one rocprofv3 run per counter group, kernel-trace only) over one C2 run; OUT dir = $1
+set -o pipefail
+O=$GRAFT_REPO_ROOT/${1:-gpurun_out/pmc}; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+B="python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 0 --no-cpu-baseline"
+timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_ATOMIC_sum TCC_ATOMIC_sum -d $O/tcc -o run -- $B > $O/tcc.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES -d $O/sq -o run -- $B > $O/sq.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM -d $O/sq2 -o run -- $B > $O/sq2.log 2>&1
+rc=$?; echo rc=$rc; exit $rc

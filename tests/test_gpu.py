@@ -35,11 +35,9 @@ def test_parity_against_oracle(raftmc, name):
         sha, n = states_sha(mc)
     assert r.verdict == "OK", r.error
     assert (r.generated, r.distinct, r.depth) == (g["generated"], g["distinct"], g["depth"])
-    # per-action GENERATED counts are order-independent and must match exactly;
-    # per-action DISTINCT counts depend on which successor reaches a state first
-    # (TLC: FIFO order of one worker), so only their sum is compared here
-    assert {k: v[0] for k, v in r.actions.items()} == {k: v[0] for k, v in g["actions"].items()}
-    assert sum(v[1] for v in r.actions.values()) == g["distinct"] - 1
+    # per-action generated AND distinct counts: distinct ones depend on which successor reaches a
+    # state first (TLC: FIFO order of one worker), which the GPU reproduces (min key per state)
+    assert r.actions == g["actions"]
     assert [lv[0] for lv in r.levels] == g["levels"]
     assert n == g["distinct"] and sha == g["states_sha256"]
 
@@ -50,26 +48,69 @@ def test_depth_limit_kat(raftmc):
     assert (r.generated, r.distinct, r.verdict) == (7, 5, "DEPTH_LIMIT")
 
 
-def test_violation_shortest_trace(raftmc):
-    from oracle_util import run_oracle
-    cfg = os.path.join(CONFIGS, "scenario_first_leader.cfg")
-    ref = run_oracle("bfs", ORIG_MC, cfg, "--trace")
-    r = raftmc.check(ORIG_MC, cfg, **SMALL)
-    assert r.verdict == "INVARIANT_VIOLATION" and r.violated == "NoLeader" and r.exit_code == 12
-    states = r.trace_text.strip().split("\n\n")
-    assert len(states) == ref["trace_len"] == 10
-    # the trace starts in Init and ends in a state with a leader, reached by BecomeLeader
-    assert states[0].startswith("State 1: <Initial predicate>")
-    assert ref["trace"][0]["state"] == " ".join(states[0].split("\n")[1:])
-    assert "<BecomeLeader>" in states[-1].split("\n")[0] and "Leader" in states[-1]
+EVENTS = json.load(open(os.path.join(GOLDEN, "orig_events.json")))
+
+
+def trace_states(r):
+    """(action, one-line state) per "State k:" block of a trace"""
+    out = []
+    for blk in r.trace_text.strip().split("\n\n"):
+        head, *body = blk.split("\n")
+        act = "Init" if "<Initial predicate>" in head else head.split("<", 1)[1].split(" ")[0].rstrip(">")
+        out.append((act, " ".join(body)))
+    return out
+
+
+@pytest.mark.parametrize("name", sorted(EVENTS))
+def test_fifo_stop_point_against_oracle(raftmc, name):
+    """TLC's stop point (tests/golden/orig_events.json): the first violating successor in TLC's
+    single-worker FIFO order, its counterexample state by state, and TLC's counters at that
+    point (generated = whole successor lists up to the violating parent; distinct, per-action
+    counts and left-on-queue at the violating successor; completed levels).  Deterministic: a
+    second run and another fingerprint seed give the identical report."""
+    g = EVENTS[name]
+    cfg = os.path.join(CONFIGS, name + ".cfg")
+    a = raftmc.check(ORIG_MC, cfg, **SMALL)
+    b = raftmc.check(ORIG_MC, cfg, seed=0xC0FFEE, **SMALL)
+    for r in (a, b):
+        assert (r.verdict, r.violated, r.exit_code) == (g["verdict"], g["violated"], 12), r.error
+        assert (r.generated, r.distinct, r.left_on_queue, r.depth) == (g["generated"], g["distinct"], g["left_on_queue"],
+                                                                       g["depth"])
+        assert [lv[0] for lv in r.levels] == g["levels"]
+        assert r.actions == g["actions"]
+        assert trace_states(r) == [(t["action"], t["state"]) for t in g["trace"]]
+    assert a.trace_text == b.trace_text
+
+
+def test_stop_point_independent_of_chunking_and_spill(raftmc):
+    """The counterexample does not depend on chunking: a state store small enough to split the
+    levels into several chunks and to spill completed levels reports the same stop point."""
+    g = EVENTS["c2_noleader"]
+    cfg = os.path.join(CONFIGS, "c2_noleader.cfg")
+    cap = max(4 * 4096, 3 * max(g["levels"]))
+    r = raftmc.check(ORIG_MC, cfg, fp_table_bytes=1 << 26, state_store_bytes=cap * _slot_bytes(raftmc, cfg))
+    assert (r.verdict, r.generated, r.distinct, r.left_on_queue) == (g["verdict"], g["generated"], g["distinct"],
+                                                                     g["left_on_queue"]), r.error
+    assert r.actions == g["actions"]
+    assert trace_states(r) == [(t["action"], t["state"]) for t in g["trace"]]
+
+
+def test_capacity_overflow_verdicts(raftmc):
+    """Compiled-capacity limits are a CAPACITY_OVERFLOW verdict, never a silent clamp: a seen-set
+    or a state store too small for the model."""
+    cfg = os.path.join(CONFIGS, "parity_pair.cfg")
+    r = raftmc.check(ORIG_MC, cfg, fp_table_bytes=1 << 14, state_store_bytes=1 << 26)   # 1024 entries, 20938 states
+    assert r.verdict == "CAPACITY_OVERFLOW" and "fingerprint table full" in r.error, (r.verdict, r.error)
+    r = raftmc.check(ORIG_MC, cfg, fp_table_bytes=1 << 26, state_store_bytes=3000 * _slot_bytes(raftmc, cfg))
+    assert r.verdict == "CAPACITY_OVERFLOW" and "state store full" in r.error, (r.verdict, r.error)
+    assert r.exit_code != 0
 
 
 def test_trace_headers_carry_action_locations(raftmc, tmp_path):
     """TLC's "State k: <Action line L1, col C1 to line L2, col C2 of module M>" headers: with the
     spec module next to the wrapper (as TLC resolves EXTENDS), every step names the span of its
-    action's definition body.  (raft_original reports the first violating successor a workgroup
-    records at the shortest depth, so two runs may show different traces of the same length.)"""
-    import re
+    action's definition body, and the steps are exactly the oracle's counterexample (TLC's FIFO
+    first violating state, tests/golden/orig_events.json)."""
     wrapper = tmp_path / "raft_original_mc.tla"
     wrapper.write_text(open(ORIG_MC).read())
     with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c1.cfg")) as mc:
@@ -82,14 +123,13 @@ def test_trace_headers_carry_action_locations(raftmc, tmp_path):
     r = raftmc.check(str(wrapper), cfg, **SMALL)
     assert r.verdict == "INVARIANT_VIOLATION"
     heads = [b.split("\n")[0] for b in r.trace_text.strip().split("\n\n")]
-    assert len(heads) == 10 and heads[0] == "State 1: <Initial predicate>"
-    for k, h in enumerate(heads[1:]):
-        act = re.match(r"State %d: <(\w+) " % (k + 2), h).group(1)
-        line = 2 * names.index(act) + 3
-        col = len(act) + 8                            # after "Act(i) == "
-        assert h == "State %d: <%s line %d, col %d to line %d, col %d of module raft>" % (
-            k + 2, act, line, col, line, col + 3)
-    assert "<BecomeLeader " in heads[-1]
+    want = [t["action"] for t in EVENTS["scenario_first_leader"]["trace"]]
+    assert len(heads) == len(want) == 10
+    expect = ["State 1: <Initial predicate>"]
+    for k, act in enumerate(want[1:]):
+        line, col = 2 * names.index(act) + 3, len(act) + 8   # after "Act(i) == "
+        expect.append("State %d: <%s line %d, col %d to line %d, col %d of module raft>" % (k + 2, act, line, col, line, col + 3))
+    assert heads == expect
     assert heads[-1] in r.report
 
 
@@ -241,20 +281,19 @@ def test_spill_state_set_c1(raftmc):
 
 def test_spill_violation_trace(raftmc, tmp_path):
     """Trace reconstruction across the host/device split: with a store that forces spills,
-    NoLeader's witness has the in-HBM (shortest) length and the oracle replays it step by step
-    (which shortest witness is kept depends on thread timing, as with TLC's workers)."""
+    NoLeader's witness is still TLC's FIFO-first one (the oracle's, state by state), and the
+    oracle's check-trace replays it step by step."""
     from oracle_util import run_oracle
+    g = EVENTS["scenario_first_leader"]
     cfg = os.path.join(CONFIGS, "scenario_first_leader.cfg")
-    a = raftmc.check(ORIG_MC, cfg, **SMALL)
-    sizes = [lv[0] for lv in a.levels]
+    sizes = g["levels"]
     cap = max(64, int(max(x + y for x, y in zip(sizes, sizes[1:])) * 1.6))
     b = raftmc.check(ORIG_MC, cfg, fp_table_bytes=1 << 26, state_store_bytes=cap * _slot_bytes(raftmc, cfg))
-    assert b.verdict == a.verdict == "INVARIANT_VIOLATION"
-    assert (b.distinct, b.generated) == (a.distinct, a.generated)
-    states = b.trace_text.strip().split("\n\n")
-    assert len(states) == len(a.trace_text.strip().split("\n\n")) == 10
+    assert b.verdict == "INVARIANT_VIOLATION"
+    assert (b.distinct, b.generated, b.left_on_queue) == (g["distinct"], g["generated"], g["left_on_queue"])
+    assert trace_states(b) == [(t["action"], t["state"]) for t in g["trace"]]
     p = tmp_path / "trace.txt"
-    p.write_text("\n".join(" ".join(st.split("\n")[1:]) for st in states) + "\n")
+    p.write_text("\n".join(st for _, st in trace_states(b)) + "\n")
     r = run_oracle("check-trace", ORIG_MC, cfg, "--golden", str(p))
     assert r["valid"] and r["length"] == 10 and r["violated"] == "NoLeader", r
 

@@ -45,3 +45,22 @@ def test_packed_successors_match_oracle(name):
     lines = sorted(l.rstrip("\n") for l in open(dump))
     os.unlink(dump)
     assert hashlib.sha256("\n".join(lines).encode()).hexdigest() == g["states_sha256"]
+
+
+EVENT_SHAPES = {"scenario_first_leader": (2, 1, 2, 1, 5), "c2_noleader": (3, 2, 3, 2, 5), "pair6_nocommit": (2, 1, 2, 1, 6)}
+
+
+@pytest.mark.parametrize("name", sorted(EVENT_SHAPES))
+def test_packed_fifo_stop_point_matches_oracle(name):
+    """TLC's single-worker FIFO order with the product's packed successor function: the bag slot
+    order of the order-preserving message codes is the enumeration order of `\\E m \\in DOMAIN
+    messages`, so a sequential BFS over instance order reproduces the oracle's first violating
+    state, its counterexample and TLC's counters at the stop point exactly
+    (tests/golden/orig_events.json)."""
+    g = json.load(open(os.path.join(GOLDEN, "orig_events.json")))[name]
+    exe = build_harness(EVENT_SHAPES[name])
+    r = json.loads(subprocess.run([exe, os.path.join(CONFIGS, name + ".cfg"), "-"],
+                                  capture_output=True, text=True, check=True).stdout)
+    for k in ("verdict", "violated", "generated", "distinct", "left_on_queue", "depth", "levels", "actions"):
+        assert r[k] == g[k], k
+    assert [(t["action"], t["state"]) for t in r["trace"]] == [(t["action"], t["state"]) for t in g["trace"]]
