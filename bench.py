@@ -16,17 +16,18 @@ all-to-alls (raft-tla_amd/shard.py); value = the model's distinct states /
 max-over-ranks time of one run, "scaling": "strong" (total work fixed).
 
 The JSON line adds:
-  roofline      dominant kernel (orig_generate): algorithmic bytes F*S + G_in*8 +
-                D*(16+S) / summed HIP-event kernel time,
-                against the 8 TB/s HBM peak; traffic from rocprofv3 PMC passes
-                when --traffic-json points at their summary (else null); the
-                dominant kernel is integer-VALU bound, so valu_issue_frac = its
-                PMC VALU wave-instructions per launch (--valu-json) / (live
-                launch time x 256 CUs x 2.4 GHz) is reported beside it
-  cpu_baseline  the CPU oracle (oracle/, test infrastructure: "port") on a
-                bounded sample of the same model (first --cpu-states distinct
-                states of its BFS), --cpu-workers threads (successor expansion in
-                parallel, merged in FIFO order; identical results to 1 thread)
+  roofline      dominant kernel (the one with the most HIP-event time, orig_generate): SURVEY.md
+                §8(d)'s algorithmic bytes of the run, B = F*S + G_in*8 + D*(16+S) (F frontier
+                states expanded, S stored state bytes, G_in in-model successors, D new states),
+                per launch of that kernel / its average launch time (HIP events on the library's
+                stream), against the 8 TB/s HBM peak; traffic = HBM bytes per launch from the
+                rocprofv3 PMC passes committed under profiles/ (FETCH_SIZE x2 + WRITE_SIZE,
+                MI355X_MICROARCH.md), or null; valu_issue_frac = PMC VALU wave-instructions per
+                launch / (launch time x 256 CUs x 2 wave64 issues per CU-cycle x 2.4 GHz)
+  dedup_set     the BASELINE metric's second half: dedup-set GB/s (G_in*8 + D*16) / (merge +
+                probe kernel time) and seen-set probes/s (G_in / that time)
+  cpu_baseline  the CPU oracle (oracle/, test infrastructure: "port") on a bounded sample of the
+                same model (first --cpu-states distinct states of its BFS)
 """
 import argparse
 import importlib
@@ -43,19 +44,32 @@ TLA = os.path.join(ROOT, "configs", "raft_original_mc.tla")
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def cpu_baseline(cfg, max_states, workers):
-    exe = os.path.join(ROOT, "oracle", "_build", "raft_oracle")
-    if not os.path.exists(exe):
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-    t0 = time.time()
-    out = subprocess.run([exe, "bfs", "--tla", TLA, "--cfg", cfg, "--max-states", str(max_states),
-                          "--workers", str(workers)], capture_output=True, text=True, check=True, timeout=600)
-    wall = time.time() - t0
+def cpu_baseline(cfg, max_states, workers, oracle_states):
+    """SURVEY.md §8(d)'s CPU baseline: TLC is not available offline, so the builder's multithreaded
+    C++ BFS (oracle/cpu_bfs.cpp: TLC-style workers, lock-free fingerprint set, the packed successor
+    function) with threads = the host cores this job may use, on the same model; beside it the
+    value-model oracle (oracle/main.cpp, the literal restatement, one thread) on a bounded prefix."""
+    odir = os.path.join(ROOT, "oracle")
+    exe = os.path.join(odir, "_build", "cpu_bfs_c2")
+    orc = os.path.join(odir, "_build", "raft_oracle")
+    if not (os.path.exists(exe) and os.path.exists(orc)):
+        subprocess.run(["make", "-s", "-C", odir], check=True)
+    out = subprocess.run([exe, cfg, "--threads", str(workers), "--max-states", str(max_states)], capture_output=True,
+                         text=True, check=True, timeout=600)
     r = json.loads(out.stdout.strip().splitlines()[-1])
-    secs = r["seconds"] or wall
-    return {"value": r["distinct"] / secs, "unit": "distinct states/s", "cores": workers, "kind": "port",
-            "sample": "oracle BFS of the same model stopped after %d distinct states (%d generated, %.1f s, "
-                      "%d threads expanding, merge in FIFO order)" % (r["distinct"], r["generated"], secs, workers)}
+    whole = r["verdict"] == "OK"
+    res = {"value": r["distinct"] / r["seconds"], "unit": "distinct states/s", "cores": r["threads"], "kind": "port",
+           "sample": "%s: %d distinct / %d generated states in %.2f s, %d threads (oracle/cpu_bfs.cpp: TLC-style "
+                     "multithreaded BFS, lock-free 64-bit fingerprint set, packed states)"
+                     % ("the whole C2 state space" if whole else "C2 BFS stopped after %d distinct" % r["distinct"],
+                        r["distinct"], r["generated"], r["seconds"], r["threads"])}
+    out = subprocess.run([orc, "bfs", "--tla", TLA, "--cfg", cfg, "--max-states", str(oracle_states)],
+                         capture_output=True, text=True, check=True, timeout=600)
+    o = json.loads(out.stdout.strip().splitlines()[-1])
+    res["oracle_value_model"] = {"value": o["distinct"] / o["seconds"], "cores": 1,
+                                 "sample": "oracle/main.cpp (literal TLA+ value-model restatement) stopped after %d "
+                                           "distinct states, %.1f s" % (o["distinct"], o["seconds"])}
+    return res
 
 
 def main():
@@ -64,16 +78,15 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default=os.path.join(ROOT, "configs", "c2.cfg"))
-    ap.add_argument("--cpu-states", type=int, default=400000)
-    # 1 thread: the oracle's value model shares reference-counted sub-values between states,
-    # so its parallel expansion does not scale (MI355X box, 800k-state sample: 16 threads
-    # 25.2k distinct/s vs 1 thread 35.6k distinct/s); the fastest configuration is reported
-    ap.add_argument("--cpu-workers", type=int, default=1)
+    ap.add_argument("--cpu-states", type=int, default=60000000, help="bound of the multithreaded CPU BFS (C2: 54.4M)")
+    ap.add_argument("--oracle-states", type=int, default=300000, help="bound of the value-model oracle's BFS")
+    # the host cores this job may use (the GPU box exports OMP_NUM_THREADS = its CPU share)
+    ap.add_argument("--cpu-workers", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count())
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fp-table-bytes", type=int, default=0, help="seen-set bytes (0 = library default)")
     ap.add_argument("--state-store-bytes", type=int, default=0, help="state store bytes (0 = library default)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_r02.json"))
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -125,7 +138,11 @@ def main():
         per_step = elapsed / args.steps
         # dominant kernel = the one with the most HIP-event time in the last run
         kname, kst = max(res.kernels.items(), key=lambda kv: kv[1]["ms"])
-        achieved = kst["algo_bytes"] / (kst["ms"] / 1e3) / 1e9
+        launches = max(1, kst["launches"])
+        avg_s = kst["ms"] / launches / 1e3
+        # F*S + G_in*8 + D*(16+S) summed over the levels of the run (mc_summary.algo_bytes)
+        bytes_per_launch = res.algo_bytes / launches
+        achieved = bytes_per_launch / avg_s / 1e9
         traffic = None
         if os.path.exists(args.traffic_json):
             try:
@@ -134,6 +151,8 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        ded = [v for k, v in res.kernels.items() if k in ("orig_merge_probe", "orig_dedup")]
+        ded_s = sum(v["ms"] for v in ded) / 1e3
         line = {
             "metric": "distinct states/sec (node) on Raft BFS",
             "value": total_distinct / per_step,
@@ -149,28 +168,32 @@ def main():
             "data": "synthetic: the model's own reachable state space (no external data)",
             "config": {"workload": "C2: raft_original.tla + configs/c2.cfg (3 servers, 2 values, term<=3, log<=2, msgs<=5)",
                        "distinct_per_run": res.distinct, "generated_per_run": res.generated, "depth": res.depth,
+                       "generated_in_model_per_run": res.generated_in_model,
                        "kernel_ms_per_run": res.kernel_seconds * 1000.0, "launches_per_run": res.n_launches,
                        "state_bytes": res.state_bytes,
                        "parallelism": "single" if world == 1 else "fp-owner-sharded x%d (RCCL all-to-all)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": kname, "algo_bytes_per_launch": kst["algo_bytes"] / max(1, kst["launches"]),
-                         "avg_launch_ms": kst["ms"] / max(1, kst["launches"])},
+                         "kernel": kname, "algo_bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_s * 1e3,
+                         "bytes": "SURVEY.md 8(d): F*S + G_in*8 + D*(16+S) of the run / launches of the dominant kernel"},
             "kernels": {k: {"ms": v["ms"], "launches": v["launches"],
                             "algo_GBps": v["algo_bytes"] / max(v["ms"], 1e-9) / 1e6} for k, v in res.kernels.items()},
         }
-        # the dominant kernel is integer-VALU bound: its VALU issue fraction (PMC instruction count per
-        # launch from profiles/, live launch time) next to the HBM roofline
+        if ded_s > 0:
+            line["dedup_set"] = {"GBps": (res.generated_in_model * 8 + res.distinct * 16) / ded_s / 1e9,
+                                 "probes_per_s": res.generated_in_model / ded_s, "ms": ded_s * 1e3,
+                                 "bytes": "G_in*8 + D*16 (SURVEY.md 8(d) dedup-set metric) / (merge + probe kernel time)"}
+        # VALU issue fraction of the dominant kernel: PMC instruction count per launch from profiles/, live
+        # launch time; MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 VALU instruction issues in 2 cycles
         if os.path.exists(args.valu_json):
             try:
                 vj = json.load(open(args.valu_json))
                 if vj.get("kernel_name") == kname:
-                    avg_s = kst["ms"] / max(1, kst["launches"]) / 1e3
-                    line["roofline"]["valu_issue_frac"] = vj["valu_insts_per_launch"] / (avg_s * vj["peak_valu_insts_per_s"])
+                    line["roofline"]["valu_issue_frac"] = vj["valu_insts_per_launch"] / (avg_s * 256 * 2 * 2.4e9)
             except Exception:
                 pass
         if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_states, args.cpu_workers)
+            line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_states, args.cpu_workers, args.oracle_states)
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

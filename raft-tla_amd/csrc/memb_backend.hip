@@ -935,6 +935,9 @@ class MembGpu : public Backend {
     }
     r.generated += gen;
     r.distinct = (int64_t)(total_ + new_before_chunk + before);
+    // TLC's queue at the stop point (oracle/engine.h): the level's parents after this one and the
+    // new states found before it
+    r.left_on_queue = (int64_t)(level_count - rank - 1 + new_before_chunk + before);
     W s;
     read_state(gid, s);
     int k, sub;
@@ -962,9 +965,8 @@ class MembGpu : public Backend {
     } else {
       r.verdict = MC_VERDICT_INVARIANT_VIOLATION;
       r.violated = kMembInvNames[id];
-      r.depth = (int64_t)level + 2;
-      r.left_on_queue = (int64_t)(level_count - rank - 1 + new_before_chunk + before);
     }
+    r.depth = (int64_t)level + 2;   // the successor's depth (oracle: level + 1, Init = 1)
     build_trace(gid, act >= 0 ? kMembActNames[act] : "?", t, r);
   }
 
@@ -1315,9 +1317,9 @@ class MembGpu : public Backend {
       } else {
         sres_.verdict = MC_VERDICT_INVARIANT_VIOLATION;
         sres_.violated = g[32] ? kMembInvNames[g[32] - 1] : "?";
-        sres_.depth = (int64_t)s_level_ + 2;
-        sres_.left_on_queue = (int64_t)(s_F_ - R - 1) + g[31];
       }
+      if (kind >= EV_INV_ERROR) sres_.depth = (int64_t)s_level_ + 2;   // the successor's depth
+      sres_.left_on_queue = (int64_t)(s_F_ - R - 1) + g[31];          // TLC's queue at the stop point
       s_finished_ = true; *done = 1;
       finish(sres_, t0_);
       return 0;

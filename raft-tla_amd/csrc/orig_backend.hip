@@ -237,8 +237,9 @@ __device__ __forceinline__ u32 probe_batch(u64* table, u64 mask, const u64 (&fp)
     u64 slot = (pos[j] + 1) & mask;
     for (u64 probe = 0;; ++probe) {
       if (probe > mask || probe >= (1u << 20)) { err |= OE_TABLE_FULL; break; }   // visited every entry
-      const u64 c = table[2 * slot];
-      if (c == fp[j]) { lower |= 1u << j; break; }
+      const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(table + 2 * slot);
+      const u64 c = e.x;
+      if (c == fp[j]) { if (KEYED && e.y < nk[j]) lower |= 1u << j; break; }
       if (c == 0ull) {
         const u64 old = (u64)atomicCAS((unsigned long long*)&table[2 * slot], 0ull, (unsigned long long)fp[j]);
         if (old == 0ull) { ins |= 1u << j; lower |= 1u << j; break; }

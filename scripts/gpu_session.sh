@@ -13,7 +13,7 @@ if [ "$TESTS" != "none" ]; then
   tail -4 "$OUT/pytest.log"
   if [ $rc -ge 124 ]; then exit $rc; fi
 fi
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
+timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 ${BENCH_ARGS:---no-cpu-baseline} > "$OUT/bench.jsonl" 2> "$OUT/bench.err"
 rc=$?
 echo "bench rc=$rc" | tee -a "$OUT/steps.txt"
 cut -c1-1800 "$OUT/bench.jsonl"
