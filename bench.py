@@ -84,6 +84,11 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count())
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fp-table-bytes", type=int, default=0, help="seen-set bytes (0 = library default)")
+    # TLC -workers: the CPU reference point is TLC with -workers = host cores (BASELINE north_star), whose
+    # order-dependent outputs are nondeterministic; 1 = TLC's single-worker FIFO order (also measured
+    # below, as fifo_ms_per_step, when --fifo-steps > 0)
+    ap.add_argument("--workers", type=int, default=0)
+    ap.add_argument("--fifo-steps", type=int, default=3)
     ap.add_argument("--state-store-bytes", type=int, default=0, help="state store bytes (0 = library default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_r02.json"))
@@ -106,7 +111,7 @@ def main():
         mc = shard.ShardedChecker(TLA, args.config, rank, world, device_index=local, seed=0x5EED)
     else:
         mc = mod.ModelChecker(TLA, args.config, device=local, seed=0x5EED, fp_table_bytes=args.fp_table_bytes,
-                              state_store_bytes=args.state_store_bytes)
+                              state_store_bytes=args.state_store_bytes, workers=args.workers)
 
     def barrier_sync():
         if dist is not None:
@@ -125,6 +130,19 @@ def main():
     elapsed = time.perf_counter() - t0
     mc.close()
     assert res.verdict == "OK", (res.verdict, res.error)
+    # TLC -workers 1 (FIFO order) on the same model, outside the timed region: its cost is reported
+    fifo = None
+    if world == 1 and args.workers != 1 and args.fifo_steps > 0:
+        with mod.ModelChecker(TLA, args.config, device=local, seed=0x5EED, fp_table_bytes=args.fp_table_bytes,
+                              state_store_bytes=args.state_store_bytes, workers=1) as m1:
+            m1.run()
+            f0 = time.perf_counter()
+            for _ in range(args.fifo_steps):
+                r1 = m1.run()
+            fifo = {"ms_per_step": (time.perf_counter() - f0) / args.fifo_steps * 1e3, "steps": args.fifo_steps,
+                    "distinct_per_run": r1.distinct, "generated_per_run": r1.generated,
+                    "kernels_ms": {k: v["ms"] for k, v in r1.kernels.items()}}
+        assert (r1.distinct, r1.generated, r1.depth) == (res.distinct, res.generated, res.depth)
 
     # the sharded result is global (every rank reports the whole model's counts)
     total_distinct = float(res.distinct)
@@ -167,6 +185,7 @@ def main():
             "dtype": "u32",
             "data": "synthetic: the model's own reachable state space (no external data)",
             "config": {"workload": "C2: raft_original.tla + configs/c2.cfg (3 servers, 2 values, term<=3, log<=2, msgs<=5)",
+                       "tlc_workers": args.workers,
                        "distinct_per_run": res.distinct, "generated_per_run": res.generated, "depth": res.depth,
                        "generated_in_model_per_run": res.generated_in_model,
                        "kernel_ms_per_run": res.kernel_seconds * 1000.0, "launches_per_run": res.n_launches,
@@ -179,6 +198,8 @@ def main():
             "kernels": {k: {"ms": v["ms"], "launches": v["launches"],
                             "algo_GBps": v["algo_bytes"] / max(v["ms"], 1e-9) / 1e6} for k, v in res.kernels.items()},
         }
+        if fifo is not None:
+            line["tlc_workers_1"] = fifo
         if ded_s > 0:
             line["dedup_set"] = {"GBps": (res.generated_in_model * 8 + res.distinct * 16) / ded_s / 1e9,
                                  "probes_per_s": res.generated_in_model / ded_s, "ms": ded_s * 1e3,

@@ -66,7 +66,12 @@ typedef struct mc_opts {
   int32_t abi_version;        /* RAFTMC_ABI_VERSION                                       */
   int32_t device;             /* HIP device ordinal (one process per GPU)                  */
   int32_t n_gpus;             /* 1 (multi-GPU runs use one process per GPU) */
-  int32_t workers;            /* TLC -workers (recorded only; the GPU backend is data-parallel) */
+  int32_t workers;            /* TLC -workers N: 1 (TLC's default) = TLC's single-worker FIFO order,
+                                 so every order-dependent output (kept parent of a state, per-action
+                                 distinct counts, counterexample) is TLC's; otherwise TLC -workers N
+                                 semantics: order-independent outputs (generated / distinct / depth /
+                                 per-action generated) identical, counterexamples still TLC's
+                                 single-worker ones (raft_original re-runs FIFO to the event's level) */
   uint64_t fp_table_bytes;    /* seen-set bytes (power of two used; 0 = auto)             */
   uint64_t state_store_bytes; /* bytes for the per-state store (packed states + parents); 0 = auto */
   int64_t max_depth;          /* 0 = unbounded (TLC -dfid/-depth analogue for BFS)        */

@@ -19,6 +19,11 @@ struct RunOpts {
   bool inv_out_of_model = true;
   bool check_deadlock = false;
   int block_size = 256;
+  // TLC -workers: 1 = TLC's single-worker FIFO order (order-dependent outputs — which parent of a
+  // state is kept, per-action distinct counts, which shortest counterexample — are TLC's exactly);
+  // otherwise TLC -workers N semantics (every order-independent output exact; a counterexample
+  // still is TLC's single-worker one: the search re-runs in FIFO order to the event's level)
+  int workers = 1;
   // TLC -checkpoint / -recover analogues (raft_original): write the BFS state every
   // checkpoint_every levels to checkpoint_path; resume the next run from recover_path
   std::string checkpoint_path, recover_path;

@@ -103,6 +103,7 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
   c->ro.inv_out_of_model = (o->tlc_compat_flags & MC_COMPAT_INV_OUT_OF_MODEL) != 0;
   c->ro.check_deadlock = o->check_deadlock != 0;
   c->ro.block_size = o->block_size ? o->block_size : 256;
+  c->ro.workers = o->workers;
   try {
     std::string fam = rmc::detect_spec_family(rmc::read_text_file(tla_path));
     rmc::CfgFile cfg = rmc::parse_cfg_text(rmc::read_text_file(cfg_path));

@@ -83,7 +83,7 @@ struct GenArgs {
   u64 gid0;                    // global id of the chunk's first parent
   u64* rfp;                    // [nblk][BS * NI] fingerprints of in-model successors (per-workgroup region)
   unsigned short* rkey;        // [nblk][BS * NI] local key: lane << 8 | instance
-  u32* rcnt;                   // [nblk] records per workgroup
+  u32* rcnt;                   // [nblk][4] records per wave (wave w's region starts at w * 64 * NI)
   u64 seed;
   OrigRuntime rt;
   u32 inv_oom, deadlock;
@@ -104,16 +104,19 @@ template <class S>
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 15 ? 3 : 1))) orig_generate(GenArgs a) {
   using W = typename S::Work;
   constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
-  __shared__ unsigned int lds_cnt[OA_NACT + 2];   // per-action generated, in-model total, record count
-  for (int t = threadIdx.x; t < OA_NACT + 2; t += BS) lds_cnt[t] = 0;
+  __shared__ unsigned int lds_cnt[OA_NACT + 1];   // per-action generated, in-model total
+  for (int t = threadIdx.x; t < OA_NACT + 1; t += BS) lds_cnt[t] = 0;
   __syncthreads();
   const u64 tid = (u64)blockIdx.x * BS + threadIdx.x;
   const bool active = tid < a.chunk_count;
   const u64 gid = a.gid0 + tid;
   const int lane = __lane_id();
-  const u64 lanes_below = (1ull << lane) - 1ull;
-  u64* rfp = a.rfp + (u64)blockIdx.x * (BS * S::NI);
-  unsigned short* rkey = a.rkey + (u64)blockIdx.x * (BS * S::NI);
+  // each wave appends to its own region: the running count is wave-uniform, no LDS atomic per instance
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR) region base
+  const u64 wreg = (u64)blockIdx.x * (BS * S::NI) + (u64)wave * (64 * S::NI);
+  u64* rfp = a.rfp + wreg;
+  unsigned short* rkey = a.rkey + wreg;
+  u32 wcount = 0;
   W s;
   u64 al[S::AW];
   u32 err = 0, nsucc = 0, nin = 0;
@@ -171,17 +174,12 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
       }
     }
     const u64 mask = __ballot(have);
-    if (mask) {
-      const int leader = __ffsll((unsigned long long)mask) - 1;
-      unsigned int base = 0;
-      if (lane == leader) base = atomicAdd(&lds_cnt[OA_NACT + 1], (unsigned int)__popcll(mask));   // LDS: no global contention
-      base = __shfl(base, leader);
-      if (have) {
-        const unsigned int idx = base + (unsigned int)__popcll(mask & lanes_below);
-        rfp[idx] = fp;
-        rkey[idx] = (unsigned short)((threadIdx.x << 8) | (unsigned)k);
-      }
+    if (have) {
+      const u32 idx = wcount + __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
+      rfp[idx] = fp;
+      rkey[idx] = (unsigned short)((threadIdx.x << 8) | (unsigned)k);
     }
+    wcount += (u32)__popcll(mask);
   }
   if (active) {
     if (err & OE_EVAL_LOG_INDEX) { const u64 e = ev_word(gid, 0, EV_NEXT_ERROR); ev = e < ev ? e : ev; }
@@ -197,10 +195,38 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
   __syncthreads();
   for (int t = threadIdx.x; t < OA_NACT; t += BS)
     if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + t], (unsigned long long)lds_cnt[t]);
-  if (threadIdx.x == 0) {
-    if (lds_cnt[OA_NACT]) atomicAdd(&a.ctr[K_GEN_IN], (unsigned long long)lds_cnt[OA_NACT]);
-    a.rcnt[blockIdx.x] = lds_cnt[OA_NACT + 1];
+  if (threadIdx.x == 0 && lds_cnt[OA_NACT]) atomicAdd(&a.ctr[K_GEN_IN], (unsigned long long)lds_cnt[OA_NACT]);
+  if (lane == 0) a.rcnt[blockIdx.x * 4 + wave] = wcount;
+}
+
+// Record i of workgroup b's four wave regions (concatenated in wave order): its offset in the
+// workgroup's record region.  rc: the four per-wave counts; wreg = 64 * NI.
+struct WaveRegions {
+  u32 p1, p2, p3, n;
+  u64 wreg;
+  RMC_HD WaveRegions(const u32* rc, u64 wave_region) {
+    p1 = rc[0]; p2 = p1 + rc[1]; p3 = p2 + rc[2]; n = p3 + rc[3]; wreg = wave_region;
   }
+  RMC_HD u64 at(u32 i) const {
+    const u32 w = (i >= p1) + (i >= p2) + (i >= p3);
+    const u32 base = w == 0 ? 0u : w == 1 ? p1 : w == 2 ? p2 : p3;
+    return (u64)w * wreg + (i - base);
+  }
+};
+
+// Workgroup-local first-come fingerprint filter: answers only "certainly produced here before".
+// Plain LDS loads and stores: a race can make the set forget an entry (a duplicate reaches the
+// seen-set, which decides), never report a first occurrence as a duplicate.
+RMC_HD bool lds_first(unsigned long long* set, u64 fp) {
+  u32 h = (u32)(fp >> 20) & (LDS_FP_SLOTS - 1);
+#pragma unroll 1
+  for (int p = 0; p < 8; ++p) {
+    const unsigned long long cur = set[h];
+    if (cur == fp) return false;            // produced here before
+    if (cur == 0ull) { set[h] = fp; return true; }
+    h = (h + 1) & (LDS_FP_SLOTS - 1);
+  }
+  return true;                              // window full: let the seen-set decide
 }
 
 // ------------------------------------------------------------------ seen-set probing
@@ -209,24 +235,25 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
 // to the given one (atomicMax of the complement; a key only ever decreases, so an entry that
 // already holds a smaller key needs no atomic: the common case, a duplicate of an older state).
 // ins bit j = this call inserted fp[j]; pos[j] = its entry index.
-template <int G, bool KEYED = true>
+template <int G, bool KEYED = true, int STRIDE = 2>
 __device__ __forceinline__ u32 probe_batch(u64* table, u64 mask, const u64 (&fp)[G], const u64 (&nk)[G], u64 (&pos)[G], u32& err) {
+  static_assert(!KEYED || STRIDE == 2, "keyed entries are {fp, ~key}");
   u64 cur[G], cnk[G];
 #pragma unroll
   for (int j = 0; j < G; ++j) {
     pos[j] = fp[j] & mask;
-    if (fp[j]) {
+    if (fp[j] && KEYED) {
       const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(table + 2 * pos[j]);
       cur[j] = e.x; cnk[j] = e.y;
     } else {
-      cur[j] = ~0ull; cnk[j] = ~0ull;
+      cur[j] = fp[j] ? table[STRIDE * pos[j]] : ~0ull; cnk[j] = ~0ull;
     }
   }
   u32 ins = 0, lower = 0;
 #pragma unroll
   for (int j = 0; j < G; ++j)
     if (fp[j] && cur[j] == 0ull) {
-      cur[j] = (u64)atomicCAS((unsigned long long*)&table[2 * pos[j]], 0ull, (unsigned long long)fp[j]);
+      cur[j] = (u64)atomicCAS((unsigned long long*)&table[STRIDE * pos[j]], 0ull, (unsigned long long)fp[j]);
       if (cur[j] == 0ull) { ins |= 1u << j; lower |= 1u << j; }
       else if (cur[j] == fp[j]) lower |= 1u << j;     // raced with another inserter of the same fp
     }
@@ -237,11 +264,12 @@ __device__ __forceinline__ u32 probe_batch(u64* table, u64 mask, const u64 (&fp)
     u64 slot = (pos[j] + 1) & mask;
     for (u64 probe = 0;; ++probe) {
       if (probe > mask || probe >= (1u << 20)) { err |= OE_TABLE_FULL; break; }   // visited every entry
-      const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(table + 2 * slot);
-      const u64 c = e.x;
-      if (c == fp[j]) { if (KEYED && e.y < nk[j]) lower |= 1u << j; break; }
+      u64 c, ck = ~0ull;
+      if (KEYED) { const ulonglong2 e = *reinterpret_cast<const ulonglong2*>(table + 2 * slot); c = e.x; ck = e.y; }
+      else c = table[STRIDE * slot];
+      if (c == fp[j]) { if (KEYED && ck < nk[j]) lower |= 1u << j; break; }
       if (c == 0ull) {
-        const u64 old = (u64)atomicCAS((unsigned long long*)&table[2 * slot], 0ull, (unsigned long long)fp[j]);
+        const u64 old = (u64)atomicCAS((unsigned long long*)&table[STRIDE * slot], 0ull, (unsigned long long)fp[j]);
         if (old == 0ull) { ins |= 1u << j; lower |= 1u << j; break; }
         if (old == fp[j]) { lower |= 1u << j; break; }
       }
@@ -252,12 +280,6 @@ __device__ __forceinline__ u32 probe_batch(u64* table, u64 mask, const u64 (&fp)
   if (KEYED) {
 #if defined(RMC_EXP_NOKEY)
     (void)lower;
-#elif defined(RMC_EXP_PLAINKEY)
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-      if ((ins >> j) & 1u) table[2 * pos[j] + 1] = nk[j];
-      else if ((lower >> j) & 1u) atomicMax((unsigned long long*)&table[2 * pos[j] + 1], (unsigned long long)nk[j]);
-    }
 #else
 #pragma unroll
     for (int j = 0; j < G; ++j)
@@ -330,7 +352,8 @@ __global__ void __launch_bounds__(BS) orig_merge(DedupArgs a) {
   for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) { lfp[t] = 0ull; lkey[t] = ~0u; }
   if (threadIdx.x == 0) ovf_cnt = 0;
   __syncthreads();
-  const u32 n = a.rcnt[blockIdx.x];
+  const WaveRegions wr(a.rcnt + 4 * blockIdx.x, a.region / 4);
+  const u32 n = wr.n;
   const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
   const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
   ulonglong2* out = a.urec + (u64)blockIdx.x * a.region;
@@ -343,8 +366,9 @@ __global__ void __launch_bounds__(BS) orig_merge(DedupArgs a) {
 #pragma unroll
     for (int j = 0; j < P1; ++j) {
       const u32 i = i0 + (u32)j * BS + threadIdx.x;
-      fp[j] = i < n ? fps[i] : 0ull;
-      lk[j] = i < n ? (u32)keys[i] : 0u;
+      const u64 at = wr.at(i);
+      fp[j] = i < n ? fps[at] : 0ull;
+      lk[j] = i < n ? (u32)keys[at] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < P1; ++j) {
@@ -412,6 +436,243 @@ __global__ void __launch_bounds__(BS) orig_probe(DedupArgs a) {
     atomicAdd(&a.ctr[K_PROF + 1], (unsigned long long)(t3 - t0));
     atomicAdd(&a.ctr[K_PROF + 3], 1ull);
   }
+}
+
+// ------------------------------------------------------------------ TLC -workers N semantics
+// The order-independent pipeline (mc_opts.workers != 1): every count TLC prints without -coverage
+// is the same, but which producer of a state is kept is not TLC's single-worker choice (as with
+// TLC's own workers).  8-B seen-set entries, first-come LDS filter, no keys, no winner pass: the
+// inserting thread numbers its new state directly.
+
+// workgroup b: generate-workgroup b's records through an exact LDS set (CAS); the first record of
+// each fingerprint (and every record whose probe window is full) is written compacted as
+// (fp, global key) to the workgroup's region
+__global__ void __launch_bounds__(BS) orig_merge_plain(DedupArgs a) {
+  __shared__ unsigned long long lfp[LDS_FP_SLOTS];
+  __shared__ u32 out_cnt;
+  for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lfp[t] = 0ull;
+  if (threadIdx.x == 0) out_cnt = 0;
+  __syncthreads();
+  const WaveRegions wr(a.rcnt + 4 * blockIdx.x, a.region / 4);
+  const u32 n = wr.n;
+  const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
+  const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
+  ulonglong2* out = a.urec + (u64)blockIdx.x * a.region;
+  const int lane = __lane_id();
+  constexpr int P1 = 8;
+#pragma unroll 1
+  for (u32 i0 = 0; i0 < n; i0 += P1 * BS) {
+    u64 fp[P1];
+    u32 lk[P1];
+#pragma unroll
+    for (int j = 0; j < P1; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      const u64 at = wr.at(i);
+      fp[j] = i < n ? fps[at] : 0ull;
+      lk[j] = i < n ? (u32)keys[at] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < P1; ++j) {
+      bool keep = false;
+      if (fp[j]) {
+        keep = true;                                   // window full: keep (the seen-set decides)
+        u32 h = (u32)(fp[j] >> 20) & (LDS_FP_SLOTS - 1);
+#pragma unroll 1
+        for (int p = 0; p < 8; ++p) {
+          unsigned long long c = lfp[h];
+          if (c == 0ull) c = atomicCAS(&lfp[h], 0ull, (unsigned long long)fp[j]);
+          if (c == 0ull) break;                        // first here
+          if (c == fp[j]) { keep = false; break; }     // produced here before
+          h = (h + 1) & (LDS_FP_SLOTS - 1);
+        }
+      }
+      const u64 m = __ballot(keep);
+      if (m) {
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        u32 base = 0;
+        if (lane == leader) base = atomicAdd(&out_cnt, (u32)__popcll(m));
+        base = __shfl(base, leader);
+        if (keep)
+          out[base + (u32)__popcll(m & ((1ull << lane) - 1ull))] =
+              make_ulonglong2((unsigned long long)fp[j], (unsigned long long)~nkey_of(a.gid0, blockIdx.x, lk[j]));
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) a.ucnt[blockIdx.x] = out_cnt;
+}
+
+// workgroup b probes the 8-B seen-set once per record of region b (DEDUP_PER in flight per
+// thread); the new states' producers are marked in an LDS (parent, instance) mask and written in
+// parent-major, instance order (one global atomic per workgroup): the next level keeps siblings
+// adjacent, so its diamonds land in one workgroup again and its waves hold similar states
+template <int WW>
+__global__ void __launch_bounds__(BS) orig_probe_plain(DedupArgs a) {
+  __shared__ u32 wave_tot[BS / 64];
+  __shared__ unsigned long long base_sh;
+  __shared__ unsigned long long win[BS * WW];
+  for (int t = threadIdx.x; t < BS * WW; t += BS) win[t] = 0ull;
+  __syncthreads();
+  const u32 n = a.ucnt[blockIdx.x];
+  const ulonglong2* in = a.urec + (u64)blockIdx.x * a.region;
+  const u64 pgid0 = a.gid0 + (u64)blockIdx.x * BS;   // global id of this workgroup's first parent
+  u32 err = 0;
+#pragma unroll 1
+  for (u32 i0 = 0; i0 < n; i0 += DEDUP_PER * BS) {
+    u64 fp[DEDUP_PER], key[DEDUP_PER], pos[DEDUP_PER];
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      const ulonglong2 r = i < n ? in[i] : make_ulonglong2(0ull, 0ull);
+      fp[j] = r.x; key[j] = r.y;
+    }
+    const u32 ins = probe_batch<DEDUP_PER, false, 1>(a.table, a.table_mask, fp, key, pos, err);
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j)
+      if ((ins >> j) & 1u) {
+        const u32 p = (u32)((key[j] >> 8) - pgid0), k = (u32)(key[j] & 255);
+        atomicOr(&win[p * WW + (k >> 6)], 1ull << (k & 63));
+      }
+  }
+  __syncthreads();
+  u64 wm[WW];
+  u32 mine = 0;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) { wm[q] = win[threadIdx.x * WW + q]; mine += (u32)__popcll(wm[q]); }
+  u32 total = 0;
+  const u32 off = block_excl_scan(mine, wave_tot, &total);
+  if (threadIdx.x == 0) base_sh = total ? atomicAdd(&a.ctr[K_CHUNK_NEW], (unsigned long long)total) : 0ull;
+  __syncthreads();
+  u64 o = base_sh + off;
+  const u64 pg = pgid0 + threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) {
+    u64 m = wm[q];
+    while (m) {
+      const int k = q * 64 + __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      a.newpos[o++] = (pg << 8) | (u64)k;
+    }
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+}
+
+// Fused variant for TLC -workers N (what the pipeline runs): records through a first-come LDS
+// filter (plain LDS loads and stores, 32 KB: a race can only let a duplicate through to the
+// seen-set, never drop a state), the survivors probe the 8-B seen-set DEDUP_PER at a time, and
+// the new states' producers go out parent-major as in orig_probe_plain.
+template <int WW>
+__global__ void __launch_bounds__(BS) orig_dedup_plain(DedupArgs a) {
+  __shared__ unsigned long long lfp[LDS_FP_SLOTS];
+  __shared__ u32 wave_tot[BS / 64];
+  __shared__ unsigned long long base_sh;
+  __shared__ unsigned long long win[BS * WW];
+  for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lfp[t] = 0ull;
+  for (int t = threadIdx.x; t < BS * WW; t += BS) win[t] = 0ull;
+  __syncthreads();
+  const WaveRegions wr(a.rcnt + 4 * blockIdx.x, a.region / 4);
+  const u32 n = wr.n;
+  const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
+  const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
+  u32 err = 0;
+#pragma unroll 1
+  for (u32 i0 = 0; i0 < n; i0 += DEDUP_PER * BS) {
+    u64 fp[DEDUP_PER], key[DEDUP_PER], pos[DEDUP_PER];
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      const u64 at = wr.at(i);
+      fp[j] = i < n ? fps[at] : 0ull;
+      key[j] = i < n ? (u64)keys[at] : 0ull;     // local key lane << 8 | instance
+    }
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j)
+      if (fp[j] && !lds_first(lfp, fp[j])) fp[j] = 0ull;   // produced by this workgroup's parents before
+    const u32 ins = probe_batch<DEDUP_PER, false, 1>(a.table, a.table_mask, fp, key, pos, err);
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j)
+      if ((ins >> j) & 1u) atomicOr(&win[(key[j] >> 8) * WW + ((key[j] & 255) >> 6)], 1ull << (key[j] & 63));
+  }
+  __syncthreads();
+  u64 wm[WW];
+  u32 mine = 0;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) { wm[q] = win[threadIdx.x * WW + q]; mine += (u32)__popcll(wm[q]); }
+  u32 total = 0;
+  const u32 off = block_excl_scan(mine, wave_tot, &total);
+  if (threadIdx.x == 0) base_sh = total ? atomicAdd(&a.ctr[K_CHUNK_NEW], (unsigned long long)total) : 0ull;
+  __syncthreads();
+  u64 o = base_sh + off;
+  const u64 pg = a.gid0 + (u64)blockIdx.x * BS + threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) {
+    u64 m = wm[q];
+    while (m) {
+      const int k = q * 64 + __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      a.newpos[o++] = (pg << 8) | (u64)k;
+    }
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+}
+
+struct MatPlainArgs {
+  u32* states;
+  u64* meta;
+  const u64* newrec;           // (parent gid << 8 | instance), ctr[K_CHUNK_NEW] of them
+  u64 base;                    // global id of device slot 0
+  u64 dst_base, cap;           // new state i of the chunk goes to dst_base + ctr[K_LEVEL_NEW] + i (device index)
+  OrigRuntime rt;
+  unsigned long long* ctr;
+};
+
+// grid-stride over the chunk's new states (their count stays on the device: no host wait)
+template <class S>
+__global__ void __launch_bounds__(BS) orig_materialize_plain(MatPlainArgs a) {
+  using W = typename S::Work;
+  constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
+  __shared__ unsigned int lds_cnt[OA_NACT];
+  for (int t = threadIdx.x; t < OA_NACT; t += BS) lds_cnt[t] = 0;
+  __syncthreads();
+  const u64 n_new = a.ctr[K_CHUNK_NEW];
+  const u64 base = a.dst_base + a.ctr[K_LEVEL_NEW];
+  u32 err = 0;
+  unsigned long long ev = ~0ull;
+  for (u64 i = (u64)blockIdx.x * BS + threadIdx.x; i < n_new; i += (u64)gridDim.x * BS) {
+    const u64 rec = a.newrec[i], pgid = rec >> 8;
+    const int k = (int)(rec & 0xff);
+    u32 w[NWP];
+    const uint4* src = reinterpret_cast<const uint4*>(a.states + (pgid - a.base) * NWP);
+#pragma unroll
+    for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+    W s, t;
+    u64 al[S::AW];
+    S::unpack(w, s);
+    S::all_logs_next(s, al);
+    u32 e2 = 0;
+    const int act = S::apply(s, k, t, e2);
+#pragma unroll
+    for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
+    u32 pw[NW];
+    S::pack(t, pw);
+    const u64 dst = base + i;
+    if (act >= 0 && dst < a.cap) {
+      uint4* o = reinterpret_cast<uint4*>(a.states + dst * NWP);
+#pragma unroll
+      for (int q = 0; q < NWP / 4; ++q)
+        o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
+      a.meta[dst] = (pgid << 24) | ((u64)act << 16) | (u64)k;
+      atomicAdd(&lds_cnt[act], 1u);
+      if (S::violated(t, a.rt.invariants)) { const u64 e = ev_word(pgid, (u32)k, EV_VIOLATION); ev = e < ev ? e : ev; }
+    } else {
+      err |= dst >= a.cap ? (u32)OE_CAP_STORE : (u32)OE_TABLE_FULL;
+    }
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+  if (ev != ~0ull) atomicMin(&a.ctr[K_EVENT], ev);
+  __syncthreads();
+  for (int t = threadIdx.x; t < OA_NACT; t += BS)
+    if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + OA_NACT + t], (unsigned long long)lds_cnt[t]);
 }
 
 // Winners: an entry inserted by this chunk holds, after the chunk's dedup, the minimum key over
@@ -639,7 +900,8 @@ __global__ void __launch_bounds__(BS) orig_route_blk(RouteArgs a) {
   __shared__ unsigned int hist[8];
   __shared__ unsigned long long base[8];
   for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lds_fp[t] = 0ull;
-  const u32 n = a.rcnt[blockIdx.x];
+  const WaveRegions wr(a.rcnt + 4 * blockIdx.x, a.region / 4);
+  const u32 n = wr.n;
   const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
   const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
   constexpr int G = 16;
@@ -653,8 +915,9 @@ __global__ void __launch_bounds__(BS) orig_route_blk(RouteArgs a) {
 #pragma unroll
     for (int j = 0; j < G; ++j) {
       const u32 i = i0 + (u32)j * BS + threadIdx.x;
-      fp[j] = i < n ? fps[i] : 0ull;
-      const u32 lk = i < n ? keys[i] : 0u;
+      const u64 at = wr.at(i);
+      fp[j] = i < n ? fps[at] : 0ull;
+      const u32 lk = i < n ? keys[at] : 0u;
       slot[j] = (((u64)blockIdx.x * BS + (lk >> 8)) << 8) | (u64)(lk & 255u);
       if (fp[j]) {   // produced before by this workgroup's parents?
         u32 h = (u32)(fp[j] >> 20) & (LDS_FP_SLOTS - 1);
@@ -805,7 +1068,7 @@ __global__ void __launch_bounds__(BS) orig_store(StoreArgs a) {
 // Recovery from a checkpoint: re-insert the fingerprints of every stored state into the
 // zeroed seen-set (the checkpoint holds states, not the table; FP64 is a function of the
 // packed words, so the rebuilt set is the saved one).
-template <class S>
+template <class S, int STRIDE>
 __global__ void __launch_bounds__(BS) orig_reinsert(const u32* states, u64 n, u64* table, u64 mask, u64 seed,
                                                     unsigned long long* ctr) {
   constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
@@ -818,7 +1081,7 @@ __global__ void __launch_bounds__(BS) orig_reinsert(const u32* states, u64 n, u6
   const u64 fp[1] = {fp64(w, seed)}, nk[1] = {~0ull};
   u64 pos[1];
   u32 err = 0;
-  probe_batch<1>(table, mask, fp, nk, pos, err);
+  probe_batch<1, STRIDE == 2, STRIDE>(table, mask, fp, nk, pos, err);
   if (err) atomicOr(&ctr[K_ERR], (unsigned long long)err);
 }
 
@@ -840,7 +1103,8 @@ class OrigGpu : public Backend {
 
   int observed_collision(double& v, std::string& err) override {
     if (!d_table_ || alloc_world_ != 0) { err = "after a single-GPU mc_run only"; return MC_E_STATE; }
-    return fpgap::observed(d_table_, table_mask_ + 1, 2, stream_, v, err);
+    return last_fifo_ ? fpgap::observed(d_table_, table_mask_ + 1, 2, stream_, v, err)
+                      : fpgap::observed(d_table_, 2 * (table_mask_ + 1), 1, stream_, v, err);
   }
 
   std::string describe_json() const override {
@@ -889,7 +1153,7 @@ class OrigGpu : public Backend {
     HIPCHK(hipMalloc(&d_meta_, cap_ * 8));
     HIPCHK(hipMalloc(&d_rfp_, nrec * 8));
     HIPCHK(hipMalloc(&d_rkey_, nrec * 2));
-    HIPCHK(hipMalloc(&d_rcnt_blk_, nblk * 4));
+    HIPCHK(hipMalloc(&d_rcnt_blk_, nblk * 16));
     HIPCHK(hipMalloc(&d_newrec_, nrec * 8));          // inserted entry positions (single GPU) / replies (sharded)
     HIPCHK(hipMalloc(&d_urec_, nrec * 16));           // distinct (fp, ~key) per workgroup region
     HIPCHK(hipMalloc(&d_ucnt_, nblk * 4));
@@ -941,6 +1205,10 @@ class OrigGpu : public Backend {
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
+    // TLC -workers 1: single-worker FIFO order (16-B {fp, ~key} entries); -workers N: 8-B entries
+    const bool fifo = o.workers == 1;
+    last_fifo_ = fifo;
+    const u64 tmask = fifo ? table_mask_ : 2 * (table_mask_ + 1) - 1;
 
     r = RunResult();
     r.seed = o.seed ? o.seed : 0x5EED5EED2024ull;
@@ -961,7 +1229,8 @@ class OrigGpu : public Backend {
     u32 wp[NWP] = {0}; for (int q = 0; q < S::NW; ++q) wp[q] = w0[q];
     const u64 fp0 = fp64(w0, r.seed);
     const u64 e0[2] = {fp0, ~0ull};   // key 0
-    HIPCHK(hipMemcpy(d_table_ + 2 * (fp0 & table_mask_), e0, 16, hipMemcpyHostToDevice));
+    if (fifo) HIPCHK(hipMemcpy(d_table_ + 2 * (fp0 & tmask), e0, 16, hipMemcpyHostToDevice));
+    else HIPCHK(hipMemcpy(d_table_ + (fp0 & tmask), e0, 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d_states_, wp, NWP * 4, hipMemcpyHostToDevice));
     const u64 nometa = ~0ull;
     HIPCHK(hipMemcpy(d_meta_, &nometa, 8, hipMemcpyHostToDevice));
@@ -1008,36 +1277,55 @@ class OrigGpu : public Backend {
         DedupArgs d;
         d.rfp = d_rfp_; d.rkey = d_rkey_; d.rcnt = d_rcnt_blk_; d.region = (u64)BS * S::NI; d.gid0 = cb;
         d.urec = (ulonglong2*)d_urec_; d.ucnt = d_ucnt_;
-        d.table = d_table_; d.table_mask = table_mask_; d.newpos = d_newrec_; d.ctr = (unsigned long long*)d_ctr_;
+        d.table = d_table_; d.table_mask = tmask; d.newpos = d_newrec_; d.ctr = (unsigned long long*)d_ctr_;
         d.prof = prof_ ? 1u : 0u;
         HIPCHK(hipEventRecord(e[2], stream_));
-        hipLaunchKernelGGL(orig_merge, dim3(nblk), dim3(BS), 0, stream_, d);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(orig_probe, dim3(nblk), dim3(BS), 0, stream_, d);
+        if (fifo) {
+          hipLaunchKernelGGL(orig_merge, dim3(nblk), dim3(BS), 0, stream_, d);
+          HIPCHK(hipGetLastError());
+          hipLaunchKernelGGL(orig_probe, dim3(nblk), dim3(BS), 0, stream_, d);
+        } else {
+          if (split_plain_) {
+            hipLaunchKernelGGL(orig_merge_plain, dim3(nblk), dim3(BS), 0, stream_, d);
+            HIPCHK(hipGetLastError());
+            hipLaunchKernelGGL((orig_probe_plain<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
+          } else {
+            hipLaunchKernelGGL((orig_dedup_plain<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
+          }
+        }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e[3], stream_));
-        MarkArgs mk;
-        mk.newpos = d_newrec_; mk.table = d_table_; mk.gid0 = cb; mk.chunk_count = cnt; mk.winmask = d_winmask_;
-        mk.ww = WW; mk.ctr = (unsigned long long*)d_ctr_;
         HIPCHK(hipEventRecord(e[4], stream_));
-        hipLaunchKernelGGL(orig_mark, dim3((unsigned)std::min<u64>(2048, (cnt * 2 + BS - 1) / BS)), dim3(BS), 0, stream_, mk);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL((orig_count<WW>), dim3(nblk), dim3(BS), 0, stream_, (const u64*)d_winmask_, cnt, d_wcnt_);
-        HIPCHK(hipGetLastError());
-        hipLaunchKernelGGL(orig_scan, dim3(1), dim3(SCAN_BS), 0, stream_, (const u32*)d_wcnt_, d_woff_, (u32)nblk, (unsigned long long*)d_ctr_);
-        HIPCHK(hipGetLastError());
+        if (fifo) {
+          MarkArgs mk;
+          mk.newpos = d_newrec_; mk.table = d_table_; mk.gid0 = cb; mk.chunk_count = cnt; mk.winmask = d_winmask_;
+          mk.ww = WW; mk.ctr = (unsigned long long*)d_ctr_;
+          hipLaunchKernelGGL(orig_mark, dim3((unsigned)std::min<u64>(2048, (cnt * 2 + BS - 1) / BS)), dim3(BS), 0, stream_, mk);
+          HIPCHK(hipGetLastError());
+          hipLaunchKernelGGL((orig_count<WW>), dim3(nblk), dim3(BS), 0, stream_, (const u64*)d_winmask_, cnt, d_wcnt_);
+          HIPCHK(hipGetLastError());
+          hipLaunchKernelGGL(orig_scan, dim3(1), dim3(SCAN_BS), 0, stream_, (const u32*)d_wcnt_, d_woff_, (u32)nblk, (unsigned long long*)d_ctr_);
+          HIPCHK(hipGetLastError());
+        }
         HIPCHK(hipEventRecord(e[5], stream_));
-        MatArgs m;
-        m.states = d_states_; m.meta = d_meta_; m.chunk_begin = cb - base_; m.chunk_count = cnt; m.gid0 = cb;
-        m.winmask = d_winmask_; m.woff = d_woff_; m.ww = WW; m.dst_base = level_end - base_; m.cap = cap_;
-        m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_;
         HIPCHK(hipEventRecord(e[6], stream_));
-        hipLaunchKernelGGL((orig_materialize<S>), dim3(nblk), dim3(BS), 0, stream_, m);
+        if (fifo) {
+          MatArgs m;
+          m.states = d_states_; m.meta = d_meta_; m.chunk_begin = cb - base_; m.chunk_count = cnt; m.gid0 = cb;
+          m.winmask = d_winmask_; m.woff = d_woff_; m.ww = WW; m.dst_base = level_end - base_; m.cap = cap_;
+          m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_;
+          hipLaunchKernelGGL((orig_materialize<S>), dim3(nblk), dim3(BS), 0, stream_, m);
+        } else {
+          MatPlainArgs m;
+          m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.base = base_; m.dst_base = level_end - base_;
+          m.cap = cap_; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_;
+          hipLaunchKernelGGL((orig_materialize_plain<S>), dim3((unsigned)std::min<u64>(4096, (cnt * 2 + BS - 1) / BS)), dim3(BS), 0, stream_, m);
+        }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e[7], stream_));
         hipLaunchKernelGGL(orig_advance, dim3(1), dim3(64), 0, stream_, (unsigned long long*)d_ctr_);
         HIPCHK(hipGetLastError());
-        for (auto& ks : r.kernels) ks.launches += 1;
+        for (size_t q = 0; q < r.kernels.size(); ++q) if (fifo || q != 2) r.kernels[q].launches += 1;
         r.kernels[0].algo_bytes += (double)cnt * S_B;        // + G_in * 10 record bytes per level below
       }
       u64 c[K_NCTR];
@@ -1068,6 +1356,15 @@ class OrigGpu : public Backend {
       r.seconds_kernels += level_ms / 1000.0;
       r.n_launches += 1;
       if (next_write - base_ > cap_) c[K_ERR] |= OE_CAP_STORE;
+      if (c[K_EVENT] != ~0ull && !fifo && (c[K_ERR] & ~(u64)OE_CAP_STORE) == 0) {
+        // TLC -workers N found an event: TLC's counterexample and stop point are the single-worker
+        // search's, so the model is searched again in FIFO order (it stops at this level)
+        RunOpts o1 = o;
+        o1.workers = 1;
+        o1.recover_path.clear();        // a checkpoint of this search is in its order, not TLC's: start over
+        o1.checkpoint_path.clear();
+        return run(o1, r, err);
+      }
       if (c[K_EVENT] != ~0ull && (c[K_ERR] & ~(u64)OE_CAP_STORE) == 0) {
         // the level's first event in TLC's order stops the search; a full state store only
         // matters when it cut off states that come before the event in key order
@@ -1262,16 +1559,24 @@ class OrigGpu : public Backend {
     for (u64 b = 0; b < lb; b += stage) {
       const u64 n = std::min<u64>(stage, lb - b);
       HIPCHK(hipMemcpy(d_rfp_, st.data() + b * NWP, n * NWP * 4, hipMemcpyHostToDevice));
-      hipLaunchKernelGGL((orig_reinsert<S>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_,
-                         (const u32*)d_rfp_, n, d_table_, table_mask_, (u64)h.seed, (unsigned long long*)d_ctr_);
+      if (last_fifo_)
+        hipLaunchKernelGGL((orig_reinsert<S, 2>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_,
+                           (const u32*)d_rfp_, n, d_table_, table_mask_, (u64)h.seed, (unsigned long long*)d_ctr_);
+      else
+        hipLaunchKernelGGL((orig_reinsert<S, 1>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_,
+                           (const u32*)d_rfp_, n, d_table_, 2 * table_mask_ + 1, (u64)h.seed, (unsigned long long*)d_ctr_);
       HIPCHK(hipGetLastError());
       HIPCHK(hipStreamSynchronize(stream_));
     }
     HIPCHK(hipMemcpy(d_states_, st.data() + lb * NWP, (h.total - lb) * NWP * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d_meta_, me.data() + lb, (h.total - lb) * 8, hipMemcpyHostToDevice));
     if (h.total > lb) {
-      hipLaunchKernelGGL((orig_reinsert<S>), dim3((unsigned)((h.total - lb + BS - 1) / BS)), dim3(BS), 0, stream_,
-                         (const u32*)d_states_, (u64)(h.total - lb), d_table_, table_mask_, (u64)h.seed, (unsigned long long*)d_ctr_);
+      if (last_fifo_)
+        hipLaunchKernelGGL((orig_reinsert<S, 2>), dim3((unsigned)((h.total - lb + BS - 1) / BS)), dim3(BS), 0, stream_,
+                           (const u32*)d_states_, (u64)(h.total - lb), d_table_, table_mask_, (u64)h.seed, (unsigned long long*)d_ctr_);
+      else
+        hipLaunchKernelGGL((orig_reinsert<S, 1>), dim3((unsigned)((h.total - lb + BS - 1) / BS)), dim3(BS), 0, stream_,
+                           (const u32*)d_states_, (u64)(h.total - lb), d_table_, 2 * table_mask_ + 1, (u64)h.seed, (unsigned long long*)d_ctr_);
       HIPCHK(hipGetLastError());
     }
     host_states_.assign(st.begin(), st.begin() + lb * NWP);
@@ -1806,6 +2111,8 @@ class OrigGpu : public Backend {
   u64 fill_counts_route_[8] = {0};
   u64 sviol_parent_ = 0; u32 sviol_bad_ = 0; std::string sviol_act_, sviol_text_;
   u64 sh_event_ = ~0ull;
+  bool last_fifo_ = true;
+  const bool split_plain_ = std::getenv("RAFTMC_SPLIT_PLAIN") != nullptr;   // experiment: merge + probe kernels   // seen-set layout of the last single-GPU run (16-B keyed / 8-B entries)
   // RAFTMC_PROF=1: per-phase wall-clock ticks (100 MHz) of orig_dedup, summed over workgroups
   const bool prof_ = std::getenv("RAFTMC_PROF") != nullptr;
   u64 prof_acc_[5] = {0, 0, 0, 0, 0};

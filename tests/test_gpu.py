@@ -42,6 +42,24 @@ def test_parity_against_oracle(raftmc, name):
     assert n == g["distinct"] and sha == g["states_sha256"]
 
 
+@pytest.mark.parametrize("name", sorted(FIXTURES))
+def test_parity_workers_n(raftmc, name):
+    """TLC -workers N semantics (mc_opts.workers != 1: first-come seen-set, no FIFO keys): every
+    order-independent output is the oracle's — generated, distinct, depth, level sizes, per-action
+    generated counts, the set of states; per-action distinct counts only sum right (which producer
+    of a state is kept is the workers' race, as in TLC)."""
+    g = FIXTURES[name]
+    with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, name + ".cfg"), workers=0, **SMALL) as mc:
+        r = mc.run()
+        sha, n = states_sha(mc)
+    assert r.verdict == "OK", r.error
+    assert (r.generated, r.distinct, r.depth) == (g["generated"], g["distinct"], g["depth"])
+    assert {k: v[0] for k, v in r.actions.items()} == {k: v[0] for k, v in g["actions"].items()}
+    assert sum(v[1] for v in r.actions.values()) == g["distinct"] - 1
+    assert [lv[0] for lv in r.levels] == g["levels"]
+    assert n == g["distinct"] and sha == g["states_sha256"]
+
+
 def test_depth_limit_kat(raftmc):
     # SURVEY.md §4 KAT: expanding Init gives generated 7, distinct 5
     r = raftmc.check(ORIG_MC, os.path.join(CONFIGS, "c1.cfg"), max_depth=2, **SMALL)
@@ -67,12 +85,13 @@ def test_fifo_stop_point_against_oracle(raftmc, name):
     single-worker FIFO order, its counterexample state by state, and TLC's counters at that
     point (generated = whole successor lists up to the violating parent; distinct, per-action
     counts and left-on-queue at the violating successor; completed levels).  Deterministic: a
-    second run and another fingerprint seed give the identical report."""
+    second run, another fingerprint seed and the TLC -workers N pipeline give the identical report."""
     g = EVENTS[name]
     cfg = os.path.join(CONFIGS, name + ".cfg")
     a = raftmc.check(ORIG_MC, cfg, **SMALL)
     b = raftmc.check(ORIG_MC, cfg, seed=0xC0FFEE, **SMALL)
-    for r in (a, b):
+    c = raftmc.check(ORIG_MC, cfg, workers=0, **SMALL)    # -workers N: re-searched in FIFO order on the event
+    for r in (a, b, c):
         assert (r.verdict, r.violated, r.exit_code) == (g["verdict"], g["violated"], 12), r.error
         assert (r.generated, r.distinct, r.left_on_queue, r.depth) == (g["generated"], g["distinct"], g["left_on_queue"],
                                                                        g["depth"])
@@ -138,6 +157,19 @@ def test_seed_independence_c1(raftmc):
     a = raftmc.check(ORIG_MC, cfg, seed=1, **SMALL)
     b = raftmc.check(ORIG_MC, cfg, seed=0xABCDEF, **SMALL)
     assert (a.generated, a.distinct, a.depth) == (b.generated, b.distinct, b.depth)
+
+
+def test_c2_workers_n_equals_fifo(raftmc):
+    """BASELINE configs[1] at full size in both pipelines: TLC -workers 1 (FIFO keys) and -workers N
+    give the identical order-independent results; per-action distinct counts sum to the same."""
+    cfg = os.path.join(CONFIGS, "c2.cfg")
+    a = raftmc.check(ORIG_MC, cfg)
+    b = raftmc.check(ORIG_MC, cfg, workers=0)
+    assert a.verdict == b.verdict == "OK", (a.error, b.error)
+    assert (a.generated, a.distinct, a.depth, a.generated_in_model) == (b.generated, b.distinct, b.depth, b.generated_in_model)
+    assert [lv[0] for lv in a.levels] == [lv[0] for lv in b.levels]
+    assert {k: v[0] for k, v in a.actions.items()} == {k: v[0] for k, v in b.actions.items()}
+    assert sum(v[1] for v in a.actions.values()) == sum(v[1] for v in b.actions.values())
 
 
 def test_c2_full_size_properties(raftmc):
