@@ -101,7 +101,13 @@ template <class S>
 // 3 waves per SIMD (<= 168 VGPRs) measured fastest for C2's expand (19.9 vs 22.3 ms without the
 // hint, 26.6 ms at the 2 waves the incremental fingerprint would otherwise get); larger states
 // (C5: 24 words) would spill at 3 and get no hint.
-__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 15 ? 3 : 1))) orig_generate(GenArgs a) {
+#ifndef RMC_GEN_WAVES
+#define RMC_GEN_WAVES 3
+#endif
+#ifndef RMC_GEN_INC
+#define RMC_GEN_INC 1
+#endif
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 15 ? RMC_GEN_WAVES : 1))) orig_generate(GenArgs a) {
   using W = typename S::Work;
   constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
   __shared__ unsigned int lds_cnt[OA_NACT + 1];   // per-action generated, in-model total
@@ -125,7 +131,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
   // raft_original.tla:464) and their fingerprint terms: successors re-hash changed words only
   // (C5-sized states keep the plain hash: the base terms would cost them occupancy, measured
   // 45 vs 38 ms of expand time for C5 to depth 12)
-  constexpr bool INC = NW <= 16;
+  constexpr bool INC = RMC_GEN_INC && NW <= 16;
   u32 bw[INC ? NW : 1];
   FpBase<INC ? NW : 2> fb;
   if (active) {
@@ -278,13 +284,9 @@ __device__ __forceinline__ u32 probe_batch(u64* table, u64 mask, const u64 (&fp)
     pos[j] = slot;
   }
   if (KEYED) {
-#if defined(RMC_EXP_NOKEY)
-    (void)lower;
-#else
 #pragma unroll
     for (int j = 0; j < G; ++j)
       if ((lower >> j) & 1u) atomicMax((unsigned long long*)&table[2 * pos[j] + 1], (unsigned long long)nk[j]);
-#endif
   }
   return ins;
 }
