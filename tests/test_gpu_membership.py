@@ -108,3 +108,21 @@ def test_c3_counterexample_matches_committed_trace(raftmc):
     got = [" ".join(b.split("\n")[1:]) for b in r.trace_text.strip().split("\n\n")]
     want = open(os.path.join(GOLDEN, "c3_leader_votes_quorum_trace.txt")).read().strip().split("\n")
     assert got == want
+
+
+GPU_TRACES = json.load(open(os.path.join(GOLDEN, "gpu_traces", "index.json")))["cases"]
+
+
+@pytest.mark.parametrize("cfg", sorted(GPU_TRACES))
+def test_counterexamples_beyond_oracle_reach(raftmc, cfg):
+    """Counterexamples at 14.6M-468M distinct states (tests/golden/gpu_traces/, each validated
+    state by state by the oracle's check-trace, tests/test_oracle.py): TLC's single-worker FIFO
+    order makes them reproducible — the same trace, depth and stop-point counters on every run.
+    Among them the positive controls of the invariant kernels (VotesGrantedInv_false,
+    LeaderCompleteness_false) and a LogMatching violation of the dynamic-membership model."""
+    g = GPU_TRACES[cfg]
+    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, cfg + ".cfg"), deadlock=False)
+    assert (r.verdict, r.violated) == (g["verdict"], g["violated"]), r.error
+    assert (r.depth, r.distinct, r.generated, r.left_on_queue) == (g["depth"], g["distinct"], g["generated"], g["left_on_queue"])
+    got = [" ".join(b.split("\n")[1:]) for b in r.trace_text.strip().split("\n\n")]
+    assert got == open(os.path.join(GOLDEN, "gpu_traces", cfg + ".txt")).read().strip().split("\n")

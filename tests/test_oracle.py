@@ -120,3 +120,23 @@ def test_oracle_parallel_expansion_is_identical(tla, cfg, extra):
     b = run_oracle("bfs", spec, os.path.join(CONFIGS, cfg), *extra, "--workers", "4")
     a.pop("seconds"), b.pop("seconds")
     assert a == b
+
+
+GPU_TRACES = json.load(open(os.path.join(GOLDEN, "gpu_traces", "index.json")))["cases"]
+
+
+@pytest.mark.parametrize("cfg", sorted(GPU_TRACES))
+def test_oracle_validates_gpu_counterexamples(cfg):
+    """Counterexamples the GPU finds beyond the oracle's BFS reach (tests/golden/gpu_traces/): the
+    LogMatching violation of the dynamic-membership model (InitServer = {s1, s2} grows to three
+    servers), the known-false VotesGrantedInv_false / LeaderCompleteness_false (positive controls of
+    the invariant kernels, raft.tla:1038-1046, :1079-1083) and BoundedTrace under
+    CommitWhenConcurrentLeaders_constraint (raft.tla:1182-1186).  The oracle replays each state by
+    state through its own Init, Next, constraints and invariants: valid, and the last state violates
+    the named property."""
+    from oracle_util import MEMB_MC, run_oracle
+    g = GPU_TRACES[cfg]
+    r = run_oracle("check-trace", MEMB_MC, os.path.join(CONFIGS, cfg + ".cfg"), "--golden",
+                   os.path.join(GOLDEN, "gpu_traces", cfg + ".txt"))
+    assert r["valid"] and r["length"] == g["depth"] and r["violated"] == g["violated"], r
+    assert r["actions"].split(",") == g["actions"][1:]
