@@ -229,10 +229,17 @@ int mc_shard_violation(const mc_ctx* ctx, uint64_t* parent_gid, char** action, c
  *   mc_shard_run_rccl   every rank: shard_open + ncclCommInitRank (cached on the handle for
  *                       repeated runs with the same id) + the whole level loop; afterwards
  *                       mc_summary / mc_shard_violation / mc_shard_read_state as usual.
+ *   mc_shard_run_loopback  the same level loop for `world` ranks in ONE process (one host
+ *                       thread and one handle per rank, every rank on its handle's device —
+ *                       typically all on one GPU), the exchanges as device-to-device copies
+ *                       between the ranks' buffers: the multi-rank path (routing, self
+ *                       segments, all-reduce, counterexample gather) testable on one GPU.
+ *                       ctxs[r] is rank r; results per handle as after mc_shard_run_rccl.
  * RCCL is dlopen()ed (librccl.so.1) on first use; MC_E_UNSUPPORTED if it cannot be loaded or
  * the spec has no native loop (tlc_membership uses the FIFO protocol above). */
 int mc_rccl_unique_id(mc_ctx* ctx, void* out, size_t len);
 int mc_shard_run_rccl(mc_ctx* ctx, int32_t rank, int32_t world, const void* unique_id, size_t len);
+int mc_shard_run_loopback(mc_ctx* const* ctxs, int32_t world);
 int mc_shard_layout(mc_ctx* ctx, const int64_t* frontier_counts);
 int mc_shard_select(mc_ctx* ctx, int64_t* reply_counts);
 int mc_shard_event_stats(mc_ctx* ctx, const int64_t* global_stats, int64_t* stats);

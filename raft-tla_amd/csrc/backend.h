@@ -11,6 +11,8 @@
 
 namespace rmc {
 
+struct ShardTransport;   // shard_transport.h
+
 struct RunOpts {
   int device = 0;
   uint64_t fp_table_bytes = 0, state_store_bytes = 0;
@@ -81,7 +83,7 @@ struct Backend {
   virtual const RunResult* shard_result() const = 0;
   // FIFO first-found specs (VIEW): level layout, per-level winner selection, stop-point counters
   // the whole sharded level loop natively over an RCCL communicator (after shard_open)
-  virtual int shard_run_native(void* comm, std::string& err) { (void)comm; err = "no native sharded loop for this spec"; return -4; }
+  virtual int shard_run_native(ShardTransport& t, std::string& err) { (void)t; err = "no native sharded loop for this spec"; return -4; }
   virtual int shard_layout(const int64_t* counts, std::string& err) { (void)counts; err = "not a FIFO-ranked spec"; return -4; }
   virtual int shard_select(int64_t* reply_counts, std::string& err) { (void)reply_counts; err = "not a FIFO-ranked spec"; return -4; }
   virtual int shard_event_stats(const int64_t* g, int64_t* st, std::string& err) { (void)g; (void)st; err = "not a FIFO-ranked spec"; return -4; }

@@ -7,11 +7,14 @@
 #include <memory>
 #include <sstream>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/raftmc.h"
 #include "backend.h"
 #include "model.h"
 #include "rccl_api.h"
+#include "shard_transport.h"
 #include "tla_value.h"
 
 struct mc_ctx {
@@ -431,11 +434,41 @@ int mc_shard_run_rccl(mc_ctx* c, int32_t rank, int32_t world, const void* unique
     c->comm_rank = rank; c->comm_world = world;
     std::memcpy(c->comm_id, unique_id, sizeof(ncclUniqueId));
   }
-  rc = c->be->shard_run_native(c->comm, err);
+  rmc::RcclTransport t(c->comm);
+  rc = c->be->shard_run_native(t, err);
   if (rc) { c->last_error = err; return rc; }
   c->res = *c->be->shard_result();
   c->ran = true;
   c->last_error = c->res.error;
+  return MC_OK;
+}
+
+int mc_shard_run_loopback(mc_ctx* const* ctxs, int32_t world) {
+  if (!ctxs || world < 1 || world > 8) return MC_E_INVALID;
+  for (int r = 0; r < world; ++r) {
+    if (!ctxs[r] || !ctxs[r]->be) return MC_E_INVALID;
+    for (int q = 0; q < r; ++q) if (ctxs[q] == ctxs[r]) return MC_E_INVALID;
+  }
+  rmc::LoopbackWorld w(world);
+  std::vector<int> rcs(world, MC_OK);
+  auto rank_main = [&](int r) {
+    mc_ctx* c = ctxs[r];
+    std::string err;
+    c->ran = false;
+    int rc = c->be->shard_open(c->ro, r, world, err);   // selects the device on this thread
+    if (!rc) {
+      rmc::LoopbackTransport t(w, r);
+      rc = c->be->shard_run_native(t, err);
+    }
+    if (rc) { c->last_error = err; w.abort(); }
+    else { c->res = *c->be->shard_result(); c->ran = true; c->last_error = c->res.error; }
+    rcs[r] = rc;
+  };
+  std::vector<std::thread> th;
+  for (int r = 1; r < world; ++r) th.emplace_back(rank_main, r);
+  rank_main(0);
+  for (auto& x : th) x.join();
+  for (int r = 0; r < world; ++r) if (rcs[r]) return rcs[r];
   return MC_OK;
 }
 

@@ -53,6 +53,7 @@
 #include "orig_spec.h"
 #include "orig_text.h"
 #include "rccl_api.h"
+#include "shard_transport.h"
 
 namespace rmc {
 
@@ -1858,21 +1859,14 @@ class OrigGpu : public Backend {
   }
   const RunResult* shard_result() const override { return &sres_; }
 
-  // ---------------------------------------------------------------- native level loop over RCCL
+  // ---------------------------------------------------------------- native level loop
   // The whole sharded BFS of raft-tla_amd/shard.py (sharded_bfs) in C++ on one HIP stream:
   // per chunk generate+route -> counts exchange -> ROUTE payload -> dedup -> counts exchange ->
-  // REPLY payload -> materialize -> STATES payload -> store, with grouped ncclSend/ncclRecv
-  // straight from the kernels' buffers (no staging copies) and two host synchronisations per
-  // chunk (the counts) plus one per level (the all-reduce of the level statistics).
-  int shard_run_native(void* comm_v, std::string& err) override {
-    RcclApi& R = rccl();
-    if (!R.ok) { err = "RCCL not loaded"; return MC_E_STATE; }
-    ncclComm_t comm = (ncclComm_t)comm_v;
-#define NCCLCHK(x)                                                                                   \
-  do {                                                                                               \
-    ncclResult_t r_ = (x);                                                                           \
-    if (r_ != ncclSuccess) { err = std::string(#x) + ": " + R.GetErrorString(r_); return MC_E_NO_DEVICE; } \
-  } while (0)
+  // REPLY payload -> materialize -> STATES payload -> store, over a ShardTransport
+  // (shard_transport.h: grouped ncclSend/ncclRecv straight from the kernels' buffers between
+  // GPUs, or the in-process loopback of mc_shard_run_loopback) with two host synchronisations
+  // per chunk (the counts) plus one per level (the all-reduce of the level statistics).
+  int shard_run_native(ShardTransport& T, std::string& err) override {
     const int W = world_, me = rank_;
     const u64 SBW = (u64)(NWP + 4) * 4;          // STATES record bytes
     if (!d_nat_) HIPCHK(hipMalloc(&d_nat_, (32 + 2 * MC_SHARD_NSTAT) * 8));
@@ -1897,13 +1891,9 @@ class OrigGpu : public Backend {
       HIPCHK(hipMemcpyAsync(d_xs, d_send, 8 * (u64)W, hipMemcpyDeviceToDevice, stream_));
       HIPCHK(hipMemcpyAsync(d_xr + me, d_send + me, 8, hipMemcpyDeviceToDevice, stream_));
       if (W > 1) {
-        NCCLCHK(R.GroupStart());
-        for (int r = 0; r < W; ++r) {
-          if (r == me) continue;
-          NCCLCHK(R.Send(d_xs + r, 1, ncclUint64, r, comm, stream_));
-          NCCLCHK(R.Recv(d_xr + r, 1, ncclUint64, r, comm, stream_));
-        }
-        NCCLCHK(R.GroupEnd());
+        const char* src[8]; char* dst[8]; u64 n8[8];
+        for (int r = 0; r < W; ++r) { src[r] = (const char*)(d_xs + r); dst[r] = (char*)(d_xr + r); n8[r] = 8; }
+        if (T.exchange(me, W, src, n8, dst, n8, stream_, err)) return MC_E_NO_DEVICE;
       }
       HIPCHK(hipMemcpyAsync(h_xs, d_xs, 16 * 8, hipMemcpyDeviceToHost, stream_));
       HIPCHK(hipStreamSynchronize(stream_));
@@ -1913,18 +1903,10 @@ class OrigGpu : public Backend {
     // packed in source-rank order; the self segment is not copied (its consumer reads it in
     // place), so dst + roff[me] stays unused
     auto xpay = [&](const char* const* src, const u64* sbytes, char* dst, const u64* rbytes) -> int {
-      u64 roff[8]; u64 acc = 0;
-      for (int r = 0; r < W; ++r) { roff[r] = acc; acc += rbytes[r]; }
+      char* dsts[8]; u64 acc = 0;
+      for (int r = 0; r < W; ++r) { dsts[r] = dst + acc; acc += rbytes[r]; }
       if (sbytes[me] != rbytes[me]) { err = "sharded exchange: self segment size mismatch"; return MC_E_STATE; }
-      if (W > 1) {
-        NCCLCHK(R.GroupStart());
-        for (int r = 0; r < W; ++r) {
-          if (r == me) continue;
-          if (sbytes[r]) NCCLCHK(R.Send(src[r], sbytes[r], ncclUint8, r, comm, stream_));
-          if (rbytes[r]) NCCLCHK(R.Recv(dst + roff[r], rbytes[r], ncclUint8, r, comm, stream_));
-        }
-        NCCLCHK(R.GroupEnd());
-      }
+      if (W > 1 && T.exchange(me, W, src, sbytes, dsts, rbytes, stream_, err)) return MC_E_NO_DEVICE;
       return 0;
     };
     // HIP-event timing, read back at the level's synchronisation points
@@ -1959,12 +1941,7 @@ class OrigGpu : public Backend {
       for (int k = 0; k < MC_SHARD_NSTAT; ++k) h_max[k] = 0;
       h_max[3] = g[3]; h_max[4] = g[4]; h_max[5] = g[5]; h_max[6] = next_chunks;
       HIPCHK(hipMemcpyAsync(d_sum, h_sum, 2 * MC_SHARD_NSTAT * 8, hipMemcpyHostToDevice, stream_));
-      if (W > 1) {
-        NCCLCHK(R.GroupStart());
-        NCCLCHK(R.AllReduce(d_sum, d_sum, MC_SHARD_NSTAT, ncclInt64, ncclSum, comm, stream_));
-        NCCLCHK(R.AllReduce(d_max, d_max, 8, ncclInt64, ncclMax, comm, stream_));
-        NCCLCHK(R.GroupEnd());
-      }
+      if (W > 1 && T.allreduce(d_sum, MC_SHARD_NSTAT, d_max, 8, stream_, err)) return MC_E_NO_DEVICE;
       HIPCHK(hipMemcpyAsync(h_sum, d_sum, 2 * MC_SHARD_NSTAT * 8, hipMemcpyDeviceToHost, stream_));
       HIPCHK(hipStreamSynchronize(stream_));
       for (int k = 0; k < MC_SHARD_NSTAT; ++k) g[k] = h_sum[k];
@@ -2088,7 +2065,6 @@ class OrigGpu : public Backend {
       nchunks = next_chunks;
     }
 #undef NAT_TIMED
-#undef NCCLCHK
     return 0;
   }
 

@@ -28,7 +28,7 @@ EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stat
            "mc_shard_generate", "mc_shard_fill", "mc_shard_dedup", "mc_shard_materialize", "mc_shard_store",
            "mc_shard_level_stats", "mc_shard_level_commit", "mc_shard_read_state", "mc_shard_violation",
            "mc_set_history_prefix", "mc_shard_layout", "mc_shard_select", "mc_shard_event_stats",
-           "mc_collision_observed", "mc_rccl_unique_id", "mc_shard_run_rccl",
+           "mc_collision_observed", "mc_rccl_unique_id", "mc_shard_run_rccl", "mc_shard_run_loopback",
            "mc_set_checkpoint", "mc_set_recover", "mc_action_location"]
 
 

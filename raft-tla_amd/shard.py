@@ -337,6 +337,59 @@ def fifo_sharded_bfs(shard, ex, rank, device):
     return _trace(shard, ex, rank, world)
 
 
+def _local_trace(shards):
+    """_trace for ranks that live in one process: the lowest violating rank's head, then the
+    parent chain read from each state's owner (gid bits 37..39)."""
+    head = next((v for v in (sh.violation() for sh in shards) if v is not None), None)
+    if head is None:
+        return None
+    parent, act, text = head
+    if parent == (1 << 64) - 1:
+        return [("<Initial predicate>", text)]
+    trace = [(act, text)]
+    gid = parent
+    names = shards[0].mc.describe()["actions"]
+    for _ in range(1 << 20):
+        text, meta = shards[(gid >> 37) & 7].read_state(gid)
+        if meta == (1 << 64) - 1:
+            trace.append(("<Initial predicate>", text))
+            break
+        trace.append((names[(meta >> 16) & 0xFF], text))
+        gid = meta >> 24
+    trace.reverse()
+    return trace
+
+
+def check_loopback(spec, config, world, device_index=0, **kw):
+    """The library's native sharded level loop (the one mc_shard_run_rccl drives over RCCL) for
+    `world` ranks inside this process, all on one device, exchanging through device-to-device
+    copies (mc_shard_run_loopback).  Returns one raftmc Result per rank, the counterexample (if
+    any) reassembled across ranks as .trace_text on each."""
+    mcs = [_rm.ModelChecker(spec, config, device=device_index, **kw) for _ in range(world)]
+    try:
+        if mcs[0].describe()["spec"] != "raft_original":
+            raise ValueError("the native sharded loop covers raft_original")
+        lib = mcs[0].lib
+        lib.mc_shard_run_loopback.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32]
+        hs = (ctypes.c_void_p * world)(*[m.h for m in mcs])
+        rc = lib.mc_shard_run_loopback(hs, world)
+        if rc:
+            errs = [lib.mc_last_error(m.h).decode() for m in mcs]
+            raise _rm.RaftMCError(rc, "; ".join(e for e in errs if e) or "loopback run failed")
+        shards = [LibShard(m, r, world, open_shard=False) for r, m in enumerate(mcs)]
+        trace = _local_trace(shards)
+        out = []
+        for m in mcs:
+            res = m.summary()
+            if trace:
+                res.trace_text = trace_text(trace, m.action_location)
+            out.append(res)
+        return out
+    finally:
+        for m in mcs:
+            m.close()
+
+
 def _trace(shard, ex, rank, world):
     v = shard.violation()
     # the lowest rank that recorded a violation reports it
