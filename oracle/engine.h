@@ -15,6 +15,7 @@
 // ============================================================================
 #pragma once
 #include <atomic>
+#include <cstring>
 #include <chrono>
 #include <thread>
 #include <fstream>
@@ -160,7 +161,8 @@ struct Options {
   int64_t max_states = 0;           // stop after this many distinct (sample mode)
   bool check_deadlock = false;
   std::string dump_states;          // write canonical text of every distinct state
-  bool store_text_keys = true;      // seen-set keyed by full canonical text (exact)
+  bool lean = false;                // bfs_lean: 128-bit key hashes, only two levels of states kept
+  bool progress = false;            // bfs_lean: a progress line per parent block on stderr
   int workers = 1;                  // >1: successors, constraints, keys and invariants of a batch
                                     // of parents are computed by this many threads, merged in
                                     // frontier order (results identical to workers = 1)
@@ -442,6 +444,153 @@ inline Result bfs(const Spec& sp, const Cfg& cfg, const Options& o) {
   }
 done:
   if (dump) std::fclose(dump);
+  r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return r;
+}
+
+// ----------------------------------------------------------------- lean BFS (full-size counts)
+// The same search as bfs() with its workers > 1 merge (parents in frontier order, successors in
+// Next order, so every count — per-action distinct ones included — is the single-worker FIFO
+// one), for state spaces whose canonical texts and value trees do not fit in memory: the seen-set
+// holds a 128-bit hash of each canonical key (two independent 64-bit hashes of the text; for
+// 1e8 keys the chance of any collision is ~1e-23), and only the current and next level's states
+// are kept, so there are no traces (a violation reports the verdict, the invariant and TLC's
+// counters at the stop point).  Used for the full-size raft_original C2 fixture.
+inline uint64_t text_hash(const std::string& k, uint64_t seed) {
+  uint64_t h = seed ^ (k.size() * 0x9E3779B97F4A7C15ull);
+  size_t i = 0;
+  auto mix = [](uint64_t x) { x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33; return x; };
+  for (; i + 8 <= k.size(); i += 8) { uint64_t w; std::memcpy(&w, k.data() + i, 8); h = mix(h ^ w) * 0x100000001B3ull + i; }
+  uint64_t w = 0; std::memcpy(&w, k.data() + i, k.size() - i);
+  return mix(h ^ w ^ (0xA5ull << 56));
+}
+
+struct Key128 { uint64_t a, b; };
+struct Key128Set {   // open addressing, linear probing; {0,0} = empty
+  std::vector<Key128> t; uint64_t mask = 0, n = 0;
+  explicit Key128Set(int log2) : t(1ull << log2, Key128{0, 0}), mask((1ull << log2) - 1) {}
+  bool insert(Key128 k) {
+    if (!k.a && !k.b) k.b = 1;
+    if (2 * (n + 1) > t.size()) grow();
+    for (uint64_t i = k.a & mask;; i = (i + 1) & mask) {
+      if (!t[i].a && !t[i].b) { t[i] = k; ++n; return true; }
+      if (t[i].a == k.a && t[i].b == k.b) return false;
+    }
+  }
+  void grow() {
+    std::vector<Key128> old; old.swap(t);
+    t.assign(old.size() * 2, Key128{0, 0}); mask = t.size() - 1; n = 0;
+    for (auto& k : old) if (k.a || k.b) insert(k);
+  }
+};
+
+inline Result bfs_lean(const Spec& sp, const Cfg& cfg, const Options& o) {
+  auto t0 = std::chrono::steady_clock::now();
+  Result r;
+  auto an = sp.action_names();
+  r.act_generated.assign(an.size(), 0); r.act_distinct.assign(an.size(), 0);
+  auto perms = cfg.symmetry.empty() ? std::vector<std::vector<int>>{} : sp.symmetry_perms(cfg.symmetry);
+  auto vv = cfg.view.empty() ? std::vector<int>{} : sp.view_vars(cfg.view);
+  Key128Set seen(20);
+  auto key_of = [&](const State& s) {
+    const std::string k = canon_key(sp, cfg, o, s, perms, vv);
+    return Key128{text_hash(k, 0x243F6A8885A308D3ull), text_hash(k, 0x13198A2E03707344ull)};
+  };
+  auto in_model = [&](const State& s) {
+    for (auto& c : cfg.constraints) if (!sp.constraint(c, s)) return false;
+    return true;
+  };
+  auto in_actions = [&](const State& s, const State& t) {
+    for (auto& c : cfg.action_constraints) if (!sp.action_constraint(c, s, t)) return false;
+    return true;
+  };
+  auto check_inv = [&](const State& s) -> std::string {
+    for (auto& inv : cfg.invariants) if (!sp.invariant(inv, s)) return inv;
+    return "";
+  };
+  const int W = std::max(1, o.workers);
+  try {
+    std::vector<State> frontier;
+    for (auto& s : sp.init()) {
+      r.generated++;
+      const bool im = in_model(s);
+      const bool isnew = im && seen.insert(key_of(s));
+      if (isnew) frontier.push_back(s);
+      if (isnew || (!im && o.inv_out_of_model)) {
+        auto bad = check_inv(s);
+        if (!bad.empty()) { r.verdict = "INVARIANT_VIOLATION"; r.violated = bad; r.depth = 1; goto finish; }
+      }
+    }
+    r.level_sizes.push_back((int64_t)frontier.size());
+    r.depth = frontier.empty() ? 0 : 1;
+    for (int32_t level = 1; !frontier.empty();) {
+      if (o.max_depth && level >= o.max_depth) { r.left_on_queue = (int64_t)frontier.size(); break; }
+      std::vector<State> nextf;
+      struct SRec { int action; bool im; Key128 key; std::string bad, bad_err; State s; };
+      struct PRec { std::vector<SRec> succ; bool err = false; std::string errmsg; };
+      const size_t B = 8192;
+      for (size_t b0 = 0; b0 < frontier.size(); b0 += B) {
+        const size_t b1 = std::min(frontier.size(), b0 + B);
+        std::vector<PRec> recs(b1 - b0);
+        std::atomic<size_t> next_i{b0};
+        auto work = [&]() {
+          std::vector<Succ> ss;
+          for (size_t i; (i = next_i.fetch_add(1)) < b1;) {
+            PRec& pr = recs[i - b0];
+            const State& cur = frontier[i];
+            try {
+              ss.clear();
+              sp.next(cur, ss);
+              for (auto& su : ss) {
+                SRec sr;
+                sr.action = su.action;
+                sr.im = in_model(su.s) && in_actions(cur, su.s);
+                sr.key = sr.im ? key_of(su.s) : Key128{0, 0};
+                if (sr.im || o.inv_out_of_model) {
+                  try { sr.bad = check_inv(su.s); } catch (const EvalError& e) { sr.bad_err = e.what(); }
+                }
+                if (sr.im) sr.s = std::move(su.s);
+                pr.succ.push_back(std::move(sr));
+              }
+            } catch (const EvalError& e) { pr.err = true; pr.errmsg = e.what(); }
+          }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < W; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+        for (size_t fi = b0; fi < b1; ++fi) {
+          PRec& pr = recs[fi - b0];
+          auto left = [&]() { return (int64_t)(frontier.size() - fi - 1 + nextf.size()); };
+          if (pr.err) { r.verdict = "EVAL_ERROR"; r.error = pr.errmsg; r.left_on_queue = left(); goto finish; }
+          r.generated += (int64_t)pr.succ.size();
+          if (pr.succ.empty() && o.check_deadlock) { r.verdict = "DEADLOCK"; r.left_on_queue = left(); goto finish; }
+          for (auto& su : pr.succ) {
+            r.act_generated[su.action]++;
+            const bool isnew = su.im && seen.insert(su.key);
+            if (isnew) { r.act_distinct[su.action]++; nextf.push_back(std::move(su.s)); }
+            if (isnew || (!su.im && o.inv_out_of_model)) {
+              if (!su.bad_err.empty() || !su.bad.empty()) {
+                if (su.bad_err.empty()) { r.verdict = "INVARIANT_VIOLATION"; r.violated = su.bad; }
+                else { r.verdict = "EVAL_ERROR"; r.error = su.bad_err; }
+                r.depth = level + 1; r.left_on_queue = left();
+                goto finish;
+              }
+            }
+          }
+        }
+        if (o.progress) std::fprintf(stderr, "level %d: %zu/%zu parents, %llu distinct, %.0f s\n", level, b1, frontier.size(),
+                                     (unsigned long long)seen.n,
+                                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+      }
+      if (!nextf.empty()) { level++; r.depth = level; r.level_sizes.push_back((int64_t)nextf.size()); }
+      frontier.swap(nextf);
+    }
+  } catch (const EvalError& e) {
+    r.verdict = "EVAL_ERROR"; r.error = e.what();
+  }
+finish:
+  r.distinct = (int64_t)seen.n;
   r.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return r;
 }

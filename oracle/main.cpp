@@ -5,6 +5,7 @@
 //   raft_oracle bfs    --tla F.tla --cfg F.cfg [--max-depth D] [--max-states N]
 //                      [--dump states.txt] [--sym tlc|view] [--no-inv-oom]
 //                      [--deadlock] [--golden-cwcl F] [--golden-morc F] [--trace]
+//                      [--workers T] [--lean [--progress]]   (lean: engine.h bfs_lean, no trace)
 //   raft_oracle replay --tla F.tla --cfg F.cfg --golden F [--max-steps N]
 //   raft_oracle check-trace --tla F.tla --cfg F.cfg --golden TRACE.txt   (one state per line)
 //
@@ -65,6 +66,8 @@ int main(int argc, char** argv) {
     else if (k == "--golden-cwcl") gc = nxt();
     else if (k == "--golden-morc") gm = nxt();
     else if (k == "--trace") want_trace = true;
+    else if (k == "--lean") o.lean = true;
+    else if (k == "--progress") o.progress = true;
     else if (k == "--max-steps") max_steps = std::stoll(nxt());
     else { std::fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
   }
@@ -80,7 +83,7 @@ int main(int argc, char** argv) {
       sp.reset(m);
     }
     if (mode == "bfs") {
-      Result r = bfs(*sp, cfg, o);
+      Result r = o.lean ? bfs_lean(*sp, cfg, o) : bfs(*sp, cfg, o);
       auto an = sp->action_names();
       std::string js = "{";
       js += "\"spec\": " + json_str(family) + ", \"verdict\": " + json_str(r.verdict);

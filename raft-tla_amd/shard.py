@@ -378,12 +378,13 @@ def check_loopback(spec, config, world, device_index=0, **kw):
             raise _rm.RaftMCError(rc, "; ".join(e for e in errs if e) or "loopback run failed")
         shards = [LibShard(m, r, world, open_shard=False) for r, m in enumerate(mcs)]
         trace = _local_trace(shards)
-        out = []
-        for m in mcs:
-            res = m.summary()
+        out = [m.summary() for m in mcs]
+        name = next((r.violated for r in out if r.violated), "")
+        for m, res in zip(mcs, out):
+            if res.verdict == "INVARIANT_VIOLATION":
+                res.violated = name
             if trace:
                 res.trace_text = trace_text(trace, m.action_location)
-            out.append(res)
         return out
     finally:
         for m in mcs:
@@ -462,13 +463,14 @@ class ShardedChecker:
                 self._uid = self.ex.broadcast_obj(shard.rccl_unique_id() if self.rank == 0 else None, 0)
             shard.run_rccl(self.rank, self.world, self._uid)
             trace = _trace(shard, self.ex, self.rank, self.world)
-            res = self.mc.summary()
-            if trace:
-                res.trace_text = trace_text(trace, self.mc.action_location)
-            return res
-        shard = LibShard(self.mc, self.rank, self.world)
-        trace = (fifo_sharded_bfs if self.fifo else sharded_bfs)(shard, self.ex, self.rank, self.device)
+        else:
+            shard = LibShard(self.mc, self.rank, self.world)
+            trace = (fifo_sharded_bfs if self.fifo else sharded_bfs)(shard, self.ex, self.rank, self.device)
         res = self.mc.summary()
+        if res.verdict == "INVARIANT_VIOLATION":   # the name is known on the violating ranks only
+            top = self.ex.allreduce_max(self.world - self.rank if res.violated else 0)
+            if top:
+                res.violated = self.ex.broadcast_obj(res.violated, self.world - top)
         if trace:
             res.trace_text = trace_text(trace, self.mc.action_location)
         return res

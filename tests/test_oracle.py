@@ -140,3 +140,14 @@ def test_oracle_validates_gpu_counterexamples(cfg):
                    os.path.join(GOLDEN, "gpu_traces", cfg + ".txt"))
     assert r["valid"] and r["length"] == g["depth"] and r["violated"] == g["violated"], r
     assert r["actions"].split(",") == g["actions"][1:]
+
+
+@pytest.mark.parametrize("name", ["parity_pair", "parity_trio", "c2_noleader"])
+def test_oracle_lean_mode_is_identical(name):
+    """--lean (engine.h bfs_lean: the mode of the full-size C2 fixture, tests/golden/c2_oracle.json)
+    keys the seen-set by 128-bit hashes of the canonical text and keeps two levels of states: its
+    counts, per-action counts, levels and stop point equal the exact text-keyed search's."""
+    a = run_oracle("bfs", ORIG_MC, os.path.join(CONFIGS, name + ".cfg"))
+    b = run_oracle("bfs", ORIG_MC, os.path.join(CONFIGS, name + ".cfg"), "--lean", "--workers", "4")
+    for k in ("verdict", "violated", "generated", "distinct", "depth", "left_on_queue", "levels", "actions"):
+        assert a[k] == b[k], k
