@@ -240,6 +240,12 @@ int mc_shard_violation(const mc_ctx* ctx, uint64_t* parent_gid, char** action, c
 int mc_rccl_unique_id(mc_ctx* ctx, void* out, size_t len);
 int mc_shard_run_rccl(mc_ctx* ctx, int32_t rank, int32_t world, const void* unique_id, size_t len);
 int mc_shard_run_loopback(mc_ctx* const* ctxs, int32_t world);
+
+/* Source identity of this build: the first 16 hex digits of the SHA-256 of the library's
+ * sources (raft-tla_amd/csrc/ *.h *.cpp *.hip in byte order, then this header), fixed at
+ * compile time.  The Python binding compares it with the sources next to the library and refuses
+ * a stale build, so a GPU run provably executes the tree it was shipped with. */
+const char* mc_source_hash(void);
 int mc_shard_layout(mc_ctx* ctx, const int64_t* frontier_counts);
 int mc_shard_select(mc_ctx* ctx, int64_t* reply_counts);
 int mc_shard_event_stats(mc_ctx* ctx, const int64_t* global_stats, int64_t* stats);

@@ -472,6 +472,11 @@ int mc_shard_run_loopback(mc_ctx* const* ctxs, int32_t world) {
   return MC_OK;
 }
 
+#ifndef RAFTMC_SOURCE_HASH
+#define RAFTMC_SOURCE_HASH "unknown"
+#endif
+const char* mc_source_hash(void) { return RAFTMC_SOURCE_HASH; }
+
 void mc_free(void* p) { std::free(p); }
 void mc_close(mc_ctx* c) { delete c; }
 const char* mc_last_error(const mc_ctx* c) { return c ? c->last_error.c_str() : "null handle"; }

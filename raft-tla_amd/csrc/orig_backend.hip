@@ -959,8 +959,8 @@ struct DedupShArgs {
   unsigned long long* ctr;
 };
 
-// owner-side insertion of one source rank's records (no FIFO keys in sharded raft_original: the
-// entries' key words stay 0)
+// owner-side insertion of one source rank's records into the seen-set as 8-B entries {fp} (no FIFO
+// keys in sharded raft_original: twice the entries of the keyed table in the same bytes)
 __global__ void __launch_bounds__(BS) orig_dedup_sh(DedupShArgs a) {
   __shared__ u32 wave_tot[BS / 64];
   __shared__ unsigned long long base_sh;
@@ -973,7 +973,7 @@ __global__ void __launch_bounds__(BS) orig_dedup_sh(DedupShArgs a) {
     nk[j] = 0ull;
   }
   u32 err = 0;
-  const u32 isnew = probe_batch<DEDUP_PER, false>(a.table, a.table_mask, fp, nk, pos, err);
+  const u32 isnew = probe_batch<DEDUP_PER, false, 1>(a.table, a.table_mask, fp, nk, pos, err);
   u32 total = 0;
   const u32 off = block_excl_scan((u32)__popc(isnew), wave_tot, &total);
   if (threadIdx.x == 0) base_sh = total ? atomicAdd(a.counter, (unsigned long long)total) : 0ull;
@@ -996,6 +996,11 @@ struct MatShArgs {
   u64 seed;
   OrigRuntime rt;
   unsigned long long* ctr;
+  // the generator's own segment (it owns these states): straight into its store at st_dst
+  // instead of a STATES record, when st_states is set
+  u32* st_states;
+  u64* st_meta;
+  u64 st_dst, st_cap;
 };
 
 template <class S>
@@ -1027,11 +1032,24 @@ __global__ void __launch_bounds__(BS) orig_materialize_sh(MatShArgs a) {
     S::pack(t, pw);
     const u64 fp = fp64(pw, a.seed);
     const u64 meta = ((a.rank_bits | gid) << 24) | ((u64)(act < 0 ? 0 : act) << 16) | k;
-    u32* o = a.out + i * RW;
+    if (a.st_states) {
+      const u64 dst = a.st_dst + i;
+      if (dst < a.st_cap) {
+        uint4* o = reinterpret_cast<uint4*>(a.st_states + dst * NWP);
 #pragma unroll
-    for (int q = 0; q < NWP / 4; ++q)
-      reinterpret_cast<uint4*>(o)[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
-    reinterpret_cast<uint4*>(o)[NWP / 4] = make_uint4((u32)meta, (u32)(meta >> 32), (u32)fp, (u32)(fp >> 32));
+        for (int q = 0; q < NWP / 4; ++q)
+          o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
+        a.st_meta[dst] = meta;
+      } else {
+        err |= OE_CAP_STORE;
+      }
+    } else {
+      u32* o = a.out + i * RW;
+#pragma unroll
+      for (int q = 0; q < NWP / 4; ++q)
+        reinterpret_cast<uint4*>(o)[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
+      reinterpret_cast<uint4*>(o)[NWP / 4] = make_uint4((u32)meta, (u32)(meta >> 32), (u32)fp, (u32)(fp >> 32));
+    }
     if (act >= 0) {
       atomicAdd(&lds_cnt[act], 1u);
       if (S::violated(t, a.rt.invariants)) ev = ev_word(gid, (u32)k, EV_VIOLATION);
@@ -1144,9 +1162,8 @@ class OrigGpu : public Backend {
     if (cap_ < 16) cap_ = 16;
     // frontier chunk: the record regions hold chunk_states * NI records (10 B each), their
     // distinct pairs (16 B) and the inserted-position list as many 8-B entries (worst case: every
-    // record new): ~1/4 of the store; sharded mode also needs world route regions of 16-B records
-    chunk_states_ = std::max<u64>(4096, std::min<u64>(cap_, (sb / 4) / (34 * (u64)S::NI)));
-    if (world > 1) chunk_states_ = std::max<u64>(4096, chunk_states_ / (u64)world);
+    // record new), sharded mode also world route regions of 16-B records: ~1/4 of the store
+    chunk_states_ = std::max<u64>(4096, std::min<u64>(cap_, (sb / 4) / ((34 + 16 * (u64)world) * (u64)S::NI)));
     chunk_states_ = std::min<u64>(chunk_states_, (u64)SCAN_BS * 64 * BS);   // orig_scan: <= 64 blocks per lane
     chunk_states_ = (chunk_states_ / BS) * BS;   // whole workgroups: records are grouped per generate workgroup
     const u64 nblk = chunk_states_ / BS, nrec = chunk_states_ * (u64)S::NI;
@@ -1617,6 +1634,7 @@ class OrigGpu : public Backend {
     if (world < 1 || world > 8 || rank < 0 || rank >= world) { err = "sharded mode supports 1..8 ranks"; return MC_E_INVALID; }
     if (int rc = ensure_alloc(o, world, err)) return rc;
     rank_ = rank; world_ = world; sopts_ = o;
+    last_fifo_ = false;   // 8-B entries (observed_collision)
     HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
     HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
     HIPCHK(hipMemsetAsync(d_ctr_ + K_EVENT, 0xFF, 8, stream_));
@@ -1637,8 +1655,7 @@ class OrigGpu : public Backend {
     base_ = 0; host_states_.clear(); host_meta_.clear();
     if ((int)fp_owner(fp0, (u32)world) == rank) {
       u32 wp[NWP] = {0}; for (int q = 0; q < S::NW; ++q) wp[q] = w0[q];
-      const u64 e0[2] = {fp0, ~0ull};
-      HIPCHK(hipMemcpy(d_table_ + 2 * (fp0 & table_mask_), e0, 16, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(d_table_ + (fp0 & sh_table_mask()), &fp0, 8, hipMemcpyHostToDevice));
       HIPCHK(hipMemcpy(d_states_, wp, NWP * 4, hipMemcpyHostToDevice));
       const u64 nometa = ~0ull;
       HIPCHK(hipMemcpy(d_meta_, &nometa, 8, hipMemcpyHostToDevice));
@@ -1651,6 +1668,7 @@ class OrigGpu : public Backend {
     sh_next_write_ = total_;
     return 0;
   }
+  u64 sh_table_mask() const { return 2 * table_mask_ + 1; }   // sharded seen-set: 8-B entries
   int shard_record_bytes(int what) const override {
     return what == MC_SHARD_ROUTE ? 16 : what == MC_SHARD_REPLY ? 8 : what == MC_SHARD_STATES ? (NWP + 4) * 4 : -1;
   }
@@ -1716,7 +1734,7 @@ class OrigGpu : public Backend {
       if (off + n > chunk_states_ * S::NI) { err = "shard_dedup: received more records than one chunk holds"; return MC_E_INVALID; }
       if (n) {
         DedupShArgs d;
-        d.recv = (const u64*)recv + 2 * off; d.n = n; d.table = d_table_; d.table_mask = table_mask_;
+        d.recv = (const u64*)recv + 2 * off; d.n = n; d.table = d_table_; d.table_mask = sh_table_mask();
         d.reply = d_newrec_ + off; d.counter = (unsigned long long*)(d_rcnt_ + 8 + r); d.ctr = (unsigned long long*)d_ctr_;
         hipLaunchKernelGGL(orig_dedup_sh, dim3((unsigned)((n + BS * DEDUP_PER - 1) / (BS * DEDUP_PER))), dim3(BS), 0, stream_, d);
         HIPCHK(hipGetLastError());
@@ -1749,6 +1767,7 @@ class OrigGpu : public Backend {
       m.states = d_states_; m.acks = (const u64*)acks + seg_off_ack_[r]; m.n = n; m.chunk_begin = sh_chunk_begin_;
       m.chunk_count = sh_chunk_count_; m.out = d_stout_ + seg_off_ack_[r] * (NWP + 4); m.rank_bits = (u64)rank_ << 37;
       m.seed = sres_.seed; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_;
+      m.st_states = nullptr; m.st_meta = nullptr; m.st_dst = 0; m.st_cap = 0;
       hipLaunchKernelGGL((orig_materialize_sh<S>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, m);
       HIPCHK(hipGetLastError());
     }
@@ -1995,7 +2014,7 @@ class OrigGpu : public Backend {
             if (n) {
               DedupShArgs d;
               d.recv = r == me ? d_route_ + (u64)me * route_cap * 2 : (const u64*)nat_recv_ + 2 * off;
-              d.n = n; d.table = d_table_; d.table_mask = table_mask_;
+              d.n = n; d.table = d_table_; d.table_mask = sh_table_mask();
               d.reply = d_newrec_ + off; d.counter = (unsigned long long*)(d_rcnt_ + 8 + r); d.ctr = (unsigned long long*)d_ctr_;
               NAT_TIMED(2, hipLaunchKernelGGL(orig_dedup_sh, dim3((unsigned)((n + BS * DEDUP_PER - 1) / (BS * DEDUP_PER))), dim3(BS), 0, stream_, d));
             }
@@ -2028,6 +2047,11 @@ class OrigGpu : public Backend {
             m.n = ack[r]; m.chunk_begin = sh_chunk_begin_;
             m.chunk_count = sh_chunk_count_; m.out = d_stout_ + seg_off_ack_[r] * (NWP + 4); m.rank_bits = (u64)me << 37;
             m.seed = sres_.seed; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_;
+            m.st_states = nullptr; m.st_meta = nullptr; m.st_dst = 0; m.st_cap = 0;
+            if (r == me) {   // my own new states: into my store after the ones of lower ranks
+              u64 before = 0; for (int q = 0; q < me; ++q) before += rep[q];
+              m.st_states = d_states_; m.st_meta = d_meta_; m.st_dst = sh_next_write_ + before; m.st_cap = cap_;
+            }
             NAT_TIMED(3, hipLaunchKernelGGL((orig_materialize_sh<S>), dim3((unsigned)((ack[r] + BS - 1) / BS)), dim3(BS), 0, stream_, m));
           }
           sres_.kernels[3].algo_bytes += (double)atot * (8 + NWP * 4 + SBW);
@@ -2036,13 +2060,14 @@ class OrigGpu : public Backend {
         for (int r = 0; r < W; ++r) { sb[r] = ack[r] * SBW; rb[r] = rep[r] * SBW; src[r] = (const char*)(d_stout_ + seg_off_ack_[r] * (NWP + 4)); }
         if (int rc = grow(nat_stin_, nat_stin_cap_, ntot * SBW)) return rc;
         if (int rc = xpay(src, sb, (char*)nat_stin_, rb)) return rc;
-        {   // the owner stores the states in source-rank order (its own ones straight from d_stout_)
+        {   // the owner stores the states in source-rank order (its own ones were materialized in place)
           u64 in_off = 0;
           for (int r = 0; r < W; ++r) {
             const u64 n = rep[r];
-            if (n) {
+            if (n && r == me) { sh_next_write_ += n; sh_new_ += n; }
+            else if (n) {
               StoreArgs a;
-              a.in = r == me ? d_stout_ + seg_off_ack_[me] * (NWP + 4) : (const u32*)((const char*)nat_stin_ + in_off * SBW);
+              a.in = (const u32*)((const char*)nat_stin_ + in_off * SBW);
               a.n = n; a.dst = sh_next_write_; a.cap = cap_; a.states = d_states_; a.meta = d_meta_;
               a.ctr = (unsigned long long*)d_ctr_;
               NAT_TIMED(4, hipLaunchKernelGGL((orig_store<NWP>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, a));

@@ -29,7 +29,7 @@ EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stat
            "mc_shard_level_stats", "mc_shard_level_commit", "mc_shard_read_state", "mc_shard_violation",
            "mc_set_history_prefix", "mc_shard_layout", "mc_shard_select", "mc_shard_event_stats",
            "mc_collision_observed", "mc_rccl_unique_id", "mc_shard_run_rccl", "mc_shard_run_loopback",
-           "mc_set_checkpoint", "mc_set_recover", "mc_action_location"]
+           "mc_set_checkpoint", "mc_set_recover", "mc_action_location", "mc_source_hash"]
 
 
 class McOpts(ctypes.Structure):
@@ -59,6 +59,25 @@ class RaftMCError(RuntimeError):
 _lib = None
 
 
+def source_hash():
+    """The library's source identity as raft-tla_amd/Makefile computes it (SRCHASH), or None when the
+    sources are not next to the package."""
+    import hashlib
+    here = os.path.dirname(os.path.abspath(__file__))
+    csrc = os.path.join(here, "csrc")
+    hdr = os.path.join(os.path.dirname(here), "include", "raftmc.h")
+    if not (os.path.isdir(csrc) and os.path.exists(hdr)):
+        return None
+    names = sorted(f for f in os.listdir(csrc) if f.endswith((".h", ".cpp", ".hip")))
+    h = hashlib.sha256()
+    for f in [os.path.join("csrc", n) for n in names]:
+        with open(os.path.join(here, f), "rb") as fh:
+            h.update(fh.read())
+    with open(hdr, "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def load_library(path=LIB_PATH):
     """Load libraftmc.so (raises if it has not been built: there is no fallback)."""
     global _lib
@@ -67,6 +86,12 @@ def load_library(path=LIB_PATH):
     if not os.path.exists(path):
         raise RaftMCError(-5, "libraftmc.so not built at %s (run __graft_entry__.build())" % path)
     lib = ctypes.CDLL(path)
+    lib.mc_source_hash.restype = ctypes.c_char_p
+    want = source_hash()
+    got = lib.mc_source_hash().decode()
+    if want is not None and got != want:
+        raise RaftMCError(-5, "libraftmc.so at %s was built from other sources (library %s, tree %s): rebuild it "
+                              "(make -C raft-tla_amd)" % (path, got, want))
     P = ctypes.c_void_p
     lib.mc_default_opts.argtypes = [ctypes.POINTER(McOpts)]
     lib.mc_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(McOpts), ctypes.POINTER(P)]

@@ -213,3 +213,12 @@ def test_action_location_without_module(raftmc):
     with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c1.cfg")) as mc:
         assert mc.action_location("Timeout") is None
         assert "Timeout" in mc.lib.mc_last_error(mc.h).decode()
+
+
+def test_library_is_built_from_this_tree():
+    """mc_source_hash (compiled in by raft-tla_amd/Makefile) equals the hash of the sources next to
+    the package: a stale libraftmc.so is refused at load time, so a GPU run executes HEAD's sources."""
+    import importlib
+    rm = importlib.import_module("raft-tla_amd.raftmc")
+    lib = rm.load_library()
+    assert lib.mc_source_hash().decode() == rm.source_hash()
