@@ -72,12 +72,23 @@ def cpu_baseline(cfg, max_states, workers, oracle_states):
     return res
 
 
+def workload_name(cfg, max_depth):
+    base = os.path.basename(cfg)
+    if base == "c2.cfg":
+        name = "C2: raft_original.tla + configs/c2.cfg (3 servers, 2 values, term<=3, log<=2, msgs<=5)"
+    else:
+        name = "raft_original.tla + configs/%s" % base
+    return name + (" to depth %d" % max_depth if max_depth else "")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default=os.path.join(ROOT, "configs", "c2.cfg"))
+    # depth-bounded runs of the larger models (configs/c5.cfg: BASELINE configs[4], the 8-GPU workload)
+    ap.add_argument("--max-depth", type=int, default=0)
     ap.add_argument("--cpu-states", type=int, default=60000000, help="bound of the multithreaded CPU BFS (C2: 54.4M)")
     ap.add_argument("--oracle-states", type=int, default=300000, help="bound of the value-model oracle's BFS")
     # the host cores this job may use (the GPU box exports OMP_NUM_THREADS = its CPU share)
@@ -108,10 +119,12 @@ def main():
     if world > 1:
         # owner-partitioned fingerprints, 3 RCCL all-to-alls per level chunk (raft-tla_amd/shard.py)
         shard = importlib.import_module("raft-tla_amd.shard")
-        mc = shard.ShardedChecker(TLA, args.config, rank, world, device_index=local, seed=0x5EED)
+        mc = shard.ShardedChecker(TLA, args.config, rank, world, device_index=local, seed=0x5EED,
+                                  fp_table_bytes=args.fp_table_bytes, state_store_bytes=args.state_store_bytes,
+                                  max_depth=args.max_depth)
     else:
         mc = mod.ModelChecker(TLA, args.config, device=local, seed=0x5EED, fp_table_bytes=args.fp_table_bytes,
-                              state_store_bytes=args.state_store_bytes, workers=args.workers)
+                              state_store_bytes=args.state_store_bytes, workers=args.workers, max_depth=args.max_depth)
 
     def barrier_sync():
         if dist is not None:
@@ -129,12 +142,12 @@ def main():
     barrier_sync()
     elapsed = time.perf_counter() - t0
     mc.close()
-    assert res.verdict == "OK", (res.verdict, res.error)
+    assert res.verdict == "OK" or (args.max_depth and res.verdict == "DEPTH_LIMIT"), (res.verdict, res.error)
     # TLC -workers 1 (FIFO order) on the same model, outside the timed region: its cost is reported
     fifo = None
     if world == 1 and args.workers != 1 and args.fifo_steps > 0:
         with mod.ModelChecker(TLA, args.config, device=local, seed=0x5EED, fp_table_bytes=args.fp_table_bytes,
-                              state_store_bytes=args.state_store_bytes, workers=1) as m1:
+                              state_store_bytes=args.state_store_bytes, workers=1, max_depth=args.max_depth) as m1:
             m1.run()
             f0 = time.perf_counter()
             for _ in range(args.fifo_steps):
@@ -184,7 +197,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic: the model's own reachable state space (no external data)",
-            "config": {"workload": "C2: raft_original.tla + configs/c2.cfg (3 servers, 2 values, term<=3, log<=2, msgs<=5)",
+            "config": {"workload": workload_name(args.config, args.max_depth),
                        "tlc_workers": args.workers,
                        "distinct_per_run": res.distinct, "generated_per_run": res.generated, "depth": res.depth,
                        "generated_in_model_per_run": res.generated_in_model,
@@ -213,7 +226,7 @@ def main():
                     line["roofline"]["valu_issue_frac"] = vj["valu_insts_per_launch"] / (avg_s * 256 * 2 * 2.4e9)
             except Exception:
                 pass
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and os.path.basename(args.config) == "c2.cfg" and not args.max_depth:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_states, args.cpu_workers, args.oracle_states)
         print(json.dumps(line), flush=True)
     if dist is not None:

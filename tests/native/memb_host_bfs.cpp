@@ -6,8 +6,15 @@
 // Shape: -DSHAPE_N=.. -DSHAPE_NV=..
 //   memb_host_bfs CFG MAX_DEPTH [DUMP|-] [--prefix CONSTRAINT TRACE_FILE]...
 //     -> JSON {generated, distinct, depth, left_on_queue, verdict, actions}
+// SYMCHECK=1 (environment): for every distinct state of the search (run it on a cfg WITHOUT
+// SYMMETRY, so symmetric copies are all kept), compare the product's refined symmetric fingerprint
+// (S::fingerprint with symmetry on: min over the signature-respecting permutations only) with the
+// brute-force one (min over all N! permuted views): the two must induce the same partition of the
+// states into orbits ("symcheck": [states, refined classes, brute classes, disagreements]).
 #include <cstdio>
 #include <string>
+#include <cstdlib>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -41,7 +48,10 @@ int main(int argc, char** argv) {
   const u64 seed = 0x5EED5EED2024ull;
   std::unordered_set<u64> seen;
   std::vector<W> frontier(1);
+  std::vector<W> all;   // SYMCHECK: every distinct state
+  const bool keep_all = std::getenv("SYMCHECK") != nullptr;
   S::init(frontier[0]);
+  if (keep_all) all.push_back(frontier[0]);
   seen.insert(S::fingerprint(frontier[0], seed, rt));
   if (dump) std::fprintf(dump, "%s\n", text.text(frontier[0], false).c_str());
   long long generated = 1, gen_act[MA_NACT] = {0}, dist_act[MA_NACT] = {0}, left = 0;
@@ -73,6 +83,7 @@ int main(int argc, char** argv) {
             isnew = seen.insert(S::fingerprint(t, seed, rt)).second;
             if (isnew) {
               dist_act[act]++; next.push_back(t);
+              if (keep_all) all.push_back(t);
               if (dump) std::fprintf(dump, "%s\n", text.text(t, false).c_str());
             }
           }
@@ -94,6 +105,26 @@ int main(int argc, char** argv) {
     frontier.swap(next);
   }
   if (dump) std::fclose(dump);
+  if (std::getenv("SYMCHECK")) {
+    MembRuntime rs = rt; rs.symmetry = 1;
+    std::unordered_map<u64, u64> r2b, b2r;
+    long long bad = 0;
+    for (const W& t : all) {
+      const u64 fr = S::fingerprint(t, seed, rs);
+      const bool ce = S::has_config_entries(t, rs.cfg_type);
+      u64 best = ~0ull;
+      for (int p = 0; p < S::NPERM; ++p) {
+        const u64 h = ce ? S::template view_hash1<true>(t, S::perm_of(p), seed, rs.cfg_type)
+                         : S::template view_hash1<false>(t, S::perm_of(p), seed, rs.cfg_type);
+        best = h < best ? h : best;
+      }
+      const u64 fb0 = S::fmix(best ^ seed), fb = fb0 ? fb0 : 1ull;
+      auto a = r2b.emplace(fr, fb), b = b2r.emplace(fb, fr);
+      bad += (a.first->second != fb) + (b.first->second != fr);
+    }
+    std::printf("{\"symcheck\": [%zu, %zu, %zu, %lld]}\n", all.size(), r2b.size(), b2r.size(), bad);
+    return 0;
+  }
   std::printf("{\"generated\": %lld, \"distinct\": %zu, \"depth\": %d, \"left_on_queue\": %lld, \"err\": %u, \"verdict\": \"%s\", "
               "\"violated\": \"%s\", \"actions\": {",
               generated, seen.size(), depth, left, err, verdict.c_str(), violated.c_str());

@@ -68,3 +68,17 @@ def test_packed_membership_first_violation(case):
                                   capture_output=True, text=True, check=True).stdout)
     assert (r["verdict"], r["violated"], r["depth"], r["generated"], r["distinct"], r["left_on_queue"]) == \
         (g["verdict"], g["violated"], g["depth"], g["generated"], g["distinct"], g["left_on_queue"])
+
+
+def test_refined_symmetric_fingerprint_equals_brute_force_orbits():
+    """The GPU's symmetric fingerprint hashes only the permutations that respect the servers'
+    invariant signatures (memb_spec.h fingerprint, partition refinement).  On every distinct state
+    of the 4-server model without SYMMETRY to depth 15 (all symmetric copies kept, >= 1e5 states),
+    it must induce exactly the partition of the brute-force min over all 4! permuted views: same
+    number of classes, and no refined class maps to two brute-force classes or vice versa."""
+    exe = build_harness((4, 2))
+    r = json.loads(subprocess.run([exe, os.path.join(CONFIGS, "memb_four_nosym.cfg"), "15"], capture_output=True,
+                                  text=True, check=True, env=dict(os.environ, SYMCHECK="1")).stdout)
+    states, refined, brute, bad = r["symcheck"]
+    assert states >= 100000 and bad == 0 and refined == brute, r
+    assert refined < states / 4      # symmetry really merges (24 permutations)
