@@ -59,6 +59,11 @@ extern "C" {
 
 /* tlc_compat_flags: the [ext] TLC-semantics switches */
 #define MC_COMPAT_INV_OUT_OF_MODEL 0x1u /* check invariants on !seen successors that fail a constraint (TLC default) */
+/* SYMMETRY as TLC applies it (TLCStateMut.fingerPrint): the permutation giving the least full
+ * variable tuple (history included) under TLC's value order, then the VIEW of that state; without
+ * it SYMMETRY + VIEW identify states whose VIEWs lie in one orbit (faster; fewer distinct states
+ * when histories differ).  tlc_membership only. */
+#define MC_COMPAT_SYM_TLC 0x2u
 
 typedef struct mc_ctx mc_ctx;
 

@@ -104,6 +104,7 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
   c->ro.max_depth = o->max_depth;
   c->ro.seed = o->seed;
   c->ro.inv_out_of_model = (o->tlc_compat_flags & MC_COMPAT_INV_OUT_OF_MODEL) != 0;
+  c->ro.sym_tlc = (o->tlc_compat_flags & MC_COMPAT_SYM_TLC) != 0;
   c->ro.check_deadlock = o->check_deadlock != 0;
   c->ro.block_size = o->block_size ? o->block_size : 256;
   c->ro.workers = o->workers;

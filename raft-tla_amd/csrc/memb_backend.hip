@@ -96,7 +96,7 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
       bool need = false, oom = false;
       if (active) {
         W t;
-        const int act = S::apply(s, k, sub, t, err, a.rt);
+        const int act = S::template apply<false>(s, k, sub, t, err, a.rt);
         if (act >= 0) {
           ++nsucc;
           atomicAdd(&lds_cnt[act], 1u);
@@ -184,7 +184,8 @@ __global__ void __launch_bounds__(BS) memb_expand(MGenArgs a) {
 
 // Phase 2: one lane per in-model successor (full lanes): re-derive it and store its
 // symmetric FP64 into its cell (cand[slot][state]).
-template <class S>
+// TLC = MC_COMPAT_SYM_TLC (a kernel of its own, so the orbit mode keeps its registers).
+template <class S, bool TLC>
 __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
   using W = typename S::Work;
   constexpr int NWP = S::NWP;
@@ -202,8 +203,8 @@ __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
   W s, t;
   S::unpack(w, s);
   u32 err = 0;
-  S::apply(s, k, sub, t, err, a.rt);
-  a.cand[cell] = S::fingerprint(t, a.seed, a.rt);
+  S::template apply<TLC>(s, k, sub, t, err, a.rt);
+  a.cand[cell] = TLC ? S::fingerprint_tlc(t, a.seed, a.rt) : S::fingerprint_orbit(t, a.seed, a.rt);
   }
 }
 
@@ -227,7 +228,7 @@ __global__ void __launch_bounds__(BS) memb_oom_check(MGenArgs a) {
   W s, t;
   S::unpack(w, s);
   u32 err = 0;
-  S::apply(s, k, sub, t, err, a.rt);
+  S::template apply<false>(s, k, sub, t, err, a.rt);
   const u32 r = S::check_invariants(t, a.rt);
   if (r) {
     const u64 e = (((a.rank0 + st) * (u64)S::NSLOT + slot) << 2) | ((r >> 8) == IV_BAD ? EV_VIOLATION : EV_INV_ERROR);
@@ -371,7 +372,7 @@ struct MMatArgs {
   unsigned long long* ctr;
 };
 
-template <class S>
+template <class S, bool TLC>
 __global__ void __launch_bounds__(BS) memb_materialize(MMatArgs a) {
   using W = typename S::Work;
   constexpr int NW = S::NW, NWP = S::NWP;
@@ -392,7 +393,7 @@ __global__ void __launch_bounds__(BS) memb_materialize(MMatArgs a) {
     for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
     W s, t;
     S::unpack(w, s);
-    const int act = S::apply(s, k, sub, t, err, a.rt);
+    const int act = S::template apply<TLC>(s, k, sub, t, err, a.rt);
     const u64 dst = a.dst_base + i;
     if (act >= 0 && dst < a.cap) {
       u32 pw[NW];
@@ -747,6 +748,7 @@ class MembGpu : public Backend {
       }
     if (int rc = ensure_alloc(o, err)) return rc;
     if (int rc = prepare_prefixes(err)) return rc;
+    rt_host_.sym_tlc = rt_dev_.sym_tlc = (o.sym_tlc && m_.rt.symmetry) ? 1u : 0u;
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
@@ -821,7 +823,8 @@ class MembGpu : public Backend {
         if (o.inv_out_of_model) hipLaunchKernelGGL((memb_oom_check<S>), dim3(nblk), dim3(BS), 0, stream_, g);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ev_[0], stream_));
-        hipLaunchKernelGGL((memb_fingerprint<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+        if (rt_dev_.sym_tlc) hipLaunchKernelGGL((memb_fingerprint<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
+        else hipLaunchKernelGGL((memb_fingerprint<S, false>), dim3(nblk), dim3(BS), 0, stream_, g);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ev_[1], stream_));
         hipLaunchKernelGGL(memb_dedup, dim3((unsigned)((nslots + BS * DPER - 1) / (BS * DPER))), dim3(BS), 0, stream_, d);
@@ -846,7 +849,8 @@ class MembGpu : public Backend {
           m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.n_new = nnew; m.dst_base = next_write; m.cap = cap_;
           m.level_begin = level_begin; m.gid_tag = 0; m.rt = rt_dev_; m.ctr = (unsigned long long*)d_ctr_;
           HIPCHK(hipEventRecord(ev_[5], stream_));
-          hipLaunchKernelGGL((memb_materialize<S>), dim3((unsigned)((nnew + BS - 1) / BS)), dim3(BS), 0, stream_, m);
+          if (rt_dev_.sym_tlc) hipLaunchKernelGGL((memb_materialize<S, true>), dim3((unsigned)((nnew + BS - 1) / BS)), dim3(BS), 0, stream_, m);
+          else hipLaunchKernelGGL((memb_materialize<S, false>), dim3((unsigned)((nnew + BS - 1) / BS)), dim3(BS), 0, stream_, m);
           HIPCHK(hipGetLastError());
           HIPCHK(hipEventRecord(ev_[6], stream_));
           HIPCHK(hipEventSynchronize(ev_[6]));
@@ -1006,6 +1010,7 @@ class MembGpu : public Backend {
     }
     if (int rc = ensure_alloc(so, err)) return rc;
     if (int rc = prepare_prefixes(err)) return rc;
+    rt_host_.sym_tlc = rt_dev_.sym_tlc = (o.sym_tlc && m_.rt.symmetry) ? 1u : 0u;
     sopts_ = o; s_rank_ = rank; s_world_ = world; s_finished_ = false; have_viol_ = false; sres_err_ = 0; sharded_ = true;
     // level records / sorted winners / newrec: lvl_cap_ entries each, plus the sort's scratch
     const u64 sb = so.state_store_bytes;
@@ -1101,7 +1106,8 @@ class MembGpu : public Backend {
     if (sopts_.inv_out_of_model) hipLaunchKernelGGL((memb_oom_check<S>), dim3(nblk), dim3(BS), 0, stream_, g);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev_[1], stream_));
-    hipLaunchKernelGGL((memb_fingerprint<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+    if (rt_dev_.sym_tlc) hipLaunchKernelGGL((memb_fingerprint<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
+        else hipLaunchKernelGGL((memb_fingerprint<S, false>), dim3(nblk), dim3(BS), 0, stream_, g);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev_[2], stream_));
     HIPCHK(hipMemcpyAsync(d_nsucc_lvl_ + gen_begin_, d_nsucc_, cnt * 2, hipMemcpyDeviceToDevice, stream_));
@@ -1210,7 +1216,8 @@ class MembGpu : public Backend {
     m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_lvl_; m.n_new = n; m.dst_base = total_; m.cap = cap_;
     m.level_begin = s_level_begin_ - s_B_;   // gid - level_begin = global rank (mod 2^64)
     m.gid_tag = (u64)s_rank_ << 37; m.rt = rt_dev_; m.ctr = (unsigned long long*)d_ctr_;
-    hipLaunchKernelGGL((memb_materialize<S>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, m);
+    if (rt_dev_.sym_tlc) hipLaunchKernelGGL((memb_materialize<S, true>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, m);
+    else hipLaunchKernelGGL((memb_materialize<S, false>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, m);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev_[6], stream_));
     HIPCHK(hipEventSynchronize(ev_[6]));

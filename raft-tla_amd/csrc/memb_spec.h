@@ -110,6 +110,7 @@ struct MembRuntime {
   const u64* ptab1;
   u32 plen0, plen1;
   u32 preg1_off;            // h1 bit offset of region 1's dead-binding mask
+  u32 sym_tlc;              // SYMMETRY in TLC's mode (MC_COMPAT_SYM_TLC): least permuted full state, then VIEW
 };
 
 // ------------------------------------------------------------------ small constexpr tables
@@ -163,8 +164,9 @@ struct Memb {
                        G_RECV = G_AE + N * N, G_TO = G_RECV + MK, G_RS = G_TO + N, G_DUP = G_RS + N, G_DROP = G_DUP + MK,
                        G_ADD = G_DROP + MK, G_DEL = G_ADD + N * N, NI = G_DEL + N * N;
   static constexpr int NSLOT = NI + MK;             // (instance, successor) slots; Receive has 2
-  // ---- stored (packed) layout, u32 words: term st voted commit vr vg | nexti(2) matchi(2) | logs(2N) | h0(2) h1(2) | bag(2MK)
-  static constexpr int NW = 6 + 4 + 2 * N + 4 + 2 * MK;
+  // ---- stored (packed) layout, u32 words: term st voted commit vr vg | nexti(2) matchi(2) | logs(2N) | h0(2) h1(2) |
+  //      hr0(2) hr1(2) | bag(2MK)
+  static constexpr int NW = 6 + 4 + 2 * N + 4 + 4 + 2 * MK;
   static constexpr int NWP = (NW + 3) & ~3;
 
   static_assert(N >= 1 && N <= 4, "1..4 servers");
@@ -180,6 +182,7 @@ struct Memb {
     Arr<u64, N> la;                        // log entries 0..7 (EW bits each)
     Arr<u32, N> lb;                        // entries 8..9 | length << 16
     u64 h0, h1;                            // history summary (see below)
+    u64 hr0, hr1;                          // TLC-mode symmetry: ranks of the permuted histories (see below)
     Arr<u64, MK + 1> bag;                  // sorted (code << CNTB | count), EMPTY = ~0
   };
   static constexpr u32 F = 0, C = 1, L = 2;   // Follower, Candidate, Leader
@@ -498,10 +501,11 @@ struct Memb {
   }
   // The entries this successor appended (Delta.hk), at positions glen(s), glen(s)+1, against
   // every enabled prefix region.
-  RMC_HD static void prefix_step(const Work& s, Work& t, const Delta& d, const MembRuntime& rt) {
+  // the (x, y) codes of the 0, 1 or 2 entries a successor appended
+  RMC_HD static int appended_entries(const Delta& d, u64& x0, u64& y0, u64& x1, u64& y1) {
     const u32 hk = d.hk & 15u;
-    if (hk == HK_NONE) return;
-    u64 x0, y0 = 0, x1 = 0, y1 = 0;
+    x0 = 0; y0 = 0; x1 = 0; y1 = 0;
+    if (hk == HK_NONE) return 0;
     int n = 1;
     if (hk == HK_SEND) {
       const int c = mcls(d.add), src = msg_src(d.add);
@@ -518,6 +522,12 @@ struct Memb {
       if (hk == HK_REPLY) { x1 = hx(HE_SEND, msg_src(d.add), 0); y1 = d.add; n = 2; }
       if (hk == HK_DISCARD_MC) { x1 = hx((d.hk >> 4) & 1u ? HE_ADD : HE_REM, msg_dst(d.rem), d.hk >> 5); n = 2; }
     }
+    return n;
+  }
+  RMC_HD static void prefix_step(const Work& s, Work& t, const Delta& d, const MembRuntime& rt) {
+    u64 x0, y0, x1, y1;
+    const int n = appended_entries(d, x0, y0, x1, y1);
+    if (n == 0) return;
     const int p = glen(s);
     if (rt.plen0) {
       u64 dead = (t.h1 >> H_PREFIX) & NBMASK;
@@ -540,7 +550,7 @@ struct Memb {
   RMC_HD static void launder(Work& s) {
 #if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+v"(s.term), "+v"(s.st), "+v"(s.voted), "+v"(s.commit), "+v"(s.vr), "+v"(s.vg));
-    asm volatile("" : "+v"(s.nexti), "+v"(s.matchi), "+v"(s.h0), "+v"(s.h1));
+    asm volatile("" : "+v"(s.nexti), "+v"(s.matchi), "+v"(s.h0), "+v"(s.h1), "+v"(s.hr0), "+v"(s.hr1));
 #pragma unroll
     for (int i = 0; i < N; ++i) asm volatile("" : "+v"(s.la.v[i]), "+v"(s.lb.v[i]));
 #pragma unroll
@@ -556,7 +566,7 @@ struct Memb {
     s.nexti = fsplat<IB, u64>(1, N * N); s.matchi = 0;
 #pragma unroll
     for (int i = 0; i < N; ++i) { s.la.v[i] = 0; s.lb.v[i] = 0; }
-    s.h0 = 0; s.h1 = 0;
+    s.h0 = 0; s.h1 = 0; s.hr0 = 0; s.hr1 = 0;
 #pragma unroll
     for (int k = 0; k < MK + 1; ++k) s.bag.v[k] = EMPTY;
   }
@@ -578,7 +588,9 @@ struct Memb {
   RMC_HD static int nsub(int k) { return (k >= G_RECV && k < G_TO) ? 2 : 1; }
 
   // The sub-th successor of instance k of s into t (t = s on entry is not assumed).
-  // Returns its MembAct, or -1 when it does not exist.
+  // Returns its MembAct, or -1 when it does not exist.  HR = false: the TLC-mode history ranks of
+  // t are left unrefined (kernels that never fingerprint or store t: no code for it).
+  template <bool HR = true>
   RMC_HD static int apply(const Work& s, int k, int sub, Work& t, u32& err, const MembRuntime& rt) {
     t = s;
     Delta d{0, 0, HK_NONE, false, false};
@@ -587,6 +599,7 @@ struct Memb {
       if (d.a) with_msg(t.bag, d.add, err);
       if (d.r) without_msg(t.bag, d.rem);
       if (rt.plen0 | rt.plen1) prefix_step(s, t, d, rt);
+      if (HR && rt.sym_tlc) tlc_refine(s, t, d, rt.cfg_type);
     }
     return act;
   }
@@ -1318,7 +1331,10 @@ struct Memb {
   // s those are exactly the signature-respecting permutations of s composed with pi^-1, so the
   // minimum runs over the same set of permuted views: canonical, and usually over one
   // permutation instead of N!.  Without SYMMETRY: the identity.
-  RMC_HD static u64 fingerprint(const Work& t, u64 seed, const MembRuntime& rt) {
+  RMC_HD static u64 fingerprint(const Work& t, u64 seed, const MembRuntime& rt) {   // host entry: either mode
+    return (rt.symmetry && rt.sym_tlc) ? fingerprint_tlc(t, seed, rt) : fingerprint_orbit(t, seed, rt);
+  }
+  RMC_HD static u64 fingerprint_orbit(const Work& t, u64 seed, const MembRuntime& rt) {
     const bool ce = has_config_entries(t, rt.cfg_type);
     u64 best;
     if (!rt.symmetry) {
@@ -1372,6 +1388,192 @@ struct Memb {
     return fp ? fp : 1ull;
   }
 
+  // ------------------------------------------------------------ TLC-mode symmetry (MC_COMPAT_SYM_TLC)
+  // TLC's rule ([ext], oracle/engine.h canon_key "tlc"): of the N! permuted states take the one
+  // whose variable tuple, in declaration order (raft.tla:114-185: messages, history, currentTerm,
+  // state, votedFor, log, commitIndex, votesResponded, votesGranted, nextIndex, matchIndex), is
+  // least under TLC's value order (oracle tla.h cmp), then fingerprint its VIEW.  Unlike the orbit
+  // mode this depends on history, which is not stored; what the comparison needs of it is: the
+  // order of the permuted history["global"] sequences of THIS state (kept as hr0/hr1, a
+  // competition rank per permutation, refined by every appended entry; a flag marks it discrete,
+  // after which appends cannot change it), the permutation-invariant counters, and the per-server
+  // [restarted, timeout] record (h0).
+  static constexpr int RKB = NPERM <= 2 ? 1 : bits_for(NPERM - 1);   // bits per rank
+  static constexpr int RPW = 60 / RKB;                                // ranks per word (bits 60..63 free)
+  static_assert(NPERM <= 2 * RPW, "history ranks fit hr0/hr1");
+  static constexpr u64 HR_DISCRETE = 1ull << 63;                     // in hr1: all ranks distinct
+  RMC_HD static u32 hrank(const Work& t, int p) {
+    return (u32)(((p < RPW ? t.hr0 : t.hr1) >> (RKB * (p < RPW ? p : p - RPW))) & lomask(RKB));
+  }
+  RMC_HD static int pinv(u32 pi, int s) {   // the server pi maps to s
+    int r = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r = pi_of(pi, i) == s ? i : r;
+    return r;
+  }
+  // a message code with every server-valued field renamed by pi (and config values inside its
+  // log / entry when ce); order preserving like the code itself
+  RMC_HD static u64 perm_code(u64 c, u32 pi, bool ce, u32 cfgt) {
+    const u64 dp = mdesc_packed(mcls(c));
+    const int od = (int)(dp & 127), os = (int)((dp >> 7) & 127), ov = (int)((dp >> 21) & 127);
+    const int sd = CODEB - od - SB, ss = CODEB - os - SB, sv = CODEB - ov - SB;
+    u64 x = c & ~(lomask(SB) << sd) & ~(lomask(SB) << ss);
+    if (ov) x &= ~(lomask(SB) << sv);
+    if (ce) x = perm_entries(x, pi, cfgt);
+    x |= (u64)pi_of(pi, (int)((c >> sd) & lomask(SB))) << sd | (u64)pi_of(pi, (int)((c >> ss) & lomask(SB))) << ss;
+    if (ov) x |= (u64)pi_of(pi, (int)((c >> sv) & lomask(SB))) << sv;
+    return x;
+  }
+  // Order key of pi(e) among the permutations of one history entry e = (x, y) (prefix_step's
+  // codes): the entry record's server-valued fields in field-name order (records compare field
+  // by field in name order; the invariant fields tie).
+  RMC_HD static u64 entry_key(u64 x, u64 y, u32 pi, u32 cfgt) {
+    const int kind = (int)(x & 15u), ex = pi_of(pi, (int)((x >> 4) & 15u));
+    const u32 aux = (u32)(x >> 8);
+    switch (kind) {
+      case HE_SEND: case HE_RECV: return (u64)ex << CODEB | perm_code(y, pi, true, cfgt);   // action, executedOn, msg
+      case HE_TRYADD: case HE_ADD: return (u64)pi_of(pi, (int)aux) << 2 | (u64)ex;           // action, added, executedOn
+      case HE_TRYREM: case HE_REM: return (u64)ex << 2 | (u64)pi_of(pi, (int)aux);           // action, executedOn, removed
+      case HE_BL: return (u64)ex << 4 | m2r(pmask(aux, pi));                                 // action, executedOn, leaders
+      case HE_CE: return (u64)pentry(aux, pi, cfgt) << 2 | (u64)ex;                           // action, entry, executedOn
+      case HE_CMC: return (u64)m2r(pmask(aux, pi)) << 2 | (u64)ex;                           // action, config, executedOn
+      default: return (u64)ex;                                                               // Restart, Timeout
+    }
+  }
+  // refine the history ranks by the entries this successor appended (apply).  Runtime loops and
+  // keys recomputed on the fly: small code in every kernel that inlines apply, no scratch arrays
+  // (the work only happens while the ranks are not yet discrete, i.e. in the first few levels).
+  RMC_HD static void tlc_refine(const Work& s, Work& t, const Delta& d, u32 cfgt) {
+    (void)s;
+    u64 x[2], y[2];
+    const int n = appended_entries(d, x[0], y[0], x[1], y[1]);
+#pragma unroll 1
+    for (int e = 0; e < n && !(t.hr1 & HR_DISCRETE); ++e) {
+      const u64 xe = e ? x[1] : x[0], ye = e ? y[1] : y[0];
+      u64 w0 = 0, w1 = 0;
+      bool distinct = true;
+#pragma unroll 1
+      for (int p = 0; p < NPERM; ++p) {
+        const u32 rp = hrank(t, p);
+        const u64 kp = entry_key(xe, ye, perm_of(p), cfgt);
+        u32 r = 0;
+#pragma unroll 1
+        for (int q = 0; q < NPERM; ++q) {
+          const u32 rq = hrank(t, q);
+          if (rq > rp) continue;
+          const u64 kq = entry_key(xe, ye, perm_of(q), cfgt);
+          r += (rq < rp || kq < kp) ? 1u : 0u;
+          distinct &= q == p || rq != rp || kq != kp;
+        }
+        if (p < RPW) w0 |= (u64)r << (RKB * p); else w1 |= (u64)r << (RKB * (p - RPW));
+      }
+      t.hr0 = w0; t.hr1 = w1 | (distinct ? HR_DISCRETE : 0ull);
+    }
+  }
+  // keep, among the candidate permutations, those whose key (p, pi) is least
+  template <class F>
+  RMC_HD static u32 keep_min(u32 cand, F key) {
+    u64 best = ~0ull;
+#pragma unroll 1
+    for (int p = 0; p < NPERM; ++p)
+      if ((cand >> p) & 1u) { const u64 k = key(p, perm_of(p)); best = k < best ? k : best; }
+    u32 out = 0;
+#pragma unroll 1
+    for (int p = 0; p < NPERM; ++p)
+      if (((cand >> p) & 1u) && key(p, perm_of(p)) == best) out |= 1u << p;
+    return out;
+  }
+  RMC_HD static bool single(u32 cand) { return (cand & (cand - 1u)) == 0u; }
+  RMC_HD static u64 next_perm_code(const Work& t, int len, u32 pi, bool ce, u32 cfgt, bool have_last, u64 last) {
+    u64 best = ~0ull;   // the least permuted message code above `last`
+#pragma unroll 1
+    for (int q = 0; q < len; ++q) {
+      const u64 c = perm_code(mcode(sel(t.bag, q)), pi, ce, cfgt);
+      if ((!have_last || c > last) && c < best) best = c;
+    }
+    return best;
+  }
+  // the permutation TLC picks: least permuted variable tuple, variable by variable
+  RMC_HD static u32 tlc_min_perm(const Work& t, bool ce, u32 cfgt) {
+    u32 cand = (u32)lomask(NPERM);
+    // messages: a function from message records to counts (oracle Fcn order: DOMAIN size — equal
+    // for all — then the domain elements ascending, then the counts in domain order)
+    int len = 0;
+#pragma unroll 1
+    for (int q = 0; q < MK; ++q) len += sel(t.bag, q) != EMPTY;
+    u64 last = 0;
+    bool have_last = false;
+#pragma unroll 1
+    for (int j = 0; j < len && !single(cand); ++j) {
+      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(t, len, pi, ce, cfgt, have_last, last); });
+      last = next_perm_code(t, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+      have_last = true;
+    }
+    have_last = false;
+#pragma unroll 1
+    for (int j = 0; j < len && !single(cand); ++j) {   // same permuted domain: the counts in domain order
+      const u64 code = next_perm_code(t, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+      cand = keep_min(cand, [&](int, u32 pi) {
+        u64 cnt = 0;
+#pragma unroll 1
+        for (int q = 0; q < len; ++q)
+          if (perm_code(mcode(sel(t.bag, q)), pi, ce, cfgt) == code) cnt = (u64)mcount(sel(t.bag, q));
+        return cnt;
+      });
+      last = code; have_last = true;
+    }
+    // history: [global, hadNum* (invariant), server]: the rank of the permuted global sequence,
+    // then server[x] = [restarted, timeout] of the server mapped to x
+    if (!single(cand)) cand = keep_min(cand, [&](int p, u32) { return (u64)hrank(t, p); });
+#pragma unroll 1
+    for (int x = 0; x < N && !single(cand); ++x)
+      cand = keep_min(cand, [&](int, u32 pi) { const int i = pinv(pi, x); return (u64)restarted(t, i) << 8 | (u64)timeouts(t, i); });
+    // currentTerm, state ("Candidate" < "Follower" < "Leader"), votedFor (Nil = 0 sorts before
+    // the servers), log (length, then entries), commitIndex, votesResponded, votesGranted (sets:
+    // cardinality, then elements), nextIndex, matchIndex — each a function over the servers
+#pragma unroll 1
+    for (int x = 0; x < N && !single(cand); ++x)
+      cand = keep_min(cand, [&](int, u32 pi) { return (u64)g_term(t, pinv(pi, x)); });
+#pragma unroll 1
+    for (int x = 0; x < N && !single(cand); ++x)
+      cand = keep_min(cand, [&](int, u32 pi) { const int st = g_st(t, pinv(pi, x)); return (u64)(st == (int)C ? 0 : st == (int)F ? 1 : 2); });
+#pragma unroll 1
+    for (int x = 0; x < N && !single(cand); ++x)
+      cand = keep_min(cand, [&](int, u32 pi) { const int v = g_voted(t, pinv(pi, x)); return (u64)(v == N ? 0 : 1 + pi_of(pi, v)); });
+#pragma unroll 1
+    for (int x = 0; x < N && !single(cand); ++x)
+#pragma unroll 1
+      for (int pos = -1; pos < MAXLOG && !single(cand); ++pos)
+        cand = keep_min(cand, [&](int, u32 pi) {
+          const LogV l = getlog(t, pinv(pi, x));
+          if (pos < 0) return (u64)llen(l);
+          return pos < llen(l) ? (u64)pentry(lent(l, pos), pi, cfgt) : (u64)0;
+        });
+#pragma unroll 1
+    for (int x = 0; x < N && !single(cand); ++x)
+      cand = keep_min(cand, [&](int, u32 pi) { return (u64)g_commit(t, pinv(pi, x)); });
+#pragma unroll 1
+    for (int x = 0; x < 2 * N && !single(cand); ++x)
+      cand = keep_min(cand, [&](int, u32 pi) {
+        const int i = pinv(pi, x < N ? x : x - N);
+        return (u64)m2r(pmask(x < N ? g_vr(t, i) : g_vg(t, i), pi));
+      });
+#pragma unroll 1
+    for (int xy = 0; xy < 2 * N * N && !single(cand); ++xy)
+      cand = keep_min(cand, [&](int, u32 pi) {
+        const int z = xy < N * N ? xy : xy - N * N, i = pinv(pi, z / N), j = pinv(pi, z % N);
+        return (u64)(xy < N * N ? g_next(t, i, j) : g_match(t, i, j));
+      });
+    return perm_of(__builtin_ctz(cand));   // any remaining tie: identical permuted states
+  }
+  RMC_HD static u64 fingerprint_tlc(const Work& t, u64 seed, const MembRuntime& rt) {
+    const bool ce = has_config_entries(t, rt.cfg_type);
+    const u32 pi = tlc_min_perm(t, ce, rt.cfg_type);
+    const u64 best = ce ? view_hash1<true>(t, pi, seed, rt.cfg_type) : view_hash1<false>(t, pi, seed, rt.cfg_type);
+    const u64 fp = fmix(best ^ seed);
+    return fp ? fp : 1ull;
+  }
+
   // ------------------------------------------------------------ pack / unpack (word aligned)
   RMC_HD static u64 log_store(LogV l) { return (l.a & lomask(MAXLOG * EW)) | ((u64)llen(l) << 60); }
   RMC_HD static LogV log_load(u64 w) { return LogV{w & lomask(MAXLOG * EW), (u32)(w >> 60) << 16}; }
@@ -1381,10 +1583,11 @@ struct Memb {
 #pragma unroll
     for (int i = 0; i < N; ++i) { const u64 x = log_store(LogV{t.la.v[i], t.lb.v[i]}); w[10 + 2 * i] = (u32)x; w[11 + 2 * i] = (u32)(x >> 32); }
     w[10 + 2 * N] = (u32)t.h0; w[11 + 2 * N] = (u32)(t.h0 >> 32); w[12 + 2 * N] = (u32)t.h1; w[13 + 2 * N] = (u32)(t.h1 >> 32);
+    w[14 + 2 * N] = (u32)t.hr0; w[15 + 2 * N] = (u32)(t.hr0 >> 32); w[16 + 2 * N] = (u32)t.hr1; w[17 + 2 * N] = (u32)(t.hr1 >> 32);
 #pragma unroll
     for (int q = 0; q < MK; ++q) {
       const u64 x = t.bag.v[q] == EMPTY ? 0ull : t.bag.v[q];
-      w[14 + 2 * N + 2 * q] = (u32)x; w[15 + 2 * N + 2 * q] = (u32)(x >> 32);
+      w[18 + 2 * N + 2 * q] = (u32)x; w[19 + 2 * N + 2 * q] = (u32)(x >> 32);
     }
   }
   template <int M>
@@ -1395,9 +1598,10 @@ struct Memb {
 #pragma unroll
     for (int i = 0; i < N; ++i) { const LogV l = log_load((u64)w[10 + 2 * i] | (u64)w[11 + 2 * i] << 32); t.la.v[i] = l.a; t.lb.v[i] = l.b; }
     t.h0 = (u64)w[10 + 2 * N] | (u64)w[11 + 2 * N] << 32; t.h1 = (u64)w[12 + 2 * N] | (u64)w[13 + 2 * N] << 32;
+    t.hr0 = (u64)w[14 + 2 * N] | (u64)w[15 + 2 * N] << 32; t.hr1 = (u64)w[16 + 2 * N] | (u64)w[17 + 2 * N] << 32;
 #pragma unroll
     for (int q = 0; q < MK; ++q) {
-      const u64 x = (u64)w[14 + 2 * N + 2 * q] | (u64)w[15 + 2 * N + 2 * q] << 32;
+      const u64 x = (u64)w[18 + 2 * N + 2 * q] | (u64)w[19 + 2 * N + 2 * q] << 32;
       t.bag.v[q] = x ? x : EMPTY;
     }
     t.bag.v[MK] = EMPTY;

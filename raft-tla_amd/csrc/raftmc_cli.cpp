@@ -35,6 +35,12 @@ int main(int argc, char** argv) {
     else if (k == "-store") o.state_store_bytes = std::strtoull(val(), nullptr, 10);
     else if (k == "-seed") o.seed = std::strtoull(val(), nullptr, 0);
     else if (k == "-no-inv-oom") o.tlc_compat_flags &= ~MC_COMPAT_INV_OUT_OF_MODEL;
+    else if (k == "-symmetry") {   // "tlc": TLC's least-permuted-state rule; "orbit" (default)
+      const std::string v = val();
+      if (v == "tlc") o.tlc_compat_flags |= MC_COMPAT_SYM_TLC;
+      else if (v == "orbit") o.tlc_compat_flags &= ~MC_COMPAT_SYM_TLC;
+      else { std::fprintf(stderr, "-symmetry tlc|orbit\n"); return 2; }
+    }
     else if (k == "-dump") dump = val();
     else if (k == "-json") json = true;
     else if (k == "-checkpoint") ckpt_every = std::atoi(val());

@@ -20,6 +20,7 @@ ABI_VERSION = 1
 
 VERDICTS = {0: "OK", 1: "INVARIANT_VIOLATION", 2: "EVAL_ERROR", 3: "CAPACITY_OVERFLOW", 4: "DEADLOCK", 5: "DEPTH_LIMIT"}
 MC_COMPAT_INV_OUT_OF_MODEL = 0x1
+MC_COMPAT_SYM_TLC = 0x2
 
 # every symbol include/raftmc.h declares
 EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stats", "mc_level_stats", "mc_kernel_stats",
@@ -135,7 +136,7 @@ class ModelChecker:
     """One raftmc handle: mc_open on construction, mc_run in run()."""
 
     def __init__(self, spec, config=None, workers=1, deadlock=True, device=0, max_depth=0,
-                 fp_table_bytes=0, state_store_bytes=0, seed=0, inv_out_of_model=True):
+                 fp_table_bytes=0, state_store_bytes=0, seed=0, inv_out_of_model=True, sym_tlc=False):
         self.lib = load_library()
         if config is None:
             config = spec[:-4] + ".cfg" if spec.endswith(".tla") else spec + ".cfg"
@@ -144,7 +145,7 @@ class ModelChecker:
         o.device, o.workers, o.max_depth = device, workers, max_depth
         o.fp_table_bytes, o.state_store_bytes, o.seed = fp_table_bytes, state_store_bytes, seed
         o.check_deadlock = 1 if deadlock else 0
-        o.tlc_compat_flags = MC_COMPAT_INV_OUT_OF_MODEL if inv_out_of_model else 0
+        o.tlc_compat_flags = (MC_COMPAT_INV_OUT_OF_MODEL if inv_out_of_model else 0) | (MC_COMPAT_SYM_TLC if sym_tlc else 0)
         self.h = ctypes.c_void_p()
         rc = self.lib.mc_open(spec.encode(), config.encode(), ctypes.byref(o), ctypes.byref(self.h))
         if rc:

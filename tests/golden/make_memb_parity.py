@@ -54,6 +54,13 @@ CASES = {
     "scen_AddSucessful": ("scen_AddSucessful", 0),
     "scen_MembershipChangeCommits": ("scen_MembershipChangeCommits", 0),
     "scen_AddCommits": ("scen_AddCommits", 0),
+    # SYMMETRY in TLC's mode (oracle --sym tlc, MC_COMPAT_SYM_TLC): least permuted full state, then VIEW
+    "tlc:membership_shipped@16": ("membership_shipped", 16),
+    "tlc:memb_two@16": ("memb_two", 16),
+    "tlc:memb_dynamic3@14": ("memb_dynamic3", 14),
+    "tlc:memb_four@13": ("memb_four", 13),
+    "tlc:scen_FirstCommit": ("scen_FirstCommit", 0),
+    "tlc:punct_MajorityOfClusterRestarts@30": ("scen_MajorityOfClusterRestarts_punct", 30, "MajorityOfClusterRestarts_constraint"),
 }
 OUT = os.path.join(GOLDEN, "memb_parity.json")
 
@@ -70,7 +77,8 @@ def main(names, out=OUT):
         prefix = CASES[n][2] if len(CASES[n]) > 2 else None
         fd, dump = tempfile.mkstemp(suffix=".txt")
         os.close(fd)
-        args = ["--sym", "view", "--dump", dump, "--trace"]
+        sym = "tlc" if n.startswith("tlc:") else "view"
+        args = ["--sym", sym, "--dump", dump, "--trace"]
         if prefix:
             flag, fixture = PREFIXES[prefix]
             args += [flag, golden_file(fixture)[0]]
@@ -80,7 +88,7 @@ def main(names, out=OUT):
         assert r["verdict"] in ("OK", "INVARIANT_VIOLATION"), r
         sha, cnt = digest_lines(dump)
         os.unlink(dump)
-        doc[n] = {"cfg": cfg, "max_depth": depth, "verdict": r["verdict"], "violated": r["violated"],
+        doc[n] = {"cfg": cfg, "max_depth": depth, "sym": sym, "verdict": r["verdict"], "violated": r["violated"],
                   "prefix": [prefix, PREFIXES[prefix][1]] if prefix else None,
                   "generated": r["generated"], "distinct": r["distinct"], "depth": r["depth"],
                   "left_on_queue": r["left_on_queue"], "levels": r["levels"], "actions": r["actions"],

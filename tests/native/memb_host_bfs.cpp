@@ -6,6 +6,7 @@
 // Shape: -DSHAPE_N=.. -DSHAPE_NV=..
 //   memb_host_bfs CFG MAX_DEPTH [DUMP|-] [--prefix CONSTRAINT TRACE_FILE]...
 //     -> JSON {generated, distinct, depth, left_on_queue, verdict, actions}
+// SYM_TLC=1 (environment): TLC-mode symmetry (the oracle's --sym tlc), as MC_COMPAT_SYM_TLC.
 // SYMCHECK=1 (environment): for every distinct state of the search (run it on a cfg WITHOUT
 // SYMMETRY, so symmetric copies are all kept), compare the product's refined symmetric fingerprint
 // (S::fingerprint with symmetry on: min over the signature-respecting permutations only) with the
@@ -32,6 +33,7 @@ int main(int argc, char** argv) {
   FILE* dump = argc > 3 && std::string(argv[3]) != "-" ? std::fopen(argv[3], "w") : nullptr;
   MembText<S> text(m);
   MembRuntime rt = m.rt;
+  if (std::getenv("SYM_TLC") && rt.symmetry) rt.sym_tlc = 1;   // MC_COMPAT_SYM_TLC
   // punctuated-search prefixes, laid out as the GPU backend does (memb_backend.hip prepare_prefixes)
   std::vector<u64> tabs[2];
   u32 off = S::H_PREFIX;

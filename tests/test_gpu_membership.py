@@ -30,8 +30,9 @@ VIOLATIONS = sorted(k for k, v in FIX.items() if v["verdict"] == "INVARIANT_VIOL
 
 def open_case(raftmc, g, **kw):
     """A handle for a fixture case; punctuated-search cases get their golden history trace
-    (the committed TLC trace fixture) through mc_set_history_prefix."""
-    mc = raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), **kw)
+    (the committed TLC trace fixture) through mc_set_history_prefix; "tlc:" cases run SYMMETRY in
+    TLC's mode (MC_COMPAT_SYM_TLC, the oracle's --sym tlc)."""
+    mc = raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), sym_tlc=g.get("sym") == "tlc", **kw)
     if g.get("prefix"):
         con, fixture = g["prefix"]
         mc.set_history_prefix(con, tla_text(json.load(open(os.path.join(GOLDEN, fixture)))["value"]))

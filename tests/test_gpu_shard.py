@@ -195,7 +195,7 @@ def _memb_worker(rank, world, port, case, q):
         prefixes[con] = tla_text(json.load(open(os.path.join(GOLDEN, fixture)))["value"])
     try:
         sc = shard.ShardedChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), rank, world, device_index=0,
-                                  history_prefixes=prefixes, max_depth=g["max_depth"], **MSMALL)
+                                  history_prefixes=prefixes, max_depth=g["max_depth"], sym_tlc=g.get("sym") == "tlc", **MSMALL)
         r = sc.run()
         dump = "%s.rank%d" % (os.environ["RAFTMC_DUMP"], rank)
         sc.mc.dump_states(dump)
@@ -225,7 +225,8 @@ def run_memb_sharded(case, world, tmp_path):
 
 
 @pytest.mark.parametrize("case,world", [("membership_shipped@14", 2), ("memb_dynamic3@14", 3), ("memb_four@10", 2),
-                                        ("punct_MajorityOfClusterRestarts@30", 2)])
+                                        ("punct_MajorityOfClusterRestarts@30", 2), ("tlc:membership_shipped@16", 2),
+                                        ("tlc:memb_four@13", 3)])
 def test_membership_sharded_equals_fifo_fixture(case, world, tmp_path):
     """Sharded BFS with FIFO ranking across ranks: identical counts, per-action generated AND
     distinct counts, level sizes and set of kept states (first-found representatives) as the

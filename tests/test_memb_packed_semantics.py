@@ -35,6 +35,11 @@ def build_harness(shape):
     return out
 
 
+def sym_env(g):
+    """SYMMETRY in TLC's mode for the "tlc:" fixtures (the oracle's --sym tlc)."""
+    return dict(os.environ, SYM_TLC="1") if g.get("sym") == "tlc" else None
+
+
 def prefix_args(g):
     """--prefix CONSTRAINT FILE for punctuated-search cases (golden trace from the committed fixture)."""
     if not g.get("prefix"):
@@ -50,7 +55,7 @@ def test_packed_membership_matches_oracle(case):
     fd, dump = tempfile.mkstemp(suffix=".txt")
     os.close(fd)
     r = json.loads(subprocess.run([exe, os.path.join(CONFIGS, g["cfg"] + ".cfg"), str(g["max_depth"]), dump, *prefix_args(g)],
-                                  capture_output=True, text=True, check=True).stdout)
+                                  capture_output=True, text=True, check=True, env=sym_env(g)).stdout)
     assert r["err"] == 0 and r["verdict"] == "OK"
     assert (r["generated"], r["distinct"], r["depth"], r["left_on_queue"]) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
     assert r["actions"] == g["actions"]
@@ -60,12 +65,12 @@ def test_packed_membership_matches_oracle(case):
 
 
 @pytest.mark.parametrize("case", ["scen_FirstBecomeLeader", "punct_CommitWhenConcurrentLeaders",
-                                  "punct_MajorityOfClusterRestarts"])
+                                  "punct_MajorityOfClusterRestarts", "tlc:scen_FirstCommit"])
 def test_packed_membership_first_violation(case):
     g = FIX[case]
     exe = build_harness(SHAPES.get(g["cfg"], (3, 2)))
     r = json.loads(subprocess.run([exe, os.path.join(CONFIGS, g["cfg"] + ".cfg"), "0", "-", *prefix_args(g)],
-                                  capture_output=True, text=True, check=True).stdout)
+                                  capture_output=True, text=True, check=True, env=sym_env(g)).stdout)
     assert (r["verdict"], r["violated"], r["depth"], r["generated"], r["distinct"], r["left_on_queue"]) == \
         (g["verdict"], g["violated"], g["depth"], g["generated"], g["distinct"], g["left_on_queue"])
 
