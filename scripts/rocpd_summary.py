@@ -67,8 +67,14 @@ def main():
         valu = {r[0]: r for r in pmc(sys.argv[2], "SQ_INSTS_VALU")}
         salu = {r[0]: r for r in pmc(sys.argv[2], "SQ_INSTS_SALU")}
         name = next(k for k in valu if sys.argv[3] in k)
+        extra = {}
+        for cn in ("SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY", "SQ_WAVES"):
+            rows = {r[0]: r for r in pmc(sys.argv[2], cn)}
+            if name in rows:
+                extra[cn + "_per_launch"] = rows[name][2]
         doc = {"kernel_name": sys.argv[3], "kernel_symbol": name, "dispatches": valu[name][1],
                "valu_insts_per_launch": valu[name][2], "salu_insts_per_launch": salu[name][2] if name in salu else None,
+               "sq_counters": extra,
                "peak_valu_insts_per_s": 256 * 2 * 2.4e9,
                "method": "rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU over `bench.py --steps 1 --warmup 0`; wave-instructions "
                          "per dispatch; peak per MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 VALU instruction "
