@@ -154,14 +154,15 @@ int mc_action_location(const mc_ctx* ctx, const char* action, char** text, size_
  * report's estimate line. */
 int mc_collision_observed(mc_ctx* ctx, double* val);
 
-/* Checkpoint / recover (raft_original) — TLC's `-checkpoint <minutes>` and `-recover <dir>`
+/* Checkpoint / recover (both spec families) — TLC's `-checkpoint <minutes>` and `-recover <dir>`
  * (the states/ directory, reference .gitignore:3).  mc_set_checkpoint: every `every_levels`
  * completed BFS levels mc_run writes the search state (stored states, parent pointers, level
  * position, TLC's counters, the model's identity) to `path` (atomically: path.tmp, rename);
  * NULL or 0 disables.  mc_set_recover: the next mc_run resumes from `path` instead of Init
  * (the seen-set is rebuilt on the GPU from the stored states); generated/distinct/depth/per-action
  * counts continue exactly; kernel timings cover the resumed part.  A checkpoint of another
- * model is refused (MC_E_INVALID).  MC_E_UNSUPPORTED for tlc_membership. */
+ * model (or of the other SYMMETRY mode) is refused (MC_E_INVALID).  Completed levels that do not
+ * fit the device store are kept in host memory on save and on recovery (host spill). */
 int mc_set_checkpoint(mc_ctx* ctx, const char* path, int32_t every_levels);
 int mc_set_recover(mc_ctx* ctx, const char* path);
 

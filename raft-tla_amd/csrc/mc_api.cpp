@@ -153,7 +153,6 @@ int mc_set_history_prefix(mc_ctx* c, const char* constraint, const char* trace_t
 int mc_set_checkpoint(mc_ctx* c, const char* path, int32_t every_levels) {
   if (!c || every_levels < 0) return MC_E_INVALID;
   if (!c->be) return MC_E_STATE;
-  if (c->be->family() != "raft_original") { c->last_error = "checkpoints are implemented for raft_original"; return MC_E_UNSUPPORTED; }
   c->ro.checkpoint_path = path ? path : "";
   c->ro.checkpoint_every = path ? every_levels : 0;
   return MC_OK;
@@ -162,7 +161,6 @@ int mc_set_checkpoint(mc_ctx* c, const char* path, int32_t every_levels) {
 int mc_set_recover(mc_ctx* c, const char* path) {
   if (!c) return MC_E_INVALID;
   if (!c->be) return MC_E_STATE;
-  if (c->be->family() != "raft_original") { c->last_error = "checkpoints are implemented for raft_original"; return MC_E_UNSUPPORTED; }
   c->ro.recover_path = path ? path : "";
   return MC_OK;
 }

@@ -417,6 +417,34 @@ __global__ void __launch_bounds__(BS) memb_materialize(MMatArgs a) {
     if (lds_cnt[t]) atomicAdd(&a.ctr[C_ACT + MA_NACT + t], (unsigned long long)lds_cnt[t]);
 }
 
+// Recovery from a checkpoint (TLC -recover): the fingerprints of the stored states [0, n) go back
+// into the zeroed seen-set.  Their side value is ~0 (level 0, key 0): every stored state belongs to
+// a completed level, so it beats any successor of the levels still to come, exactly as its own
+// (older-level) entry did before the checkpoint.
+template <class S, bool TLC>
+__global__ void __launch_bounds__(BS) memb_reinsert(const u32* states, u64 n, u64 seed, MembRuntime rt, u64* table,
+                                                    u64 table_mask, unsigned long long* ctr) {
+  using W = typename S::Work;
+  constexpr int NWP = S::NWP;
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  if (i >= n) return;
+  u32 w[NWP];
+  const uint4* src = reinterpret_cast<const uint4*>(states + i * NWP);
+#pragma unroll
+  for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+  W s;
+  S::unpack(w, s);
+  const u64 fp = TLC ? S::fingerprint_tlc(s, seed, rt) : S::fingerprint_orbit(s, seed, rt);
+  u64 slot = fp & table_mask;
+  for (int probe = 0;; ++probe) {
+    if (probe >= (1 << 20)) { atomicOr(&ctr[C_ERR], (unsigned long long)MERR_TABLE_FULL); return; }
+    const u64 old = (u64)atomicCAS((unsigned long long*)&table[2 * slot], 0ull, (unsigned long long)fp);
+    if (old == 0ull || old == fp) break;
+    slot = (slot + 1) & table_mask;
+  }
+  table[2 * slot + 1] = ~0ull;
+}
+
 // ------------------------------------------------------------------ sharded (multi-GPU) kernels
 // FIFO first-found across ranks: keys are global (global parent rank * NSLOT + slot),
 // every fingerprint has one owner ((fp >> 32) mod world) whose seen-set entry keeps the minimum
@@ -760,7 +788,14 @@ class MembGpu : public Backend {
     r.kernels = {{"memb_expand", 0, 0, 0}, {"memb_fingerprint", 0, 0, 0}, {"memb_dedup", 0, 0, 0},
                  {"memb_select", 0, 0, 0}, {"memb_compact", 0, 0, 0}, {"memb_materialize", 0, 0, 0}};
     const MembRuntime& rt = rt_host_;
+    base_ = 0; host_states_.clear(); host_meta_.clear();
+    u64 level_begin = 0, level_count = 1;
+    u32 level = 0;
 
+    if (!o.recover_path.empty()) {   // TLC -recover: continue the BFS saved by a checkpoint
+      if (int rc = load_checkpoint(o.recover_path, r, level_begin, level_count, err)) return rc;
+      level = (u32)(r.depth - 1);
+    } else {
     // ---- Init (raft.tla:388-393): generated 1; constraints; invariants (TLC checks them on initial states)
     W s0; S::init(s0);
     r.generated = 1; r.depth = 1;
@@ -784,12 +819,24 @@ class MembGpu : public Backend {
         finish(r, t0); return 0;
       }
     }
+    }
 
     const u64 S_B = NWP * 4;
-    u64 level_begin = 0, level_count = 1;
-    u32 level = 0;
     while (level_count > 0) {
       if (o.max_depth && r.depth >= o.max_depth) { r.left_on_queue = (int64_t)level_count; r.verdict = MC_VERDICT_DEPTH_LIMIT; break; }
+      // the device keeps what the search still reads (the frontier) and writes (the next level);
+      // when the next level, predicted from the last growth ratio with a 1.5x margin, might not
+      // fit behind what is stored, the completed levels move to host memory
+      if (level_begin > base_) {
+        const double prev = r.levels.size() >= 2 ? (double)r.levels[r.levels.size() - 2].states : 1.0;
+        const double pred = (double)level_count * std::max(1.0, (double)level_count / std::max(prev, 1.0)) * 1.5;
+        if ((double)(total_ - base_) + pred > (double)cap_)
+          if (int rc = spill(level_begin, level_count, err)) return rc;
+      }
+      // kernels index the store by global id: the device part holds [base_, base_ + cap_)
+      u32* const sp = d_states_ - base_ * NWP;
+      u64* const mp = d_meta_ - base_;
+      const u64 cap_end = base_ + cap_;
       HIPCHK(hipMemsetAsync(d_ctr_, 0, C_NCTR * 8, stream_));
       HIPCHK(hipMemsetAsync(d_ctr_ + C_EVENT, 0xFF, 8, stream_));
       u64 next_write = level_begin + level_count;
@@ -804,7 +851,7 @@ class MembGpu : public Backend {
         const u64 nslots = cnt * (u64)S::NSLOT;
         const u32 nblk = (u32)((cnt + BS - 1) / BS);
         MGenArgs g;
-        g.states = d_states_; g.chunk_begin = cb; g.chunk_count = cnt; g.rank0 = rank0; g.cand = d_cand_; g.cells = d_cells_;
+        g.states = sp; g.chunk_begin = cb; g.chunk_count = cnt; g.rank0 = rank0; g.cand = d_cand_; g.cells = d_cells_;
         g.cells_oom = d_cells_oom_; g.cell_count = d_cell_count_; g.nsucc = d_nsucc_;
         g.seed = r.seed; g.rt = rt_dev_; g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.deadlock = o.check_deadlock ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_;
         MDedupArgs d;
@@ -844,9 +891,9 @@ class MembGpu : public Backend {
         const float ms_x = ms(7, 8), ms_g = ms(0, 1), ms_d = ms(1, 2), ms_s = ms(2, 3), ms_c = ms(3, 4);
 
         float ms_m = 0;
-        if (nnew && next_write + nnew <= cap_) {
+        if (nnew && next_write + nnew <= cap_end) {
           MMatArgs m;
-          m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.n_new = nnew; m.dst_base = next_write; m.cap = cap_;
+          m.states = sp; m.meta = mp; m.newrec = d_newrec_; m.n_new = nnew; m.dst_base = next_write; m.cap = cap_end;
           m.level_begin = level_begin; m.gid_tag = 0; m.rt = rt_dev_; m.ctr = (unsigned long long*)d_ctr_;
           HIPCHK(hipEventRecord(ev_[5], stream_));
           if (rt_dev_.sym_tlc) hipLaunchKernelGGL((memb_materialize<S, true>), dim3((unsigned)((nnew + BS - 1) / BS)), dim3(BS), 0, stream_, m);
@@ -867,7 +914,7 @@ class MembGpu : public Backend {
         r.kernels[3].ms += ms_s; r.kernels[3].launches++; r.kernels[3].algo_bytes += (double)nslots * 8 + (double)ncells * 16 + (double)cnt * 4;
         r.kernels[4].ms += ms_c; r.kernels[4].launches++; r.kernels[4].algo_bytes += (double)nslots * 8 + (double)nnew * 8;
         if (ms_m > 0) { r.kernels[5].ms += ms_m; r.kernels[5].launches++; r.kernels[5].algo_bytes += (double)nnew * (8 + 2 * S_B + 8); }
-        if (next_write + nnew > cap_) { c[C_ERR] |= MERR_STORE; stop = true; }
+        if (next_write + nnew > cap_end) { c[C_ERR] |= MERR_STORE; stop = true; }
         if (c[C_EVENT] != ~0ull) {
           // first event of this chunk in key order (earlier chunks had none)
           handle_event(c, cnt, level_begin, level_count, rank0, gen_before_chunk, next_write - (level_begin + level_count), nnew, level, r);
@@ -911,8 +958,153 @@ class MembGpu : public Backend {
       level_begin += level_count;
       level_count = nnew;
       ++level;
+      if (o.checkpoint_every > 0 && !o.checkpoint_path.empty() && r.depth % o.checkpoint_every == 0 && level_count > 0)
+        if (int rc = save_checkpoint(o.checkpoint_path, r, level_begin, level_count, err)) return rc;
     }
     finish(r, t0);
+    return 0;
+  }
+
+  // ---------------------------------------------------------------- checkpoint / recover
+  // TLC -checkpoint / -recover (its states/ directory, reference .gitignore:3).  File: magic, the
+  // model's describe_json and symmetry mode (a checkpoint only resumes the same model), the BFS
+  // position and TLC's counters, then the stored states [0, total) and their parent pointers.
+  // Written straight from the host part and, in bounded blocks, from the device part (no second
+  // copy of the store in host memory).  The seen-set is rebuilt from the states on recovery.
+  struct CkptHead {
+    char magic[8];
+    u64 nwp, total, level_begin, level_count, seed, sym_tlc;
+    int64_t generated, distinct, depth, generated_in_model, n_act, n_levels, desc_len;
+  };
+  static constexpr u64 kCkptBlock = 1u << 20;   // states per device<->file block
+  int save_checkpoint(const std::string& path, const RunResult& r, u64 level_begin, u64 level_count, std::string& err) {
+    const std::string desc = describe_json();
+    CkptHead h;
+    std::memcpy(h.magic, "RAFTMCM1", 8);
+    h.nwp = NWP; h.total = total_; h.level_begin = level_begin; h.level_count = level_count; h.seed = r.seed;
+    h.sym_tlc = rt_host_.sym_tlc;
+    h.generated = r.generated; h.distinct = r.distinct; h.depth = r.depth; h.generated_in_model = r.generated_in_model;
+    h.n_act = MA_NACT; h.n_levels = (int64_t)r.levels.size(); h.desc_len = (int64_t)desc.size();
+    const std::string tmp = path + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) { err = "cannot write checkpoint " + tmp; return MC_E_IO; }
+    bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 && std::fwrite(desc.data(), 1, desc.size(), f) == desc.size() &&
+              std::fwrite(r.act_generated.data(), 8, MA_NACT, f) == (size_t)MA_NACT &&
+              std::fwrite(r.act_distinct.data(), 8, MA_NACT, f) == (size_t)MA_NACT;
+    for (const auto& lv : r.levels) ok = ok && std::fwrite(&lv.states, 8, 1, f) == 1 && std::fwrite(&lv.generated, 8, 1, f) == 1;
+    ok = ok && std::fwrite(host_states_.data(), 4, base_ * NWP, f) == base_ * NWP;
+    std::vector<u32> blk;
+    for (u64 b = base_; ok && b < total_; b += kCkptBlock) {
+      const u64 n = std::min<u64>(kCkptBlock, total_ - b);
+      blk.resize(n * NWP);
+      ok = hipMemcpy(blk.data(), d_states_ + (b - base_) * NWP, n * NWP * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+           std::fwrite(blk.data(), 4, n * NWP, f) == n * NWP;
+    }
+    ok = ok && std::fwrite(host_meta_.data(), 8, base_, f) == base_;
+    std::vector<u64> mblk;
+    for (u64 b = base_; ok && b < total_; b += kCkptBlock) {
+      const u64 n = std::min<u64>(kCkptBlock, total_ - b);
+      mblk.resize(n);
+      ok = hipMemcpy(mblk.data(), d_meta_ + (b - base_), n * 8, hipMemcpyDeviceToHost) == hipSuccess &&
+           std::fwrite(mblk.data(), 8, n, f) == n;
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) { err = "writing checkpoint " + path + " failed"; return MC_E_IO; }
+    return 0;
+  }
+  int load_checkpoint(const std::string& path, RunResult& r, u64& level_begin, u64& level_count, std::string& err) {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    if (!f) { err = "cannot read checkpoint " + path; return MC_E_IO; }
+    CkptHead h;
+    const std::string desc = describe_json();
+    std::string fdesc;
+    bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, "RAFTMCM1", 8) == 0 && h.nwp == (u64)NWP &&
+              h.n_act == MA_NACT && h.desc_len >= 0 && h.desc_len < (1 << 20) && h.n_levels > 0 && h.n_levels < (1 << 20) &&
+              h.sym_tlc == rt_host_.sym_tlc;
+    if (ok) { fdesc.resize((size_t)h.desc_len); ok = std::fread(&fdesc[0], 1, fdesc.size(), f) == fdesc.size(); }
+    if (!ok || fdesc != desc) { std::fclose(f); err = "checkpoint " + path + " is not a checkpoint of this model"; return MC_E_INVALID; }
+    // completed levels that do not fit the device store stay in host memory (spilled)
+    const u64 lb = h.total > cap_ ? h.level_begin : 0;
+    if (h.level_begin > h.total || h.total - lb > cap_) { std::fclose(f); err = "checkpoint frontier exceeds the state store (raise state_store_bytes)"; return MC_E_OOM; }
+    ok = std::fread(r.act_generated.data(), 8, MA_NACT, f) == (size_t)MA_NACT &&
+         std::fread(r.act_distinct.data(), 8, MA_NACT, f) == (size_t)MA_NACT;
+    r.levels.clear();
+    for (int64_t k = 0; ok && k < h.n_levels; ++k) {
+      LevelStat lv;
+      ok = std::fread(&lv.states, 8, 1, f) == 1 && std::fread(&lv.generated, 8, 1, f) == 1;
+      r.levels.push_back(lv);
+    }
+    HIPCHK(hipMemsetAsync(d_ctr_, 0, C_NCTR * 8, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    // states: the host part stays on the host and its fingerprints go in through the (idle)
+    // candidate buffer; the device part is read block by block into the store
+    host_states_.resize(lb * NWP);
+    ok = ok && std::fread(host_states_.data(), 4, lb * NWP, f) == lb * NWP;
+    const u64 stage = std::max<u64>(1, chunk_ * S::NSLOT * 8 / (NWP * 4));
+    for (u64 b = 0; ok && b < lb; b += stage) {
+      const u64 n = std::min<u64>(stage, lb - b);
+      HIPCHK(hipMemcpy(d_cand_, host_states_.data() + b * NWP, n * NWP * 4, hipMemcpyHostToDevice));
+      if (int rc = launch_reinsert((const u32*)d_cand_, n, h.seed, err)) return rc;
+      HIPCHK(hipStreamSynchronize(stream_));
+    }
+    std::vector<u32> blk;
+    for (u64 b = lb; ok && b < h.total; b += kCkptBlock) {
+      const u64 n = std::min<u64>(kCkptBlock, h.total - b);
+      blk.resize(n * NWP);
+      ok = std::fread(blk.data(), 4, n * NWP, f) == n * NWP;
+      if (ok) HIPCHK(hipMemcpy(d_states_ + (b - lb) * NWP, blk.data(), n * NWP * 4, hipMemcpyHostToDevice));
+    }
+    host_meta_.resize(lb);
+    ok = ok && std::fread(host_meta_.data(), 8, lb, f) == lb;
+    std::vector<u64> mblk;
+    for (u64 b = lb; ok && b < h.total; b += kCkptBlock) {
+      const u64 n = std::min<u64>(kCkptBlock, h.total - b);
+      mblk.resize(n);
+      ok = std::fread(mblk.data(), 8, n, f) == n;
+      if (ok) HIPCHK(hipMemcpy(d_meta_ + (b - lb), mblk.data(), n * 8, hipMemcpyHostToDevice));
+    }
+    std::fclose(f);
+    if (!ok) { host_states_.clear(); host_meta_.clear(); err = "checkpoint " + path + " is truncated"; return MC_E_IO; }
+    if (h.total > lb)
+      if (int rc = launch_reinsert(d_states_, h.total - lb, h.seed, err)) return rc;
+    u64 e = 0;
+    HIPCHK(hipMemcpyAsync(&e, d_ctr_ + C_ERR, 8, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    if (e) { err = "fingerprint table too small for the checkpoint (raise fp_table_bytes)"; return MC_E_OOM; }
+    base_ = lb;
+    r.seed = h.seed; r.generated = h.generated; r.distinct = h.distinct; r.depth = h.depth;
+    r.generated_in_model = h.generated_in_model;
+    total_ = h.total; level_begin = h.level_begin; level_count = h.level_count;
+    return 0;
+  }
+  int launch_reinsert(const u32* states, u64 n, u64 seed, std::string& err) {
+    const dim3 grid((unsigned)((n + BS - 1) / BS));
+    if (rt_dev_.sym_tlc)
+      hipLaunchKernelGGL((memb_reinsert<S, true>), grid, dim3(BS), 0, stream_, states, n, seed, rt_dev_, d_table_, table_mask_, (unsigned long long*)d_ctr_);
+    else
+      hipLaunchKernelGGL((memb_reinsert<S, false>), grid, dim3(BS), 0, stream_, states, n, seed, rt_dev_, d_table_, table_mask_, (unsigned long long*)d_ctr_);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
+
+  // move the completed levels [base_, level_begin) to host memory and the frontier to the front
+  // of the device store (left shift by d in blocks of <= d slots: each block's target only
+  // overlaps blocks already moved)
+  int spill(u64 level_begin, u64 level_count, std::string& err) {
+    const u64 d = level_begin - base_;
+    const u64 h0 = host_meta_.size();
+    host_states_.resize((h0 + d) * NWP);
+    host_meta_.resize(h0 + d);
+    HIPCHK(hipStreamSynchronize(stream_));
+    HIPCHK(hipMemcpy(host_states_.data() + h0 * NWP, d_states_, d * NWP * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(host_meta_.data() + h0, d_meta_, d * 8, hipMemcpyDeviceToHost));
+    for (u64 off = 0; off < level_count; off += d) {
+      const u64 n = std::min<u64>(d, level_count - off);
+      HIPCHK(hipMemcpyAsync(d_states_ + off * NWP, d_states_ + (d + off) * NWP, n * NWP * 4, hipMemcpyDeviceToDevice, stream_));
+      HIPCHK(hipMemcpyAsync(d_meta_ + off, d_meta_ + d + off, n * 8, hipMemcpyDeviceToDevice, stream_));
+      HIPCHK(hipStreamSynchronize(stream_));
+    }
+    base_ = level_begin;
     return 0;
   }
 
@@ -976,13 +1168,14 @@ class MembGpu : public Backend {
 
   int dump_states(const std::string& path, std::string& err) override {
     if (!d_states_) { err = "mc_dump_states before mc_run"; return MC_E_STATE; }
-    std::vector<u32> h(total_ * NWP);
+    std::vector<u32> h((total_ - base_) * NWP);
     HIPCHK(hipMemcpy(h.data(), d_states_, h.size() * 4, hipMemcpyDeviceToHost));
     FILE* f = std::fopen(path.c_str(), "w");
     if (!f) { err = "cannot write " + path; return MC_E_IO; }
     for (u64 g = 0; g < total_; ++g) {
       u32 w[NWP];
-      for (int q = 0; q < NWP; ++q) w[q] = h[g * NWP + q];
+      const u32* src = g < base_ ? host_states_.data() + g * NWP : h.data() + (g - base_) * NWP;
+      for (int q = 0; q < NWP; ++q) w[q] = src[q];
       W s; S::unpack(w, s);
       std::fprintf(f, "%s\n", text_.text(s, false).c_str());
     }
@@ -997,6 +1190,7 @@ class MembGpu : public Backend {
   // all-to-all / store that gives every rank an equal contiguous slice of the next level.
   int shard_open(const RunOpts& o, int rank, int world, std::string& err) override {
     if (world < 1 || world > 8 || rank < 0 || rank >= world) { err = "world must be 1..8"; return MC_E_INVALID; }
+    base_ = 0; host_states_.clear(); host_meta_.clear();   // sharded runs keep every state on the device
     for (int q = 0; q < 2; ++q)
       if (((m_.rt.constraints >> kPrefixCon[q]) & 1u) && !have_prefix_[q]) {
         err = std::string(kMembConNames[kPrefixCon[q]]) + " needs its golden history trace (mc_set_history_prefix)";
@@ -1384,6 +1578,10 @@ class MembGpu : public Backend {
   hipEvent_t ev_[9] = {};
   u64 table_mask_ = 0, cap_ = 0, total_ = 0, chunk_ = 0;
   int dev_ = -1; uint64_t req_table_ = 0, req_store_ = 0;
+  // completed levels moved to host memory: global ids [0, base_) live in host_states_/host_meta_
+  u64 base_ = 0;
+  std::vector<u32> host_states_;
+  std::vector<u64> host_meta_;
 
   // sharded mode
   RunOpts sopts_;
@@ -1420,9 +1618,16 @@ class MembGpu : public Backend {
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_cand_ = nullptr; d_newrec_ = nullptr;
     d_nsucc_ = nullptr; d_woff_ = nullptr; d_bsum_ = nullptr; d_cells_ = nullptr; d_cells_oom_ = nullptr; d_cell_count_ = nullptr; stream_ = nullptr;
   }
-  void read_state(u64 gid, W& s) const {
+  // stored state `gid` (global id) and its parent pointer, from the host part or the device
+  void read_state(u64 gid, W& s, u64* meta = nullptr) const {
     u32 w[NWP];
-    (void)hipMemcpy(w, d_states_ + gid * NWP, NWP * 4, hipMemcpyDeviceToHost);
+    if (gid < base_) {
+      std::memcpy(w, host_states_.data() + gid * NWP, NWP * 4);
+      if (meta) *meta = host_meta_[gid];
+    } else {
+      (void)hipMemcpy(w, d_states_ + (gid - base_) * NWP, NWP * 4, hipMemcpyDeviceToHost);
+      if (meta) (void)hipMemcpy(meta, d_meta_ + (gid - base_), 8, hipMemcpyDeviceToHost);
+    }
     S::unpack(w, s);
   }
   void finish(RunResult& r, std::chrono::steady_clock::time_point t0) {
@@ -1437,8 +1642,7 @@ class MembGpu : public Backend {
     u64 g = parent;
     while (true) {
       W s; u64 meta = 0;
-      read_state(g, s);
-      (void)hipMemcpy(&meta, d_meta_ + g, 8, hipMemcpyDeviceToHost);
+      read_state(g, s, &meta);
       if (meta == ~0ull) { tr.push_back({"<Initial predicate>", text_.text(s, true)}); break; }
       tr.push_back({kMembActNames[(meta >> 10) & 1023], text_.text(s, true)});
       g = meta >> 20;

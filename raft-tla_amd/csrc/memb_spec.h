@@ -1427,18 +1427,24 @@ struct Memb {
   // Order key of pi(e) among the permutations of one history entry e = (x, y) (prefix_step's
   // codes): the entry record's server-valued fields in field-name order (records compare field
   // by field in name order; the invariant fields tie).
+  // Branch-free on purpose: the kind differs from lane to lane, and the switch this replaces was
+  // compiled for gfx950 into code that gave every lane another lane's case (tests/native/
+  // tlc_refine_probe.hip: garbage keys on the device, correct ones on the host).
   RMC_HD static u64 entry_key(u64 x, u64 y, u32 pi, u32 cfgt) {
-    const int kind = (int)(x & 15u), ex = pi_of(pi, (int)((x >> 4) & 15u));
+    const int kind = (int)(x & 15u);
+    const u64 ex = (u64)pi_of(pi, (int)((x >> 4) & 15u));
     const u32 aux = (u32)(x >> 8);
-    switch (kind) {
-      case HE_SEND: case HE_RECV: return (u64)ex << CODEB | perm_code(y, pi, true, cfgt);   // action, executedOn, msg
-      case HE_TRYADD: case HE_ADD: return (u64)pi_of(pi, (int)aux) << 2 | (u64)ex;           // action, added, executedOn
-      case HE_TRYREM: case HE_REM: return (u64)ex << 2 | (u64)pi_of(pi, (int)aux);           // action, executedOn, removed
-      case HE_BL: return (u64)ex << 4 | m2r(pmask(aux, pi));                                 // action, executedOn, leaders
-      case HE_CE: return (u64)pentry(aux, pi, cfgt) << 2 | (u64)ex;                           // action, entry, executedOn
-      case HE_CMC: return (u64)m2r(pmask(aux, pi)) << 2 | (u64)ex;                           // action, config, executedOn
-      default: return (u64)ex;                                                               // Restart, Timeout
-    }
+    const bool msg = kind == HE_SEND || kind == HE_RECV;
+    const u64 pa = (u64)pi_of(pi, (int)(aux & 3u));
+    const u64 pm = m2r(pmask(aux & (u32)lomask(N), pi));
+    const u64 kmsg = ex << CODEB | perm_code(msg ? y : 0ull, pi, true, cfgt);                 // action, executedOn, msg
+    u64 k = ex;                                                                             // Restart, Timeout
+    k = (kind == HE_TRYADD || kind == HE_ADD) ? (pa << 2 | ex) : k;                         // action, added, executedOn
+    k = (kind == HE_TRYREM || kind == HE_REM) ? (ex << 2 | pa) : k;                         // action, executedOn, removed
+    k = kind == HE_BL ? (ex << 4 | pm) : k;                                                 // action, executedOn, leaders
+    k = kind == HE_CE ? ((u64)pentry(aux, pi, cfgt) << 2 | ex) : k;                         // action, entry, executedOn
+    k = kind == HE_CMC ? (pm << 2 | ex) : k;                                                // action, config, executedOn
+    return msg ? kmsg : k;
   }
   // refine the history ranks by the entries this successor appended (apply).  Runtime loops and
   // keys recomputed on the fly: small code in every kernel that inlines apply, no scratch arrays

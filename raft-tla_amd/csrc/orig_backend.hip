@@ -1529,12 +1529,6 @@ class OrigGpu : public Backend {
     h.nwp = NWP; h.total = total_; h.level_begin = level_begin; h.level_count = level_count; h.seed = r.seed;
     h.generated = r.generated; h.distinct = r.distinct; h.depth = r.depth; h.generated_in_model = r.generated_in_model;
     h.n_act = OA_NACT; h.n_levels = (int64_t)r.levels.size(); h.desc_len = (int64_t)desc.size();
-    std::vector<u32> st(total_ * NWP);
-    std::vector<u64> me(total_);
-    std::memcpy(st.data(), host_states_.data(), base_ * NWP * 4);
-    std::memcpy(me.data(), host_meta_.data(), base_ * 8);
-    HIPCHK(hipMemcpy(st.data() + base_ * NWP, d_states_, (total_ - base_) * NWP * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(me.data() + base_, d_meta_, (total_ - base_) * 8, hipMemcpyDeviceToHost));
     const std::string tmp = path + ".tmp";
     FILE* f = std::fopen(tmp.c_str(), "wb");
     if (!f) { err = "cannot write checkpoint " + tmp; return MC_E_IO; }
@@ -1542,7 +1536,25 @@ class OrigGpu : public Backend {
               std::fwrite(r.act_generated.data(), 8, OA_NACT, f) == (size_t)OA_NACT &&
               std::fwrite(r.act_distinct.data(), 8, OA_NACT, f) == (size_t)OA_NACT;
     for (const auto& lv : r.levels) ok = ok && std::fwrite(&lv.states, 8, 1, f) == 1 && std::fwrite(&lv.generated, 8, 1, f) == 1;
-    ok = ok && std::fwrite(st.data(), 4, st.size(), f) == st.size() && std::fwrite(me.data(), 8, me.size(), f) == me.size();
+    // the host part straight from host memory, the device part in bounded blocks (no second copy
+    // of the store in host memory)
+    constexpr u64 BLK = 1u << 20;
+    ok = ok && std::fwrite(host_states_.data(), 4, base_ * NWP, f) == base_ * NWP;
+    std::vector<u32> blk;
+    for (u64 b = base_; ok && b < total_; b += BLK) {
+      const u64 n = std::min<u64>(BLK, total_ - b);
+      blk.resize(n * NWP);
+      ok = hipMemcpy(blk.data(), d_states_ + (b - base_) * NWP, n * NWP * 4, hipMemcpyDeviceToHost) == hipSuccess &&
+           std::fwrite(blk.data(), 4, n * NWP, f) == n * NWP;
+    }
+    ok = ok && std::fwrite(host_meta_.data(), 8, base_, f) == base_;
+    std::vector<u64> mblk;
+    for (u64 b = base_; ok && b < total_; b += BLK) {
+      const u64 n = std::min<u64>(BLK, total_ - b);
+      mblk.resize(n);
+      ok = hipMemcpy(mblk.data(), d_meta_ + (b - base_), n * 8, hipMemcpyDeviceToHost) == hipSuccess &&
+           std::fwrite(mblk.data(), 8, n, f) == n;
+    }
     ok = (std::fclose(f) == 0) && ok;
     if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) { err = "writing checkpoint " + path + " failed"; return MC_E_IO; }
     return 0;

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <unordered_set>
 #include <vector>
@@ -51,7 +52,8 @@ int main(int argc, char** argv) {
   CfgFile cfg = parse_cfg_text(read_text_file(argv[1]));
   MembModel m = resolve_memb_model(cfg);
   const int depth = std::atoi(argv[2]);
-  const MembRuntime& rt = m.rt;
+  MembRuntime rt = m.rt;
+  if (std::getenv("SYM_TLC") && rt.symmetry) rt.sym_tlc = 1;   // MC_COMPAT_SYM_TLC
   const u64 seed = 0x5EED5EED2024ull;
   std::vector<W> all, fr(1);
   S::init(fr[0]);
@@ -166,7 +168,8 @@ int main(int argc, char** argv) {
         return 4;
       }
     }
-    hipLaunchKernelGGL((memb_fingerprint<S>), dim3((unsigned)nblk), dim3(256), 0, 0, g);
+    if (rt.sym_tlc) hipLaunchKernelGGL((memb_fingerprint<S, true>), dim3((unsigned)nblk), dim3(256), 0, 0, g);
+    else hipLaunchKernelGGL((memb_fingerprint<S, false>), dim3((unsigned)nblk), dim3(256), 0, 0, g);
     if (hipDeviceSynchronize() != hipSuccess) { std::printf("{\"error\": \"fingerprint kernel\"}\n"); return 1; }
     hipLaunchKernelGGL((memb_oom_check<S>), dim3((unsigned)nblk), dim3(256), 0, 0, g);
     if (hipDeviceSynchronize() != hipSuccess) { std::printf("{\"error\": \"oom check kernel\"}\n"); return 1; }

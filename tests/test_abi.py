@@ -167,11 +167,14 @@ def test_prefix_taken_from_extended_module(raftmc, tmp_path):
 
 
 def test_checkpoint_api_scope(raftmc):
-    """Checkpoints are a raft_original feature; tlc_membership handles refuse them."""
+    """Checkpoints exist for both spec families (TLC -checkpoint / -recover); a negative
+    interval is refused."""
     lib = raftmc.load_library()
     with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, "membership_shipped.cfg")) as mc:
-        assert lib.mc_set_checkpoint(mc.h, b"/tmp/x.ckpt", 1) == -4
-        assert lib.mc_set_recover(mc.h, b"/tmp/x.ckpt") == -4
+        assert lib.mc_set_checkpoint(mc.h, b"/tmp/x.ckpt", 1) == 0
+        assert lib.mc_set_checkpoint(mc.h, b"/tmp/x.ckpt", -1) == -1
+        assert lib.mc_set_recover(mc.h, b"/tmp/x.ckpt") == 0
+        mc.set_recover(None)
     with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c1.cfg")) as mc:
         assert lib.mc_set_checkpoint(mc.h, b"/tmp/x.ckpt", -1) == -1
         mc.set_checkpoint("/tmp/x.ckpt", 2)

@@ -127,3 +127,89 @@ def test_counterexamples_beyond_oracle_reach(raftmc, cfg):
     assert (r.depth, r.distinct, r.generated, r.left_on_queue) == (g["depth"], g["distinct"], g["generated"], g["left_on_queue"])
     got = [" ".join(b.split("\n")[1:]) for b in r.trace_text.strip().split("\n\n")]
     assert got == open(os.path.join(GOLDEN, "gpu_traces", cfg + ".txt")).read().strip().split("\n")
+
+
+def _memb_slot_bytes(raftmc, cfg):
+    """device bytes per stored state: packed state + parent pointer"""
+    with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, cfg + ".cfg")) as mc:
+        return mc.describe()["state_bytes_stored"] + 8
+
+
+def _spill_store(raftmc, g, margin=1.6):
+    """a state store too small for the search but large enough for two consecutive levels"""
+    sizes = g["levels"]
+    cap = max(512, int(max(x + y for x, y in zip(sizes, sizes[1:])) * margin))
+    assert cap < g["distinct"]
+    return cap * _memb_slot_bytes(raftmc, g["cfg"])
+
+
+@pytest.mark.parametrize("case", ["memb_two@16", "tlc:membership_shipped@16"])
+def test_membership_checkpoint_recover(raftmc, case, tmp_path):
+    """TLC -checkpoint / -recover for tlc_membership: a search stopped at depth 9 with a
+    checkpoint per level, resumed by a fresh handle (seen-set rebuilt on the GPU with the
+    checkpoint's seed and SYMMETRY mode), ends exactly like the oracle's uninterrupted search:
+    counts, levels, per-action generated AND distinct counts (FIFO first-found), state set."""
+    g = FIX[case]
+    ck = str(tmp_path / "m.ckpt")
+    kw = dict(SMALL)
+    with open_case(raftmc, g, max_depth=9, seed=11, **kw) as mc:
+        mc.set_checkpoint(ck, 1)
+        a = mc.run()
+    assert a.verdict == "DEPTH_LIMIT" and os.path.exists(ck), a.error
+    with open_case(raftmc, g, max_depth=g["max_depth"], seed=12345, **kw) as mc:   # the checkpoint's seed wins
+        mc.set_recover(ck)
+        r = mc.run()
+        sha, n = states_sha(mc)
+    assert (r.generated, r.distinct, r.depth, r.left_on_queue) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"]), r.error
+    assert [lv[0] for lv in r.levels] == g["levels"]
+    assert r.actions == g["actions"]
+    assert n == g["distinct"] and sha == g["states_sha256"]
+    # a checkpoint only resumes its own model, in its own SYMMETRY mode
+    other = dict(g, sym=None if g.get("sym") == "tlc" else "tlc")
+    with open_case(raftmc, other, **kw) as mc:
+        mc.set_recover(ck)
+        with pytest.raises(raftmc.RaftMCError) as e:
+            mc.run()
+    assert e.value.code == -1
+
+
+@pytest.mark.parametrize("case", ["memb_two@16", "tlc:membership_shipped@16"])
+def test_membership_spill_completed_levels(raftmc, case, tmp_path):
+    """Host spill for tlc_membership: with a store that holds about two levels, the completed
+    levels move to host memory and the search still equals the oracle's (counts, per-action
+    distinct counts, the state set read across the host/device split); a checkpoint written
+    after spills resumes into the same small store."""
+    g = FIX[case]
+    kw = dict(SMALL, state_store_bytes=_spill_store(raftmc, g, margin=1.05))   # the last two levels are ~95% of the states
+    ck = str(tmp_path / "ms.ckpt")
+    with open_case(raftmc, g, max_depth=g["max_depth"], **kw) as mc:
+        mc.set_checkpoint(ck, g["max_depth"] - 2)
+        r = mc.run()
+        sha, n = states_sha(mc)
+    assert (r.generated, r.distinct, r.depth, r.left_on_queue) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"]), r.error
+    assert [lv[0] for lv in r.levels] == g["levels"] and r.actions == g["actions"]
+    assert n == g["distinct"] and sha == g["states_sha256"]
+    with open_case(raftmc, g, max_depth=g["max_depth"], **kw) as mc:
+        mc.set_recover(ck)
+        c = mc.run()
+        sha2, _ = states_sha(mc)
+    assert (c.generated, c.distinct, c.depth, c.actions) == (r.generated, r.distinct, r.depth, r.actions), c.error
+    assert sha2 == sha
+
+
+@pytest.mark.parametrize("case", ["scen_BoundedTrace", "tlc:scen_FirstCommit"])
+def test_membership_spill_counterexample(raftmc, case):
+    """Trace reconstruction and TLC's stop-point counters across the host/device split: the
+    oracle's shortest counterexample, state by state."""
+    g = FIX[case]
+    # the store must hold the last complete level and the new states the GPU materializes before
+    # the stop (the violation is late in its level): between that and the whole search
+    s = g["levels"]
+    need = max(max(x + y for x, y in zip(s, s[1:])), s[-1] + g["distinct"] - sum(s))
+    cap = need + (g["distinct"] - need) * 3 // 4
+    with open_case(raftmc, g, **dict(SMALL, state_store_bytes=cap * _memb_slot_bytes(raftmc, g["cfg"]))) as mc:
+        r = mc.run()
+    assert r.verdict == "INVARIANT_VIOLATION" and r.violated == g["violated"], (r, r.error)
+    assert (r.depth, r.generated, r.distinct, r.left_on_queue) == (g["depth"], g["generated"], g["distinct"], g["left_on_queue"])
+    blocks = r.trace_text.strip().split("\n\n")
+    assert [" ".join(b.split("\n")[1:]) for b in blocks] == [t["state"] for t in g["trace"]]
