@@ -844,6 +844,13 @@ __global__ void orig_advance(unsigned long long* ctr) {
   }
 }
 
+// the level's counters back to their initial values (event word all ones); queued right after
+// the level's counter readback, so it runs while the host looks at the counters and the next
+// level starts with its generate kernel (one tiny kernel instead of two fills on the critical path)
+__global__ void orig_reset_ctr(unsigned long long* ctr) {
+  for (int t = threadIdx.x; t < K_NCTR; t += blockDim.x) ctr[t] = t == K_EVENT ? ~0ull : 0ull;
+}
+
 // ------------------------------------------------------------------ TLC's stop point
 // On the level's first event (parent gid_stop, instance k_stop, kind): TLC's generated counts
 // are the whole successor lists of the parents before it and of the event's parent (none when
@@ -1181,6 +1188,7 @@ class OrigGpu : public Backend {
     HIPCHK(hipMalloc(&d_wcnt_, nblk * 4));
     HIPCHK(hipMalloc(&d_woff_, nblk * 8));
     HIPCHK(hipMalloc(&d_ctr_, K_NCTR * 8));
+    HIPCHK(hipHostMalloc((void**)&h_ctr_, K_NCTR * 8, hipHostMallocDefault));
     HIPCHK(hipMalloc(&d_stop_, (1 + OA_NACT) * 8));
     HIPCHK(hipMemset(d_winmask_, 0, chunk_states_ * WW * 8));
     if (world >= 1) {   // sharded mode
@@ -1229,6 +1237,7 @@ class OrigGpu : public Backend {
     const bool fifo = o.workers == 1;
     last_fifo_ = fifo;
     const u64 tmask = fifo ? table_mask_ : 2 * (table_mask_ + 1) - 1;
+    ctr_clean_ = false;
 
     r = RunResult();
     r.seed = o.seed ? o.seed : 0x5EED5EED2024ull;
@@ -1276,8 +1285,11 @@ class OrigGpu : public Backend {
         if ((double)(total_ - base_) + pred > (double)cap_)
           if (int rc = spill(level_begin, level_count, err)) return rc;
       }
-      HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
-      HIPCHK(hipMemsetAsync(d_ctr_ + K_EVENT, 0xFF, 8, stream_));
+      if (!ctr_clean_) {
+        hipLaunchKernelGGL(orig_reset_ctr, dim3(1), dim3(64), 0, stream_, (unsigned long long*)d_ctr_);
+        HIPCHK(hipGetLastError());
+      }
+      ctr_clean_ = false;
       const u64 level_end = level_begin + level_count;
       // every chunk's kernels are queued without waiting: the chunk's insert and winner counts
       // stay on the device (grid-stride / scanned offsets), so the host synchronises once per
@@ -1299,7 +1311,7 @@ class OrigGpu : public Backend {
         d.urec = (ulonglong2*)d_urec_; d.ucnt = d_ucnt_;
         d.table = d_table_; d.table_mask = tmask; d.newpos = d_newrec_; d.ctr = (unsigned long long*)d_ctr_;
         d.prof = prof_ ? 1u : 0u;
-        HIPCHK(hipEventRecord(e[2], stream_));
+        // kernel boundaries share an event (each event record costs ~5 us of stream time)
         if (fifo) {
           hipLaunchKernelGGL(orig_merge, dim3(nblk), dim3(BS), 0, stream_, d);
           HIPCHK(hipGetLastError());
@@ -1315,7 +1327,6 @@ class OrigGpu : public Backend {
         }
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e[3], stream_));
-        HIPCHK(hipEventRecord(e[4], stream_));
         if (fifo) {
           MarkArgs mk;
           mk.newpos = d_newrec_; mk.table = d_table_; mk.gid0 = cb; mk.chunk_count = cnt; mk.winmask = d_winmask_;
@@ -1327,8 +1338,7 @@ class OrigGpu : public Backend {
           hipLaunchKernelGGL(orig_scan, dim3(1), dim3(SCAN_BS), 0, stream_, (const u32*)d_wcnt_, d_woff_, (u32)nblk, (unsigned long long*)d_ctr_);
           HIPCHK(hipGetLastError());
         }
-        HIPCHK(hipEventRecord(e[5], stream_));
-        HIPCHK(hipEventRecord(e[6], stream_));
+        if (fifo) HIPCHK(hipEventRecord(e[5], stream_));
         if (fifo) {
           MatArgs m;
           m.states = d_states_; m.meta = d_meta_; m.chunk_begin = cb - base_; m.chunk_count = cnt; m.gid0 = cb;
@@ -1348,16 +1358,24 @@ class OrigGpu : public Backend {
         for (size_t q = 0; q < r.kernels.size(); ++q) if (fifo || q != 2) r.kernels[q].launches += 1;
         r.kernels[0].algo_bytes += (double)cnt * S_B;        // + G_in * 10 record bytes per level below
       }
-      u64 c[K_NCTR];
-      HIPCHK(hipMemcpyAsync(c, d_ctr_, sizeof c, hipMemcpyDeviceToHost, stream_));
+      u64* const c = h_ctr_;   // pinned: the readback is one direct copy
+      HIPCHK(hipMemcpyAsync(c, d_ctr_, K_NCTR * 8, hipMemcpyDeviceToHost, stream_));
+      hipLaunchKernelGGL(orig_reset_ctr, dim3(1), dim3(64), 0, stream_, (unsigned long long*)d_ctr_);
+      HIPCHK(hipGetLastError());
+      ctr_clean_ = true;
       HIPCHK(hipStreamSynchronize(stream_));
       double level_ms = 0;
-      for (int q = 0; q < nch; ++q)
+      for (int q = 0; q < nch; ++q) {
+        // event pairs per kernel: generate (e0, e1), dedup (e1, e3), mark/scan (e3, e5; FIFO only),
+        // materialize (e5 or e3, e7)
+        const hipEvent_t* e = &lvl_ev_[8 * q];
+        const std::pair<int, int> pr[4] = {{0, 1}, {1, 3}, {3, fifo ? 5 : 3}, {fifo ? 5 : 3, 7}};
         for (int k = 0; k < 4; ++k) {
           float ms = 0;
-          (void)hipEventElapsedTime(&ms, lvl_ev_[8 * q + 2 * k], lvl_ev_[8 * q + 2 * k + 1]);
+          if (pr[k].first != pr[k].second) (void)hipEventElapsedTime(&ms, e[pr[k].first], e[pr[k].second]);
           r.kernels[k].ms += ms; level_ms += ms;
         }
+      }
       const u64 nnew = c[K_LEVEL_NEW];
       const u64 next_write = level_end + nnew;
       if (prof_) {
@@ -2109,6 +2127,8 @@ class OrigGpu : public Backend {
   OrigModel m_;
   static constexpr int WW = (S::NI + 63) / 64;   // winner-mask words per parent
   u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr; u64* d_stop_ = nullptr;
+  u64* h_ctr_ = nullptr;     // pinned host copy of the level counters
+  bool ctr_clean_ = false;   // d_ctr_ already reset for the next level (queued after the readback)
   u64* d_rfp_ = nullptr; unsigned short* d_rkey_ = nullptr; u32* d_rcnt_blk_ = nullptr; u64* d_newrec_ = nullptr;
   u64* d_winmask_ = nullptr; u32* d_wcnt_ = nullptr; u64* d_woff_ = nullptr; u64* d_urec_ = nullptr; u32* d_ucnt_ = nullptr;
   u64* d_route_ = nullptr; u64* d_rcnt_ = nullptr; u32* d_stout_ = nullptr; u64 stout_cap_ = 0;
@@ -2158,6 +2178,8 @@ class OrigGpu : public Backend {
     lvl_ev_.clear();
     for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
     if (stream_) (void)hipStreamDestroy(stream_);
+    if (h_ctr_) (void)hipHostFree(h_ctr_);
+    h_ctr_ = nullptr; ctr_clean_ = false;
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_stop_ = nullptr;
     d_rfp_ = nullptr; d_rkey_ = nullptr; d_rcnt_blk_ = nullptr; d_newrec_ = nullptr; d_winmask_ = nullptr; d_wcnt_ = nullptr; d_woff_ = nullptr; d_urec_ = nullptr; d_ucnt_ = nullptr; d_route_ = nullptr; d_rcnt_ = nullptr; d_stout_ = nullptr; stout_cap_ = 0;
     stream_ = nullptr; alloc_world_ = 0;
