@@ -194,6 +194,16 @@ def test_c2_full_size_properties(raftmc):
     assert sum(v[0] for v in a.actions.values()) + 1 == a.generated
     # TLC's "calculated (optimistic)" collision estimate: M * (N - M) / 2^64
     assert a.collision_prob_optimistic == pytest.approx(a.distinct * (a.generated - a.distinct) / 2.0 ** 64)
+    # the oracle pin (tests/golden/make_c2_oracle.py: the CPU restatement of raft_original.tla run
+    # over the whole C2 in its lean mode): counts, depth, level sizes and the per-action generated
+    # AND distinct counts of TLC's single-worker FIFO order (the handle's default, -workers 1)
+    pin = os.path.join(GOLDEN, "c2_oracle.json")
+    if not os.path.exists(pin):
+        pytest.skip("tests/golden/c2_oracle.json not generated yet")
+    o = json.load(open(pin))
+    assert (a.generated, a.distinct, a.depth) == (o["generated"], o["distinct"], o["depth"])
+    assert [lv[0] for lv in a.levels] == o["levels"]
+    assert {k: list(v) for k, v in a.actions.items()} == {k: list(v) for k, v in o["actions"].items()}
 
 
 def test_c5_prefix_parity(raftmc):
