@@ -91,6 +91,22 @@ struct GenArgs {
   unsigned long long* ctr;
 };
 
+#if defined(RMC_EXP_DOUBLE_PACKFP) || defined(RMC_EXP_DOUBLE_APPLY)
+// opaque redefinition of a Work's registers (cost-attribution experiments only)
+template <class S>
+__device__ __forceinline__ void exp_launder(typename S::Work& s) {
+  asm volatile("" : "+v"(s.term), "+v"(s.st), "+v"(s.voted), "+v"(s.commit), "+v"(s.vresp), "+v"(s.vgrant));
+#pragma unroll
+  for (int i = 0; i < S::N; ++i) asm volatile("" : "+v"(s.nexti.v[i]), "+v"(s.matchi.v[i]), "+v"(s.log.v[i]), "+v"(s.vl.v[i]));
+#pragma unroll
+  for (int q = 0; q < S::AW; ++q) asm volatile("" : "+v"(s.allLogs[q]));
+#pragma unroll
+  for (int q = 0; q < S::EMAX; ++q) asm volatile("" : "+v"(s.el[q]));
+#pragma unroll
+  for (int q = 0; q < S::MK + 1; ++q) asm volatile("" : "+v"(s.bag.v[q]));
+}
+#endif
+
 // One lane per frontier state, a wave-uniform loop over the action instances; successor,
 // constraints, TLC generated counts, out-of-model invariants, canonical pack and FP64 in one
 // pass.  (A split expand + full-lane fingerprint pipeline measured 51.4 vs 49.4 ms/run on C2:
@@ -161,6 +177,14 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
     if (active) {
       W t;
       const int act = S::apply(s, k, t, err);
+#ifdef RMC_EXP_DOUBLE_APPLY
+      {   // cost-attribution experiment: apply a second time on a laundered copy (same result)
+        W s2 = s, t2;
+        exp_launder<S>(s2);
+        u32 e2 = 0;
+        if (S::apply(s2, k, t2, e2) != act) err |= e2 | 1u;
+      }
+#endif
       if (act >= 0) {
 #pragma unroll
         for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
@@ -173,6 +197,16 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
           S::pack(t, pw);
           if constexpr (INC) fp = fb.fp(pw, bw, a.seed);
           else fp = fp64(pw, a.seed);
+#ifdef RMC_EXP_DOUBLE_PACKFP
+          {   // cost-attribution experiment: pack + fingerprint a second time (laundered, same value)
+            W t2 = t;
+            exp_launder<S>(t2);
+            u32 pw2[NW];
+            S::pack(t2, pw2);
+            const u64 fp2 = INC ? fb.fp(pw2, bw, a.seed) : fp64(pw2, a.seed);
+            if (fp2 != fp) fp = 0;
+          }
+#endif
         } else if (a.inv_oom && S::violated(t, a.rt.invariants)) {
           // TLC checks invariants on out-of-model successors ([ext] switch (ii)); first in key order wins
           const u64 e = ev_word(gid, (u32)k, EV_VIOLATION);

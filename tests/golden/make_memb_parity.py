@@ -36,7 +36,7 @@ CASES = {
     "memb_dynamic3@14": ("memb_dynamic3", 14),
     "memb_nosym@13": ("memb_nosym", 13),
     "memb_four@10": ("memb_four", 10),
-    "memb_four@23": ("memb_four", 23),   # >= 1e5 states: signature ties in the 4-server refinement
+    "memb_four@16": ("memb_four", 16),   # >= 1e5 states: signature ties in the 4-server refinement
     "scen_FirstBecomeLeader": ("scen_FirstBecomeLeader", 0),
     "scen_FirstCommit": ("scen_FirstCommit", 0),
     "scen_EntryCommitted": ("scen_EntryCommitted", 0),
