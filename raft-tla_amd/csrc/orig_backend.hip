@@ -2302,7 +2302,8 @@ class OrigGpu : public Backend {
   X(2, 1, 2, 1, 6)          \
   X(2, 1, 3, 2, 5)          \
   X(2, 2, 3, 2, 6)          \
-  X(5, 1, 3, 3, 4) /* C5 */
+  X(5, 1, 3, 3, 4) /* C5 */ \
+  X(5, 2, 3, 3, 8) /* C5 with 2 values and 8 messages (compact election records) */
 #endif
 
 static Backend* orig_factory(const OrigModel& m) {

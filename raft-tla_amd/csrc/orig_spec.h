@@ -83,7 +83,18 @@ struct Orig {
   static constexpr int BODY = BODY_A > BODY_B ? BODY_A : BODY_B;
   static constexpr int MSGB = 2 + BODY;
   static constexpr int ENTB = MSGB + CNTB;          // bag entry width
-  static constexpr int ELB = TB + SB + LIB + N + N * VLB;   // election record width
+  // election record [eterm, eleader, elog, evotes, evoterLog] (raft_original.tla:236-241).  When
+  // the full voterLog row does not fit 64 bits (5 servers with 2 values: 69 bits), the row's
+  // per-cell presence bits are left out: DOMAIN voterLog[i] = votesGranted[i] in every reachable
+  // state (both change together in HandleRequestVoteResponse :313-318 and are emptied together by
+  // Init, Restart and Timeout), so evotes already holds them; BecomeLeader checks the identity
+  // and raises a capacity error if it ever failed (never a silent loss).
+  // The compact form also stores eterm in bits_for(MT): BecomeLeader's parent is in the model, so
+  // its term is <= MaxTerm (checked, like the voterLog identity).
+  static constexpr bool ECOMPACT = TB + SB + LIB + N + N * VLB > 64;
+  static constexpr int ETB = ECOMPACT ? bits_for(MT) : TB;        // eterm in a record
+  static constexpr int EVB = ECOMPACT ? LIB : VLB;                // evoterLog cell in a record
+  static constexpr int ELB = ETB + SB + LIB + N + N * EVB;        // election record width
   // ---- packed (stored) layout
   static constexpr int PBITS = N * TB + N * 2 + N * VB + N * CIB + N * N + N * N + N * N * NIB + N * N * CIB +
                                N * (SLLB + ML * EB) + N * N * VLB + (int)U + EMAX * ELB + MK * ENTB;
@@ -95,7 +106,8 @@ struct Orig {
   static_assert(N * NIB <= 32 && N * CIB <= 32, "index rows");
   static_assert(LLB + (ML + 1) * EB <= 32, "working log word");
   static_assert(N * VLB <= 64, "voterLog row");
-  static_assert(MSGB + CNTB <= 64 && ELB <= 64, "message / election codes");
+  static_assert(MSGB + CNTB <= 64, "message codes");
+  static_assert(ELB <= 64, "election codes");
 
   struct Work {
     u32 term, st, voted, commit, vresp, vgrant;
@@ -329,8 +341,9 @@ struct Orig {
       const u32 li = sel(s.log, i);
       put(t.nexti, i, fsplat<NIB, u32>((u32)(llen(li) + 1), N));
       put(t.matchi, i, (u32)0);
-      const u64 rec = (u64)g_term(s, i) | ((u64)i << TB) | ((u64)lidx(li) << (TB + SB)) | ((u64)vg << (TB + SB + LIB)) |
-                      (sel(s.vl, i) << (TB + SB + LIB + N));
+      if (g_term(s, i) > (int)lomask(ETB)) err |= OE_CAP_ELECTIONS;
+      const u64 rec = (u64)g_term(s, i) | ((u64)i << ETB) | ((u64)lidx(li) << (ETB + SB)) | ((u64)vg << (ETB + SB + LIB)) |
+                      (evoter_code(sel(s.vl, i), vg, err) << (ETB + SB + LIB + N));
       set_insert(t.el, rec, err);
       return OA_BecomeLeader;
     }
@@ -400,6 +413,28 @@ struct Orig {
     }
   }
 
+  // the evoterLog field of an election record from voterLog[i]'s row (see ECOMPACT)
+  RMC_HD static u64 evoter_code(u64 row, u32 vg, u32& err) {
+    if constexpr (!ECOMPACT) { (void)vg; (void)err; return row; }
+    u64 c = 0;
+    u32 pres = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      pres |= (u32)((row >> (j * VLB)) & 1ull) << j;
+      c |= ((row >> (j * VLB + 1)) & lomask(LIB)) << (j * LIB);
+    }
+    if (pres != vg) err |= OE_CAP_ELECTIONS;
+    return c;
+  }
+  // ... and back to a voterLog row (text, traces)
+  RMC_HD static u64 evoter_row(u64 code, u32 evotes) {
+    if constexpr (!ECOMPACT) { (void)evotes; return code; }
+    u64 row = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      if ((evotes >> j) & 1u) row |= ((((code >> (j * LIB)) & lomask(LIB)) << 1) | 1ull) << (j * VLB);
+    return row;
+  }
   RMC_HD static void set_insert(u64 (&el)[EMAX], u64 x, u32& err) {   // elections' = elections \cup {x}
     bool found = false;
 #pragma unroll
@@ -516,8 +551,8 @@ struct Orig {
       for (int a = 0; a < EMAX; ++a)
 #pragma unroll
         for (int b = a + 1; b < EMAX; ++b)
-          if (t.el[a] != EMPTY && t.el[b] != EMPTY && (t.el[a] & lomask(TB)) == (t.el[b] & lomask(TB)) &&
-              ((t.el[a] >> TB) & lomask(SB)) != ((t.el[b] >> TB) & lomask(SB)))
+          if (t.el[a] != EMPTY && t.el[b] != EMPTY && (t.el[a] & lomask(ETB)) == (t.el[b] & lomask(ETB)) &&
+              ((t.el[a] >> ETB) & lomask(SB)) != ((t.el[b] >> ETB) & lomask(SB)))
             ok = false;
       if (!ok) bad |= OI_ElectionSafety;
     }

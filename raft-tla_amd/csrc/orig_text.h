@@ -109,7 +109,8 @@ struct OrigText {
         const u64 e = s.el[k];
         int off = 0;
         auto take = [&](int w) { u64 x = (e >> off) & lomask(w); off += w; return x; };
-        const u64 et = take(S::TB), el = take(S::SB), elog = take(S::LIB), ev = take(S::N), evl = take(S::N * S::VLB);
+        const u64 et = take(S::ETB), el = take(S::SB), elog = take(S::LIB), ev = take(S::N);
+        const u64 evl = S::evoter_row(take(S::N * S::EVB), (u32)ev);
         xs.push_back(record({{"eterm", std::to_string(et)}, {"eleader", sv((int)el)}, {"elog", log_text(S::lfrom_idx((u32)elog))},
                              {"evotes", server_set((u32)ev)}, {"evoterLog", voterlog_text(evl)}}));
       }
