@@ -43,6 +43,7 @@
 #include "../../include/raftmc.h"
 #include "backend.h"
 #include "fp_gap.h"
+#include "host_store.h"
 #include "memb_prefix.h"
 #include "memb_spec.h"
 #include "memb_text.h"
@@ -788,7 +789,7 @@ class MembGpu : public Backend {
     r.kernels = {{"memb_expand", 0, 0, 0}, {"memb_fingerprint", 0, 0, 0}, {"memb_dedup", 0, 0, 0},
                  {"memb_select", 0, 0, 0}, {"memb_compact", 0, 0, 0}, {"memb_materialize", 0, 0, 0}};
     const MembRuntime& rt = rt_host_;
-    base_ = 0; host_states_.clear(); host_meta_.clear();
+    base_ = 0; host_.clear();
     u64 level_begin = 0, level_count = 1;
     u32 level = 0;
 
@@ -992,7 +993,7 @@ class MembGpu : public Backend {
               std::fwrite(r.act_generated.data(), 8, MA_NACT, f) == (size_t)MA_NACT &&
               std::fwrite(r.act_distinct.data(), 8, MA_NACT, f) == (size_t)MA_NACT;
     for (const auto& lv : r.levels) ok = ok && std::fwrite(&lv.states, 8, 1, f) == 1 && std::fwrite(&lv.generated, 8, 1, f) == 1;
-    ok = ok && std::fwrite(host_states_.data(), 4, base_ * NWP, f) == base_ * NWP;
+    ok = ok && host_.write_states(f);
     std::vector<u32> blk;
     for (u64 b = base_; ok && b < total_; b += kCkptBlock) {
       const u64 n = std::min<u64>(kCkptBlock, total_ - b);
@@ -1000,7 +1001,7 @@ class MembGpu : public Backend {
       ok = hipMemcpy(blk.data(), d_states_ + (b - base_) * NWP, n * NWP * 4, hipMemcpyDeviceToHost) == hipSuccess &&
            std::fwrite(blk.data(), 4, n * NWP, f) == n * NWP;
     }
-    ok = ok && std::fwrite(host_meta_.data(), 8, base_, f) == base_;
+    ok = ok && host_.write_meta(f);
     std::vector<u64> mblk;
     for (u64 b = base_; ok && b < total_; b += kCkptBlock) {
       const u64 n = std::min<u64>(kCkptBlock, total_ - b);
@@ -1038,12 +1039,14 @@ class MembGpu : public Backend {
     HIPCHK(hipStreamSynchronize(stream_));
     // states: the host part stays on the host and its fingerprints go in through the (idle)
     // candidate buffer; the device part is read block by block into the store
-    host_states_.resize(lb * NWP);
-    ok = ok && std::fread(host_states_.data(), 4, lb * NWP, f) == lb * NWP;
+    host_.clear();
+    u32* hs = nullptr; u64* hm = nullptr;
+    if (lb) host_.append(lb, &hs, &hm);
+    ok = ok && std::fread(hs, 4, lb * NWP, f) == lb * NWP;
     const u64 stage = std::max<u64>(1, chunk_ * S::NSLOT * 8 / (NWP * 4));
     for (u64 b = 0; ok && b < lb; b += stage) {
       const u64 n = std::min<u64>(stage, lb - b);
-      HIPCHK(hipMemcpy(d_cand_, host_states_.data() + b * NWP, n * NWP * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(d_cand_, hs + b * NWP, n * NWP * 4, hipMemcpyHostToDevice));
       if (int rc = launch_reinsert((const u32*)d_cand_, n, h.seed, err)) return rc;
       HIPCHK(hipStreamSynchronize(stream_));
     }
@@ -1054,8 +1057,7 @@ class MembGpu : public Backend {
       ok = std::fread(blk.data(), 4, n * NWP, f) == n * NWP;
       if (ok) HIPCHK(hipMemcpy(d_states_ + (b - lb) * NWP, blk.data(), n * NWP * 4, hipMemcpyHostToDevice));
     }
-    host_meta_.resize(lb);
-    ok = ok && std::fread(host_meta_.data(), 8, lb, f) == lb;
+    ok = ok && std::fread(hm, 8, lb, f) == lb;
     std::vector<u64> mblk;
     for (u64 b = lb; ok && b < h.total; b += kCkptBlock) {
       const u64 n = std::min<u64>(kCkptBlock, h.total - b);
@@ -1064,7 +1066,7 @@ class MembGpu : public Backend {
       if (ok) HIPCHK(hipMemcpy(d_meta_ + (b - lb), mblk.data(), n * 8, hipMemcpyHostToDevice));
     }
     std::fclose(f);
-    if (!ok) { host_states_.clear(); host_meta_.clear(); err = "checkpoint " + path + " is truncated"; return MC_E_IO; }
+    if (!ok) { host_.clear(); err = "checkpoint " + path + " is truncated"; return MC_E_IO; }
     if (h.total > lb)
       if (int rc = launch_reinsert(d_states_, h.total - lb, h.seed, err)) return rc;
     u64 e = 0;
@@ -1092,12 +1094,11 @@ class MembGpu : public Backend {
   // overlaps blocks already moved)
   int spill(u64 level_begin, u64 level_count, std::string& err) {
     const u64 d = level_begin - base_;
-    const u64 h0 = host_meta_.size();
-    host_states_.resize((h0 + d) * NWP);
-    host_meta_.resize(h0 + d);
+    u32* hs = nullptr; u64* hm = nullptr;
+    host_.append(d, &hs, &hm);   // a segment of its own: the host part is never reallocated
     HIPCHK(hipStreamSynchronize(stream_));
-    HIPCHK(hipMemcpy(host_states_.data() + h0 * NWP, d_states_, d * NWP * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(host_meta_.data() + h0, d_meta_, d * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hs, d_states_, d * NWP * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hm, d_meta_, d * 8, hipMemcpyDeviceToHost));
     for (u64 off = 0; off < level_count; off += d) {
       const u64 n = std::min<u64>(d, level_count - off);
       HIPCHK(hipMemcpyAsync(d_states_ + off * NWP, d_states_ + (d + off) * NWP, n * NWP * 4, hipMemcpyDeviceToDevice, stream_));
@@ -1174,7 +1175,7 @@ class MembGpu : public Backend {
     if (!f) { err = "cannot write " + path; return MC_E_IO; }
     for (u64 g = 0; g < total_; ++g) {
       u32 w[NWP];
-      const u32* src = g < base_ ? host_states_.data() + g * NWP : h.data() + (g - base_) * NWP;
+      const u32* src = g < base_ ? host_.state(g) : h.data() + (g - base_) * NWP;
       for (int q = 0; q < NWP; ++q) w[q] = src[q];
       W s; S::unpack(w, s);
       std::fprintf(f, "%s\n", text_.text(s, false).c_str());
@@ -1190,7 +1191,7 @@ class MembGpu : public Backend {
   // all-to-all / store that gives every rank an equal contiguous slice of the next level.
   int shard_open(const RunOpts& o, int rank, int world, std::string& err) override {
     if (world < 1 || world > 8 || rank < 0 || rank >= world) { err = "world must be 1..8"; return MC_E_INVALID; }
-    base_ = 0; host_states_.clear(); host_meta_.clear();   // sharded runs keep every state on the device
+    base_ = 0; host_.clear();   // sharded runs keep every state on the device
     for (int q = 0; q < 2; ++q)
       if (((m_.rt.constraints >> kPrefixCon[q]) & 1u) && !have_prefix_[q]) {
         err = std::string(kMembConNames[kPrefixCon[q]]) + " needs its golden history trace (mc_set_history_prefix)";
@@ -1578,10 +1579,9 @@ class MembGpu : public Backend {
   hipEvent_t ev_[9] = {};
   u64 table_mask_ = 0, cap_ = 0, total_ = 0, chunk_ = 0;
   int dev_ = -1; uint64_t req_table_ = 0, req_store_ = 0;
-  // completed levels moved to host memory: global ids [0, base_) live in host_states_/host_meta_
+  // completed levels moved to host memory: global ids [0, base_) live in host_ (segments)
   u64 base_ = 0;
-  std::vector<u32> host_states_;
-  std::vector<u64> host_meta_;
+  HostStore host_{NWP};
 
   // sharded mode
   RunOpts sopts_;
@@ -1622,8 +1622,8 @@ class MembGpu : public Backend {
   void read_state(u64 gid, W& s, u64* meta = nullptr) const {
     u32 w[NWP];
     if (gid < base_) {
-      std::memcpy(w, host_states_.data() + gid * NWP, NWP * 4);
-      if (meta) *meta = host_meta_[gid];
+      std::memcpy(w, host_.state(gid), NWP * 4);
+      if (meta) *meta = host_.meta(gid);
     } else {
       (void)hipMemcpy(w, d_states_ + (gid - base_) * NWP, NWP * 4, hipMemcpyDeviceToHost);
       if (meta) (void)hipMemcpy(meta, d_meta_ + (gid - base_), 8, hipMemcpyDeviceToHost);

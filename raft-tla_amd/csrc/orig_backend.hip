@@ -50,6 +50,7 @@
 #include "../../include/raftmc.h"
 #include "backend.h"
 #include "fp_gap.h"
+#include "host_store.h"
 #include "orig_spec.h"
 #include "orig_text.h"
 #include "rccl_api.h"
@@ -1279,7 +1280,7 @@ class OrigGpu : public Backend {
     for (int k = 0; k < OA_NACT; ++k) r.action_names.push_back(kOrigActNames[k]);
     r.act_generated.assign(OA_NACT, 0); r.act_distinct.assign(OA_NACT, 0);
     r.kernels = {{"orig_generate", 0, 0, 0}, {"orig_merge_probe", 0, 0, 0}, {"orig_mark_scan", 0, 0, 0}, {"orig_materialize", 0, 0, 0}};
-    base_ = 0; host_states_.clear(); host_meta_.clear();
+    base_ = 0; host_.clear();
 
     W s0; S::init(s0);
     const u64 S_B = NWP * 4;
@@ -1591,7 +1592,7 @@ class OrigGpu : public Backend {
     // the host part straight from host memory, the device part in bounded blocks (no second copy
     // of the store in host memory)
     constexpr u64 BLK = 1u << 20;
-    ok = ok && std::fwrite(host_states_.data(), 4, base_ * NWP, f) == base_ * NWP;
+    ok = ok && host_.write_states(f);
     std::vector<u32> blk;
     for (u64 b = base_; ok && b < total_; b += BLK) {
       const u64 n = std::min<u64>(BLK, total_ - b);
@@ -1599,7 +1600,7 @@ class OrigGpu : public Backend {
       ok = hipMemcpy(blk.data(), d_states_ + (b - base_) * NWP, n * NWP * 4, hipMemcpyDeviceToHost) == hipSuccess &&
            std::fwrite(blk.data(), 4, n * NWP, f) == n * NWP;
     }
-    ok = ok && std::fwrite(host_meta_.data(), 8, base_, f) == base_;
+    ok = ok && host_.write_meta(f);
     std::vector<u64> mblk;
     for (u64 b = base_; ok && b < total_; b += BLK) {
       const u64 n = std::min<u64>(BLK, total_ - b);
@@ -1632,17 +1633,36 @@ class OrigGpu : public Backend {
       ok = std::fread(&lv.states, 8, 1, f) == 1 && std::fread(&lv.generated, 8, 1, f) == 1;
       r.levels.push_back(lv);
     }
-    std::vector<u32> st(h.total * NWP);
-    std::vector<u64> me(h.total);
-    ok = ok && std::fread(st.data(), 4, st.size(), f) == st.size() && std::fread(me.data(), 8, me.size(), f) == me.size();
+    // streamed: the host part into one host segment, the device part block by block into the
+    // store (no second copy of the checkpoint in host memory)
+    host_.clear();
+    u32* hs = nullptr; u64* hm = nullptr;
+    if (lb) host_.append(lb, &hs, &hm);
+    ok = ok && std::fread(hs, 4, lb * NWP, f) == lb * NWP;
+    constexpr u64 BLK = 1u << 20;
+    std::vector<u32> blk;
+    for (u64 b = lb; ok && b < h.total; b += BLK) {
+      const u64 n = std::min<u64>(BLK, h.total - b);
+      blk.resize(n * NWP);
+      ok = std::fread(blk.data(), 4, n * NWP, f) == n * NWP &&
+           hipMemcpy(d_states_ + (b - lb) * NWP, blk.data(), n * NWP * 4, hipMemcpyHostToDevice) == hipSuccess;
+    }
+    ok = ok && std::fread(hm, 8, lb, f) == lb;
+    std::vector<u64> mblk;
+    for (u64 b = lb; ok && b < h.total; b += BLK) {
+      const u64 n = std::min<u64>(BLK, h.total - b);
+      mblk.resize(n);
+      ok = std::fread(mblk.data(), 8, n, f) == n &&
+           hipMemcpy(d_meta_ + (b - lb), mblk.data(), n * 8, hipMemcpyHostToDevice) == hipSuccess;
+    }
     std::fclose(f);
-    if (!ok) { err = "checkpoint " + path + " is truncated"; return MC_E_IO; }
+    if (!ok) { host_.clear(); err = "checkpoint " + path + " is truncated"; return MC_E_IO; }
     HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
     // the host part's fingerprints go in through the (idle) candidate buffer, chunk by chunk
     const u64 stage = std::max<u64>(1, chunk_states_ * S::NI * 8 / (NWP * 4));
     for (u64 b = 0; b < lb; b += stage) {
       const u64 n = std::min<u64>(stage, lb - b);
-      HIPCHK(hipMemcpy(d_rfp_, st.data() + b * NWP, n * NWP * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(d_rfp_, hs + b * NWP, n * NWP * 4, hipMemcpyHostToDevice));
       if (last_fifo_)
         hipLaunchKernelGGL((orig_reinsert<S, 2>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_,
                            (const u32*)d_rfp_, n, d_table_, table_mask_, (u64)h.seed, (unsigned long long*)d_ctr_);
@@ -1652,8 +1672,6 @@ class OrigGpu : public Backend {
       HIPCHK(hipGetLastError());
       HIPCHK(hipStreamSynchronize(stream_));
     }
-    HIPCHK(hipMemcpy(d_states_, st.data() + lb * NWP, (h.total - lb) * NWP * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d_meta_, me.data() + lb, (h.total - lb) * 8, hipMemcpyHostToDevice));
     if (h.total > lb) {
       if (last_fifo_)
         hipLaunchKernelGGL((orig_reinsert<S, 2>), dim3((unsigned)((h.total - lb + BS - 1) / BS)), dim3(BS), 0, stream_,
@@ -1663,8 +1681,6 @@ class OrigGpu : public Backend {
                            (const u32*)d_states_, (u64)(h.total - lb), d_table_, 2 * table_mask_ + 1, (u64)h.seed, (unsigned long long*)d_ctr_);
       HIPCHK(hipGetLastError());
     }
-    host_states_.assign(st.begin(), st.begin() + lb * NWP);
-    host_meta_.assign(me.begin(), me.begin() + lb);
     base_ = lb;
     u64 e = 0;
     HIPCHK(hipMemcpyAsync(&e, d_ctr_ + K_ERR, 8, hipMemcpyDeviceToHost, stream_));
@@ -1679,7 +1695,7 @@ class OrigGpu : public Backend {
   int dump_states(const std::string& path, std::string& err) override {
     if (!d_states_) { err = "mc_dump_states before mc_run"; return MC_E_STATE; }
     std::vector<u32> h(total_ * NWP);
-    std::memcpy(h.data(), host_states_.data(), base_ * NWP * 4);
+    host_.for_each_segment([&](u64 g0, u64 n, const u32* st, const u64*) { std::memcpy(h.data() + g0 * NWP, st, n * NWP * 4); });
     HIPCHK(hipMemcpy(h.data() + base_ * NWP, d_states_, (total_ - base_) * NWP * 4, hipMemcpyDeviceToHost));
     FILE* f = std::fopen(path.c_str(), "w");
     if (!f) { err = "cannot write " + path; return MC_E_IO; }
@@ -1716,7 +1732,7 @@ class OrigGpu : public Backend {
     u32 w0[S::NW]; S::pack(s0, w0);
     const u64 fp0 = fp64(w0, sres_.seed);
     total_ = 0; sh_level_begin_ = 0; sh_level_count_ = 0; sh_new_ = 0;
-    base_ = 0; host_states_.clear(); host_meta_.clear();
+    base_ = 0; host_.clear();
     if ((int)fp_owner(fp0, (u32)world) == rank) {
       u32 wp[NWP] = {0}; for (int q = 0; q < S::NW; ++q) wp[q] = w0[q];
       HIPCHK(hipMemcpy(d_table_ + (fp0 & sh_table_mask()), &fp0, 8, hipMemcpyHostToDevice));
@@ -2191,10 +2207,9 @@ class OrigGpu : public Backend {
   u64 nat_recv_cap_ = 0, nat_acks_cap_ = 0, nat_stin_cap_ = 0;
   std::vector<hipEvent_t> nat_ev_;
   std::vector<hipEvent_t> lvl_ev_;
-  // completed levels moved to host memory: global ids [0, base_) live in host_states_/host_meta_
+  // completed levels moved to host memory: global ids [0, base_) live in host_ (segments)
   u64 base_ = 0;
-  std::vector<u32> host_states_;
-  std::vector<u64> host_meta_;
+  HostStore host_{NWP};
 
   void release() {
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_stop_, (void*)d_rfp_, (void*)d_rkey_,
@@ -2235,8 +2250,8 @@ class OrigGpu : public Backend {
   // stored state `gid` (global id) and its parent pointer, from the host part or the device
   bool stored_state(u64 gid, u32 (&w)[NWP], u64& meta) const {
     if (gid < base_) {
-      std::memcpy(w, host_states_.data() + gid * NWP, NWP * 4);
-      meta = host_meta_[gid];
+      std::memcpy(w, host_.state(gid), NWP * 4);
+      meta = host_.meta(gid);
       return true;
     }
     const u64 d = gid - base_;
@@ -2249,12 +2264,11 @@ class OrigGpu : public Backend {
   // only overlaps blocks already moved)
   int spill(u64 level_begin, u64 level_count, std::string& err) {
     const u64 d = level_begin - base_;
-    const u64 h0 = host_meta_.size();
-    host_states_.resize((h0 + d) * NWP);
-    host_meta_.resize(h0 + d);
+    u32* hs = nullptr; u64* hm = nullptr;
+    host_.append(d, &hs, &hm);   // a segment of its own: the host part is never reallocated
     HIPCHK(hipStreamSynchronize(stream_));
-    HIPCHK(hipMemcpy(host_states_.data() + h0 * NWP, d_states_, d * NWP * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(host_meta_.data() + h0, d_meta_, d * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hs, d_states_, d * NWP * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hm, d_meta_, d * 8, hipMemcpyDeviceToHost));
     for (u64 off = 0; off < level_count; off += d) {
       const u64 n = std::min<u64>(d, level_count - off);
       HIPCHK(hipMemcpyAsync(d_states_ + off * NWP, d_states_ + (d + off) * NWP, n * NWP * 4, hipMemcpyDeviceToDevice, stream_));
