@@ -18,6 +18,8 @@
 // bit order; equal TLA+ states <=> equal packed words (sets/bags sorted,
 // unused slots zero).  Semantics cite raft_original.tla line numbers.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 
 namespace rmc {
@@ -83,6 +85,7 @@ struct Orig {
   static constexpr int BODY = BODY_A > BODY_B ? BODY_A : BODY_B;
   static constexpr int MSGB = 2 + BODY;
   static constexpr int ENTB = MSGB + CNTB;          // bag entry width
+  using BE = typename std::conditional<(ENTB <= 31), u32, u64>::type;   // bag entry register type
   // election record [eterm, eleader, elog, evotes, evoterLog] (raft_original.tla:236-241).  When
   // the full voterLog row does not fit 64 bits (5 servers with 2 values: 69 bits), the row's
   // per-cell presence bits are left out: DOMAIN voterLog[i] = votesGranted[i] in every reachable
@@ -115,7 +118,7 @@ struct Orig {
     Arr<u64, N> vl;
     u64 allLogs[AW];
     u64 el[EMAX];
-    Arr<u64, MK + 1> bag;
+    Arr<BE, MK + 1> bag;
   };
   static constexpr u32 F = 0, C = 1, L = 2;   // Follower, Candidate, Leader
 
@@ -218,29 +221,31 @@ struct Orig {
     b = (b << CIB) | (u64)mmi; b = (b << SB) | (u64)src; b = (b << 1) | (u64)success; b = (b << TB) | (u64)term;
     return ((u64)AEP << BODY) | b;
   }
-  // bag entries: code << CNTB | (count + 8); ~0 = empty; kept sorted ascending
+  // bag entries: code << CNTB | (count + 8); all ones = empty; kept sorted ascending.  32-bit
+  // entries when they fit (C2: 29 bits), halving the bag's compare / select work
   static constexpr u64 EMPTY = ~0ull;
-  RMC_HD static u64 ecode_of(u64 ent) { return ent >> CNTB; }
-  RMC_HD static int ecount(u64 ent) { return (int)(ent & lomask(CNTB)) - 8; }
+  static constexpr BE BEMPTY = (BE)~(BE)0;
+  RMC_HD static u64 ecode_of(BE ent) { return (u64)ent >> CNTB; }
+  RMC_HD static int ecount(BE ent) { return (int)((u64)ent & lomask(CNTB)) - 8; }
   // WithMessage (raft_original.tla:106-110)
-  RMC_HD static void with_msg(Arr<u64, MK + 1>& bag, u64 code, u32& err) {
+  RMC_HD static void with_msg(Arr<BE, MK + 1>& bag, u64 code, u32& err) {
     bool found = false;
 #pragma unroll
     for (int k = 0; k < MK + 1; ++k) {
-      if (bag.v[k] != EMPTY && ecode_of(bag.v[k]) == code) {
+      if (bag.v[k] != BEMPTY && ecode_of(bag.v[k]) == code) {
         found = true;
         int c = ecount(bag.v[k]) + 1;
         if (c > 7) err |= OE_CAP_COUNT;
-        bag.v[k] = (code << CNTB) | (u64)(c + 8);
+        bag.v[k] = (BE)((code << CNTB) | (u64)(c + 8));
       }
     }
     if (!found) {
-      const u64 x = (code << CNTB) | (u64)(1 + 8);
-      if (bag.v[MK] != EMPTY) err |= OE_CAP_COUNT;   // cannot happen from an in-model pre-state
-      u64 prev = 0; bool prev_lt = true;
+      const BE x = (BE)((code << CNTB) | (u64)(1 + 8));
+      if (bag.v[MK] != BEMPTY) err |= OE_CAP_COUNT;   // cannot happen from an in-model pre-state
+      BE prev = 0; bool prev_lt = true;
 #pragma unroll
       for (int k = 0; k < MK + 1; ++k) {
-        const u64 cur = bag.v[k];
+        const BE cur = bag.v[k];
         const bool cur_lt = cur < x;
         bag.v[k] = cur_lt ? cur : (prev_lt ? x : prev);
         prev = cur; prev_lt = cur_lt;
@@ -248,13 +253,13 @@ struct Orig {
     }
   }
   // WithoutMessage (raft_original.tla:114-118): decrement, entry stays (G1)
-  RMC_HD static void without_msg(Arr<u64, MK + 1>& bag, u64 code, u32& err) {
+  RMC_HD static void without_msg(Arr<BE, MK + 1>& bag, u64 code, u32& err) {
 #pragma unroll
     for (int k = 0; k < MK + 1; ++k) {
-      if (bag.v[k] != EMPTY && ecode_of(bag.v[k]) == code) {
+      if (bag.v[k] != BEMPTY && ecode_of(bag.v[k]) == code) {
         int c = ecount(bag.v[k]) - 1;
         if (c < -8) err |= OE_CAP_COUNT;
-        bag.v[k] = (code << CNTB) | (u64)(c + 8);
+        bag.v[k] = (BE)((code << CNTB) | (u64)(c + 8));
       }
     }
   }
@@ -278,7 +283,7 @@ struct Orig {
     for (int i = 0; i < N; ++i) { s.nexti.v[i] = fsplat<NIB, u32>(1, N); s.matchi.v[i] = 0; s.log.v[i] = 0; s.vl.v[i] = 0; }
     for (int k = 0; k < AW; ++k) s.allLogs[k] = 0;
     for (int k = 0; k < EMAX; ++k) s.el[k] = EMPTY;
-    for (int k = 0; k < MK + 1; ++k) s.bag.v[k] = EMPTY;
+    for (int k = 0; k < MK + 1; ++k) s.bag.v[k] = BEMPTY;
   }
 
   // allLogs' = allLogs \cup {log[i] : i \in Server} (raft_original.tla:464, G3): same for every successor
@@ -393,21 +398,21 @@ struct Orig {
     }
     k -= N * N;
     if (k < MK) {                                                  // Receive(m) :420-435
-      const u64 ent = sel(s.bag, k);
-      if (ent == EMPTY) return -1;
+      const BE ent = sel(s.bag, k);
+      if (ent == BEMPTY) return -1;
       return receive(s, ecode_of(ent), t, err);
     }
     k -= MK;
     if (k < MK) {                                                  // DuplicateMessage(m) :442-444
-      const u64 ent = sel(s.bag, k);
-      if (ent == EMPTY) return -1;
+      const BE ent = sel(s.bag, k);
+      if (ent == BEMPTY) return -1;
       with_msg(t.bag, ecode_of(ent), err);
       return OA_DuplicateMessage;
     }
     k -= MK;
     {                                                              // DropMessage(m) :447-449
-      const u64 ent = sel(s.bag, k);
-      if (ent == EMPTY) return -1;
+      const BE ent = sel(s.bag, k);
+      if (ent == BEMPTY) return -1;
       without_msg(t.bag, ecode_of(ent), err);
       return OA_DropMessage;
     }
@@ -531,11 +536,11 @@ struct Orig {
       for (int i = 0; i < N; ++i) ok &= llen(t.log.v[i]) <= ML;
     }
     if (rt.constraints & OC_BoundedMessages) {
-      ok &= t.bag.v[MK] == EMPTY;
+      ok &= t.bag.v[MK] == BEMPTY;
 #pragma unroll
       for (int k = 0; k < MK; ++k) {
         const int c = ecount(t.bag.v[k]);
-        ok &= t.bag.v[k] == EMPTY || (c >= rt.min_count && c <= rt.max_count);
+        ok &= t.bag.v[k] == BEMPTY || (c >= rt.min_count && c <= rt.max_count);
       }
     }
     return ok;
@@ -610,7 +615,7 @@ struct Orig {
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) o.put(t.el[k] == EMPTY ? 0ull : t.el[k], ELB);
 #pragma unroll
-    for (int k = 0; k < MK; ++k) o.put(t.bag.v[k] == EMPTY ? 0ull : t.bag.v[k], ENTB);
+    for (int k = 0; k < MK; ++k) o.put(t.bag.v[k] == BEMPTY ? 0ull : (u64)t.bag.v[k], ENTB);
 #pragma unroll
     for (int k = 0; k < NW; ++k) w[k] = o.w[k];
   }
@@ -637,8 +642,8 @@ struct Orig {
 #pragma unroll
     for (int k = 0; k < EMAX; ++k) { const u64 x = in.get(ELB); t.el[k] = x ? x : EMPTY; }
 #pragma unroll
-    for (int k = 0; k < MK; ++k) { const u64 x = in.get(ENTB); t.bag.v[k] = x ? x : EMPTY; }
-    t.bag.v[MK] = EMPTY;
+    for (int k = 0; k < MK; ++k) { const u64 x = in.get(ENTB); t.bag.v[k] = x ? (BE)x : BEMPTY; }
+    t.bag.v[MK] = BEMPTY;
   }
 };
 

@@ -99,7 +99,7 @@ struct OrigText {
     {   // messages
       std::vector<std::string> xs;
       for (int k = 0; k < S::MK + 1; ++k)
-        if (s.bag.v[k] != S::EMPTY) xs.push_back(msg_text(S::ecode_of(s.bag.v[k])) + " :> " + std::to_string(S::ecount(s.bag.v[k])));
+        if (s.bag.v[k] != S::BEMPTY) xs.push_back(msg_text(S::ecode_of(s.bag.v[k])) + " :> " + std::to_string(S::ecount(s.bag.v[k])));
       v.push_back({"messages", xs.empty() ? "<<>>" : join_sorted(xs, "(", " @@ ", ")")});
     }
     {   // elections
