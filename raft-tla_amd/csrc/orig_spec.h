@@ -86,6 +86,8 @@ struct Orig {
   static constexpr int MSGB = 2 + BODY;
   static constexpr int ENTB = MSGB + CNTB;          // bag entry width
   using BE = typename std::conditional<(ENTB <= 31), u32, u64>::type;   // bag entry register type
+  using MC = typename std::conditional<(MSGB <= 32), u32, u64>::type;   // message code register type
+  using VR = typename std::conditional<(N * VLB <= 32), u32, u64>::type;   // voterLog row register type
   // election record [eterm, eleader, elog, evotes, evoterLog] (raft_original.tla:236-241).  When
   // the full voterLog row does not fit 64 bits (5 servers with 2 values: 69 bits), the row's
   // per-cell presence bits are left out: DOMAIN voterLog[i] = votesGranted[i] in every reachable
@@ -115,7 +117,7 @@ struct Orig {
   struct Work {
     u32 term, st, voted, commit, vresp, vgrant;
     Arr<u32, N> nexti, matchi, log;
-    Arr<u64, N> vl;
+    Arr<VR, N> vl;
     u64 allLogs[AW];
     u64 el[EMAX];
     Arr<BE, MK + 1> bag;
@@ -178,57 +180,57 @@ struct Orig {
   // so the class order is RVQ < RVP < AEP (second field name "mla" < "mlo" < "mma") < AEQ (more
   // fields); mtype is constant within a class.  Bodies are MSB-first in field-name order.
   enum { RVQ = 0, RVP = 1, AEP = 2, AEQ = 3 };
-  RMC_HD static int mtype(u64 c) { return (int)(c >> BODY); }
-  RMC_HD static u64 fld(u64 c, int off, int w) { return (c >> off) & lomask(w); }
+  RMC_HD static int mtype(MC c) { return (int)(c >> BODY); }
+  RMC_HD static u32 fld(MC c, int off, int w) { return (u32)((c >> off) & (MC)lomask(w)); }
   // offsets from bit 0 (the last field of each body is its least significant)
-  RMC_HD static int mterm(u64 c) { return (int)fld(c, mtype(c) == RVP ? 1 : 0, TB); }
-  RMC_HD static int msrc(u64 c) { const int t = mtype(c); return (int)fld(c, TB + ((t == RVP || t == AEP) ? 1 : 0), SB); }
-  RMC_HD static int mdst(u64 c) {
+  RMC_HD static int mterm(MC c) { return (int)fld(c, mtype(c) == RVP ? 1 : 0, TB); }
+  RMC_HD static int msrc(MC c) { const int t = mtype(c); return (int)fld(c, TB + ((t == RVP || t == AEP) ? 1 : 0), SB); }
+  RMC_HD static int mdst(MC c) {
     const int t = mtype(c);
     const int off = t == RVQ ? TB + SB + TB + CIB : t == RVP ? 1 + TB + SB + LIB : t == AEP ? TB + 1 + SB + CIB
                                                                                              : TB + SB + TB + CIB + LIB + EB;
     return (int)fld(c, off, SB);
   }
-  RMC_HD static int rvq_llt(u64 c) { return (int)fld(c, TB + SB, TB); }
-  RMC_HD static int rvq_lli(u64 c) { return (int)fld(c, TB + SB + TB, CIB); }
-  RMC_HD static int rvp_granted(u64 c) { return (int)fld(c, 0, 1); }
-  RMC_HD static u32 rvp_log(u64 c) { return (u32)fld(c, 1 + TB + SB, LIB); }
-  RMC_HD static int aep_success(u64 c) { return (int)fld(c, TB, 1); }
-  RMC_HD static int aep_mmi(u64 c) { return (int)fld(c, TB + 1 + SB, CIB); }
-  RMC_HD static int aeq_plt(u64 c) { return (int)fld(c, TB + SB, TB); }
-  RMC_HD static int aeq_pli(u64 c) { return (int)fld(c, TB + SB + TB, CIB); }
-  RMC_HD static u32 aeq_log(u64 c) { return (u32)fld(c, TB + SB + TB + CIB, LIB); }
-  RMC_HD static int aeq_ent(u64 c) { return (int)fld(c, TB + SB + TB + CIB + LIB, EB); }
-  RMC_HD static int aeq_mci(u64 c) { return (int)fld(c, TB + SB + TB + CIB + LIB + EB + SB, CIB); }
-  RMC_HD static u64 m_rvq(int term, int llt, int lli, int src, int dst) {
-    u64 b = (u64)dst;
-    b = (b << CIB) | (u64)lli; b = (b << TB) | (u64)llt; b = (b << SB) | (u64)src; b = (b << TB) | (u64)term;
-    return ((u64)RVQ << BODY) | b;
+  RMC_HD static int rvq_llt(MC c) { return (int)fld(c, TB + SB, TB); }
+  RMC_HD static int rvq_lli(MC c) { return (int)fld(c, TB + SB + TB, CIB); }
+  RMC_HD static int rvp_granted(MC c) { return (int)fld(c, 0, 1); }
+  RMC_HD static u32 rvp_log(MC c) { return (u32)fld(c, 1 + TB + SB, LIB); }
+  RMC_HD static int aep_success(MC c) { return (int)fld(c, TB, 1); }
+  RMC_HD static int aep_mmi(MC c) { return (int)fld(c, TB + 1 + SB, CIB); }
+  RMC_HD static int aeq_plt(MC c) { return (int)fld(c, TB + SB, TB); }
+  RMC_HD static int aeq_pli(MC c) { return (int)fld(c, TB + SB + TB, CIB); }
+  RMC_HD static u32 aeq_log(MC c) { return (u32)fld(c, TB + SB + TB + CIB, LIB); }
+  RMC_HD static int aeq_ent(MC c) { return (int)fld(c, TB + SB + TB + CIB + LIB, EB); }
+  RMC_HD static int aeq_mci(MC c) { return (int)fld(c, TB + SB + TB + CIB + LIB + EB + SB, CIB); }
+  RMC_HD static MC m_rvq(int term, int llt, int lli, int src, int dst) {
+    MC b = (MC)dst;
+    b = (b << CIB) | (MC)lli; b = (b << TB) | (MC)llt; b = (b << SB) | (MC)src; b = (b << TB) | (MC)term;
+    return ((MC)RVQ << BODY) | b;
   }
-  RMC_HD static u64 m_rvp(int term, bool granted, u32 logidx, int src, int dst) {
-    u64 b = (u64)dst;
-    b = (b << LIB) | (u64)logidx; b = (b << SB) | (u64)src; b = (b << TB) | (u64)term; b = (b << 1) | (u64)granted;
-    return ((u64)RVP << BODY) | b;
+  RMC_HD static MC m_rvp(int term, bool granted, u32 logidx, int src, int dst) {
+    MC b = (MC)dst;
+    b = (b << LIB) | (MC)logidx; b = (b << SB) | (MC)src; b = (b << TB) | (MC)term; b = (b << 1) | (MC)granted;
+    return ((MC)RVP << BODY) | b;
   }
-  RMC_HD static u64 m_aeq(int term, int pli, int plt, int entry, u32 logidx, int commit, int src, int dst) {
-    u64 b = (u64)commit;
-    b = (b << SB) | (u64)dst; b = (b << EB) | (u64)entry; b = (b << LIB) | (u64)logidx; b = (b << CIB) | (u64)pli;
-    b = (b << TB) | (u64)plt; b = (b << SB) | (u64)src; b = (b << TB) | (u64)term;
-    return ((u64)AEQ << BODY) | b;
+  RMC_HD static MC m_aeq(int term, int pli, int plt, int entry, u32 logidx, int commit, int src, int dst) {
+    MC b = (MC)commit;
+    b = (b << SB) | (MC)dst; b = (b << EB) | (MC)entry; b = (b << LIB) | (MC)logidx; b = (b << CIB) | (MC)pli;
+    b = (b << TB) | (MC)plt; b = (b << SB) | (MC)src; b = (b << TB) | (MC)term;
+    return ((MC)AEQ << BODY) | b;
   }
-  RMC_HD static u64 m_aep(int term, bool success, int mmi, int src, int dst) {
-    u64 b = (u64)dst;
-    b = (b << CIB) | (u64)mmi; b = (b << SB) | (u64)src; b = (b << 1) | (u64)success; b = (b << TB) | (u64)term;
-    return ((u64)AEP << BODY) | b;
+  RMC_HD static MC m_aep(int term, bool success, int mmi, int src, int dst) {
+    MC b = (MC)dst;
+    b = (b << CIB) | (MC)mmi; b = (b << SB) | (MC)src; b = (b << 1) | (MC)success; b = (b << TB) | (MC)term;
+    return ((MC)AEP << BODY) | b;
   }
   // bag entries: code << CNTB | (count + 8); all ones = empty; kept sorted ascending.  32-bit
   // entries when they fit (C2: 29 bits), halving the bag's compare / select work
   static constexpr u64 EMPTY = ~0ull;
   static constexpr BE BEMPTY = (BE)~(BE)0;
-  RMC_HD static u64 ecode_of(BE ent) { return (u64)ent >> CNTB; }
+  RMC_HD static MC ecode_of(BE ent) { return (MC)(ent >> CNTB); }
   RMC_HD static int ecount(BE ent) { return (int)((u64)ent & lomask(CNTB)) - 8; }
   // WithMessage (raft_original.tla:106-110)
-  RMC_HD static void with_msg(Arr<BE, MK + 1>& bag, u64 code, u32& err) {
+  RMC_HD static void with_msg(Arr<BE, MK + 1>& bag, MC code, u32& err) {
     bool found = false;
 #pragma unroll
     for (int k = 0; k < MK + 1; ++k) {
@@ -236,11 +238,11 @@ struct Orig {
         found = true;
         int c = ecount(bag.v[k]) + 1;
         if (c > 7) err |= OE_CAP_COUNT;
-        bag.v[k] = (BE)((code << CNTB) | (u64)(c + 8));
+        bag.v[k] = (BE)(((BE)code << CNTB) | (BE)(c + 8));
       }
     }
     if (!found) {
-      const BE x = (BE)((code << CNTB) | (u64)(1 + 8));
+      const BE x = (BE)(((BE)code << CNTB) | (BE)(1 + 8));
       if (bag.v[MK] != BEMPTY) err |= OE_CAP_COUNT;   // cannot happen from an in-model pre-state
       BE prev = 0; bool prev_lt = true;
 #pragma unroll
@@ -253,13 +255,13 @@ struct Orig {
     }
   }
   // WithoutMessage (raft_original.tla:114-118): decrement, entry stays (G1)
-  RMC_HD static void without_msg(Arr<BE, MK + 1>& bag, u64 code, u32& err) {
+  RMC_HD static void without_msg(Arr<BE, MK + 1>& bag, MC code, u32& err) {
 #pragma unroll
     for (int k = 0; k < MK + 1; ++k) {
       if (bag.v[k] != BEMPTY && ecode_of(bag.v[k]) == code) {
         int c = ecount(bag.v[k]) - 1;
         if (c < -8) err |= OE_CAP_COUNT;
-        bag.v[k] = (BE)((code << CNTB) | (u64)(c + 8));
+        bag.v[k] = (BE)(((BE)code << CNTB) | (BE)(c + 8));
       }
     }
   }
@@ -310,7 +312,7 @@ struct Orig {
       const int i = k;
       fset<2>(t.st, i, F);
       set_row_bits(t.vresp, i, 0); set_row_bits(t.vgrant, i, 0);
-      put(t.vl, i, (u64)0);
+      put(t.vl, i, (VR)0);
       put(t.nexti, i, fsplat<NIB, u32>(1, N));
       put(t.matchi, i, (u32)0);
       fset<CIB>(t.commit, i, 0u);
@@ -324,7 +326,7 @@ struct Orig {
       fset<TB>(t.term, i, (u32)(g_term(s, i) + 1));
       fset<VB>(t.voted, i, (u32)N);
       set_row_bits(t.vresp, i, 0); set_row_bits(t.vgrant, i, 0);
-      put(t.vl, i, (u64)0);
+      put(t.vl, i, (VR)0);
       return OA_Timeout;
     }
     k -= N;
@@ -348,7 +350,7 @@ struct Orig {
       put(t.matchi, i, (u32)0);
       if (g_term(s, i) > (int)lomask(ETB)) err |= OE_CAP_ELECTIONS;
       const u64 rec = (u64)g_term(s, i) | ((u64)i << ETB) | ((u64)lidx(li) << (ETB + SB)) | ((u64)vg << (ETB + SB + LIB)) |
-                      (evoter_code(sel(s.vl, i), vg, err) << (ETB + SB + LIB + N));
+                      (evoter_code((u64)sel(s.vl, i), vg, err) << (ETB + SB + LIB + N));
       set_insert(t.el, rec, err);
       return OA_BecomeLeader;
     }
@@ -456,7 +458,7 @@ struct Orig {
   }
 
   // Receive(m): UpdateTerm excludes every handler (they need mterm <= currentTerm), so <= 1 successor.
-  RMC_HD static int receive(const Work& s, u64 m, Work& t, u32& err) {
+  RMC_HD static int receive(const Work& s, MC m, Work& t, u32& err) {
     const int i = mdst(m), j = msrc(m), mt = mterm(m), ct = g_term(s, i), ty = mtype(m);
     if (mt > ct) {                                                 // UpdateTerm :405-411
       fset<TB>(t.term, i, (u32)mt);
@@ -481,9 +483,9 @@ struct Orig {
       set_row_bits(t.vresp, i, row_bits(s.vresp, i) | (1u << j));                 // HandleRequestVoteResponse :306-320
       if (rvp_granted(m)) {
         set_row_bits(t.vgrant, i, row_bits(s.vgrant, i) | (1u << j));
-        u64 row = sel(s.vl, i);
+        VR row = sel(s.vl, i);
         if (!((row >> (j * VLB)) & 1ull))                                         // voterLog[i] @@ (j :> m.mlog): left-biased
-          row |= (((u64)rvp_log(m) << 1) | 1ull) << (j * VLB);
+          row |= (VR)((((u64)rvp_log(m) << 1) | 1ull) << (j * VLB));
         put(t.vl, i, row);
       }
       without_msg(t.bag, m, err);
@@ -636,7 +638,7 @@ struct Orig {
       t.log.v[i] = len | (ents << LLB);
     }
 #pragma unroll
-    for (int i = 0; i < N; ++i) t.vl.v[i] = in.get(N * VLB);
+    for (int i = 0; i < N; ++i) t.vl.v[i] = (VR)in.get(N * VLB);
 #pragma unroll
     for (int k = 0; k < AW; ++k) t.allLogs[k] = in.get((k == AW - 1) ? (int)(U - 64 * (AW - 1)) : 64);
 #pragma unroll
