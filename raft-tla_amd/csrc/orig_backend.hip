@@ -175,6 +175,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
   for (int k = 0; k < S::NI; ++k) {
     u64 fp = 0;
     bool have = false;
+    int cnt_act = -1;   // this lane's successor action (RMC_GEN_WAVE_COUNTS: counted per wave)
     if (active) {
       W t;
       const int act = S::apply(s, k, t, err);
@@ -190,7 +191,11 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
 #pragma unroll
         for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
         ++nsucc;
+#ifdef RMC_GEN_WAVE_COUNTS
+        cnt_act = act;
+#else
         atomicAdd(&lds_cnt[act], 1u);
+#endif
         if (S::in_model(t, a.rt)) {
           ++nin;
           have = true;
@@ -215,6 +220,19 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
         }
       }
     }
+#ifdef RMC_GEN_WAVE_COUNTS
+    {   // per-action generated counts: one LDS atomic per wave when its lanes agree on the action
+      const u64 am = __ballot(cnt_act >= 0);
+      if (am) {
+        const int first = __ffsll((unsigned long long)am) - 1;
+        const int a0 = __shfl(cnt_act, first);
+        if (__ballot(cnt_act == a0) == am) { if (lane == first) atomicAdd(&lds_cnt[a0], (unsigned)__popcll(am)); }
+        else if (cnt_act >= 0) atomicAdd(&lds_cnt[cnt_act], 1u);
+      }
+    }
+#else
+    (void)cnt_act;
+#endif
     const u64 mask = __ballot(have);
     if (have) {
       const u32 idx = wcount + __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
