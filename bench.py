@@ -15,19 +15,31 @@ exchanges candidates, acknowledgements and new states with three RCCL
 all-to-alls (raft-tla_amd/shard.py); value = the model's distinct states /
 max-over-ranks time of one run, "scaling": "strong" (total work fixed).
 
+Beside the headline, every invocation measures (same N, same path, outside the headline's timed
+region; each with its own barrier-bracketed max-over-ranks timing):
+  scale_workload  C5v2 to depth 12 (configs/c5v2.cfg: BASELINE configs[4]'s 5-server model,
+                  482M distinct states), the workload large enough for a 1/2/4/8-GPU curve
+  variants        C2 with MaxMsgDomain = 6 (configs/c2_md6.cfg): AppendEntries responses and
+                  commits fire, which C2 as frozen (5 messages) never reaches
+
 The JSON line adds:
-  roofline      dominant kernel (the one with the most HIP-event time, orig_generate): SURVEY.md
+  roofline      dominant kernel (the one with the most HIP-event time): SURVEY.md
                 §8(d)'s algorithmic bytes of the run, B = F*S + G_in*8 + D*(16+S) (F frontier
                 states expanded, S stored state bytes, G_in in-model successors, D new states),
                 per launch of that kernel / its average launch time (HIP events on the library's
                 stream), against the 8 TB/s HBM peak; traffic = HBM bytes per launch from the
                 rocprofv3 PMC passes committed under profiles/ (FETCH_SIZE x2 + WRITE_SIZE,
                 MI355X_MICROARCH.md), or null; valu_issue_frac = PMC VALU wave-instructions per
-                launch / (launch time x 256 CUs x 2 wave64 issues per CU-cycle x 2.4 GHz)
+                launch / (launch time x 256 CUs x 2 wave64 issues per CU-cycle x 2.4 GHz); both PMC
+                figures only when the summary names the same kernel AND workload; pipeline_frac =
+                the same bytes over the whole step time (every kernel and the host between them)
   dedup_set     the BASELINE metric's second half: dedup-set GB/s (G_in*8 + D*16) / (merge +
                 probe kernel time) and seen-set probes/s (G_in / that time)
-  cpu_baseline  the CPU oracle (oracle/, test infrastructure: "port") on a bounded sample of the
-                same model (first --cpu-states distinct states of its BFS)
+  cpu_baseline  the builder's multithreaded C++ CPU BFS (oracle/cpu_bfs.cpp: TLC-style workers, a
+                lock-free fingerprint set, the product's packed successor function and invariants;
+                "port") with threads = the host cores of this job, on the whole C2 (bounded by
+                --cpu-states); beside it the value-model oracle (oracle/main.cpp, one thread) on a
+                bounded prefix
 """
 import argparse
 import importlib
@@ -101,8 +113,9 @@ def main():
     ap.add_argument("--workers", type=int, default=0)
     ap.add_argument("--fifo-steps", type=int, default=3)
     ap.add_argument("--state-store-bytes", type=int, default=0, help="state store bytes (0 = library default)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
-    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_r02.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
+    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_r03.json"))
+    ap.add_argument("--no-extra", action="store_true", help="skip the scale_workload / variants measurements")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,15 +129,15 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     mod = importlib.import_module("raft-tla_amd")
-    if world > 1:
-        # owner-partitioned fingerprints, 3 RCCL all-to-alls per level chunk (raft-tla_amd/shard.py)
-        shard = importlib.import_module("raft-tla_amd.shard")
-        mc = shard.ShardedChecker(TLA, args.config, rank, world, device_index=local, seed=0x5EED,
-                                  fp_table_bytes=args.fp_table_bytes, state_store_bytes=args.state_store_bytes,
-                                  max_depth=args.max_depth)
-    else:
-        mc = mod.ModelChecker(TLA, args.config, device=local, seed=0x5EED, fp_table_bytes=args.fp_table_bytes,
-                              state_store_bytes=args.state_store_bytes, workers=args.workers, max_depth=args.max_depth)
+    shard = importlib.import_module("raft-tla_amd.shard") if world > 1 else None
+
+    def checker(cfg, max_depth, store, table, workers):
+        if world > 1:
+            # owner-partitioned fingerprints, 3 RCCL all-to-alls per level chunk (raft-tla_amd/shard.py)
+            return shard.ShardedChecker(TLA, cfg, rank, world, device_index=local, seed=0x5EED, fp_table_bytes=table,
+                                        state_store_bytes=store, max_depth=max_depth)
+        return mod.ModelChecker(TLA, cfg, device=local, seed=0x5EED, fp_table_bytes=table, state_store_bytes=store,
+                                workers=workers, max_depth=max_depth)
 
     def barrier_sync():
         if dist is not None:
@@ -132,57 +145,81 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    for _ in range(args.warmup):
-        mc.run()
-    barrier_sync()
-    t0 = time.perf_counter()
-    res = None
-    for _ in range(args.steps):
-        res = mc.run()
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
-    mc.close()
-    assert res.verdict == "OK" or (args.max_depth and res.verdict == "DEPTH_LIMIT"), (res.verdict, res.error)
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t[0])
+
+    def measure(cfg, max_depth, steps, warmup, store, table, workers):
+        """W untimed runs, then K timed runs bracketed by barrier + device sync; max over ranks"""
+        mc = checker(cfg, max_depth, store, table, workers)
+        try:
+            for _ in range(warmup):
+                mc.run()
+            barrier_sync()
+            t0 = time.perf_counter()
+            r = None
+            for _ in range(steps):
+                r = mc.run()
+            barrier_sync()
+            elapsed = time.perf_counter() - t0
+        finally:
+            mc.close()
+        assert r.verdict == "OK" or (max_depth and r.verdict == "DEPTH_LIMIT"), (r.verdict, r.error)
+        return r, max_over_ranks(elapsed) / steps
+
+    res, per_step = measure(args.config, args.max_depth, args.steps, args.warmup, args.state_store_bytes,
+                            args.fp_table_bytes, args.workers)
     # TLC -workers 1 (FIFO order) on the same model, outside the timed region: its cost is reported
     fifo = None
     if world == 1 and args.workers != 1 and args.fifo_steps > 0:
-        with mod.ModelChecker(TLA, args.config, device=local, seed=0x5EED, fp_table_bytes=args.fp_table_bytes,
-                              state_store_bytes=args.state_store_bytes, workers=1, max_depth=args.max_depth) as m1:
-            m1.run()
-            f0 = time.perf_counter()
-            for _ in range(args.fifo_steps):
-                r1 = m1.run()
-            fifo = {"ms_per_step": (time.perf_counter() - f0) / args.fifo_steps * 1e3, "steps": args.fifo_steps,
-                    "distinct_per_run": r1.distinct, "generated_per_run": r1.generated,
-                    "kernels_ms": {k: v["ms"] for k, v in r1.kernels.items()}}
+        r1, t1 = measure(args.config, args.max_depth, args.fifo_steps, 1, args.state_store_bytes, args.fp_table_bytes, 1)
+        fifo = {"ms_per_step": t1 * 1e3, "steps": args.fifo_steps, "distinct_per_run": r1.distinct,
+                "generated_per_run": r1.generated, "kernels_ms": {k: v["ms"] for k, v in r1.kernels.items() if v["launches"]}}
         assert (r1.distinct, r1.generated, r1.depth) == (res.distinct, res.generated, res.depth)
 
-    # the sharded result is global (every rank reports the whole model's counts)
-    total_distinct = float(res.distinct)
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t[0])
+    def side(cfg, max_depth, store_gib, table_gib, steps):
+        """a second workload at the same N through the same path; its failure is reported, not fatal"""
+        try:
+            store = int(store_gib * (1 << 30) / world * (1.3 if world > 1 else 1.0))
+            r, t = measure(cfg, max_depth, steps, 1, store, int(table_gib * (1 << 30)), args.workers)
+            return {"workload": workload_name(cfg, max_depth), "value": r.distinct / t, "unit": "distinct states/s",
+                    "ms_per_step": t * 1e3, "steps": steps, "distinct_per_run": r.distinct, "generated_per_run": r.generated,
+                    "depth": r.depth, "verdict": r.verdict,
+                    "kernels_ms": {k: v["ms"] for k, v in r.kernels.items() if v["launches"]}}
+        except Exception as e:   # noqa: BLE001 - the headline stands on its own
+            return {"workload": workload_name(cfg, max_depth), "error": str(e)[:300]}
+
+    extra = {}
+    if not args.no_extra:
+        extra["scale_workload"] = side(os.path.join(ROOT, "configs", "c5v2.cfg"), 12, 96, 16, 2)
+        extra["variants"] = {"c2_md6": side(os.path.join(ROOT, "configs", "c2_md6.cfg"), 0, 64, 8, 2)}
 
     if rank == 0:
-        per_step = elapsed / args.steps
+        total_distinct = float(res.distinct)    # the sharded result is global (every rank reports the model's counts)
+        kernels = {k: v for k, v in res.kernels.items() if v["launches"] > 0}
         # dominant kernel = the one with the most HIP-event time in the last run
-        kname, kst = max(res.kernels.items(), key=lambda kv: kv[1]["ms"])
+        kname, kst = max(kernels.items(), key=lambda kv: kv[1]["ms"])
         launches = max(1, kst["launches"])
         avg_s = kst["ms"] / launches / 1e3
         # SURVEY.md §8(d): F*S + G_in*8 + D*(16+S) summed over the levels of the run (mc_summary.algo_bytes)
         bytes_per_launch = res.algo_bytes / launches
         achieved = bytes_per_launch / avg_s / 1e9
-        traffic = None
-        if os.path.exists(args.traffic_json):
+        wl_key = os.path.basename(args.config) + ("@%d" % args.max_depth if args.max_depth else "")
+
+        def pmc_summary(path):
+            """a committed rocprofv3 summary of this kernel on this workload, else None"""
             try:
-                tj = json.load(open(args.traffic_json))
-                if tj.get("kernel_name") == kname:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        ded = [v for k, v in res.kernels.items() if k in ("orig_merge_probe", "orig_dedup")]
+                doc = json.load(open(path))
+            except (OSError, ValueError):
+                return None
+            return doc if doc.get("kernel_name") == kname and doc.get("workload") == wl_key else None
+
+        tj = pmc_summary(args.traffic_json)
+        ded = [v for k, v in kernels.items() if k in ("orig_merge_probe", "orig_dedup")]
         ded_s = sum(v["ms"] for v in ded) / 1e3
         line = {
             "metric": "distinct states/sec (node) on Raft BFS",
@@ -205,11 +242,12 @@ def main():
                        "state_bytes": res.state_bytes,
                        "parallelism": "single" if world == 1 else "fp-owner-sharded x%d (RCCL all-to-all)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": tj.get("hbm_bytes_per_launch") if tj else None,
                          "kernel": kname, "algo_bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_s * 1e3,
+                         "pipeline_frac": res.algo_bytes / per_step / 1e9 / HBM_PEAK_GBS,
                          "bytes": "SURVEY.md 8(d): F*S + G_in*8 + D*(16+S) of the run / launches of the dominant kernel"},
             "kernels": {k: {"ms": v["ms"], "launches": v["launches"],
-                            "algo_GBps": v["algo_bytes"] / max(v["ms"], 1e-9) / 1e6} for k, v in res.kernels.items()},
+                            "algo_GBps": v["algo_bytes"] / max(v["ms"], 1e-9) / 1e6} for k, v in kernels.items()},
         }
         if fifo is not None:
             line["tlc_workers_1"] = fifo
@@ -219,13 +257,10 @@ def main():
                                  "bytes": "G_in*8 + D*16 (SURVEY.md 8(d) dedup-set metric) / (merge + probe kernel time)"}
         # VALU issue fraction of the dominant kernel: PMC instruction count per launch from profiles/, live
         # launch time; MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 VALU instruction issues in 2 cycles
-        if os.path.exists(args.valu_json):
-            try:
-                vj = json.load(open(args.valu_json))
-                if vj.get("kernel_name") == kname:
-                    line["roofline"]["valu_issue_frac"] = vj["valu_insts_per_launch"] / (avg_s * 256 * 2 * 2.4e9)
-            except Exception:
-                pass
+        vj = pmc_summary(args.valu_json)
+        if vj:
+            line["roofline"]["valu_issue_frac"] = vj["valu_insts_per_launch"] / (avg_s * 256 * 2 * 2.4e9)
+        line.update(extra)
         if not args.no_cpu_baseline and os.path.basename(args.config) == "c2.cfg" and not args.max_depth:
             line["cpu_baseline"] = cpu_baseline(args.config, args.cpu_states, args.cpu_workers, args.oracle_states)
         print(json.dumps(line), flush=True)

@@ -60,9 +60,10 @@ extern "C" {
 /* tlc_compat_flags: the [ext] TLC-semantics switches */
 #define MC_COMPAT_INV_OUT_OF_MODEL 0x1u /* check invariants on !seen successors that fail a constraint (TLC default) */
 /* SYMMETRY as TLC applies it (TLCStateMut.fingerPrint): the permutation giving the least full
- * variable tuple (history included) under TLC's value order, then the VIEW of that state; without
- * it SYMMETRY + VIEW identify states whose VIEWs lie in one orbit (faster; fewer distinct states
- * when histories differ).  tlc_membership only. */
+ * variable tuple (history included) under TLC's value order, then the VIEW of that state.  Set by
+ * mc_default_opts (the drop-in default: TLC's counts for a cfg with SYMMETRY, tlc_membership/raft.cfg:29-30);
+ * cleared, SYMMETRY + VIEW identify states whose VIEWs lie in one orbit (the opt-in "orbit" mode,
+ * CLI -symmetry orbit: faster, fewer distinct states when histories differ).  tlc_membership only. */
 #define MC_COMPAT_SYM_TLC 0x2u
 
 typedef struct mc_ctx mc_ctx;
@@ -81,7 +82,7 @@ typedef struct mc_opts {
   uint64_t state_store_bytes; /* bytes for the per-state store (packed states + parents); 0 = auto */
   int64_t max_depth;          /* 0 = unbounded (TLC -dfid/-depth analogue for BFS)        */
   uint64_t seed;              /* fingerprint seed (0 = default)                           */
-  uint32_t tlc_compat_flags;  /* MC_COMPAT_* (default MC_COMPAT_INV_OUT_OF_MODEL)         */
+  uint32_t tlc_compat_flags;  /* MC_COMPAT_* (default MC_COMPAT_INV_OUT_OF_MODEL | MC_COMPAT_SYM_TLC) */
   int32_t check_deadlock;     /* 1 = report states without successors (TLC default; -deadlock disables) */
   int32_t block_size;         /* expand kernel workgroup size (0 = 256)                   */
   int32_t reserved[7];
@@ -161,8 +162,10 @@ int mc_collision_observed(mc_ctx* ctx, double* val);
  * NULL or 0 disables.  mc_set_recover: the next mc_run resumes from `path` instead of Init
  * (the seen-set is rebuilt on the GPU from the stored states); generated/distinct/depth/per-action
  * counts continue exactly; kernel timings cover the resumed part.  A checkpoint of another
- * model (or of the other SYMMETRY mode) is refused (MC_E_INVALID).  Completed levels that do not
- * fit the device store are kept in host memory on save and on recovery (host spill). */
+ * model (or of the other SYMMETRY mode, or — raft_original — a -workers N checkpoint for a -workers 1
+ * search) is refused (MC_E_INVALID).  Completed levels that do not fit the device store are kept in
+ * host memory on save and on recovery (host spill).  Single-GPU runs only: the mc_shard_* calls
+ * return MC_E_UNSUPPORTED on a handle with a checkpoint or recover path set. */
 int mc_set_checkpoint(mc_ctx* ctx, const char* path, int32_t every_levels);
 int mc_set_recover(mc_ctx* ctx, const char* path);
 

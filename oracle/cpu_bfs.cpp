@@ -12,6 +12,7 @@
 // next-level buffer.  The successor relation, constraints and packing are the product's
 // (raft-tla_amd/csrc/orig_spec.h, checked against the oracle by tests/test_packed_semantics.py),
 // so the comparison with the GPU is engine against engine, not spec encoding against spec encoding.
+// Like the GPU pipeline (and TLC) it evaluates the cfg's invariants on every new state.
 //
 //   cpu_bfs CFG [--threads T] [--max-states N] [--max-depth D] [--table-log2 K]
 //   -> one JSON line {generated, distinct, depth, seconds, threads, verdict}
@@ -84,6 +85,7 @@ int main(int argc, char** argv) {
   long long depth = 1;
   bool sample_stop = false;
   std::atomic<u32> err{0};
+  std::atomic<bool> violation{false};
   while (!frontier.empty() && !sample_stop) {
     if (max_depth && depth >= max_depth) break;
     std::vector<std::vector<Packed>> next(threads);
@@ -110,6 +112,9 @@ int main(int argc, char** argv) {
             if (!S::in_model(t2, m.rt)) continue;
             Packed pk; S::pack(t2, pk.w);
             if (insert(fp64(pk.w, seed))) {
+              // the configured invariants on every new state, as the GPU pipeline does (TLC: every
+              // distinct state); a violation stops the search
+              if (S::violated(t2, m.rt.invariants)) { violation.store(true, std::memory_order_relaxed); stop.store(true, std::memory_order_relaxed); }
               out.push_back(pk);
               const long long d = distinct.fetch_add(1, std::memory_order_relaxed) + 1;
               if (max_states && d >= max_states) stop.store(true, std::memory_order_relaxed);
@@ -136,7 +141,7 @@ int main(int argc, char** argv) {
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   std::printf("{\"verdict\": \"%s\", \"generated\": %lld, \"distinct\": %lld, \"depth\": %lld, \"seconds\": %.6f, "
               "\"threads\": %d, \"err\": %u, \"table_log2\": %d}\n",
-              sample_stop ? "SAMPLE_LIMIT" : (max_depth && !frontier.empty() ? "DEPTH_LIMIT" : "OK"), generated.load(),
+              violation.load() ? "INVARIANT_VIOLATION" : sample_stop ? "SAMPLE_LIMIT" : (max_depth && !frontier.empty() ? "DEPTH_LIMIT" : "OK"), generated.load(),
               distinct.load(), depth, secs, threads, err.load(), table_log2);
   return 0;
 }

@@ -177,8 +177,18 @@ int main(int argc, char** argv) {
       if (!f) throw EvalError("cannot open trace file " + golden);
       std::vector<std::string> lines;
       for (std::string l; std::getline(f, l);) if (!l.empty()) lines.push_back(l);
+      // an invariant whose evaluation raises a TLC evaluation error (e.g. Committed(i) out of range,
+      // tlc_membership/raft.tla:969) counts as the trace's stop: TLC reports the error on that state
+      std::string eval_error;
       auto check_inv = [&](const State& st) -> std::string {
-        for (auto& inv : cfg.invariants) if (!sp->invariant(inv, st)) return inv;
+        for (auto& inv : cfg.invariants) {
+          try {
+            if (!sp->invariant(inv, st)) return inv;
+          } catch (const EvalError& e) {
+            eval_error = e.what();
+            return inv;
+          }
+        }
         return "";
       };
       auto in_model = [&](const State& a, const State& b) {
@@ -204,8 +214,13 @@ int main(int argc, char** argv) {
         if (!found) { ok = false; bad_step = (int64_t)k; }
       }
       if (ok) violated = check_inv(cur);
+      if (ok && violated.empty()) {   // or: computing the last state's successors raises the error
+        try { succ.clear(); sp->next(cur, succ); }
+        catch (const EvalError& e) { eval_error = e.what(); violated = "<next-state relation>"; }
+      }
       std::cout << "{\"valid\": " << ((ok && !violated.empty()) ? "true" : "false") << ", \"length\": " << lines.size()
-                << ", \"violated\": " << json_str(violated) << ", \"bad_step\": " << bad_step
+                << ", \"violated\": " << json_str(violated) << ", \"eval_error\": " << json_str(eval_error)
+                << ", \"bad_step\": " << bad_step
                 << ", \"actions\": " << json_str(actions) << "}" << std::endl;
       return 0;
     }

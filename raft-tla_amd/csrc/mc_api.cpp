@@ -84,7 +84,7 @@ void mc_default_opts(mc_opts* o) {
   o->abi_version = RAFTMC_ABI_VERSION;
   o->n_gpus = 1;
   o->workers = 1;
-  o->tlc_compat_flags = MC_COMPAT_INV_OUT_OF_MODEL;
+  o->tlc_compat_flags = MC_COMPAT_INV_OUT_OF_MODEL | MC_COMPAT_SYM_TLC;   // TLC's defaults: the drop-in semantics
   o->check_deadlock = 1;
   o->block_size = 256;
 }
@@ -242,7 +242,11 @@ int mc_report(const mc_ctx* c, char** text, size_t* len) {
     o << "Error: The behavior up to this point is:\n" << trace_text(c, r);
   } else if (r.verdict == MC_VERDICT_DEADLOCK) {
     o << "Error: Deadlock reached.\nError: The behavior up to this point is:\n" << trace_text(c, r);
-  } else if (r.verdict == MC_VERDICT_EVAL_ERROR || r.verdict == MC_VERDICT_CAPACITY_OVERFLOW) {
+  } else if (r.verdict == MC_VERDICT_EVAL_ERROR) {
+    // TLC: the evaluation error, then the behavior up to the state it was evaluating
+    o << "Error: " << r.error << "\n";
+    if (!r.trace.empty()) o << "Error: The behavior up to this point is:\n" << trace_text(c, r);
+  } else if (r.verdict == MC_VERDICT_CAPACITY_OVERFLOW) {
     o << "Error: " << r.error << "\n";
   } else if (r.verdict == MC_VERDICT_OK) {
     o << "Model checking completed. No error has been found.\n";
@@ -299,7 +303,14 @@ int mc_dump_states(const mc_ctx* c, const char* path) {
 int mc_describe(const mc_ctx* c, char** text, size_t* len) {
   if (!c || !text) return MC_E_INVALID;
   if (!c->be) return MC_E_STATE;
-  *text = dup_text(c->be->describe_json(), len);
+  // the model's own description plus the run options that decide TLC semantics
+  std::string d = c->be->describe_json();
+  if (!d.empty() && d.back() == '}') {
+    d.pop_back();
+    d += std::string(", \"symmetry_mode\": \"") + (c->ro.sym_tlc ? "tlc" : "orbit") + "\", \"workers\": " +
+         std::to_string(c->ro.workers) + ", \"check_deadlock\": " + (c->ro.check_deadlock ? "true" : "false") + "}";
+  }
+  *text = dup_text(d, len);
   return *text ? MC_OK : MC_E_OOM;
 }
 
@@ -314,9 +325,15 @@ int mc_exit_code(const mc_ctx* c) {
 }
 
 // ------------------------------------------------------------------ sharded BFS
+// checkpoint / recover apply to single-GPU runs only: a sharded run refuses them rather than
+// silently writing no checkpoint or starting from Init
 #define SHARD_GUARD() \
   if (!c) return MC_E_INVALID; \
-  if (!c->be) return MC_E_STATE;
+  if (!c->be) return MC_E_STATE; \
+  if (!c->ro.checkpoint_path.empty() || !c->ro.recover_path.empty()) { \
+    c->last_error = "checkpoint/recover apply to single-GPU runs (mc_run); a sharded run cannot use them"; \
+    return MC_E_UNSUPPORTED; \
+  }
 #define SHARD_RC(expr)                      \
   do {                                      \
     std::string err;                        \
@@ -447,6 +464,10 @@ int mc_shard_run_loopback(mc_ctx* const* ctxs, int32_t world) {
   for (int r = 0; r < world; ++r) {
     if (!ctxs[r] || !ctxs[r]->be) return MC_E_INVALID;
     for (int q = 0; q < r; ++q) if (ctxs[q] == ctxs[r]) return MC_E_INVALID;
+    if (!ctxs[r]->ro.checkpoint_path.empty() || !ctxs[r]->ro.recover_path.empty()) {
+      ctxs[r]->last_error = "checkpoint/recover apply to single-GPU runs (mc_run); a sharded run cannot use them";
+      return MC_E_UNSUPPORTED;
+    }
   }
   rmc::LoopbackWorld w(world);
   std::vector<int> rcs(world, MC_OK);

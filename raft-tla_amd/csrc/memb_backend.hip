@@ -1157,8 +1157,8 @@ class MembGpu : public Backend {
     const int id = (int)(res & 255);
     if (kind == EV_INV_ERROR) {
       r.verdict = MC_VERDICT_EVAL_ERROR;
-      r.error = std::string("TLC evaluation error while checking invariant ") + kMembInvNames[id] +
-                " (Committed(i) = SubSeq(log[i], 1, commitIndex[i]) or log[l][idx] outside its domain)";
+      r.error = std::string("Evaluating invariant ") + kMembInvNames[id] +
+                " failed: Committed(i) == SubSeq(log[i], 1, commitIndex[i]) or log[l][idx] outside its domain (raft.tla:969, :1099)";
     } else {
       r.verdict = MC_VERDICT_INVARIANT_VIOLATION;
       r.violated = kMembInvNames[id];
@@ -1514,8 +1514,8 @@ class MembGpu : public Backend {
         sres_.error = "TLC evaluation error while computing the successors of a state (SubSeq index out of domain, raft.tla:551/764)";
       } else if (kind == EV_INV_ERROR) {
         sres_.verdict = MC_VERDICT_EVAL_ERROR;
-        sres_.error = std::string("TLC evaluation error while checking invariant ") + (g[32] ? kMembInvNames[g[32] - 1] : "?") +
-                      " (Committed(i) = SubSeq(log[i], 1, commitIndex[i]) or log[l][idx] outside its domain)";
+        sres_.error = std::string("Evaluating invariant ") + (g[32] ? kMembInvNames[g[32] - 1] : "?") +
+                      " failed: Committed(i) == SubSeq(log[i], 1, commitIndex[i]) or log[l][idx] outside its domain (raft.tla:969, :1099)";
       } else {
         sres_.verdict = MC_VERDICT_INVARIANT_VIOLATION;
         sres_.violated = g[32] ? kMembInvNames[g[32] - 1] : "?";

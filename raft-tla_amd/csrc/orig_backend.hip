@@ -1304,7 +1304,7 @@ class OrigGpu : public Backend {
     const u64 S_B = NWP * 4;
     u64 level_begin = 0, level_count = 1;
     if (!o.recover_path.empty()) {   // TLC -recover: continue the BFS saved by a checkpoint
-      if (int rc = load_checkpoint(o.recover_path, r, level_begin, level_count, err)) return rc;
+      if (int rc = load_checkpoint(o.recover_path, fifo, r, level_begin, level_count, err)) return rc;
     } else {
     // ---- Init (raft_original.tla:139-159): one state, generated and distinct
     u32 w0[S::NW]; S::pack(s0, w0);
@@ -1471,7 +1471,9 @@ class OrigGpu : public Backend {
         os << "error flags 0x" << std::hex << e << std::dec << " while expanding state " << (c[K_ERRGID] ? (int64_t)(c[K_ERRGID] - 1) : -1) << ":";
         if (e & OE_CAP_ELECTIONS) os << " elections set exceeds the compiled capacity;";
         if (e & OE_CAP_COUNT) os << " message count / bag capacity exceeded;";
-        if (e & OE_CAP_STORE) os << " state store full (raise state_store_bytes);";
+        if (e & OE_CAP_STORE)
+          os << " state store full (raise state_store_bytes): " << cap_ << " state slots, " << base_
+             << " states on the host, level ends at " << level_end << ", " << nnew << " new;";
         if (e & OE_TABLE_FULL) os << " fingerprint table full (raise fp_table_bytes);";
         r.error = os.str();
         total_ = std::min<u64>(next_write, base_ + cap_);
@@ -1588,15 +1590,20 @@ class OrigGpu : public Backend {
   // File: magic, the model's describe_json (a checkpoint only resumes the same model), the BFS
   // position (level_begin/count, stored states) and TLC's counters, then the stored states and
   // parent pointers [0, total).  The seen-set is rebuilt from the states on recovery.
+  // fifo: the search order the stored levels are in — 1 = TLC's single-worker FIFO order (-workers 1:
+  // kept parents, per-action distinct counts and counterexamples are TLC's), 0 = the -workers N
+  // pipeline (first-come dedup).  A -workers N checkpoint cannot resume a -workers 1 search (its
+  // kept parents are not TLC's); the reverse is safe.
   struct CkptHead {
     char magic[8];
     u64 nwp, total, level_begin, level_count, seed;
-    int64_t generated, distinct, depth, generated_in_model, n_act, n_levels, desc_len;
+    int64_t generated, distinct, depth, generated_in_model, n_act, n_levels, desc_len, fifo;
   };
   int save_checkpoint(const std::string& path, const RunResult& r, u64 level_begin, u64 level_count, std::string& err) {
     const std::string desc = describe_json();
     CkptHead h;
-    std::memcpy(h.magic, "RAFTMCK1", 8);
+    std::memcpy(h.magic, "RAFTMCK2", 8);
+    h.fifo = last_fifo_ ? 1 : 0;
     h.nwp = NWP; h.total = total_; h.level_begin = level_begin; h.level_count = level_count; h.seed = r.seed;
     h.generated = r.generated; h.distinct = r.distinct; h.depth = r.depth; h.generated_in_model = r.generated_in_model;
     h.n_act = OA_NACT; h.n_levels = (int64_t)r.levels.size(); h.desc_len = (int64_t)desc.size();
@@ -1630,16 +1637,22 @@ class OrigGpu : public Backend {
     if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) { err = "writing checkpoint " + path + " failed"; return MC_E_IO; }
     return 0;
   }
-  int load_checkpoint(const std::string& path, RunResult& r, u64& level_begin, u64& level_count, std::string& err) {
+  int load_checkpoint(const std::string& path, bool fifo, RunResult& r, u64& level_begin, u64& level_count, std::string& err) {
     FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) { err = "cannot read checkpoint " + path; return MC_E_IO; }
     CkptHead h;
     const std::string desc = describe_json();
     std::string fdesc;
-    bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, "RAFTMCK1", 8) == 0 && h.nwp == (u64)NWP &&
+    bool ok = std::fread(&h, sizeof h, 1, f) == 1 && std::memcmp(h.magic, "RAFTMCK2", 8) == 0 && h.nwp == (u64)NWP &&
               h.n_act == OA_NACT && h.desc_len >= 0 && h.desc_len < (1 << 20) && h.n_levels > 0 && h.n_levels < (1 << 20);
     if (ok) { fdesc.resize((size_t)h.desc_len); ok = std::fread(&fdesc[0], 1, fdesc.size(), f) == fdesc.size(); }
     if (!ok || fdesc != desc) { std::fclose(f); err = "checkpoint " + path + " is not a checkpoint of this model"; return MC_E_INVALID; }
+    if (fifo && !h.fifo) {
+      std::fclose(f);
+      err = "checkpoint " + path + " was written by a -workers N search: its kept parents are not TLC's single-worker "
+            "FIFO ones, so it cannot resume a -workers 1 search";
+      return MC_E_INVALID;
+    }
     // completed levels that do not fit the device store stay in host memory (spilled)
     const u64 lb = h.total > cap_ ? h.level_begin : 0;
     if (h.total - lb > cap_ || h.level_begin > h.total) { std::fclose(f); err = "checkpoint frontier exceeds the state store (raise state_store_bytes)"; return MC_E_OOM; }

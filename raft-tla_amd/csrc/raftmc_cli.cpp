@@ -1,7 +1,7 @@
 // raftmc — command-line front end mirroring TLC's flags:
 //   raftmc [-config F.cfg] [-workers N] [-deadlock] [-depth D] [-device K]
 //          [-fptable BYTES] [-store BYTES] [-seed S] [-no-inv-oom] [-dump FILE] [-json]
-//          [-checkpoint LEVELS] [-checkpoint-file FILE] [-recover FILE] F.tla
+//          [-checkpoint LEVELS] [-checkpoint-file FILE] [-recover FILE] [-symmetry tlc|orbit] F.tla
 // (-checkpoint counts BFS levels where TLC counts minutes; the file defaults to states/raftmc.ckpt)
 // Prints TLC-style lines and exits with TLC-like codes (0 ok, 12 safety
 // violation, 11 deadlock, 75 error).
@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
     else if (k == "-store") o.state_store_bytes = std::strtoull(val(), nullptr, 10);
     else if (k == "-seed") o.seed = std::strtoull(val(), nullptr, 0);
     else if (k == "-no-inv-oom") o.tlc_compat_flags &= ~MC_COMPAT_INV_OUT_OF_MODEL;
-    else if (k == "-symmetry") {   // "tlc": TLC's least-permuted-state rule; "orbit" (default)
+    else if (k == "-symmetry") {   // "tlc" (default): TLC's least-permuted-state rule; "orbit": the faster orbit mode
       const std::string v = val();
       if (v == "tlc") o.tlc_compat_flags |= MC_COMPAT_SYM_TLC;
       else if (v == "orbit") o.tlc_compat_flags &= ~MC_COMPAT_SYM_TLC;

@@ -135,8 +135,9 @@ class Result:
 class ModelChecker:
     """One raftmc handle: mc_open on construction, mc_run in run()."""
 
+    # sym_tlc: SYMMETRY as TLC applies it (the default, MC_COMPAT_SYM_TLC); False = the orbit mode
     def __init__(self, spec, config=None, workers=1, deadlock=True, device=0, max_depth=0,
-                 fp_table_bytes=0, state_store_bytes=0, seed=0, inv_out_of_model=True, sym_tlc=False):
+                 fp_table_bytes=0, state_store_bytes=0, seed=0, inv_out_of_model=True, sym_tlc=True):
         self.lib = load_library()
         if config is None:
             config = spec[:-4] + ".cfg" if spec.endswith(".tla") else spec + ".cfg"
@@ -283,6 +284,11 @@ def tlc_main(argv):
             kw["deadlock"] = False
         elif a == "-depth":
             kw["max_depth"] = int(next(it))
+        elif a == "-symmetry":                   # raftmc: tlc (TLC's rule, default) | orbit
+            v = next(it)
+            if v not in ("tlc", "orbit"):
+                raise ValueError("-symmetry tlc|orbit")
+            kw["sym_tlc"] = v == "tlc"
         else:
             spec = a
     with ModelChecker(spec, config, **kw) as mc:

@@ -2,8 +2,12 @@
 
     python scripts/rocpd_summary.py stats  RUN_DB OUT.csv          # per-kernel calls / total / avg (us)
     python scripts/rocpd_summary.py pmc    RUN_DB COUNTER OUT.csv  # per-kernel mean counter value per dispatch
-    python scripts/rocpd_summary.py traffic FETCH_DB WRITE_DB KERNEL_SUBSTR OUT.json
-    python scripts/rocpd_summary.py valu   PMC_DB KERNEL_SUBSTR OUT.json   # VALU/SALU wave-instructions per dispatch
+    python scripts/rocpd_summary.py traffic FETCH_DB WRITE_DB KERNEL_SUBSTR OUT.json [WORKLOAD]
+    python scripts/rocpd_summary.py valu   PMC_DB KERNEL_SUBSTR OUT.json [WORKLOAD]   # VALU/SALU wave-instructions per dispatch
+
+WORKLOAD (default "c2.cfg") names the model the profiled command checked, as bench.py's workload key
+(cfg basename, "@depth" when depth-bounded): bench.py only attaches a summary to its line when both the
+kernel and the workload match.
 
 `traffic` follows /opt/skills/guides/MI355X_MICROARCH.md (HBM/rocprofv3 section):
 FETCH_SIZE and WRITE_SIZE come from separate --pmc passes, both in KiB per
@@ -56,6 +60,7 @@ def main():
         name = next(k for k in fetch if sys.argv[4] in k)
         f_kib, w_kib = fetch[name][2], write[name][2]
         doc = {"kernel_name": sys.argv[4], "kernel_symbol": name, "dispatches": fetch[name][1],
+               "workload": sys.argv[6] if len(sys.argv) > 6 else "c2.cfg",
                "fetch_bytes_per_launch_raw": f_kib * 1024, "write_bytes_per_launch": w_kib * 1024,
                "hbm_bytes_per_launch": 2 * f_kib * 1024 + w_kib * 1024,
                "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over `bench.py --steps 1 "
@@ -73,6 +78,7 @@ def main():
             if name in rows:
                 extra[cn + "_per_launch"] = rows[name][2]
         doc = {"kernel_name": sys.argv[3], "kernel_symbol": name, "dispatches": valu[name][1],
+               "workload": sys.argv[5] if len(sys.argv) > 5 else "c2.cfg",
                "valu_insts_per_launch": valu[name][2], "salu_insts_per_launch": salu[name][2] if name in salu else None,
                "sq_counters": extra,
                "peak_valu_insts_per_s": 256 * 2 * 2.4e9,

@@ -54,6 +54,9 @@ CASES = {
     "scen_AddSucessful": ("scen_AddSucessful", 0),
     "scen_MembershipChangeCommits": ("scen_MembershipChangeCommits", 0),
     "scen_AddCommits": ("scen_AddCommits", 0),
+    # on the smallest growing cluster (InitServer = {s1}, Server = {s1, s2}; configs/scen_*.cfg headers)
+    "scen_MultipleMembershipChangesCommit": ("scen_MultipleMembershipChangesCommit", 0),
+    "scen_LeaderChangesDuringConfChange": ("scen_LeaderChangesDuringConfChange", 0),
     # SYMMETRY in TLC's mode (oracle --sym tlc, MC_COMPAT_SYM_TLC): least permuted full state, then VIEW
     "tlc:membership_shipped@16": ("membership_shipped", 16),
     "tlc:memb_two@16": ("memb_two", 16),
@@ -61,7 +64,14 @@ CASES = {
     "tlc:memb_four@13": ("memb_four", 13),
     "tlc:scen_FirstCommit": ("scen_FirstCommit", 0),
     "tlc:punct_MajorityOfClusterRestarts@30": ("scen_MajorityOfClusterRestarts_punct", 30, "MajorityOfClusterRestarts_constraint"),
+    # the NEXT relations on their own (raft.tla:909-916, :924-932) and the other verdict classes
+    "memb_async@16": ("memb_async", 16),
+    "tlc:memb_async@16": ("memb_async", 16),
+    "deadlock:memb_unreliable": ("memb_unreliable", 0),        # Init has no successor: TLC's deadlock, exit 11
+    "eval:memb_eval_single": ("memb_eval_single", 0),          # Committed(i) out of range: TLC's evaluation error, exit 75
 }
+# cases searched with TLC's deadlock check on (the oracle's --deadlock; the GPU's default check_deadlock = 1)
+DEADLOCK = {"deadlock:memb_unreliable", "eval:memb_eval_single", "memb_async@16", "tlc:memb_async@16"}
 OUT = os.path.join(GOLDEN, "memb_parity.json")
 
 
@@ -78,17 +88,18 @@ def main(names, out=OUT):
         fd, dump = tempfile.mkstemp(suffix=".txt")
         os.close(fd)
         sym = "tlc" if n.startswith("tlc:") else "view"
-        args = ["--sym", sym, "--dump", dump, "--trace"]
+        args = ["--sym", sym, "--dump", dump, "--trace"] + (["--deadlock"] if n in DEADLOCK else [])
         if prefix:
             flag, fixture = PREFIXES[prefix]
             args += [flag, golden_file(fixture)[0]]
         if depth:
             args += ["--max-depth", depth]
         r = run_oracle("bfs", MEMB_MC, os.path.join(CONFIGS, cfg + ".cfg"), *args, timeout=100000)
-        assert r["verdict"] in ("OK", "INVARIANT_VIOLATION"), r
+        assert r["verdict"] in ("OK", "INVARIANT_VIOLATION", "DEADLOCK", "EVAL_ERROR"), r
         sha, cnt = digest_lines(dump)
         os.unlink(dump)
         doc[n] = {"cfg": cfg, "max_depth": depth, "sym": sym, "verdict": r["verdict"], "violated": r["violated"],
+                  "deadlock": n in DEADLOCK, "error": r["error"],
                   "prefix": [prefix, PREFIXES[prefix][1]] if prefix else None,
                   "generated": r["generated"], "distinct": r["distinct"], "depth": r["depth"],
                   "left_on_queue": r["left_on_queue"], "levels": r["levels"], "actions": r["actions"],

@@ -225,3 +225,39 @@ def test_library_is_built_from_this_tree():
     rm = importlib.import_module("raft-tla_amd.raftmc")
     lib = rm.load_library()
     assert lib.mc_source_hash().decode() == rm.source_hash()
+
+
+REF_MEMB = "/root/reference/tlc_membership"
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF_MEMB, "raft.tla")), reason="the reference exists only in the build container")
+def test_open_reference_tlc_membership_unmodified(raftmc):
+    """The drop-in claim on the reference's own files: mc_open takes the unmodified
+    tlc_membership/raft.tla and raft.cfg (as `tlc2.TLC -config raft.cfg raft.tla` would) and resolves
+    the shipped model — 3 servers, Value {1, 2}, SYMMETRY perms in TLC's rule (the default), VIEW
+    vars, NEXT NextAsyncCrash, the 12 constraints and 8 invariants of raft.cfg:37-87.  Container-only
+    (the reference is not on the GPU box); reads nothing but the reference's text, runs no GPU work."""
+    with raftmc.ModelChecker(os.path.join(REF_MEMB, "raft.tla"), os.path.join(REF_MEMB, "raft.cfg")) as mc:
+        d = mc.describe()
+    assert d["spec"] == "tlc_membership" and (d["N"], d["NV"]) == (3, 2) and d["init_server_mask"] == 7
+    assert d["symmetry"] is True and d["permutations"] == 6 and d["symmetry_mode"] == "tlc"
+    assert d["next"] == "NextAsyncCrash" and d["check_deadlock"] is True and d["workers"] == 1
+    assert d["invariants"] == ["LeaderVotesQuorum", "CandidateTermNotInLog", "ElectionSafety", "LogMatching",
+                               "VotesGrantedInv", "QuorumLogInv", "MoreUpToDateCorrect", "LeaderCompleteness"]
+    assert len(d["constraints"]) == 12
+
+
+def test_sharded_runs_refuse_checkpoints(raftmc, tmp_path):
+    """Checkpoint/recover are single-GPU features: a sharded run on a handle that has either set
+    fails with MC_E_UNSUPPORTED before any device work, instead of silently ignoring them."""
+    import ctypes
+    with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c1.cfg")) as mc:
+        mc.set_checkpoint(str(tmp_path / "x.ckpt"), 1)
+        mc.lib.mc_shard_open.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
+        assert mc.lib.mc_shard_open(mc.h, 0, 2) == -4
+        assert b"single-GPU" in mc.lib.mc_last_error(mc.h)
+        mc.set_checkpoint(None)
+        mc.set_recover(str(tmp_path / "x.ckpt"))
+        hs = (ctypes.c_void_p * 1)(mc.h)
+        mc.lib.mc_shard_run_loopback.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32]
+        assert mc.lib.mc_shard_run_loopback(hs, 1) == -4

@@ -240,6 +240,48 @@ def test_c5_deep_properties(raftmc):
     assert sum(v[0] for v in a.actions.values()) + 1 == a.generated
 
 
+def test_c5v2_deep_properties(raftmc):
+    """C5v2 (configs/c5v2.cfg: 5 servers, 2 values, 8 messages) three levels past the oracle's
+    depth-7 pin: the TLC -workers 1 (FIFO) and -workers N pipelines agree on every
+    order-independent count, the counts do not depend on the fingerprint seed, the levels sum to
+    the distinct count and the per-action counts to TLC's generated/distinct bookkeeping."""
+    cfg = os.path.join(CONFIGS, "c5v2.cfg")
+    a = raftmc.check(ORIG_MC, cfg, max_depth=10, seed=3)
+    b = raftmc.check(ORIG_MC, cfg, max_depth=10, seed=0xC5C5C5, workers=0)
+    assert a.verdict == b.verdict == "DEPTH_LIMIT", (a.error, b.error)
+    assert (a.generated, a.distinct, a.left_on_queue) == (b.generated, b.distinct, b.left_on_queue)
+    assert [lv[0] for lv in a.levels] == [lv[0] for lv in b.levels]
+    assert {k: v[0] for k, v in a.actions.items()} == {k: v[0] for k, v in b.actions.items()}
+    assert sum(lv[0] for lv in a.levels) == a.distinct and a.left_on_queue == a.levels[-1][0]
+    assert sum(v[0] for v in a.actions.values()) + 1 == a.generated
+    assert sum(v[1] for v in a.actions.values()) + 1 == a.distinct
+
+
+def test_c5v2_compact_election_records(raftmc, tmp_path):
+    """5 servers with two values store election records in the compact form (orig_spec.h
+    ECOMPACT: the voterLog row's presence bits come from evotes, eterm in bits_for(MaxTerm)).
+    NoLeader's counterexample is TLC's single-worker FIFO first election, at depth 12 behind
+    ~4.8e8 states: its last state carries such a record, printed through the compact decoding,
+    and the oracle's check-trace replays the trace state by state through the literal
+    restatement of raft_original.tla.  The store holds the whole search (482M states of 160 B +
+    8 B parent pointers: 81 GB; round 2's run used the 32 GiB default store and stopped with a
+    CAPACITY_OVERFLOW at 222M states)."""
+    from oracle_util import run_oracle
+    cfg = os.path.join(CONFIGS, "c5v2_noleader.cfg")
+    with raftmc.ModelChecker(ORIG_MC, cfg, fp_table_bytes=16 << 30, state_store_bytes=112 << 30) as mc:
+        assert mc.describe()["state_bytes_stored"] == 160
+        r = mc.run()
+    assert r.verdict == "INVARIANT_VIOLATION" and r.violated == "NoLeader", (r, r.error)
+    assert r.depth == 12 and r.exit_code == 12
+    states = [st for _, st in trace_states(r)]
+    assert len(states) == 12
+    assert "evoterLog" in states[-1] and "evotes" in states[-1]
+    p = tmp_path / "trace.txt"
+    p.write_text("\n".join(states) + "\n")
+    o = run_oracle("check-trace", ORIG_MC, cfg, "--golden", str(p))
+    assert o["valid"] and o["length"] == len(states) and o["violated"] == "NoLeader", o
+
+
 def test_checkpoint_recover_c1(raftmc, tmp_path):
     """TLC -checkpoint / -recover: a search stopped at depth 6 with a checkpoint per level,
     resumed by a fresh handle, ends exactly like the uninterrupted search (counts, levels,
@@ -265,6 +307,30 @@ def test_checkpoint_recover_c1(raftmc, tmp_path):
         with pytest.raises(raftmc.RaftMCError) as e:
             mc.run()
     assert e.value.code == -1
+
+
+def test_checkpoint_search_order_guard(raftmc, tmp_path):
+    """A checkpoint records its search order: one written by the TLC -workers N pipeline (first-come
+    dedup, kept parents not TLC's) is refused by a -workers 1 search (TLC's single-worker FIFO
+    order); the reverse direction and a -workers N resume are accepted and end with the oracle's
+    counts."""
+    g = FIXTURES["c1"]
+    cfg = os.path.join(CONFIGS, "c1.cfg")
+    ckn, ck1 = str(tmp_path / "n.ckpt"), str(tmp_path / "one.ckpt")
+    for path, workers in ((ckn, 0), (ck1, 1)):
+        with raftmc.ModelChecker(ORIG_MC, cfg, max_depth=6, workers=workers, **SMALL) as mc:
+            mc.set_checkpoint(path, 1)
+            assert mc.run().verdict == "DEPTH_LIMIT"
+    with raftmc.ModelChecker(ORIG_MC, cfg, workers=1, **SMALL) as mc:
+        mc.set_recover(ckn)
+        with pytest.raises(raftmc.RaftMCError) as e:
+            mc.run()
+    assert e.value.code == -1 and "-workers N" in str(e.value)
+    for path, workers in ((ckn, 0), (ck1, 0), (ck1, 1)):
+        with raftmc.ModelChecker(ORIG_MC, cfg, workers=workers, **SMALL) as mc:
+            mc.set_recover(path)
+            r = mc.run()
+        assert (r.verdict, r.generated, r.distinct, r.depth) == ("OK", g["generated"], g["distinct"], g["depth"]), (path, workers)
 
 
 def test_checkpoint_recover_c2(raftmc, tmp_path):

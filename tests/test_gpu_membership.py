@@ -22,16 +22,19 @@ from oracle_util import CONFIGS, GOLDEN, MEMB_MC, tla_text
 
 pytestmark = pytest.mark.gpu
 
-SMALL = dict(fp_table_bytes=1 << 26, state_store_bytes=1 << 29, deadlock=False)
+SMALL = dict(fp_table_bytes=1 << 26, state_store_bytes=1 << 29)
 FIX = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))
 EXHAUSTIVE = sorted(k for k, v in FIX.items() if v["verdict"] == "OK")
 VIOLATIONS = sorted(k for k, v in FIX.items() if v["verdict"] == "INVARIANT_VIOLATION")
+ERRORS = sorted(k for k, v in FIX.items() if v["verdict"] in ("DEADLOCK", "EVAL_ERROR"))
+EXIT = {"DEADLOCK": 11, "EVAL_ERROR": 75, "INVARIANT_VIOLATION": 12}
 
 
 def open_case(raftmc, g, **kw):
     """A handle for a fixture case; punctuated-search cases get their golden history trace
     (the committed TLC trace fixture) through mc_set_history_prefix; "tlc:" cases run SYMMETRY in
     TLC's mode (MC_COMPAT_SYM_TLC, the oracle's --sym tlc)."""
+    kw = dict(kw, deadlock=g.get("deadlock", False))   # TLC's deadlock check as the fixture was searched
     mc = raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), sym_tlc=g.get("sym") == "tlc", **kw)
     if g.get("prefix"):
         con, fixture = g["prefix"]
@@ -77,6 +80,44 @@ def test_scenario_shortest_counterexample(raftmc, case):
             assert head == "State %d: <%s>" % (k + 1, ref["action"])
 
 
+@pytest.mark.parametrize("case", ERRORS)
+def test_error_verdicts(raftmc, case):
+    """TLC's other two verdict classes, against the oracle's fixtures: "Deadlock reached" (NEXT
+    NextUnreliable on its own: Init has no successor) and an evaluation error (Committed(i) ==
+    SubSeq(log[i], 1, commitIndex[i]) out of range after HandleCatchupRequest empties a committed
+    log, raft.tla:734-736, :969): verdict, TLC's exit code (11 / 75), the counters at the stop point
+    and the trace state by state; with TLC's -deadlock (check off) the deadlock case completes."""
+    g = FIX[case]
+    with open_case(raftmc, g, **SMALL) as mc:
+        r = mc.run()
+    assert r.verdict == g["verdict"] and r.exit_code == EXIT[g["verdict"]], (r, r.error)
+    assert (r.depth, r.generated, r.distinct, r.left_on_queue) == (g["depth"], g["generated"], g["distinct"], g["left_on_queue"])
+    assert r.actions == g["actions"]
+    blocks = r.trace_text.strip().split("\n\n")
+    assert [" ".join(b.split("\n")[1:]) for b in blocks] == [t["state"] for t in g["trace"]]
+    if g["verdict"] == "EVAL_ERROR":
+        assert "Committed" in r.error and "Error:" in r.report
+    else:
+        assert "Deadlock reached" in r.report
+        with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), deadlock=False, **SMALL) as mc:
+            q = mc.run()
+        assert (q.verdict, q.exit_code, q.distinct) == ("OK", 0, 1)
+
+
+def test_deadlock_check_changes_no_count(raftmc):
+    """No state of the shipped NEXT relations lacks a successor (Restart is always
+    enabled in NextAsyncCrash/NextDynamic; under NextAsync a server of its own config is a Leader
+    with ClientRequest or can Timeout): TLC's default deadlock check (check_deadlock = 1) gives
+    the oracle's counts exactly."""
+    for case in ("membership_shipped@14", "memb_dynamic3@14", "memb_async@16"):
+        g = FIX[case]
+        with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), max_depth=g["max_depth"],
+                                 deadlock=True, sym_tlc=g.get("sym") == "tlc", **SMALL) as mc:
+            r = mc.run()
+        assert r.verdict == "DEPTH_LIMIT", (case, r.error)
+        assert (r.generated, r.distinct, r.actions) == (g["generated"], g["distinct"], g["actions"]), case
+
+
 def test_membership_seed_independence(raftmc):
     cfg = os.path.join(CONFIGS, "memb_dynamic3.cfg")
     a = raftmc.check(MEMB_MC, cfg, max_depth=12, seed=3, **SMALL)
@@ -99,13 +140,20 @@ def test_membership_handle_rerun(raftmc):
     assert (a.generated, a.distinct, a.actions) == (b.generated, b.distinct, b.actions)
 
 
-def test_c3_counterexample_matches_committed_trace(raftmc):
-    """C3 (BASELINE configs[2], 4 servers, NextDynamic) to completion: the first
-    violation in TLC FIFO order is LeaderVotesQuorum at depth 21; the trace equals
-    the committed one, which the oracle validates (tests/test_oracle.py)."""
-    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, "memb_four.cfg"), deadlock=False)
+# C3's stop point in both SYMMETRY modes (GPU-measured; the deepest oracle pins of this model are
+# memb_four@16 in tests/golden/memb_parity.json and tests/golden/memb_deep.json)
+C3_STOP = {"orbit": (21, 162883559, 1113410993), "tlc": (21, 163766653, 1118891169)}
+
+
+@pytest.mark.parametrize("mode", ["tlc", "orbit"])
+def test_c3_counterexample_matches_committed_trace(raftmc, mode):
+    """C3 (BASELINE configs[2], 4 servers, NextDynamic) to completion, in TLC's SYMMETRY rule (the
+    drop-in default) and in the orbit mode: the first violation in TLC FIFO order is
+    LeaderVotesQuorum at depth 21 in both; the trace equals the committed one, which the oracle
+    validates (tests/test_oracle.py)."""
+    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, "memb_four.cfg"), deadlock=False, sym_tlc=mode == "tlc")
     assert r.verdict == "INVARIANT_VIOLATION" and r.violated == "LeaderVotesQuorum", (r, r.error)
-    assert (r.depth, r.distinct, r.generated) == (21, 162883559, 1113410993)
+    assert (r.depth, r.distinct, r.generated) == C3_STOP[mode]
     got = [" ".join(b.split("\n")[1:]) for b in r.trace_text.strip().split("\n\n")]
     want = open(os.path.join(GOLDEN, "c3_leader_votes_quorum_trace.txt")).read().strip().split("\n")
     assert got == want
@@ -122,7 +170,7 @@ def test_counterexamples_beyond_oracle_reach(raftmc, cfg):
     Among them the positive controls of the invariant kernels (VotesGrantedInv_false,
     LeaderCompleteness_false) and a LogMatching violation of the dynamic-membership model."""
     g = GPU_TRACES[cfg]
-    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, cfg + ".cfg"), deadlock=False)
+    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, cfg + ".cfg"), deadlock=False, sym_tlc=g.get("sym") == "tlc")
     assert (r.verdict, r.violated) == (g["verdict"], g["violated"]), r.error
     assert (r.depth, r.distinct, r.generated, r.left_on_queue) == (g["depth"], g["distinct"], g["generated"], g["left_on_queue"])
     got = [" ".join(b.split("\n")[1:]) for b in r.trace_text.strip().split("\n\n")]

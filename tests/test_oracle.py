@@ -151,3 +151,36 @@ def test_oracle_lean_mode_is_identical(name):
     b = run_oracle("bfs", ORIG_MC, os.path.join(CONFIGS, name + ".cfg"), "--lean", "--workers", "4")
     for k in ("verdict", "violated", "generated", "distinct", "depth", "left_on_queue", "levels", "actions"):
         assert a[k] == b[k], k
+
+
+def test_oracle_check_trace_of_an_evaluation_error(tmp_path):
+    """TLC's evaluation-error verdict (tests/golden/memb_parity.json "eval:memb_eval_single"): a
+    duplicated CatchupRequest handled twice empties s2's committed log (raft.tla:734-736), so
+    QuorumLogInv's Committed(s2) == SubSeq(log[s2], 1, commitIndex[s2]) is out of range (:969).
+    check-trace replays the fixture's trace and reports the error on its last state only."""
+    g = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))["eval:memb_eval_single"]
+    assert g["verdict"] == "EVAL_ERROR" and len(g["trace"]) == g["depth"]
+    p = tmp_path / "eval.txt"
+    p.write_text("\n".join(t["state"] for t in g["trace"]) + "\n")
+    r = run_oracle("check-trace", MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), "--golden", str(p))
+    assert r["valid"] and r["violated"] == "QuorumLogInv" and "SubSeq" in r["eval_error"], r
+    assert r["actions"].split(",") == [t["action"] for t in g["trace"][1:]]
+    # the same search in the oracle's lean mode stops at the same point
+    b = run_oracle("bfs", MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), "--deadlock", "--lean", "--workers", "4")
+    for k in ("verdict", "generated", "distinct", "depth", "left_on_queue", "levels", "actions"):
+        assert b[k] == g[k], k
+
+
+def test_deadlock_verdict_and_no_deadlock_in_shipped_next_relations():
+    """TLC's deadlock check: NEXT NextUnreliable alone (raft.tla:924-932) has no successor of Init
+    (empty bag) — "Deadlock reached" at State 1; the shipped NEXT relations never deadlock (Restart
+    is always enabled; under NextAsync a server of its own config can Timeout or is a Leader with
+    ClientRequest), so checking deadlock changes no count of their fixtures."""
+    fix = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))
+    g = fix["deadlock:memb_unreliable"]
+    assert (g["verdict"], g["depth"], g["distinct"], len(g["trace"])) == ("DEADLOCK", 1, 1, 1)
+    for case in ("membership_shipped@14", "memb_dynamic3@14"):
+        f = fix[case]
+        r = run_oracle("bfs", MEMB_MC, os.path.join(CONFIGS, f["cfg"] + ".cfg"), "--sym", f.get("sym", "view"), "--deadlock",
+                       "--max-depth", f["max_depth"])
+        assert (r["verdict"], r["generated"], r["distinct"], r["actions"]) == ("OK", f["generated"], f["distinct"], f["actions"])
