@@ -71,7 +71,11 @@ typedef struct mc_ctx mc_ctx;
 typedef struct mc_opts {
   int32_t abi_version;        /* RAFTMC_ABI_VERSION                                       */
   int32_t device;             /* HIP device ordinal (one process per GPU)                  */
-  int32_t n_gpus;             /* 1 (multi-GPU runs use one process per GPU) */
+  int32_t n_gpus;             /* GPUs of this node that mc_run uses (1..8).  > 1: the fingerprints are
+                                 owner-partitioned over devices device .. device + n_gpus - 1, one host
+                                 thread per GPU inside the library, exchanging over an in-process RCCL
+                                 communicator (xGMI); the result (counts, verdict, counterexample) is the
+                                 single-GPU one.  One process per GPU instead: mc_shard_run_rccl.      */
   int32_t workers;            /* TLC -workers N: 1 (TLC's default) = TLC's single-worker FIFO order,
                                  so every order-dependent output (kept parent of a state, per-action
                                  distinct counts, counterexample) is TLC's; otherwise TLC -workers N
@@ -85,7 +89,10 @@ typedef struct mc_opts {
   uint32_t tlc_compat_flags;  /* MC_COMPAT_* (default MC_COMPAT_INV_OUT_OF_MODEL | MC_COMPAT_SYM_TLC) */
   int32_t check_deadlock;     /* 1 = report states without successors (TLC default; -deadlock disables) */
   int32_t block_size;         /* expand kernel workgroup size (0 = 256)                   */
-  int32_t reserved[7];
+  int32_t same_device;        /* n_gpus > 1 only: 1 = every rank on `device` (the ranks exchange through
+                                 an in-process loopback of device copies): the multi-GPU level loop on
+                                 a one-GPU machine (tests); 0 = one device per rank (default)        */
+  int32_t reserved[6];
 } mc_opts;
 
 typedef struct mc_summary_t {

@@ -33,10 +33,19 @@ struct mc_ctx {
   ncclComm_t comm = nullptr;
   int comm_rank = -1, comm_world = 0;
   char comm_id[sizeof(ncclUniqueId)] = {0};
+  // mc_opts.n_gpus > 1: the backends of ranks 1.. (rank 0 is `be`), one per GPU, and their in-process
+  // RCCL communicators (ncclCommInitAll, kept across runs)
+  int n_gpus = 1;
+  bool same_device = false;
+  std::vector<std::unique_ptr<rmc::Backend>> peers;
+  std::vector<ncclComm_t> local_comms;
   ~mc_ctx() {
     be.reset();
+    peers.clear();
     if (comm) (void)rmc::rccl().CommDestroy(comm);
+    for (ncclComm_t x : local_comms) if (x) (void)rmc::rccl().CommDestroy(x);
   }
+  rmc::Backend* rank_backend(int r) const { return r == 0 ? be.get() : peers[r - 1].get(); }
 };
 
 namespace {
@@ -97,7 +106,9 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
   mc_opts d; mc_default_opts(&d);
   if (!o) o = &d;
   if (o->abi_version != RAFTMC_ABI_VERSION) { delete c; return MC_E_INVALID; }
-  if (o->n_gpus != 1) { delete c; return MC_E_UNSUPPORTED; }
+  if (o->n_gpus < 1 || o->n_gpus > 8) { delete c; return MC_E_INVALID; }
+  c->n_gpus = o->n_gpus;
+  c->same_device = o->same_device != 0;
   c->ro.device = o->device;
   c->ro.fp_table_bytes = o->fp_table_bytes;
   c->ro.state_store_bytes = o->state_store_bytes;
@@ -111,16 +122,21 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
   try {
     std::string fam = rmc::detect_spec_family(rmc::read_text_file(tla_path));
     rmc::CfgFile cfg = rmc::parse_cfg_text(rmc::read_text_file(cfg_path));
-    if (fam == "raft_original") c->be.reset(rmc::make_orig_backend(cfg));
-    else if (fam == "tlc_membership") c->be.reset(rmc::make_memb_backend(cfg));
-    else throw rmc::CfgError(MC_E_UNSUPPORTED, "spec family '" + fam + "' has no GPU backend in this build");
+    auto make = [&]() -> rmc::Backend* {
+      if (fam == "raft_original") return rmc::make_orig_backend(cfg);
+      if (fam == "tlc_membership") return rmc::make_memb_backend(cfg);
+      throw rmc::CfgError(MC_E_UNSUPPORTED, "spec family '" + fam + "' has no GPU backend in this build");
+    };
+    c->be.reset(make());
+    for (int r = 1; r < c->n_gpus; ++r) c->peers.emplace_back(make());   // one compiled model per GPU
     // the golden traces of punctuated-search constraints are operator definitions of the module
     // (or of a module it EXTENDS, next to it); the caller may also pass them (mc_set_history_prefix)
     for (const auto& con : c->be->history_prefixes_needed()) {
       const std::string lit = rmc::find_trace_literal(tla_path, con);
       if (lit.empty()) continue;
       std::string err;
-      if (int rc = c->be->set_history_prefix(con, rmc::parse_tla_value(lit), err)) throw rmc::CfgError(rc, con + ": " + err);
+      for (int r = 0; r < c->n_gpus; ++r)
+        if (int rc = c->rank_backend(r)->set_history_prefix(con, rmc::parse_tla_value(lit), err)) throw rmc::CfgError(rc, con + ": " + err);
     }
   } catch (const rmc::CfgError& e) {
     c->last_error = e.what();
@@ -141,8 +157,10 @@ int mc_set_history_prefix(mc_ctx* c, const char* constraint, const char* trace_t
   if (!c->be) return MC_E_STATE;
   try {
     std::string err;
-    const int rc = c->be->set_history_prefix(constraint, rmc::parse_tla_value(trace_text), err);
-    if (rc) { c->last_error = err; return rc; }
+    for (int r = 0; r < c->n_gpus; ++r) {
+      const int rc = c->rank_backend(r)->set_history_prefix(constraint, rmc::parse_tla_value(trace_text), err);
+      if (rc) { c->last_error = err; return rc; }
+    }
   } catch (const rmc::CfgError& e) {
     c->last_error = e.what();
     return e.code;
@@ -165,9 +183,96 @@ int mc_set_recover(mc_ctx* c, const char* path) {
   return MC_OK;
 }
 
+namespace {
+// mc_opts.n_gpus > 1: the sharded BFS (owner-partitioned fingerprints) inside this
+// process, one host thread per GPU running the backend's native level loop (raft_original:
+// orig_backend.hip shard_run_native; tlc_membership: fifo_shard_loop.h) over an in-process RCCL
+// communicator (ncclCommInitAll over the devices), or over the loopback of device copies when every
+// rank shares one device (same_device) or RCCL cannot be loaded.  The counterexample is
+// reassembled by chasing parent pointers across the ranks' stores (gid bits 37..39 = owner rank).
+int run_multi(mc_ctx* c) {
+  const int W = c->n_gpus;
+  std::string err;
+  if (!c->ro.checkpoint_path.empty() || !c->ro.recover_path.empty()) {
+    c->last_error = "checkpoint/recover apply to single-GPU runs (n_gpus = 1)";
+    return MC_E_UNSUPPORTED;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) { c->last_error = "no HIP device available (raftmc has no CPU fallback)"; return MC_E_NO_DEVICE; }
+  std::vector<int> dev(W);
+  for (int r = 0; r < W; ++r) dev[r] = c->same_device ? c->ro.device : c->ro.device + r;
+  if (dev[W - 1] >= ndev) {
+    c->last_error = "n_gpus = " + std::to_string(W) + " from device " + std::to_string(c->ro.device) + " needs " +
+                    std::to_string(dev[W - 1] + 1) + " HIP devices, this node has " + std::to_string(ndev);
+    return MC_E_NO_DEVICE;
+  }
+  bool use_rccl = !c->same_device && rmc::rccl().load(err) == 0;
+  if (use_rccl && (int)c->local_comms.size() != W) {
+    for (ncclComm_t x : c->local_comms) if (x) (void)rmc::rccl().CommDestroy(x);
+    c->local_comms.assign(W, nullptr);
+    if (rmc::rccl().CommInitAll(c->local_comms.data(), W, dev.data()) != ncclSuccess) { c->local_comms.clear(); use_rccl = false; }
+  }
+  if (!use_rccl && !c->same_device) {   // loopback between devices: device copies over xGMI peer access
+    for (int a = 0; a < W; ++a)
+      for (int b = 0; b < W; ++b)
+        if (a != b && hipSetDevice(dev[a]) == hipSuccess) (void)hipDeviceEnablePeerAccess(dev[b], 0);
+    (void)hipGetLastError();   // "already enabled" is not an error here
+  }
+  rmc::LoopbackWorld world(W);
+  std::vector<int> rcs(W, MC_OK);
+  std::vector<std::string> errs(W);
+  auto rank_main = [&](int r) {
+    rmc::Backend* be = c->rank_backend(r);
+    rmc::RunOpts o = c->ro;
+    o.device = dev[r];
+    std::string e;
+    int rc = be->shard_open(o, r, W, e);   // selects the device on this thread
+    if (!rc) {
+      if (use_rccl) { rmc::RcclTransport t(c->local_comms[r]); rc = be->shard_run_native(t, e); }
+      else { rmc::LoopbackTransport t(world, r); rc = be->shard_run_native(t, e); }
+    }
+    if (rc) world.abort();
+    rcs[r] = rc; errs[r] = e;
+  };
+  std::vector<std::thread> th;
+  for (int r = 1; r < W; ++r) th.emplace_back(rank_main, r);
+  rank_main(0);
+  for (auto& x : th) x.join();
+  for (int r = 0; r < W; ++r)
+    if (rcs[r]) { c->last_error = "rank " + std::to_string(r) + ": " + errs[r]; return rcs[r]; }
+  c->res = *c->be->shard_result();                 // every rank holds the global counts
+  for (int r = 0; r < W && c->res.violated.empty(); ++r) c->res.violated = c->rank_backend(r)->shard_result()->violated;
+  // the counterexample: the lowest rank holding the stop's head, then the parent chain by owner
+  c->res.trace.clear();
+  for (int r = 0; r < W; ++r) {
+    uint64_t parent = 0;
+    std::string act, text;
+    if (c->rank_backend(r)->shard_violation(&parent, act, text)) continue;
+    std::vector<std::pair<std::string, std::string>> tr{{act, text}};
+    uint64_t gid = parent;
+    for (int hop = 0; gid != ~0ull && hop < (1 << 20); ++hop) {
+      uint64_t meta = 0;
+      std::string t2;
+      const int owner = (int)((gid >> 37) & 7);
+      if (owner >= W || c->rank_backend(owner)->shard_read_state(gid, t2, &meta, err)) { c->last_error = "trace: " + err; return MC_E_STATE; }
+      const size_t a = (size_t)((meta >> 16) & 0xFF);
+      tr.push_back({meta == ~0ull ? std::string("<Initial predicate>")
+                                  : (a < c->res.action_names.size() ? c->res.action_names[a] : std::string("?")), t2});
+      gid = meta == ~0ull ? ~0ull : meta >> 24;
+    }
+    c->res.trace.assign(tr.rbegin(), tr.rend());
+    break;
+  }
+  c->ran = true;
+  c->last_error = c->res.error;
+  return MC_OK;
+}
+}  // namespace
+
 int mc_run(mc_ctx* c) {
   if (!c) return MC_E_INVALID;
   if (!c->be) return MC_E_STATE;
+  if (c->n_gpus > 1) { c->ran = false; return run_multi(c); }
   std::string err;
   int rc = c->be->run(c->ro, c->res, err);
   c->last_error = err.empty() ? c->res.error : err;
@@ -308,7 +413,8 @@ int mc_describe(const mc_ctx* c, char** text, size_t* len) {
   if (!d.empty() && d.back() == '}') {
     d.pop_back();
     d += std::string(", \"symmetry_mode\": \"") + (c->ro.sym_tlc ? "tlc" : "orbit") + "\", \"workers\": " +
-         std::to_string(c->ro.workers) + ", \"check_deadlock\": " + (c->ro.check_deadlock ? "true" : "false") + "}";
+         std::to_string(c->ro.workers) + ", \"check_deadlock\": " + (c->ro.check_deadlock ? "true" : "false") +
+         ", \"n_gpus\": " + std::to_string(c->n_gpus) + "}";
   }
   *text = dup_text(d, len);
   return *text ? MC_OK : MC_E_OOM;

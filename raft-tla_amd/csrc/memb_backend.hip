@@ -42,6 +42,7 @@
 
 #include "../../include/raftmc.h"
 #include "backend.h"
+#include "fifo_shard_loop.h"
 #include "fp_gap.h"
 #include "host_store.h"
 #include "memb_prefix.h"
@@ -416,6 +417,68 @@ __global__ void __launch_bounds__(BS) memb_materialize(MMatArgs a) {
   __syncthreads();
   for (int t = threadIdx.x; t < MA_NACT; t += BS)
     if (lds_cnt[t]) atomicAdd(&a.ctr[C_ACT + MA_NACT + t], (unsigned long long)lds_cnt[t]);
+}
+
+// TLC's per-action counters at a stop point (oracle/engine.h: a parent's successors are counted in
+// enumeration order up to the event's own successor; a next-state error counts none of the
+// parent's).  Parents [0, n) of a level range starting at gid `first`; parent `stop` is the event's
+// (n = stop + 1 when the event is in this range, else every parent counts whole).
+template <class S, int K0, int K1, int NS>
+__device__ __forceinline__ void stop_group(typename S::Work& s, const MembRuntime& rt, bool whole, int stop_slot, u32& err,
+                                           unsigned int* lds_cnt) {
+  using W = typename S::Work;
+  for (int k = K0; k < K1; ++k) {
+    const bool en = S::group_enabled(k, rt.next);                     // wave-uniform
+    for (int sub = 0; sub < NS; ++sub) {
+      if (!en) continue;
+      S::launder(s);
+      W t;
+      const int act = S::template apply<false>(s, k, sub, t, err, rt);
+      if (act >= 0 && (whole || S::slot_of(k, sub) <= stop_slot)) atomicAdd(&lds_cnt[act], 1u);
+    }
+  }
+}
+template <class S>
+__global__ void __launch_bounds__(BS) memb_stop_generated(const u32* states, u64 first, u64 n, u64 stop, int stop_slot, u32 kind,
+                                                          MembRuntime rt, unsigned long long* out) {
+  using W = typename S::Work;
+  constexpr int NWP = S::NWP;
+  __shared__ unsigned int lds_cnt[MA_NACT];
+  for (int t = threadIdx.x; t < MA_NACT; t += BS) lds_cnt[t] = 0;
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  const bool active = i < n && !(i == stop && kind == EV_NEXT_ERROR);
+  W s;
+  if (active) {
+    u32 w[NWP];
+    const uint4* src = reinterpret_cast<const uint4*>(states + (first + i) * NWP);
+#pragma unroll
+    for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+    S::unpack(w, s);
+  } else {
+    S::init(s);
+  }
+  u32 err = 0;
+  if (active) {   // (active is per lane; the groups' loops are wave-uniform, inactive lanes idle)
+    const bool whole = i < stop;
+    stop_group<S, S::G_RV, S::G_RECV, 1>(s, rt, whole, stop_slot, err, lds_cnt);
+    stop_group<S, S::G_RECV, S::G_TO, 2>(s, rt, whole, stop_slot, err, lds_cnt);
+    stop_group<S, S::G_TO, S::NI, 1>(s, rt, whole, stop_slot, err, lds_cnt);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < MA_NACT; t += BS)
+    if (lds_cnt[t]) atomicAdd(&out[t], (unsigned long long)lds_cnt[t]);
+}
+// per-action distinct counts of n stored new states (their meta: parent << 20 | action << 10 | slot)
+__global__ void __launch_bounds__(BS) memb_stop_distinct(const u64* meta, u64 n, unsigned long long* out) {
+  __shared__ unsigned int lds_cnt[MA_NACT];
+  for (int t = threadIdx.x; t < MA_NACT; t += BS) lds_cnt[t] = 0;
+  __syncthreads();
+  const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
+  if (i < n) atomicAdd(&lds_cnt[((meta[i] >> 10) & 1023) % MA_NACT], 1u);
+  __syncthreads();
+  for (int t = threadIdx.x; t < MA_NACT; t += BS)
+    if (lds_cnt[t]) atomicAdd(&out[t], (unsigned long long)lds_cnt[t]);
 }
 
 // Recovery from a checkpoint (TLC -recover): the fingerprints of the stored states [0, n) go back
@@ -843,6 +906,7 @@ class MembGpu : public Backend {
       u64 next_write = level_begin + level_count;
       double level_ms = 0;
       int64_t gen_before_chunk = 0;       // generated in earlier chunks of this level
+      std::vector<u64> act_before_chunk(2 * MA_NACT, 0);   // per-action generated / distinct in earlier chunks
       u64 gen_in_level = 0;               // in-model successors of this level (G_in)
       u64 gin_seen = 0;                   // ... counted up to the previous chunk
       u64 c[C_NCTR] = {0};
@@ -919,6 +983,7 @@ class MembGpu : public Backend {
         if (c[C_EVENT] != ~0ull) {
           // first event of this chunk in key order (earlier chunks had none)
           handle_event(c, cnt, level_begin, level_count, rank0, gen_before_chunk, next_write - (level_begin + level_count), nnew, level, r);
+          stop_action_counts(c, sp, mp, cb, level_begin, rank0, next_write, act_before_chunk, r);
           stop = true;
         }
         if (c[C_ERR]) stop = true;
@@ -926,6 +991,7 @@ class MembGpu : public Backend {
         next_write += nnew;
         int64_t g_all = 0; for (int k = 0; k < MA_NACT; ++k) g_all += (int64_t)c[C_ACT + k];
         gen_before_chunk = g_all;
+        for (int k = 0; k < 2 * MA_NACT; ++k) act_before_chunk[k] = c[C_ACT + k];
       }
       r.seconds_kernels += level_ms / 1000.0;
       r.n_launches += 1;
@@ -1165,6 +1231,44 @@ class MembGpu : public Backend {
     }
     r.depth = (int64_t)level + 2;   // the successor's depth (oracle: level + 1, Init = 1)
     build_trace(gid, act >= 0 ? kMembActNames[act] : "?", t, r);
+  }
+
+  // TLC's per-action (generated, distinct) counters at the stop point: the level's earlier chunks
+  // whole, this chunk's parents before the event's whole, the event's parent up to its own successor
+  // (none for a next-state error), and the new states before the event (key order = store order)
+  int stop_counts_dev(const u32* sp, u64 first, u64 npar, u64 stop, int stop_slot, u32 kind, const u64* meta, u64 before,
+                      u64* gen, u64* dist) {
+    unsigned long long* d = nullptr;
+    if (hipMalloc(&d, 2 * MA_NACT * 8) != hipSuccess) return MC_E_OOM;
+    int rc = 0;
+    if (hipMemsetAsync(d, 0, 2 * MA_NACT * 8, stream_) != hipSuccess) rc = MC_E_NO_DEVICE;
+    if (!rc && npar)
+      hipLaunchKernelGGL((memb_stop_generated<S>), dim3((unsigned)((npar + BS - 1) / BS)), dim3(BS), 0, stream_, sp, first, npar, stop,
+                         stop_slot, kind, rt_dev_, d);
+    if (!rc && before)
+      hipLaunchKernelGGL(memb_stop_distinct, dim3((unsigned)((before + BS - 1) / BS)), dim3(BS), 0, stream_, meta, before, d + MA_NACT);
+    u64 h[2 * MA_NACT];
+    if (!rc && (hipGetLastError() != hipSuccess || hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, stream_) != hipSuccess ||
+                hipStreamSynchronize(stream_) != hipSuccess)) rc = MC_E_NO_DEVICE;
+    (void)hipFree(d);
+    if (rc) return rc;
+    for (int k = 0; k < MA_NACT; ++k) { gen[k] = h[k]; dist[k] = h[MA_NACT + k]; }
+    return 0;
+  }
+  void stop_action_counts(const u64* c, const u32* sp, const u64* mp, u64 cb, u64 level_begin, u64 rank0, u64 next_write,
+                          const std::vector<u64>& before_chunk, RunResult& r) {
+    const u64 ev = c[C_EVENT], key = ev >> 2;
+    const int kind = (int)(ev & 3);
+    const u64 rank = key / S::NSLOT, slot = key % S::NSLOT;
+    (void)level_begin;
+    // the new states of this chunk before the event: r.distinct - (stored before this chunk)
+    const u64 before = (u64)r.distinct - next_write;
+    u64 gen[MA_NACT], dist[MA_NACT];
+    if (stop_counts_dev(sp, cb, rank - rank0 + 1, rank - rank0, (int)slot, (u32)kind, mp + next_write, before, gen, dist)) return;
+    for (int k = 0; k < MA_NACT; ++k) {
+      r.act_generated[k] += (int64_t)(before_chunk[k] + gen[k]);
+      r.act_distinct[k] += (int64_t)(before_chunk[MA_NACT + k] + dist[k]);
+    }
   }
 
   int dump_states(const std::string& path, std::string& err) override {
@@ -1474,6 +1578,13 @@ class MembGpu : public Backend {
     int64_t before = 0;
     for (u64 k : ks) if (k < key || (k == key && kind >= EV_INV_ERROR)) ++before;
     st[30] = gen; st[31] = before;
+    {   // this rank's share of TLC's per-action counters at the stop point ([8, 8+A) generated, [40, 40+A) distinct)
+      const u64 npar = R < s_B_ ? 0 : std::min<u64>(s_level_count_, R - s_B_ + 1);
+      u64 ag[MA_NACT], ad[MA_NACT];
+      if (int rc = stop_counts_dev(d_states_, s_level_begin_, npar, R - std::min<u64>(R, s_B_), (int)slot, (u32)kind,
+                                   d_meta_ + total_, (u64)before, ag, ad)) { err = "stop-point counters"; return rc; }
+      for (int k = 0; k < MA_NACT; ++k) { st[8 + k] = (int64_t)ag[k]; st[40 + k] = (int64_t)ad[k]; }
+    }
     if (R >= s_B_ && R < s_B_ + s_level_count_) {   // the event's parent is ours: the counterexample head
       const u64 gid = s_level_begin_ + (R - s_B_);
       W s; read_state(gid, s);
@@ -1508,6 +1619,7 @@ class MembGpu : public Backend {
       const u64 R = key / S::NSLOT;
       sres_.generated += g[30];
       sres_.distinct += g[31];
+      for (int k = 0; k < MA_NACT; ++k) { sres_.act_generated[k] += g[8 + k]; sres_.act_distinct[k] += g[40 + k]; }
       if (kind == EV_DEADLOCK) sres_.verdict = MC_VERDICT_DEADLOCK;
       else if (kind == EV_NEXT_ERROR) {
         sres_.verdict = MC_VERDICT_EVAL_ERROR;
@@ -1567,6 +1679,12 @@ class MembGpu : public Backend {
     return 0;
   }
   const RunResult* shard_result() const override { return &sres_; }
+  // the whole FIFO-ranked level loop natively over a transport (RCCL or the in-process loopback),
+  // after shard_open: fifo_shard_loop.h
+  int shard_run_native(ShardTransport& t, std::string& err) override {
+    FifoShardLoop loop(*this, t, s_rank_, s_world_);
+    return loop.run(err);
+  }
 
  private:
   MembModel m_;

@@ -60,7 +60,9 @@ namespace rmc {
 
 enum {
   K_NEW = 0, K_GEN_IN = 1, K_ERR = 2, K_EVENT = 3, K_ERRGID = 4, K_INS = 5, K_CHUNK_NEW = 6, K_LEVEL_NEW = 7,
-  K_ACT = 8, K_PROF = K_ACT + 2 * OA_NACT, K_NCTR = K_PROF + 8   // K_PROF: phase timers (RAFTMC_PROF)
+  K_ACT = 8, K_PROF = K_ACT + 2 * OA_NACT,   // K_PROF: phase timers (RAFTMC_PROF, slots 0..5)
+  K_LEAD = K_PROF + 7,                         // the chunk's leader-work parents (orig_generate_lead)
+  K_NCTR = K_PROF + 8
 };
 enum { EV_NEXT_ERROR = 0, EV_DEADLOCK = 1, EV_INV_ERROR = 2, EV_VIOLATION = 3 };
 enum { OE_CAP_STORE = 0x100, OE_TABLE_FULL = 0x200 };
@@ -90,6 +92,7 @@ struct GenArgs {
   OrigRuntime rt;
   u32 inv_oom, deadlock;
   unsigned long long* ctr;
+  u32* lead;                   // [chunk] parents with leader work (chunk index | 1 << 31 if no other successor)
 };
 
 #if defined(RMC_EXP_DOUBLE_PACKFP) || defined(RMC_EXP_DOUBLE_APPLY)
@@ -171,8 +174,19 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
     S::pack(b, bw);
     fb.init(bw, a.seed);
   }
+  // leader work (S::leader_work: a Leader or a Candidate with a quorum, ~1% of C2's states) is
+  // left to orig_generate_lead, which runs those instances on full waves of just such parents: here
+  // a wave with one leader lane would pay all of [LEAD_LO, LEAD_HI) for it (measured: a third of
+  // this kernel's time for 0.7% of C2's successors)
+  const bool lead = active && S::leader_work(s);
 #pragma unroll 1
   for (int k = 0; k < S::NI; ++k) {
+#ifndef RMC_DBG_NO_SKIP
+    if (k == S::LEAD_LO) k = S::LEAD_HI;      // wave-uniform
+#endif
+#ifdef RMC_EXP_SKIP_HI
+    if (k >= RMC_EXP_SKIP_LO && k < RMC_EXP_SKIP_HI) continue;   // cost-attribution experiment only
+#endif
     u64 fp = 0;
     bool have = false;
     int cnt_act = -1;   // this lane's successor action (RMC_GEN_WAVE_COUNTS: counted per wave)
@@ -243,8 +257,20 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
   }
   if (active) {
     if (err & OE_EVAL_LOG_INDEX) { const u64 e = ev_word(gid, 0, EV_NEXT_ERROR); ev = e < ev ? e : ev; }
-    if (nsucc == 0 && a.deadlock) { const u64 e = ev_word(gid, 0, EV_DEADLOCK); ev = e < ev ? e : ev; }
+    if (nsucc == 0 && a.deadlock && !lead) { const u64 e = ev_word(gid, 0, EV_DEADLOCK); ev = e < ev ? e : ev; }
   }
+#ifndef RMC_DBG_NO_PUSH
+  {   // leader-work parents to the chunk's list: one global atomic per wave
+    const u64 lm = __ballot(lead);
+    if (lm) {
+      const int first = __ffsll((unsigned long long)lm) - 1;
+      u32 base = 0;
+      if (lane == first) base = (u32)atomicAdd(&a.ctr[K_LEAD], (unsigned long long)__popcll(lm));
+      base = __shfl(base, first);
+      if (lead) a.lead[base + (u32)__popcll(lm & ((1ull << lane) - 1ull))] = (u32)tid | (nsucc == 0 ? 0x80000000u : 0u);
+    }
+  }
+#endif
   const u32 cap_err = err & ~(u32)OE_EVAL_LOG_INDEX;   // compiled-capacity limits, not TLC semantics
   if (cap_err) {
     atomicOr(&a.ctr[K_ERR], (unsigned long long)cap_err);
@@ -257,6 +283,98 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
     if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + t], (unsigned long long)lds_cnt[t]);
   if (threadIdx.x == 0 && lds_cnt[OA_NACT]) atomicAdd(&a.ctr[K_GEN_IN], (unsigned long long)lds_cnt[OA_NACT]);
   if (lane == 0) a.rcnt[blockIdx.x * 4 + wave] = wcount;
+}
+
+// The instances [LEAD_LO, LEAD_HI) of the chunk's leader-work parents (the list orig_generate wrote),
+// one lane per parent on full waves: the same successor / constraint / count / pack / FP64 work as
+// orig_generate, the in-model records appended to the parent's own wave region of its generate
+// workgroup (global atomic on that wave's record count: the dedup kernels read whole regions, and
+// record order inside a region is immaterial: the FIFO merge keeps the minimum key, the -workers N
+// filter decides by key).
+template <class S>
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 15 ? RMC_GEN_WAVES : 1))) orig_generate_lead(GenArgs a) {
+  using W = typename S::Work;
+  constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
+  __shared__ unsigned int lds_cnt[OA_NACT + 1];
+  for (int t = threadIdx.x; t < OA_NACT + 1; t += BS) lds_cnt[t] = 0;
+  __syncthreads();
+  const u64 n = a.ctr[K_LEAD];
+  constexpr bool INC = RMC_GEN_INC && NW <= 16;
+  u32 err = 0, nin = 0;
+  unsigned long long ev = ~0ull;
+  // grid-stride with a wave-uniform trip count (every lane of a wave runs the same instance loop)
+  for (u64 i0 = (u64)blockIdx.x * BS; i0 < n; i0 += (u64)gridDim.x * BS) {
+    const u64 i = i0 + threadIdx.x;
+    const bool active = i < n;
+    const u32 ent = active ? a.lead[i] : 0u;
+    const u64 p = ent & 0x7fffffffu;                 // chunk index of the parent
+    const u64 gid = a.gid0 + p;
+    W s;
+    u64 al[S::AW];
+    if (active) {
+      u32 w[NWP];
+      const uint4* src = reinterpret_cast<const uint4*>(a.states + (a.chunk_begin + p) * NWP);
+#pragma unroll
+      for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+      S::unpack(w, s);
+      S::all_logs_next(s, al);
+    } else {
+      S::init(s);
+#pragma unroll
+      for (int q = 0; q < S::AW; ++q) al[q] = 0;
+    }
+    u32 bw[INC ? NW : 1];
+    FpBase<INC ? NW : 2> fb;
+    if constexpr (INC) {
+      W b = s;
+#pragma unroll
+      for (int q = 0; q < S::AW; ++q) b.allLogs[q] = al[q];
+      S::pack(b, bw);
+      fb.init(bw, a.seed);
+    }
+    const u32 blk = (u32)(p / BS), plane = (u32)(p % BS);
+    const u64 wreg = (u64)blk * (BS * S::NI) + (u64)(plane >> 6) * (64 * S::NI);
+    u32* wcnt = a.rcnt + blk * 4 + (plane >> 6);
+    u32 nsucc = 0, perr = 0;
+#pragma unroll 1
+    for (int k = S::LEAD_LO; k < S::LEAD_HI; ++k) {
+      if (!active) continue;
+      W t;
+      const int act = S::apply(s, k, t, perr);
+      if (act < 0) continue;
+#pragma unroll
+      for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
+      ++nsucc;
+      atomicAdd(&lds_cnt[act], 1u);
+      if (S::in_model(t, a.rt)) {
+        ++nin;
+        u32 pw[NW];
+        S::pack(t, pw);
+        u64 fp;
+        if constexpr (INC) fp = fb.fp(pw, bw, a.seed);
+        else fp = fp64(pw, a.seed);
+        const u32 idx = atomicAdd(wcnt, 1u);
+        a.rfp[wreg + idx] = fp;
+        a.rkey[wreg + idx] = (unsigned short)((plane << 8) | (unsigned)k);
+      } else if (a.inv_oom && S::violated(t, a.rt.invariants)) {
+        const u64 e = ev_word(gid, (u32)k, EV_VIOLATION);
+        ev = e < ev ? e : ev;
+      }
+    }
+    if (active) {
+      if (perr & OE_EVAL_LOG_INDEX) { const u64 e = ev_word(gid, 0, EV_NEXT_ERROR); ev = e < ev ? e : ev; }
+      if ((ent >> 31) && nsucc == 0 && a.deadlock) { const u64 e = ev_word(gid, 0, EV_DEADLOCK); ev = e < ev ? e : ev; }
+      const u32 ce = perr & ~(u32)OE_EVAL_LOG_INDEX;
+      if (ce) { atomicCAS(&a.ctr[K_ERRGID], 0ull, (unsigned long long)(gid + 1)); err |= ce; }
+    }
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+  if (ev != ~0ull) atomicMin(&a.ctr[K_EVENT], ev);
+  if (nin) atomicAdd(&lds_cnt[OA_NACT], nin);
+  __syncthreads();
+  for (int t = threadIdx.x; t < OA_NACT; t += BS)
+    if (lds_cnt[t]) atomicAdd(&a.ctr[K_ACT + t], (unsigned long long)lds_cnt[t]);
+  if (threadIdx.x == 0 && lds_cnt[OA_NACT]) atomicAdd(&a.ctr[K_GEN_IN], (unsigned long long)lds_cnt[OA_NACT]);
 }
 
 // Record i of workgroup b's four wave regions (concatenated in wave order): its offset in the
@@ -889,11 +1007,16 @@ __global__ void __launch_bounds__(BS) orig_materialize(MatArgs a) {
 
 // after a chunk's materialize: fold its new-state count into the level's; re-arm the chunk's
 // insert counter (the level's first chunk starts from the per-level counter reset)
+// (Vector atomics only: with plain accesses the compiler reads the counters with a scalar load
+// and may issue the vector store that zeroes K_CHUNK_NEW before that load has returned — on the
+// GPU the load then sometimes sees the zero and the chunk's new states are lost.  Found when a
+// fourth counter store moved the scalar wait behind the stores.)
 __global__ void orig_advance(unsigned long long* ctr) {
   if (threadIdx.x == 0) {
-    ctr[K_LEVEL_NEW] += ctr[K_CHUNK_NEW];
-    ctr[K_CHUNK_NEW] = 0;
-    ctr[K_INS] = 0;
+    const unsigned long long n = atomicExch(&ctr[K_CHUNK_NEW], 0ull);
+    atomicAdd(&ctr[K_LEVEL_NEW], n);
+    atomicExch(&ctr[K_INS], 0ull);
+    atomicExch(&ctr[K_LEAD], 0ull);
   }
 }
 
@@ -914,29 +1037,43 @@ __global__ void __launch_bounds__(BS) orig_stop_generated(const u32* states, u64
                                                          u32 k_stop, u32 kind, unsigned long long* out) {
   using W = typename S::Work;
   constexpr int NWP = (S::NW + 3) & ~3;
+  // counts in LDS, one global atomic per workgroup and action (a global atomic per successor on
+  // 16 addresses serialises: minutes for C5v2's 93M-parent level 11)
+  __shared__ unsigned int lds_cnt[1 + OA_NACT];
+  for (int q = threadIdx.x; q < 1 + OA_NACT; q += BS) lds_cnt[q] = 0;
+  __syncthreads();
   const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
-  if (i >= n) return;
   const u64 gid = gid0 + i;
-  if (gid == gid_stop && kind == EV_NEXT_ERROR) return;
-  u32 w[NWP];
+  if (i < n && !(gid == gid_stop && kind == EV_NEXT_ERROR)) {
+    u32 w[NWP];
 #pragma unroll
-  for (int q = 0; q < NWP; ++q) w[q] = states[(first + i) * NWP + q];
-  W s, t;
-  S::unpack(w, s);
-  u32 err = 0, tot = 0;
-  for (int k = 0; k < S::NI; ++k) {
-    const int act = S::apply(s, k, t, err);
-    if (act < 0) continue;
-    ++tot;
-    if (gid < gid_stop || (u32)k <= k_stop) atomicAdd(&out[1 + act], 1ull);
+    for (int q = 0; q < NWP; ++q) w[q] = states[(first + i) * NWP + q];
+    W s, t;
+    S::unpack(w, s);
+    u32 err = 0, tot = 0;
+    for (int k = 0; k < S::NI; ++k) {
+      const int act = S::apply(s, k, t, err);
+      if (act < 0) continue;
+      ++tot;
+      if (gid < gid_stop || (u32)k <= k_stop) atomicAdd(&lds_cnt[1 + act], 1u);
+    }
+    if (tot) atomicAdd(&lds_cnt[0], tot);
   }
-  if (tot) atomicAdd(&out[0], (unsigned long long)tot);
+  __syncthreads();
+  for (int q = threadIdx.x; q < 1 + OA_NACT; q += BS)
+    if (lds_cnt[q]) atomicAdd(&out[q], (unsigned long long)lds_cnt[q]);
 }
 
 // per-action distinct counts of the level's first n new states (stored in key order)
 __global__ void __launch_bounds__(BS) orig_stop_distinct(const u64* meta, u64 n, unsigned long long* out) {
+  __shared__ unsigned int lds_cnt[OA_NACT];
+  for (int q = threadIdx.x; q < OA_NACT; q += BS) lds_cnt[q] = 0;
+  __syncthreads();
   const u64 i = (u64)blockIdx.x * BS + threadIdx.x;
-  if (i < n) atomicAdd(&out[(meta[i] >> 16) & 0xff], 1ull);
+  if (i < n) atomicAdd(&lds_cnt[((meta[i] >> 16) & 0xff) % OA_NACT], 1u);
+  __syncthreads();
+  for (int q = threadIdx.x; q < OA_NACT; q += BS)
+    if (lds_cnt[q]) atomicAdd(&out[q], (unsigned long long)lds_cnt[q]);
 }
 
 // ------------------------------------------------------------------ sharded (multi-GPU) kernels
@@ -1240,6 +1377,7 @@ class OrigGpu : public Backend {
     HIPCHK(hipMalloc(&d_winmask_, chunk_states_ * WW * 8));
     HIPCHK(hipMalloc(&d_wcnt_, nblk * 4));
     HIPCHK(hipMalloc(&d_woff_, nblk * 8));
+    HIPCHK(hipMalloc(&d_lead_, chunk_states_ * 4));
     HIPCHK(hipMalloc(&d_ctr_, K_NCTR * 8));
     HIPCHK(hipHostMalloc((void**)&h_ctr_, K_NCTR * 8, hipHostMallocDefault));
     HIPCHK(hipMalloc(&d_stop_, (1 + OA_NACT) * 8));
@@ -1271,7 +1409,17 @@ class OrigGpu : public Backend {
     g.rfp = d_rfp_; g.rkey = d_rkey_; g.rcnt = d_rcnt_blk_; g.seed = seed; g.rt = m_.rt;
     g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.deadlock = o.check_deadlock ? 1u : 0u;
     g.ctr = (unsigned long long*)d_ctr_;
+    g.lead = d_lead_;
     return g;
+  }
+
+  // the successor pass of one chunk: orig_generate over every parent, then orig_generate_lead over
+  // the parents with leader work (its grid strides over the count the first kernel left on the
+  // device); K_LEAD must be zero before (level start: orig_reset_ctr, later chunks: orig_advance)
+  void launch_generate(const GenArgs& g, unsigned nblk) {
+    hipLaunchKernelGGL((orig_generate<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+    const unsigned lblk = std::min<unsigned>(nblk, std::max<unsigned>(64u, nblk / 8));
+    if (!dbg_no_lead_) hipLaunchKernelGGL((orig_generate_lead<S>), dim3(lblk), dim3(BS), 0, stream_, g);
   }
 
   RouteArgs route_args(u32 world) const {
@@ -1335,8 +1483,10 @@ class OrigGpu : public Backend {
       if (level_begin > base_) {
         const double prev = r.levels.size() >= 2 ? (double)r.levels[r.levels.size() - 2].states : 1.0;
         const double pred = (double)level_count * std::max(1.0, (double)level_count / std::max(prev, 1.0)) * 1.5;
-        if ((double)(total_ - base_) + pred > (double)cap_)
+        if ((double)(total_ - base_) + pred > (double)cap_) {
+          if (progress_) std::fprintf(stderr, "spilling %llu completed states to host memory\n", (unsigned long long)(level_begin - base_));
           if (int rc = spill(level_begin, level_count, err)) return rc;
+        }
       }
       if (!ctr_clean_) {
         hipLaunchKernelGGL(orig_reset_ctr, dim3(1), dim3(64), 0, stream_, (unsigned long long*)d_ctr_);
@@ -1356,7 +1506,7 @@ class OrigGpu : public Backend {
         // kernels index the device store (global id - base_); keys and parent pointers are global
         const GenArgs g = gen_args(cb - base_, cnt, cb, r.seed, o);
         HIPCHK(hipEventRecord(e[0], stream_));
-        hipLaunchKernelGGL((orig_generate<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+        launch_generate(g, nblk);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e[1], stream_));
         DedupArgs d;
@@ -1431,6 +1581,17 @@ class OrigGpu : public Backend {
       }
       const u64 nnew = c[K_LEVEL_NEW];
       const u64 next_write = level_end + nnew;
+      if (progress_)   // TLC's progress line, per BFS level (RAFTMC_PROGRESS=1), on stderr
+        std::fprintf(stderr, "Progress(%lld) at %.3f s: %lld states generated, %llu distinct states found, %llu states left on queue "
+                             "(level kernels %.1f ms, %d chunk(s), store %llu/%llu, %llu on the host)\n",
+                     (long long)r.depth + 1,
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(),
+                     (long long)(r.generated + (int64_t)[&] { u64 g = 0; for (int k = 0; k < OA_NACT; ++k) g += c[K_ACT + k]; return g; }()),
+                     (unsigned long long)(level_end + nnew), (unsigned long long)nnew, level_ms, nch,
+                     (unsigned long long)(next_write - base_), (unsigned long long)cap_, (unsigned long long)base_);
+      if (progress_ && (c[K_EVENT] != ~0ull || c[K_ERR]))
+        std::fprintf(stderr, "level %lld: event word 0x%llx, error flags 0x%llx\n", (long long)r.depth + 1,
+                     (unsigned long long)c[K_EVENT], (unsigned long long)c[K_ERR]);
       if (prof_) {
         for (int q = 0; q < 4; ++q) prof_acc_[q] += c[K_PROF + q];
         prof_acc_[4] = std::max<u64>(prof_acc_[4], c[K_PROF + 5]);
@@ -1536,6 +1697,11 @@ class OrigGpu : public Backend {
     }
     const u64 before = lo;
     decided = before < stored || stored == nnew;
+    const auto te0 = std::chrono::steady_clock::now();
+    auto since = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - te0).count(); };
+    if (progress_)
+      std::fprintf(stderr, "event kind %d at parent %llu instance %u: %llu new states before it (%s)\n", kind,
+                   (unsigned long long)pg, k, (unsigned long long)before, decided ? "decided" : "beyond the stored states");
     if (!decided) return 0;
     (void)nnew;
     // generated (device: re-derive the successor lists of the level's parents up to pg)
@@ -1555,6 +1721,7 @@ class OrigGpu : public Backend {
     u64 ds[1 + OA_NACT];
     HIPCHK(hipMemcpyAsync(ds, d_stop_, sizeof ds, hipMemcpyDeviceToHost, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
+    if (progress_) std::fprintf(stderr, "stop-point counters over %llu parents: %.3f s\n", (unsigned long long)npar, since());
     r.generated += (int64_t)gs[0];
     for (int a = 0; a < OA_NACT; ++a) { r.act_generated[a] += (int64_t)gs[1 + a]; r.act_distinct[a] += (int64_t)ds[a]; }
     r.distinct = (int64_t)(level_end + before);
@@ -1583,6 +1750,7 @@ class OrigGpu : public Backend {
     r.violated = first_violated(S::violated(t, m_.rt.invariants));
     r.depth += 1;
     build_trace(pg, act >= 0 ? kOrigActNames[act] : "?", t, r, err);
+    if (progress_) std::fprintf(stderr, "trace of %zu states: %.3f s\n", r.trace.size(), since());
     return 0;
   }
 
@@ -1799,7 +1967,8 @@ class OrigGpu : public Backend {
       const RouteArgs ra = route_args((u32)world_);
       const unsigned nblk = (unsigned)((count + BS - 1) / BS);
       HIPCHK(hipEventRecord(ev_[5], stream_));
-      hipLaunchKernelGGL((orig_generate<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+      HIPCHK(hipMemsetAsync(d_ctr_ + K_LEAD, 0, 8, stream_));
+      launch_generate(g, nblk);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(ev_[6], stream_));
       hipLaunchKernelGGL(orig_route_blk, dim3(nblk), dim3(BS), 0, stream_, ra);
@@ -2098,7 +2267,8 @@ class OrigGpu : public Backend {
         if (count > 0) {
           const GenArgs g = gen_args(sh_chunk_begin_, count, sh_chunk_begin_, sres_.seed, sopts_);
           const unsigned nblk = (unsigned)((count + BS - 1) / BS);
-          NAT_TIMED(0, hipLaunchKernelGGL((orig_generate<S>), dim3(nblk), dim3(BS), 0, stream_, g));
+          HIPCHK(hipMemsetAsync(d_ctr_ + K_LEAD, 0, 8, stream_));
+          NAT_TIMED(0, launch_generate(g, nblk));
           sres_.kernels[0].algo_bytes += (double)count * NWP * 4;
           const RouteArgs ra = route_args((u32)W);
           NAT_TIMED(1, hipLaunchKernelGGL(orig_route_blk, dim3(nblk), dim3(BS), 0, stream_, ra));
@@ -2213,6 +2383,7 @@ class OrigGpu : public Backend {
   u64* d_rfp_ = nullptr; unsigned short* d_rkey_ = nullptr; u32* d_rcnt_blk_ = nullptr; u64* d_newrec_ = nullptr;
   u64* d_winmask_ = nullptr; u32* d_wcnt_ = nullptr; u64* d_woff_ = nullptr; u64* d_urec_ = nullptr; u32* d_ucnt_ = nullptr;
   u64* d_route_ = nullptr; u64* d_rcnt_ = nullptr; u32* d_stout_ = nullptr; u64 stout_cap_ = 0;
+  u32* d_lead_ = nullptr;      // [chunk] the chunk's leader-work parents (orig_generate -> orig_generate_lead)
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_[9] = {};
   u64 table_mask_ = 0, cap_ = 0, total_ = 0, chunk_states_ = 0;
@@ -2231,6 +2402,8 @@ class OrigGpu : public Backend {
   const bool split_plain_ = std::getenv("RAFTMC_SPLIT_PLAIN") != nullptr;   // experiment: merge + probe kernels   // seen-set layout of the last single-GPU run (16-B keyed / 8-B entries)
   // RAFTMC_PROF=1: per-phase wall-clock ticks (100 MHz) of orig_dedup, summed over workgroups
   const bool prof_ = std::getenv("RAFTMC_PROF") != nullptr;
+  const bool progress_ = std::getenv("RAFTMC_PROGRESS") != nullptr;
+  const bool dbg_no_lead_ = std::getenv("RAFTMC_DBG_NO_LEAD") != nullptr;   // debugging only: leader work dropped
   u64 prof_acc_[5] = {0, 0, 0, 0, 0};
   // native (RCCL) level loop buffers
   u64* d_nat_ = nullptr; u64* h_nat_ = nullptr;
@@ -2245,7 +2418,7 @@ class OrigGpu : public Backend {
   void release() {
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_stop_, (void*)d_rfp_, (void*)d_rkey_,
                     (void*)d_rcnt_blk_, (void*)d_newrec_, (void*)d_winmask_, (void*)d_wcnt_, (void*)d_woff_, (void*)d_urec_, (void*)d_ucnt_,
-                    (void*)d_route_, (void*)d_rcnt_, (void*)d_stout_})
+                    (void*)d_route_, (void*)d_rcnt_, (void*)d_stout_, (void*)d_lead_})
       if (p) (void)hipFree(p);
     for (void* p : {(void*)d_nat_, nat_recv_, nat_acks_, nat_stin_})
       if (p) (void)hipFree(p);
@@ -2262,6 +2435,7 @@ class OrigGpu : public Backend {
     h_ctr_ = nullptr; ctr_clean_ = false;
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_stop_ = nullptr;
     d_rfp_ = nullptr; d_rkey_ = nullptr; d_rcnt_blk_ = nullptr; d_newrec_ = nullptr; d_winmask_ = nullptr; d_wcnt_ = nullptr; d_woff_ = nullptr; d_urec_ = nullptr; d_ucnt_ = nullptr; d_route_ = nullptr; d_rcnt_ = nullptr; d_stout_ = nullptr; stout_cap_ = 0;
+    d_lead_ = nullptr;
     stream_ = nullptr; alloc_world_ = 0;
   }
 
@@ -2296,10 +2470,14 @@ class OrigGpu : public Backend {
   int spill(u64 level_begin, u64 level_count, std::string& err) {
     const u64 d = level_begin - base_;
     u32* hs = nullptr; u64* hm = nullptr;
+    const auto ts = std::chrono::steady_clock::now();
+    auto since = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count(); };
     host_.append(d, &hs, &hm);   // a segment of its own: the host part is never reallocated
+    if (progress_) std::fprintf(stderr, "spill: %.1f GB of host memory allocated in %.3f s\n", d * (NWP * 4.0 + 8) / 1e9, since());
     HIPCHK(hipStreamSynchronize(stream_));
     HIPCHK(hipMemcpy(hs, d_states_, d * NWP * 4, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(hm, d_meta_, d * 8, hipMemcpyDeviceToHost));
+    if (progress_) std::fprintf(stderr, "spill: copied to host at %.3f s\n", since());
     for (u64 off = 0; off < level_count; off += d) {
       const u64 n = std::min<u64>(d, level_count - off);
       HIPCHK(hipMemcpyAsync(d_states_ + off * NWP, d_states_ + (d + off) * NWP, n * NWP * 4, hipMemcpyDeviceToDevice, stream_));

@@ -105,6 +105,11 @@ struct Orig {
                                N * (SLLB + ML * EB) + N * N * VLB + (int)U + EMAX * ELB + MK * ENTB;
   static constexpr int NW = (PBITS + 31) / 32;      // u32 words per stored state
   static constexpr int NI = 3 * N + 2 * N * N + N * NV + N + 3 * MK;   // action instances per state
+  // the instances that need a Leader (ClientRequest, AdvanceCommitIndex, AppendEntries) or a
+  // Candidate holding a quorum (BecomeLeader): one contiguous range [LEAD_LO, LEAD_HI) of apply's
+  // order; rare states (C2: ~1% of the frontier), so the generate kernel skips the range and a
+  // second pass runs it on full waves of just those parents (leader_work)
+  static constexpr int LEAD_LO = 2 * N + N * N, LEAD_HI = LEAD_LO + N + N * NV + N + N * N;
 
   static_assert(N >= 1 && N <= 7, "N");
   static_assert(N * TB <= 32 && N * VB <= 32 && N * CIB <= 32 && N * N <= 32, "scalar field words");
@@ -298,6 +303,18 @@ struct Orig {
 #pragma unroll
       for (int k = 0; k < AW; ++k) if ((int)(ix >> 6) == k) al[k] |= 1ull << (ix & 63);
     }
+  }
+
+  // true iff some instance in [LEAD_LO, LEAD_HI) can be enabled in s: a Leader (ClientRequest,
+  // AdvanceCommitIndex, AppendEntries) or a Candidate with a vote quorum (BecomeLeader :228-231)
+  RMC_HD static bool leader_work(const Work& s) {
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const int st = g_st(s, i);
+      any |= st == L || (st == C && popc32(row_bits(s.vgrant, i)) * 2 > N);
+    }
+    return any;
   }
 
   // ---------------------------------------------------------------- instance -> successor

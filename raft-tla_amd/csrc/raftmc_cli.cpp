@@ -1,7 +1,10 @@
 // raftmc — command-line front end mirroring TLC's flags:
 //   raftmc [-config F.cfg] [-workers N] [-deadlock] [-depth D] [-device K]
 //          [-fptable BYTES] [-store BYTES] [-seed S] [-no-inv-oom] [-dump FILE] [-json]
-//          [-checkpoint LEVELS] [-checkpoint-file FILE] [-recover FILE] [-symmetry tlc|orbit] F.tla
+//          [-checkpoint LEVELS] [-checkpoint-file FILE] [-recover FILE] [-symmetry tlc|orbit]
+//          [-gpus N] F.tla
+// (-gpus N: the node's GPUs -device .. -device+N-1 share one search, owner-partitioned fingerprints,
+// one host thread per GPU over an in-process RCCL communicator; TLC's -workers keeps its meaning)
 // (-checkpoint counts BFS levels where TLC counts minutes; the file defaults to states/raftmc.ckpt)
 // Prints TLC-style lines and exits with TLC-like codes (0 ok, 12 safety
 // violation, 11 deadlock, 75 error).
@@ -31,6 +34,7 @@ int main(int argc, char** argv) {
     else if (k == "-deadlock") o.check_deadlock = 0;   // TLC: -deadlock turns deadlock checking OFF
     else if (k == "-depth") o.max_depth = std::atoll(val());
     else if (k == "-device") o.device = std::atoi(val());
+    else if (k == "-gpus") o.n_gpus = std::atoi(val());
     else if (k == "-fptable") o.fp_table_bytes = std::strtoull(val(), nullptr, 10);
     else if (k == "-store") o.state_store_bytes = std::strtoull(val(), nullptr, 10);
     else if (k == "-seed") o.seed = std::strtoull(val(), nullptr, 0);
@@ -64,7 +68,7 @@ int main(int argc, char** argv) {
   if (rc == 0) {   // TLC prints its fingerprint-based estimate after a completed search
     mc_summary_t s;
     double v = 0;
-    if (mc_summary(c, &s) == 0 && s.verdict == MC_VERDICT_OK) (void)mc_collision_observed(c, &v);
+    if (mc_summary(c, &s) == 0 && s.verdict == MC_VERDICT_OK && o.n_gpus == 1) (void)mc_collision_observed(c, &v);
   }
   if (rc) { std::fprintf(stderr, "raftmc: %s (code %d)\n", mc_last_error(c), rc); mc_close(c); return 75; }
   char* text = nullptr; size_t len = 0;

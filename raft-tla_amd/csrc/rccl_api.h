@@ -15,6 +15,7 @@ namespace rmc {
 struct RcclApi {
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;   // one process, one rank per device
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
   ncclResult_t (*GroupEnd)() = nullptr;
@@ -35,6 +36,7 @@ struct RcclApi {
   if (!f) { err = std::string("RCCL symbol missing: ") + name; return -1; }
     RMC_SYM(GetUniqueId, "ncclGetUniqueId");
     RMC_SYM(CommInitRank, "ncclCommInitRank");
+    RMC_SYM(CommInitAll, "ncclCommInitAll");
     RMC_SYM(CommDestroy, "ncclCommDestroy");
     RMC_SYM(GroupStart, "ncclGroupStart");
     RMC_SYM(GroupEnd, "ncclGroupEnd");

@@ -38,7 +38,8 @@ class McOpts(ctypes.Structure):
                 ("workers", ctypes.c_int32), ("fp_table_bytes", ctypes.c_uint64),
                 ("state_store_bytes", ctypes.c_uint64), ("max_depth", ctypes.c_int64), ("seed", ctypes.c_uint64),
                 ("tlc_compat_flags", ctypes.c_uint32), ("check_deadlock", ctypes.c_int32),
-                ("block_size", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7)]
+                ("block_size", ctypes.c_int32), ("same_device", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 6)]
 
 
 class McSummary(ctypes.Structure):
@@ -90,7 +91,9 @@ def load_library(path=LIB_PATH):
     lib.mc_source_hash.restype = ctypes.c_char_p
     want = source_hash()
     got = lib.mc_source_hash().decode()
-    if want is not None and got != want:
+    # RAFTMC_LIB names an experiment build (scripts/build_variant.sh) made beside the product: its
+    # identity is the experiment's, not the tree's
+    if want is not None and got != want and not os.environ.get("RAFTMC_LIB"):
         raise RaftMCError(-5, "libraftmc.so at %s was built from other sources (library %s, tree %s): rebuild it "
                               "(make -C raft-tla_amd)" % (path, got, want))
     P = ctypes.c_void_p
@@ -137,13 +140,18 @@ class ModelChecker:
 
     # sym_tlc: SYMMETRY as TLC applies it (the default, MC_COMPAT_SYM_TLC); False = the orbit mode
     def __init__(self, spec, config=None, workers=1, deadlock=True, device=0, max_depth=0,
-                 fp_table_bytes=0, state_store_bytes=0, seed=0, inv_out_of_model=True, sym_tlc=True):
+                 fp_table_bytes=0, state_store_bytes=0, seed=0, inv_out_of_model=True, sym_tlc=True, n_gpus=1,
+                 same_device=False):
+        """n_gpus > 1: one search over the GPUs device .. device + n_gpus - 1 (owner-partitioned
+        fingerprints, one host thread per GPU inside the library, in-process RCCL); same_device: all
+        those ranks on `device` (the multi-GPU level loop on a one-GPU machine)."""
         self.lib = load_library()
         if config is None:
             config = spec[:-4] + ".cfg" if spec.endswith(".tla") else spec + ".cfg"
         o = McOpts()
         self.lib.mc_default_opts(ctypes.byref(o))
         o.device, o.workers, o.max_depth = device, workers, max_depth
+        o.n_gpus, o.same_device = n_gpus, 1 if same_device else 0
         o.fp_table_bytes, o.state_store_bytes, o.seed = fp_table_bytes, state_store_bytes, seed
         o.check_deadlock = 1 if deadlock else 0
         o.tlc_compat_flags = (MC_COMPAT_INV_OUT_OF_MODEL if inv_out_of_model else 0) | (MC_COMPAT_SYM_TLC if sym_tlc else 0)
@@ -284,6 +292,8 @@ def tlc_main(argv):
             kw["deadlock"] = False
         elif a == "-depth":
             kw["max_depth"] = int(next(it))
+        elif a == "-gpus":
+            kw["n_gpus"] = int(next(it))
         elif a == "-symmetry":                   # raftmc: tlc (TLC's rule, default) | orbit
             v = next(it)
             if v not in ("tlc", "orbit"):

@@ -326,6 +326,7 @@ def fifo_sharded_bfs(shard, ex, rank, device):
         if g[4]:                                                   # the level's first event stops the search
             e = ex.allreduce_sum(shard.event_stats(g))
             g[30], g[31], g[32] = e[30], e[31], e[32]
+            g[8:30], g[40:62] = e[8:30], e[40:62]                  # per-action counters at the stop point
         if shard.level_commit(g):
             break
         send_counts, recv_counts = rebalance_counts(news, rank, world)
@@ -360,15 +361,18 @@ def _local_trace(shards):
     return trace
 
 
-def check_loopback(spec, config, world, device_index=0, **kw):
-    """The library's native sharded level loop (the one mc_shard_run_rccl drives over RCCL) for
-    `world` ranks inside this process, all on one device, exchanging through device-to-device
-    copies (mc_shard_run_loopback).  Returns one raftmc Result per rank, the counterexample (if
-    any) reassembled across ranks as .trace_text on each."""
+def check_loopback(spec, config, world, device_index=0, history_prefixes=None, dump=None, **kw):
+    """The library's native sharded level loop (the one mc_shard_run_rccl drives over RCCL; for
+    tlc_membership the FIFO-ranked loop of csrc/fifo_shard_loop.h) for `world` ranks inside this
+    process, all on one device, exchanging through device-to-device copies
+    (mc_shard_run_loopback).  Returns one raftmc Result per rank, the counterexample (if any)
+    reassembled across ranks as .trace_text on each; dump: a path prefix, each rank's kept states
+    are written to dump.rank<r>."""
     mcs = [_rm.ModelChecker(spec, config, device=device_index, **kw) for _ in range(world)]
     try:
-        if mcs[0].describe()["spec"] != "raft_original":
-            raise ValueError("the native sharded loop covers raft_original")
+        for m in mcs:
+            for con, text in (history_prefixes or {}).items():
+                m.set_history_prefix(con, text)
         lib = mcs[0].lib
         lib.mc_shard_run_loopback.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32]
         hs = (ctypes.c_void_p * world)(*[m.h for m in mcs])
@@ -385,6 +389,9 @@ def check_loopback(spec, config, world, device_index=0, **kw):
                 res.violated = name
             if trace:
                 res.trace_text = trace_text(trace, m.action_location)
+        if dump:
+            for r, m in enumerate(mcs):
+                m.dump_states("%s.rank%d" % (dump, r))
         return out
     finally:
         for m in mcs:
@@ -438,9 +445,9 @@ class ShardedChecker:
     def __init__(self, spec, config, rank, world, device_index=0, group=None, history_prefixes=None,
                  transport="auto", **kw):
         """transport: "rccl" = the library's native level loop over its own RCCL communicator
-        (mc_shard_run_rccl; raft_original only), "torch" = this module's level loop with
-        torch.distributed collectives, "auto" = rccl for raft_original when the process group's
-        backend is nccl (RCCL), else torch."""
+        (mc_shard_run_rccl; both spec families), "torch" = this module's level loop with
+        torch.distributed collectives, "auto" = rccl when the process group's backend is nccl
+        (RCCL), else torch."""
         self.rank, self.world = rank, world
         self.device = torch.device("cuda", device_index)
         self.mc = _rm.ModelChecker(spec, config, device=device_index, **kw)
@@ -450,9 +457,7 @@ class ShardedChecker:
         self.fifo = self.mc.describe()["spec"] == "tlc_membership"
         if transport == "auto":
             backend = dist.get_backend(group) if dist.is_initialized() else "none"
-            transport = "rccl" if (not self.fifo and backend == "nccl") else "torch"
-        if transport == "rccl" and self.fifo:
-            raise ValueError("the native RCCL loop covers raft_original; tlc_membership needs transport='torch'")
+            transport = "rccl" if backend == "nccl" else "torch"
         self.transport = transport
         self._uid = None
 

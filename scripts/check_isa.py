@@ -7,7 +7,10 @@ s_setpc_b64, emitted when a kernel outgrows the 16-bit branch range) and the
 private (scratch) segment size.  Round 1 found that kernels large enough to
 need long branches computed wrong results and faulted on MI355X, so the build
 keeps every kernel within short-branch range and free of scratch; the CPU test
-suite runs this check (tests/test_abi.py).
+suite runs this check (tests/test_abi.py).  Round 3 adds a memory-ordering check:
+no vector store or atomic may issue while a scalar load (other than of the kernel
+arguments) is outstanding — the compiler reordered a counter store ahead of the
+scalar load of the same counter, and the GPU intermittently lost new states.
 """
 import json
 import os
@@ -50,16 +53,28 @@ def kernels(co):
     dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", co], capture_output=True,
                          text=True, check=True).stdout
     out, cur = {}, None
+    smem_pending = False
     for line in dis.splitlines():
         m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
         if m:
             cur = m.group(1)
-            out[cur] = {"instructions": 0, "long_branches": 0}
+            out[cur] = {"instructions": 0, "long_branches": 0, "smem_store_hazards": 0}
+            smem_pending = False
             continue
         if cur and line.startswith("\t"):
             out[cur]["instructions"] += 1
             if "s_setpc_b64" in line:
                 out[cur]["long_branches"] += 1
+            # a scalar load from memory other than the kernel arguments (s[0:1]) still in flight
+            # while a vector store / atomic is issued: the two paths are not ordered, so a store
+            # to the loaded address can overtake the load (round 3: orig_advance lost counts)
+            ops = line.split()
+            if ops and ops[0].startswith("s_load_dword") and len(ops) > 2 and ops[2].rstrip(",") != "s[0:1]":
+                smem_pending = True
+            elif ops and ops[0] == "s_waitcnt" and "lgkmcnt(0)" in line:
+                smem_pending = False
+            elif smem_pending and ops and ops[0].startswith(("global_store", "global_atomic", "flat_store", "flat_atomic")):
+                out[cur]["smem_store_hazards"] += 1
     notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], capture_output=True, text=True, check=True).stdout
     # amdhsa metadata: a list of kernel maps (keys sorted): private segment size, then symbol
     priv = re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)
@@ -82,7 +97,7 @@ def main():
     for co in code_objects(lib):
         ks.update(kernels(co))
     print(json.dumps(ks, indent=1, sort_keys=True))
-    bad = {k: v for k, v in ks.items() if v["long_branches"] or v["scratch_bytes"]}
+    bad = {k: v for k, v in ks.items() if v["long_branches"] or v["scratch_bytes"] or v["smem_store_hazards"]}
     return 1 if bad else 0
 
 

@@ -96,14 +96,16 @@ def test_kernels_short_branch_and_no_scratch():
     """Every gfx950 kernel in libraftmc.so stays within the short-branch range
     (no s_getpc/s_setpc long-branch sequences) and uses no scratch: round 1
     found a membership kernel that outgrew the branch range computing wrong
-    fingerprints and faulting."""
+    fingerprints and faulting; and no vector store / atomic issues while a scalar
+    load of device memory is outstanding (round 3: a counter store overtook the scalar load of the
+    same counter and the GPU intermittently lost a chunk's new states)."""
     import subprocess
     import sys
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_isa.py")], capture_output=True, text=True)
     import json
     ks = json.loads(r.stdout)
     assert len(ks) > 40 and any("memb_fingerprint" in k for k in ks) and any("orig_generate" in k for k in ks)
-    bad = {k: v for k, v in ks.items() if v["long_branches"] or v["scratch_bytes"]}
+    bad = {k: v for k, v in ks.items() if v["long_branches"] or v["scratch_bytes"] or v["smem_store_hazards"]}
     assert not bad, bad
 
 
@@ -261,3 +263,15 @@ def test_sharded_runs_refuse_checkpoints(raftmc, tmp_path):
         hs = (ctypes.c_void_p * 1)(mc.h)
         mc.lib.mc_shard_run_loopback.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32]
         assert mc.lib.mc_shard_run_loopback(hs, 1) == -4
+
+
+def test_n_gpus_options(raftmc):
+    """mc_opts.n_gpus: 1..8 GPUs of the node for one search (no GPU work at mc_open); out of range
+    is MC_E_INVALID; a multi-GPU handle refuses checkpoints (single-GPU runs only) when it runs."""
+    for n in (0, 9):
+        with pytest.raises(raftmc.RaftMCError) as e:
+            raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c1.cfg"), n_gpus=n)
+        assert e.value.code == -1
+    for tla, cfg in ((ORIG_MC, "c1.cfg"), (MEMB_MC, "membership_shipped.cfg")):
+        with raftmc.ModelChecker(tla, os.path.join(CONFIGS, cfg), n_gpus=4) as mc:
+            assert mc.describe()["n_gpus"] == 4

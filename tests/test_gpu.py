@@ -268,7 +268,9 @@ def test_c5v2_compact_election_records(raftmc, tmp_path):
     CAPACITY_OVERFLOW at 222M states)."""
     from oracle_util import run_oracle
     cfg = os.path.join(CONFIGS, "c5v2_noleader.cfg")
-    with raftmc.ModelChecker(ORIG_MC, cfg, fp_table_bytes=16 << 30, state_store_bytes=112 << 30) as mc:
+    # TLC -workers 1 keeps 16-B {fp, ~key} entries: 32 GiB = 2^31 entries, load 0.22 at the 482M states
+    # of depth 12 (a 16 GiB table would run at load 0.94, where linear probing crawls)
+    with raftmc.ModelChecker(ORIG_MC, cfg, fp_table_bytes=32 << 30, state_store_bytes=112 << 30) as mc:
         assert mc.describe()["state_bytes_stored"] == 160
         r = mc.run()
     assert r.verdict == "INVARIANT_VIOLATION" and r.violated == "NoLeader", (r, r.error)

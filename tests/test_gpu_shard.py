@@ -257,3 +257,120 @@ def test_membership_sharded_counterexample(case, world, tmp_path):
         assert " ".join(body) == ref["state"], "trace state %d differs" % (k + 1)
         if k:
             assert head == "State %d: <%s>" % (k + 1, ref["action"])
+
+
+def _memb_prefixes(g):
+    if not g.get("prefix"):
+        return {}
+    con, fixture = g["prefix"]
+    return {con: tla_text(json.load(open(os.path.join(GOLDEN, fixture)))["value"])}
+
+
+@pytest.mark.parametrize("case,world", [("membership_shipped@14", 2), ("memb_dynamic3@14", 3), ("tlc:memb_four@13", 2),
+                                        ("punct_MajorityOfClusterRestarts@30", 3)])
+def test_membership_native_loop_loopback(case, world, tmp_path):
+    """The FIFO-ranked sharded level loop in C++ (csrc/fifo_shard_loop.h, what mc_shard_run_rccl runs
+    for tlc_membership on a node) with W ranks in one process on one GPU: the oracle's single-worker
+    counts, per-action generated and distinct counts, level sizes and set of kept states."""
+    import hashlib
+    shard = importlib.import_module("raft-tla_amd.shard")
+    g = MEMB_FIX[case]
+    dump = str(tmp_path / "dump")
+    out = shard.check_loopback(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), world, history_prefixes=_memb_prefixes(g),
+                               dump=dump, max_depth=g["max_depth"], sym_tlc=g.get("sym") == "tlc", **MSMALL)
+    for r in out:
+        assert r.verdict in ("OK", "DEPTH_LIMIT"), r.error
+        assert (r.generated, r.distinct, r.depth, r.left_on_queue) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
+        assert r.actions == g["actions"]
+        assert [lv[0] for lv in r.levels] == g["levels"]
+    lines = []
+    for k in range(world):
+        lines += [l.rstrip("\n") for l in open("%s.rank%d" % (dump, k))]
+    assert len(lines) == g["distinct"]
+    assert hashlib.sha256("\n".join(sorted(lines)).encode()).hexdigest() == g["states_sha256"]
+
+
+def _trace_blocks_match(trace_text, g):
+    blocks = trace_text.strip().split("\n\n")
+    assert len(blocks) == len(g["trace"]) == g["depth"]
+    for k, (blk, ref) in enumerate(zip(blocks, g["trace"])):
+        head, *body = blk.split("\n")
+        assert " ".join(body) == ref["state"], "trace state %d differs" % (k + 1)
+        if k:
+            assert head.startswith("State %d: <%s" % (k + 1, ref["action"]))
+
+
+@pytest.mark.parametrize("case,world", [("scen_FirstCommit", 3), ("punct_CommitWhenConcurrentLeaders", 2),
+                                        ("eval:memb_eval_single", 2)])
+def test_membership_native_loop_loopback_stop(case, world):
+    """A stop found on some rank (invariant violation / evaluation error): TLC's stop-point counters
+    all-reduced across ranks and the counterexample chased across the ranks' stores, state by state."""
+    shard = importlib.import_module("raft-tla_amd.shard")
+    g = MEMB_FIX[case]
+    kw = dict(MSMALL, deadlock=g.get("deadlock", False))   # TLC's deadlock check as the fixture was searched
+    out = shard.check_loopback(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), world, history_prefixes=_memb_prefixes(g),
+                               sym_tlc=g.get("sym") == "tlc", **kw)
+    for r in out:
+        assert r.verdict == g["verdict"], r.error
+        assert (r.generated, r.distinct, r.depth, r.left_on_queue) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
+        if g["verdict"] == "INVARIANT_VIOLATION":
+            assert r.violated == g["violated"]
+    _trace_blocks_match(out[0].trace_text, g)
+
+
+# ---------------------------------------------------------------- mc_opts.n_gpus (one process, one thread per GPU)
+@pytest.mark.parametrize("name,world", [("c1", 2), ("parity_pair_neg", 3), ("c2", 2)])
+def test_n_gpus_raft_original(raftmc, name, world):
+    """mc_opts.n_gpus > 1 through plain mc_open / mc_run: the library's own multi-GPU search (one host
+    thread per rank inside the library).  On a one-GPU box every rank shares cuda:0 (same_device,
+    loopback device copies); on a node the ranks are GPUs 0..W-1 over an in-process RCCL
+    communicator.  The single-GPU counts, every rank's share summed."""
+    cfg = os.path.join(CONFIGS, name + ".cfg")
+    if name == "c2":
+        g = json.load(open(os.path.join(GOLDEN, "c2_exact.json")))
+        want = (g["generated"], g["distinct"], g["depth"], g["actions_generated"])
+        kw = dict(fp_table_bytes=2 << 30, state_store_bytes=2 << 30)
+    else:
+        g = json.load(open(os.path.join(GOLDEN, "orig_parity.json")))[name]
+        want = (g["generated"], g["distinct"], g["depth"], {k: v[0] for k, v in g["actions"].items()})
+        kw = dict(SMALL)
+    ndev = torch.cuda.device_count()
+    same = ndev < world
+    with raftmc.ModelChecker(ORIG_MC, cfg, n_gpus=world, same_device=same, **kw) as mc:
+        assert mc.describe()["n_gpus"] == world
+        r = mc.run()
+    assert r.verdict == "OK", r.error
+    assert (r.generated, r.distinct, r.depth, {k: v[0] for k, v in r.actions.items()}) == want
+
+
+def test_n_gpus_raft_original_counterexample(raftmc):
+    ev = json.load(open(os.path.join(GOLDEN, "orig_events.json")))["scenario_first_leader"]
+    with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "scenario_first_leader.cfg"), n_gpus=2,
+                             same_device=torch.cuda.device_count() < 2, **SMALL) as mc:
+        r = mc.run()
+    assert r.verdict == "INVARIANT_VIOLATION" and r.violated == "NoLeader" and r.exit_code == 12, r.error
+    assert r.depth == ev["depth"]
+    states = r.trace_text.strip().split("\n\n")
+    assert len(states) == len(ev["trace"]) == 10
+    assert states[0].startswith("State 1: <Initial predicate>")
+    assert "<BecomeLeader" in states[-1].split("\n")[0]
+    assert "Error: Invariant NoLeader is violated." in r.report
+
+
+@pytest.mark.parametrize("case,world", [("memb_four@10", 2), ("tlc:membership_shipped@16", 3), ("scen_FirstCommit", 2)])
+def test_n_gpus_membership(raftmc, case, world):
+    """n_gpus > 1 for tlc_membership (FIFO-ranked: TLC's single-worker kept representatives across
+    ranks): the oracle fixture's counts and, for a stop, its counterexample."""
+    g = MEMB_FIX[case]
+    with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), n_gpus=world,
+                             same_device=torch.cuda.device_count() < world, max_depth=g.get("max_depth", 0),
+                             sym_tlc=g.get("sym") == "tlc", **dict(MSMALL, deadlock=g.get("deadlock", False))) as mc:
+        r = mc.run()
+    assert r.verdict == g["verdict"] if g["verdict"] != "OK" or not g.get("max_depth") else r.verdict in ("OK", "DEPTH_LIMIT"), r.error
+    assert (r.generated, r.distinct, r.depth, r.left_on_queue) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
+    if g["verdict"] == "OK":
+        assert r.actions == g["actions"]
+        assert [lv[0] for lv in r.levels] == g["levels"]
+    else:
+        assert r.violated == g["violated"]
+        _trace_blocks_match(r.trace_text, g)
