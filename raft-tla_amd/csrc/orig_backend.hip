@@ -190,7 +190,11 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
     u64 fp = 0;
     bool have = false;
     int cnt_act = -1;   // this lane's successor action (RMC_GEN_WAVE_COUNTS: counted per wave)
-    if (active) {
+    const int qa = active ? S::quick_out_of_model(s, k, a.rt) : -1;
+    if (qa >= 0) {      // generated, out of the model, no invariant to check: counted only
+      ++nsucc;
+      atomicAdd(&lds_cnt[qa], 1u);
+    } else if (active) {
       W t;
       const int act = S::apply(s, k, t, err);
 #ifdef RMC_EXP_DOUBLE_APPLY
@@ -227,8 +231,9 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
             if (fp2 != fp) fp = 0;
           }
 #endif
-        } else if (a.inv_oom && S::violated(t, a.rt.invariants)) {
+        } else if (a.inv_oom && S::violated(t, a.rt.invariants & S::inv_frame(act))) {
           // TLC checks invariants on out-of-model successors ([ext] switch (ii)); first in key order wins
+          // (only those the action can change: the parent satisfies all of them, S::inv_frame)
           const u64 e = ev_word(gid, (u32)k, EV_VIOLATION);
           ev = e < ev ? e : ev;
         }
@@ -356,7 +361,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
         const u32 idx = atomicAdd(wcnt, 1u);
         a.rfp[wreg + idx] = fp;
         a.rkey[wreg + idx] = (unsigned short)((plane << 8) | (unsigned)k);
-      } else if (a.inv_oom && S::violated(t, a.rt.invariants)) {
+      } else if (a.inv_oom && S::violated(t, a.rt.invariants & S::inv_frame(act))) {
         const u64 e = ev_word(gid, (u32)k, EV_VIOLATION);
         ev = e < ev ? e : ev;
       }
@@ -837,7 +842,7 @@ __global__ void __launch_bounds__(BS) orig_materialize_plain(MatPlainArgs a) {
         o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
       a.meta[dst] = (pgid << 24) | ((u64)act << 16) | (u64)k;
       atomicAdd(&lds_cnt[act], 1u);
-      if (S::violated(t, a.rt.invariants)) { const u64 e = ev_word(pgid, (u32)k, EV_VIOLATION); ev = e < ev ? e : ev; }
+      if (S::violated(t, a.rt.invariants & S::inv_frame(act))) { const u64 e = ev_word(pgid, (u32)k, EV_VIOLATION); ev = e < ev ? e : ev; }
     } else {
       err |= dst >= a.cap ? (u32)OE_CAP_STORE : (u32)OE_TABLE_FULL;
     }
@@ -988,7 +993,7 @@ __global__ void __launch_bounds__(BS) orig_materialize(MatArgs a) {
         const u64 pgid = a.gid0 + par;
         a.meta[dst] = (pgid << 24) | ((u64)act << 16) | (u64)k;
         atomicAdd(&lds_cnt[act], 1u);
-        if (S::violated(t, a.rt.invariants)) {
+        if (S::violated(t, a.rt.invariants & S::inv_frame(act))) {
           const u64 e = ev_word(pgid, (u32)k, EV_VIOLATION);
           ev = e < ev ? e : ev;
         }
@@ -1249,7 +1254,7 @@ __global__ void __launch_bounds__(BS) orig_materialize_sh(MatShArgs a) {
     }
     if (act >= 0) {
       atomicAdd(&lds_cnt[act], 1u);
-      if (S::violated(t, a.rt.invariants)) ev = ev_word(gid, (u32)k, EV_VIOLATION);
+      if (S::violated(t, a.rt.invariants & S::inv_frame(act))) ev = ev_word(gid, (u32)k, EV_VIOLATION);
     } else {
       err |= OE_TABLE_FULL;   // an acknowledged slot always re-derives
     }

@@ -110,6 +110,7 @@ struct Orig {
   // order; rare states (C2: ~1% of the frontier), so the generate kernel skips the range and a
   // second pass runs it on full waves of just those parents (leader_work)
   static constexpr int LEAD_LO = 2 * N + N * N, LEAD_HI = LEAD_LO + N + N * NV + N + N * N;
+  static constexpr int I_RECV = LEAD_HI, I_DUP = I_RECV + MK, I_DROP = I_DUP + MK;   // Receive / Duplicate / Drop
 
   static_assert(N >= 1 && N <= 7, "N");
   static_assert(N * TB <= 32 && N * VB <= 32 && N * CIB <= 32 && N * N <= 32, "scalar field words");
@@ -271,6 +272,16 @@ struct Orig {
     }
   }
 
+  // the count of the message in bag slot k (k uniform: a select chain, no code search) changed by
+  // delta: WithoutMessage (-1, G1: may go negative, the entry stays) / WithMessage of a message
+  // already in the bag (+1) when the caller knows its slot
+  RMC_HD static void bag_add_at(Arr<BE, MK + 1>& bag, int k, int delta, u32& err) {
+    const BE e = sel(bag, k);
+    const int c = ecount(e) + delta;
+    if (c < -8 || c > 7) err |= OE_CAP_COUNT;
+    put(bag, k, (BE)((e & ~(BE)lomask(CNTB)) | (BE)((c + 8) & (int)lomask(CNTB))));
+  }
+
   // ---------------------------------------------------------------- per-server fields
   RMC_HD static int g_term(const Work& s, int i) { return (int)fget<TB>(s.term, i); }
   RMC_HD static int g_st(const Work& s, int i) { return (int)fget<2>(s.st, i); }
@@ -315,6 +326,20 @@ struct Orig {
       any |= st == L || (st == C && popc32(row_bits(s.vgrant, i)) * 2 > N);
     }
     return any;
+  }
+
+  // DuplicateMessage(m) / DropMessage(m) change one message count and nothing else (:442-449): the
+  // successor is out of the model iff BoundedMessages puts that count outside [MinMsgCount,
+  // MaxMsgCount], and no invariant reads the bag (inv_frame).  Returns the action when instance k
+  // (wave-uniform) yields such a successor, so the kernel counts it without building it (C2: most of
+  // the 266M duplicates); -1 otherwise (apply decides).
+  RMC_HD static int quick_out_of_model(const Work& s, int k, const OrigRuntime& rt) {
+    if (k < I_DUP || !(rt.constraints & OC_BoundedMessages)) return -1;
+    const bool dup = k < I_DROP;
+    const BE ent = sel(s.bag, dup ? k - I_DUP : k - I_DROP);
+    if (ent == BEMPTY) return -1;
+    const int c = ecount(ent) + (dup ? 1 : -1);
+    return (c < rt.min_count || c > rt.max_count) ? (dup ? (int)OA_DuplicateMessage : (int)OA_DropMessage) : -1;
   }
 
   // ---------------------------------------------------------------- instance -> successor
@@ -419,20 +444,20 @@ struct Orig {
     if (k < MK) {                                                  // Receive(m) :420-435
       const BE ent = sel(s.bag, k);
       if (ent == BEMPTY) return -1;
-      return receive(s, ecode_of(ent), t, err);
+      return receive(s, k, ecode_of(ent), t, err);
     }
     k -= MK;
     if (k < MK) {                                                  // DuplicateMessage(m) :442-444
       const BE ent = sel(s.bag, k);
       if (ent == BEMPTY) return -1;
-      with_msg(t.bag, ecode_of(ent), err);
+      bag_add_at(t.bag, k, +1, err);                               // WithMessage of a message in slot k
       return OA_DuplicateMessage;
     }
     k -= MK;
     {                                                              // DropMessage(m) :447-449
       const BE ent = sel(s.bag, k);
       if (ent == BEMPTY) return -1;
-      without_msg(t.bag, ecode_of(ent), err);
+      bag_add_at(t.bag, k, -1, err);                               // WithoutMessage (G1)
       return OA_DropMessage;
     }
   }
@@ -475,7 +500,9 @@ struct Orig {
   }
 
   // Receive(m): UpdateTerm excludes every handler (they need mterm <= currentTerm), so <= 1 successor.
-  RMC_HD static int receive(const Work& s, MC m, Work& t, u32& err) {
+  // m is the message in bag slot km: its own count is changed in place (before any reply is
+  // inserted, which can shift the slots), the reply goes through WithMessage's search
+  RMC_HD static int receive(const Work& s, int km, MC m, Work& t, u32& err) {
     const int i = mdst(m), j = msrc(m), mt = mterm(m), ct = g_term(s, i), ty = mtype(m);
     if (mt > ct) {                                                 // UpdateTerm :405-411
       fset<TB>(t.term, i, (u32)mt);
@@ -491,12 +518,12 @@ struct Orig {
       const int vf = g_voted(s, i);
       const bool grant = mt == ct && logOk && (vf == N || vf == j);
       if (grant) fset<VB>(t.voted, i, (u32)j);
-      with_msg(t.bag, m_rvp(ct, grant, lidx(li), i, j), err);      // Reply (:128-129)
-      without_msg(t.bag, m, err);
+      bag_add_at(t.bag, km, -1, err);                              // Reply (:128-129): discard m ...
+      with_msg(t.bag, m_rvp(ct, grant, lidx(li), i, j), err);      // ... and send the response
       return OA_HandleRequestVoteRequest;
     }
     if (ty == RVP) {
-      if (mt < ct) { without_msg(t.bag, m, err); return OA_DropStaleResponse; }   // :414-417
+      if (mt < ct) { bag_add_at(t.bag, km, -1, err); return OA_DropStaleResponse; }   // :414-417
       set_row_bits(t.vresp, i, row_bits(s.vresp, i) | (1u << j));                 // HandleRequestVoteResponse :306-320
       if (rvp_granted(m)) {
         set_row_bits(t.vgrant, i, row_bits(s.vgrant, i) | (1u << j));
@@ -505,7 +532,7 @@ struct Orig {
           row |= (VR)((((u64)rvp_log(m) << 1) | 1ull) << (j * VLB));
         put(t.vl, i, row);
       }
-      without_msg(t.bag, m, err);
+      bag_add_at(t.bag, km, -1, err);
       return OA_HandleRequestVoteResponse;
     }
     if (ty == AEQ) {                                               // HandleAppendEntriesRequest :326-388
@@ -514,8 +541,8 @@ struct Orig {
       const int st = g_st(s, i);
       const bool logOk = pli == 0 || (pli > 0 && pli <= n && plt == eterm(lent(li, pli - 1)));
       if (mt < ct || (st == F && !logOk)) {                        // reject request
+        bag_add_at(t.bag, km, -1, err);
         with_msg(t.bag, m_aep(ct, false, 0, i, j), err);
-        without_msg(t.bag, m, err);
         return OA_HandleAppendEntriesRequest;
       }
       if (st == C) { fset<2>(t.st, i, F); return OA_HandleAppendEntriesRequest; }   // return to follower state
@@ -523,8 +550,8 @@ struct Orig {
         const int index = pli + 1;
         if (ment == 0 || (n >= index && eterm(lent(li, index - 1)) == eterm(ment))) {   // already done
           fset<CIB>(t.commit, i, (u32)mci);
+          bag_add_at(t.bag, km, -1, err);
           with_msg(t.bag, m_aep(ct, true, pli + (ment ? 1 : 0), i, j), err);
-          without_msg(t.bag, m, err);
           return OA_HandleAppendEntriesRequest;
         }
         if (n >= index) { put(t.log, i, ldrop_last(li)); return OA_HandleAppendEntriesRequest; }   // conflict: remove 1 entry
@@ -533,12 +560,12 @@ struct Orig {
       return -1;                                                   // Leader in the same term: nothing enabled
     }
     // AppendEntriesResponse
-    if (mt < ct) { without_msg(t.bag, m, err); return OA_DropStaleResponse; }
+    if (mt < ct) { bag_add_at(t.bag, km, -1, err); return OA_DropStaleResponse; }
     {                                                              // HandleAppendEntriesResponse :392-402
       const int mmi = aep_mmi(m);
       if (aep_success(m)) { s_ni(t, i, j, mmi + 1); s_mi(t, i, j, mmi); }
       else { const int ni = g_ni(s, i, j); s_ni(t, i, j, ni - 1 > 1 ? ni - 1 : 1); }
-      without_msg(t.bag, m, err);
+      bag_add_at(t.bag, km, -1, err);
       return OA_HandleAppendEntriesResponse;
     }
   }
@@ -610,6 +637,23 @@ struct Orig {
       if (t.commit != 0u) bad |= OI_NoCommit;
     }
     return bad;
+  }
+
+  // The invariants an action can change (a frame condition over raft_original.tla's variables):
+  // ElectionSafety reads elections (written only by BecomeLeader :236-241), LogMatching reads log
+  // (ClientRequest :248, HandleAppendEntriesRequest :360-384), NoLeader reads state (Restart,
+  // Timeout, BecomeLeader, UpdateTerm, HandleAppendEntriesRequest), NoCommit reads commitIndex
+  // (Restart, AdvanceCommitIndex, HandleAppendEntriesRequest).  Every expanded parent satisfies every
+  // invariant (a new state that violates one stops the search at its level), so a successor can
+  // only violate the invariants its action may change: the others need no evaluation.
+  RMC_HD static u32 inv_frame(int act) {
+    u32 m = 0;
+    if (act == OA_BecomeLeader) m |= OI_ElectionSafety;
+    if (act == OA_ClientRequest || act == OA_HandleAppendEntriesRequest) m |= OI_LogMatching;
+    if (act == OA_Restart || act == OA_Timeout || act == OA_BecomeLeader || act == OA_UpdateTerm ||
+        act == OA_HandleAppendEntriesRequest) m |= OI_NoLeader;
+    if (act == OA_Restart || act == OA_AdvanceCommitIndex || act == OA_HandleAppendEntriesRequest) m |= OI_NoCommit;
+    return m;
   }
 
   // ---------------------------------------------------------------- pack / unpack (canonical stored form)
