@@ -2531,7 +2531,8 @@ class OrigGpu : public Backend {
   X(2, 1, 3, 2, 5)          \
   X(2, 2, 3, 2, 6)          \
   X(5, 1, 3, 3, 4) /* C5 */ \
-  X(5, 2, 3, 3, 8) /* C5 with 2 values and 8 messages (compact election records) */
+  X(5, 2, 3, 3, 8) /* C5 with 2 values and 8 messages (compact election records) */ \
+  X(5, 2, 2, 4, 6) /* 5 servers, one election term, 6 messages: compact election records within reach */
 #endif
 
 static Backend* orig_factory(const OrigModel& m) {

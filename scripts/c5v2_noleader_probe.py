@@ -11,7 +11,7 @@ sys.path.insert(0, ROOT)
 faulthandler.dump_traceback_later(30, repeat=True)
 os.environ["RAFTMC_PROGRESS"] = "1"
 rm = importlib.import_module("raft-tla_amd")
-cfg = os.path.join(ROOT, "configs", sys.argv[1] if len(sys.argv) > 1 else "c5v2_noleader.cfg")
+cfg = os.path.join(ROOT, "configs", sys.argv[1] if len(sys.argv) > 1 else "c5e_noleader.cfg")
 workers = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 store = int(float(sys.argv[3]) * (1 << 30)) if len(sys.argv) > 3 else 112 << 30
 table = int(float(sys.argv[4]) * (1 << 30)) if len(sys.argv) > 4 else 32 << 30

@@ -3,12 +3,12 @@
 # passes in runs of their own (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE separately; one SQ
 # group), summarised by scripts/rocpd_summary.py.   scripts/prof_session.sh OUTDIR TAG
 set -o pipefail
-O=$GRAFT_REPO_ROOT/${1:-gpurun_out/prof}; TAG=${2:-r02}
+O=$GRAFT_REPO_ROOT/${1:-gpurun_out/prof}; TAG=${2:-r03}
 mkdir -p $O
 R=$GRAFT_REPO_ROOT
-B="$R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --fifo-steps 0"
+B="$R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --fifo-steps 0 --no-extra"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o run -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline --fifo-steps 0 > $O/stats.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o run -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline --fifo-steps 0 --no-extra > $O/stats.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run -- python3 $B > $O/fetch.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run -- python3 $B > $O/write.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAVES -d $O/sq -o run -- python3 $B > $O/sq.log 2>&1

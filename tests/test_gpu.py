@@ -257,32 +257,31 @@ def test_c5v2_deep_properties(raftmc):
     assert sum(v[1] for v in a.actions.values()) + 1 == a.distinct
 
 
-def test_c5v2_compact_election_records(raftmc, tmp_path):
-    """5 servers with two values store election records in the compact form (orig_spec.h
-    ECOMPACT: the voterLog row's presence bits come from evotes, eterm in bits_for(MaxTerm)).
-    NoLeader's counterexample is TLC's single-worker FIFO first election, at depth 12 behind
-    ~4.8e8 states: its last state carries such a record, printed through the compact decoding,
-    and the oracle's check-trace replays the trace state by state through the literal
-    restatement of raft_original.tla.  The store holds the whole search (482M states of 160 B +
-    8 B parent pointers: 81 GB; round 2's run used the 32 GiB default store and stopped with a
-    CAPACITY_OVERFLOW at 222M states)."""
+def test_c5_compact_election_records(raftmc, tmp_path):
+    """A reachable 5-server election on the GPU: election records of 5 servers with a 341-log universe
+    do not fit 64 bits, so the shape stores them compactly (orig_spec.h ECOMPACT: the voterLog row's
+    presence bits come from evotes, eterm in bits_for(MaxTerm)).  configs/c5e_noleader.cfg (one
+    election term, 6 messages) reaches TLC's single-worker FIFO first election at depth 14 behind
+    301.6M states (c5v2.cfg would need ~1e10); NoLeader's counterexample ends in that BecomeLeader,
+    its election record printed through the compact decoding, and the oracle's check-trace replays
+    the trace state by state through the literal restatement of raft_original.tla.  (Round 2's
+    c5v2 variant of this test could not reach an election: its first one lies at depth 14, not 12.)"""
     from oracle_util import run_oracle
-    cfg = os.path.join(CONFIGS, "c5v2_noleader.cfg")
-    # TLC -workers 1 keeps 16-B {fp, ~key} entries: 32 GiB = 2^31 entries, load 0.22 at the 482M states
-    # of depth 12 (a 16 GiB table would run at load 0.94, where linear probing crawls)
+    cfg = os.path.join(CONFIGS, "c5e_noleader.cfg")
     with raftmc.ModelChecker(ORIG_MC, cfg, fp_table_bytes=32 << 30, state_store_bytes=112 << 30) as mc:
-        assert mc.describe()["state_bytes_stored"] == 160
+        d = mc.describe()
+        assert (d["N"], d["MaxTerm"], d["MaxLogLen"], d["log_universe"]) == (5, 2, 4, 341)
         r = mc.run()
     assert r.verdict == "INVARIANT_VIOLATION" and r.violated == "NoLeader", (r, r.error)
-    assert r.depth == 12 and r.exit_code == 12
+    assert r.depth == 14 and r.exit_code == 12
     states = [st for _, st in trace_states(r)]
-    assert len(states) == 12
-    assert "evoterLog" in states[-1] and "evotes" in states[-1]
+    assert len(states) == 14
+    assert "<BecomeLeader" in r.trace_text.strip().split("\n\n")[-1].split("\n")[0]
+    assert "evoterLog |-> (" in states[-1] and "evotes |-> {" in states[-1]
     p = tmp_path / "trace.txt"
     p.write_text("\n".join(states) + "\n")
     o = run_oracle("check-trace", ORIG_MC, cfg, "--golden", str(p))
     assert o["valid"] and o["length"] == len(states) and o["violated"] == "NoLeader", o
-
 
 def test_checkpoint_recover_c1(raftmc, tmp_path):
     """TLC -checkpoint / -recover: a search stopped at depth 6 with a checkpoint per level,
