@@ -235,11 +235,14 @@ int mc_shard_violation(const mc_ctx* ctx, uint64_t* parent_gid, char** action, c
  *   rebalance: STATES records of the level's new states (key order, one run per rank) to equal
  *   contiguous slices of the next level, then mc_shard_store.
  * The driver is raft-tla_amd/shard.py (fifo_sharded_bfs). */
-/* Native sharded BFS over RCCL (raft_original).  The same protocol as the caller-driven
- * mc_shard_* loop above, run entirely inside the library on one HIP stream with grouped
- * ncclSend/ncclRecv between the kernels' own buffers: two host synchronisations per chunk (the
- * record counts) and one per level (all-reduce of the level statistics).  Replaces, like the
- * whole sharded path, TLC's multi-worker BFS (one JVM, shared FPSet).
+/* Native sharded BFS over RCCL (both spec families).  The same protocols as the caller-driven
+ * mc_shard_* loops above, run entirely inside the library with grouped ncclSend/ncclRecv between
+ * the kernels' own buffers — raft_original: three exchanges per level chunk on one HIP stream,
+ * two host synchronisations per chunk (the record counts) and one per level (all-reduce of the
+ * level statistics); tlc_membership: the FIFO-ranked protocol (layout all-gather, ROUTE per
+ * chunk, select + REPLY, statistics, rebalance; csrc/fifo_shard_loop.h).  Replaces, like the
+ * whole sharded path, TLC's multi-worker BFS (one JVM, shared FPSet).  The
+ * same loops run behind mc_run when mc_opts.n_gpus > 1 (one host thread per GPU).
  *   mc_rccl_unique_id   rank 0 creates the communicator id (ncclGetUniqueId, 128 B) which
  *                       the caller broadcasts (torch.distributed in raft-tla_amd/shard.py)
  *   mc_shard_run_rccl   every rank: shard_open + ncclCommInitRank (cached on the handle for
@@ -251,8 +254,7 @@ int mc_shard_violation(const mc_ctx* ctx, uint64_t* parent_gid, char** action, c
  *                       between the ranks' buffers: the multi-rank path (routing, self
  *                       segments, all-reduce, counterexample gather) testable on one GPU.
  *                       ctxs[r] is rank r; results per handle as after mc_shard_run_rccl.
- * RCCL is dlopen()ed (librccl.so.1) on first use; MC_E_UNSUPPORTED if it cannot be loaded or
- * the spec has no native loop (tlc_membership uses the FIFO protocol above). */
+ * RCCL is dlopen()ed (librccl.so.1) on first use; MC_E_UNSUPPORTED if it cannot be loaded. */
 int mc_rccl_unique_id(mc_ctx* ctx, void* out, size_t len);
 int mc_shard_run_rccl(mc_ctx* ctx, int32_t rank, int32_t world, const void* unique_id, size_t len);
 int mc_shard_run_loopback(mc_ctx* const* ctxs, int32_t world);

@@ -1476,54 +1476,103 @@ struct Memb {
       t.hr0 = w0; t.hr1 = w1 | (distinct ? HR_DISCRETE : 0ull);
     }
   }
+  RMC_HD static bool single(u32 cand) { return (cand & (cand - 1u)) == 0u; }
   // keep, among the candidate permutations, those whose key (p, pi) is least
+  // (one pass: each candidate's key is evaluated once)
   template <class F>
   RMC_HD static u32 keep_min(u32 cand, F key) {
     u64 best = ~0ull;
-#pragma unroll 1
-    for (int p = 0; p < NPERM; ++p)
-      if ((cand >> p) & 1u) { const u64 k = key(p, perm_of(p)); best = k < best ? k : best; }
     u32 out = 0;
 #pragma unroll 1
     for (int p = 0; p < NPERM; ++p)
-      if (((cand >> p) & 1u) && key(p, perm_of(p)) == best) out |= 1u << p;
+      if ((cand >> p) & 1u) {
+        const u64 k = key(p, perm_of(p));
+        out = k < best ? (1u << p) : k == best ? (out | 1u << p) : out;
+        best = k < best ? k : best;
+      }
     return out;
   }
-  RMC_HD static bool single(u32 cand) { return (cand & (cand - 1u)) == 0u; }
-  RMC_HD static u64 next_perm_code(const Work& t, int len, u32 pi, bool ce, u32 cfgt, bool have_last, u64 last) {
+  // 64-bit hash of the permuted state pi(t) as far as TLC's order sees it: its VIEW (view_hash1), the
+  // rank of its permuted history["global"] and its per-server [restarted, timeout] records
+  template <bool CE>
+  RMC_HD static u64 perm_state_hash(const Work& t, int p, u32 pi, u32 cfgt) {
+    u64 h = view_hash1<CE>(t, pi, 0x243F6A8885A308D3ull, cfgt) ^ fmix((u64)hrank(t, p) ^ 0x13198A2E03707344ull);
+#pragma unroll
+    for (int x = 0; x < N; ++x) {
+      const int i = pinv(pi, x);
+      h += fmix(((u64)restarted(t, i) << 8 | (u64)timeouts(t, i)) ^ ((u64)(x + 1) * P1));
+    }
+    return h;
+  }
+  // Candidates whose permuted states coincide (pi' = pi o sigma, sigma an automorphism of t) tie on
+  // every criterion, so a lane holding a symmetric state walked all of them (its wave with it).  Keep
+  // one candidate per permuted state: equal hashes <=> equal permuted states up to a 2^-64
+  // coincidence, the fingerprint's own collision class.  O(|cand|^2) hashes (small sets only), one
+  // call site (the kernels stay within short-branch range); the config-entry hash variant is exact
+  // for states without config entries too.
+  RMC_HD static u32 dedup_auto(const Work& t, u32 cand, u32 cfgt) {
+    u32 out = 0, todo = cand, cmp = 0;
+    int p = 0;
+    u64 hp = 0;
+    bool placing = false;   // hp holds candidate p's hash; cmp: kept candidates not yet compared with p
+#pragma unroll 1
+    while (placing || todo) {
+      if (!placing) { p = __builtin_ctz(todo); todo &= todo - 1u; cmp = out; }
+      const int idx = placing ? __builtin_ctz(cmp) : p;
+      const u64 h = perm_state_hash<true>(t, idx, perm_of(idx), cfgt);
+      if (!placing) { hp = h; placing = true; }
+      else {
+        cmp &= cmp - 1u;
+        if (h == hp) { placing = false; continue; }        // p repeats a kept candidate's state
+      }
+      if (!cmp) { out |= 1u << p; placing = false; }
+    }
+    return out;
+  }
+  // The bag as an array indexed at run time (tlc_min_perm reads entries by runtime index inside its
+  // permutation loops; from the register array every read is a select chain over MK+1 entries): on
+  // the device a per-lane slice of LDS (lane-interleaved, conflict-free), on the host a local array.
+  struct BagRef {
+    const u64* p;
+    int stride;
+    RMC_HD u64 operator[](int q) const { return p[q * stride]; }
+  };
+  RMC_HD static u64 next_perm_code(const BagRef& bag, int len, u32 pi, bool ce, u32 cfgt, bool have_last, u64 last) {
     u64 best = ~0ull;   // the least permuted message code above `last`
 #pragma unroll 1
     for (int q = 0; q < len; ++q) {
-      const u64 c = perm_code(mcode(sel(t.bag, q)), pi, ce, cfgt);
+      const u64 c = perm_code(mcode(bag[q]), pi, ce, cfgt);
       if ((!have_last || c > last) && c < best) best = c;
     }
     return best;
   }
   // the permutation TLC picks: least permuted variable tuple, variable by variable
-  RMC_HD static u32 tlc_min_perm(const Work& t, bool ce, u32 cfgt) {
+  RMC_HD static u32 tlc_min_perm(const Work& t, const BagRef& bag, int len, bool ce, u32 cfgt) {
     u32 cand = (u32)lomask(NPERM);
     // messages: a function from message records to counts (oracle Fcn order: DOMAIN size — equal
     // for all — then the domain elements ascending, then the counts in domain order)
-    int len = 0;
-#pragma unroll 1
-    for (int q = 0; q < MK; ++q) len += sel(t.bag, q) != EMPTY;
     u64 last = 0;
     bool have_last = false;
 #pragma unroll 1
-    for (int j = 0; j < len && !single(cand); ++j) {
-      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(t, len, pi, ce, cfgt, have_last, last); });
-      last = next_perm_code(t, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+    for (int j = 0; j == 0 || (j < len && !single(cand)); ++j) {   // (one pass even for an empty bag)
+      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); });
+      last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
       have_last = true;
+#ifdef RMC_TLC_DEDUP
+      if (j == 0 && !single(cand) && popc32(cand) <= 8) cand = dedup_auto(t, cand, cfgt);
+#endif
     }
     have_last = false;
 #pragma unroll 1
     for (int j = 0; j < len && !single(cand); ++j) {   // same permuted domain: the counts in domain order
-      const u64 code = next_perm_code(t, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+      const u64 code = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
       cand = keep_min(cand, [&](int, u32 pi) {
         u64 cnt = 0;
 #pragma unroll 1
-        for (int q = 0; q < len; ++q)
-          if (perm_code(mcode(sel(t.bag, q)), pi, ce, cfgt) == code) cnt = (u64)mcount(sel(t.bag, q));
+        for (int q = 0; q < len; ++q) {
+          const u64 e = bag[q];
+          if (perm_code(mcode(e), pi, ce, cfgt) == code) cnt = (u64)mcount(e);
+        }
         return cnt;
       });
       last = code; have_last = true;
@@ -1574,7 +1623,19 @@ struct Memb {
   }
   RMC_HD static u64 fingerprint_tlc(const Work& t, u64 seed, const MembRuntime& rt) {
     const bool ce = has_config_entries(t, rt.cfg_type);
-    const u32 pi = tlc_min_perm(t, ce, rt.cfg_type);
+#if defined(__HIP_DEVICE_COMPILE__)
+    __shared__ u64 sbag[MK * 256];   // every kernel runs 256-lane workgroups; one slice per lane
+    u64* const base = sbag + (threadIdx.x & 255u);
+    constexpr int stride = 256;
+#else
+    u64 hbag[MK];
+    u64* const base = hbag;
+    constexpr int stride = 1;
+#endif
+    int len = 0;
+#pragma unroll
+    for (int q = 0; q < MK; ++q) { base[q * stride] = t.bag.v[q]; len += t.bag.v[q] != EMPTY; }
+    const u32 pi = tlc_min_perm(t, BagRef{base, stride}, len, ce, rt.cfg_type);
     const u64 best = ce ? view_hash1<true>(t, pi, seed, rt.cfg_type) : view_hash1<false>(t, pi, seed, rt.cfg_type);
     const u64 fp = fmix(best ^ seed);
     return fp ? fp : 1ull;
