@@ -10,7 +10,8 @@ TLC-pinned.
 
     python tests/golden/make_c5_prefix.py [max_depth] [cfg]
 
-`cfg` c5v2.cfg (two values, compact election records) writes tests/golden/c5v2_prefix.json.
+`cfg` c5v2.cfg (two values, compact election records) writes tests/golden/c5v2_prefix.json;
+c2_md6.cfg (C2 with 6 messages: AppendEntries responses and commits fire) tests/golden/c2_md6_prefix.json.
 """
 import hashlib
 import json
@@ -24,8 +25,9 @@ from oracle_util import CONFIGS, GOLDEN, ORIG_MC, run_oracle  # noqa: E402
 def main(depth, cfg="c5.cfg"):
     fd, dump = tempfile.mkstemp(suffix=".txt")
     os.close(fd)
+    workers = os.environ.get("ORACLE_WORKERS", "1")
     r = run_oracle("bfs", ORIG_MC, os.path.join(CONFIGS, cfg), "--max-depth", str(depth), "--dump", dump,
-                   timeout=100000)
+                   "--workers", workers, timeout=100000)
     lines = sorted(l.rstrip("\n") for l in open(dump))
     os.unlink(dump)
     assert len(lines) == r["distinct"], (len(lines), r["distinct"])

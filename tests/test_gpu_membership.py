@@ -261,3 +261,25 @@ def test_membership_spill_counterexample(raftmc, case):
     assert (r.depth, r.generated, r.distinct, r.left_on_queue) == (g["depth"], g["generated"], g["distinct"], g["left_on_queue"])
     blocks = r.trace_text.strip().split("\n\n")
     assert [" ".join(b.split("\n")[1:]) for b in blocks] == [t["state"] for t in g["trace"]]
+
+
+DEEP_PATH = os.path.join(GOLDEN, "memb_deep.json")
+DEEP = json.load(open(DEEP_PATH)) if os.path.exists(DEEP_PATH) else {}
+
+
+@pytest.mark.parametrize("case", sorted(DEEP) or ["(memb_deep.json not generated)"])
+def test_c3_deep_oracle_pin(raftmc, case):
+    """C3's model (memb_four: 4 servers, NextDynamic, SYMMETRY) pinned deep by the oracle's lean mode
+    (tests/golden/make_memb_deep.py: millions of states, in both SYMMETRY modes): TLC's counts,
+    per-level sizes and per-action generated AND distinct counts (the latter depend on TLC's
+    single-worker first-found order under VIEW) at the fixture's depth."""
+    if case not in DEEP:
+        pytest.skip("tests/golden/memb_deep.json not generated")
+    g = DEEP[case]
+    with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, g["cfg"] + ".cfg"), sym_tlc=g["sym"] == "tlc",
+                             max_depth=g["max_depth"], deadlock=False) as mc:
+        r = mc.run()
+    assert r.verdict == ("DEPTH_LIMIT" if g["verdict"] == "OK" else g["verdict"]), r.error
+    assert (r.generated, r.distinct, r.depth, r.left_on_queue) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
+    assert [lv[0] for lv in r.levels] == g["levels"]
+    assert r.actions == g["actions"]
