@@ -206,7 +206,7 @@ def test_c2_full_size_properties(raftmc):
     assert {k: list(v) for k, v in a.actions.items()} == {k: list(v) for k, v in o["actions"].items()}
 
 
-@pytest.mark.parametrize("fixture", ["c5_prefix", "c5v2_prefix"])
+@pytest.mark.parametrize("fixture", ["c5_prefix", "c5v2_prefix", "c2_md6_prefix"])
 def test_c5_prefix_parity(raftmc, fixture):
     """BASELINE configs[4] (C5: 5 servers, term <= 3, log <= 3; 87 action instances per
     state, 96-B packed states; c5v2: two values and 8 messages, 104 instances, 160-B states,

@@ -66,7 +66,8 @@ def test_packed_fifo_stop_point_matches_oracle(name):
     assert [(t["action"], t["state"]) for t in r["trace"]] == [(t["action"], t["state"]) for t in g["trace"]]
 
 
-@pytest.mark.parametrize("fixture,shape", [("c5_prefix", (5, 1, 3, 3, 4)), ("c5v2_prefix", (5, 2, 3, 3, 8))])
+@pytest.mark.parametrize("fixture,shape", [("c5_prefix", (5, 1, 3, 3, 4)), ("c5v2_prefix", (5, 2, 3, 3, 8)),
+                                           ("c2_md6_prefix", (3, 2, 3, 2, 6))])
 def test_packed_c5_prefix_matches_oracle(fixture, shape):
     """The 5-server shapes (one and two values; the two-value one stores election records in
     the compact form, orig_spec.h ECOMPACT) against the oracle's depth-limited fixtures:
