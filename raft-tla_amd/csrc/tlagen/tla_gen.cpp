@@ -1,0 +1,668 @@
+// tla_gen.cpp — TLA+ (SANY subset) to C++ over tlv.h; see tla_gen.h for the semantics.
+#include "tla_gen.h"
+
+#include <cctype>
+#include <functional>
+#include <map>
+#include <set>
+#include <sstream>
+
+#include "../../../include/raftmc.h"
+
+namespace rmc {
+namespace tlagen {
+
+namespace {
+
+struct Sym {
+  enum Kind { Val, LetOp } kind = Val;
+  std::string cxx;                 // Val: handle expression; LetOp: lambda name
+  std::shared_ptr<Def> def;        // LetOp
+  std::shared_ptr<std::vector<std::pair<std::string, Sym>>> scope;   // LetOp: scope at its definition
+};
+typedef std::vector<std::pair<std::string, Sym>> Scope;
+
+const Sym* find(const Scope& sc, const std::string& n) {
+  for (auto it = sc.rbegin(); it != sc.rend(); ++it) if (it->first == n) return &it->second;
+  return nullptr;
+}
+
+std::string cstr(const std::string& s) {
+  std::string o = "\"";
+  for (char ch : s) { if (ch == '"' || ch == '\\') o += '\\'; if (ch == '\n') { o += "\\n"; continue; } o += ch; }
+  return o + "\"";
+}
+
+struct Gen {
+  const Program& P;
+  const CfgFile& cfg;
+  std::map<std::string, int> var_idx, const_idx;
+  std::map<std::string, int> atom_ids;
+  std::vector<std::string> atoms;
+  std::vector<std::string> actions;
+  std::map<std::string, int> action_ids;
+  std::map<std::string, std::string> op_fn;       // global op -> C++ function name
+  std::vector<std::string> fn_protos, fn_bodies;
+  std::map<std::string, int> level_memo;          // 0 pure, 1 action
+  int uid = 0;
+  bool init_mode = false;
+
+  Gen(const Program& p, const CfgFile& c) : P(p), cfg(c) {
+    for (size_t i = 0; i < P.variables.size(); ++i) var_idx[P.variables[i]] = (int)i;
+    for (size_t i = 0; i < P.constants.size(); ++i) const_idx[P.constants[i]] = (int)i;
+  }
+
+  std::string fresh(const char* p) { return std::string(p) + std::to_string(uid++); }
+  [[noreturn]] void unsup(const Node& n, const std::string& what) {
+    throw CfgError(MC_E_UNSUPPORTED, node_where(n) + ": " + what + " is outside the front end's subset");
+  }
+  int atom(const std::string& key, const std::string& text) {
+    auto it = atom_ids.find(key);
+    if (it != atom_ids.end()) return it->second;
+    const int id = (int)atoms.size();
+    atoms.push_back(text);
+    atom_ids[key] = id;
+    return id;
+  }
+  int str_atom(const std::string& s) { return atom("s:" + s, "\"" + s + "\""); }
+  int mv_atom(const std::string& s) { return atom("m:" + s, s); }
+  int action_id(const std::string& n) {
+    auto it = action_ids.find(n);
+    if (it != action_ids.end()) return it->second;
+    action_ids[n] = (int)actions.size();
+    actions.push_back(n);
+    return (int)actions.size() - 1;
+  }
+  std::shared_ptr<Def> global(const std::string& n) {
+    auto it = P.defs.find(n);
+    return it == P.defs.end() ? nullptr : it->second;
+  }
+  const Def& body_of(const std::shared_ptr<Def>& d, const Node& at) {
+    if (!d->body) throw CfgError(MC_E_UNSUPPORTED, node_where(at) + ": definition " + d->name + " does not parse: " + d->error);
+    return *d;
+  }
+
+  // ---- level: does a definition (transitively) contain primes / UNCHANGED?
+  bool has_action(const NP& e, std::set<std::string>& visiting) {
+    if (!e) return false;
+    if (e->k == K::Prime || e->k == K::Unchanged) return true;
+    if (e->k == K::Ident || e->k == K::OpApp) {
+      auto d = global(e->s);
+      if (d && d->body && is_action(d, visiting)) return true;
+    }
+    for (auto& c : e->a) if (has_action(c, visiting)) return true;
+    for (auto& b : e->binds) if (has_action(b.set, visiting)) return true;
+    for (auto& u : e->ups) { if (has_action(u.rhs, visiting)) return true; for (auto& s : u.path) if (has_action(s.idx, visiting)) return true; }
+    for (auto& d : e->defs) if (has_action(d->body, visiting)) return true;
+    return false;
+  }
+  bool is_action(const std::shared_ptr<Def>& d, std::set<std::string>& visiting) {
+    auto it = level_memo.find(d->name);
+    if (it != level_memo.end()) return it->second != 0;
+    if (visiting.count(d->name)) return false;
+    visiting.insert(d->name);
+    const bool r = has_action(d->body, visiting);
+    visiting.erase(d->name);
+    level_memo[d->name] = r;
+    return r;
+  }
+  bool is_action(const std::shared_ptr<Def>& d) { std::set<std::string> v; return d->body && is_action(d, v); }
+
+  // ---- a global operator as a C++ function (emitted once)
+  std::string op_function(const std::shared_ptr<Def>& d, const Node& at) {
+    auto it = op_fn.find(d->name);
+    if (it != op_fn.end()) return it->second;
+    body_of(d, at);
+    std::string fn = "op_" + std::to_string(op_fn.size()) + "_";
+    for (char ch : d->name) fn += std::isalnum((unsigned char)ch) ? ch : '_';
+    op_fn[d->name] = fn;
+    std::string sig = "TLV_HD u32 " + fn + "(Cx& c";
+    Scope sc;
+    for (size_t i = 0; i < d->params.size(); ++i) {
+      sig += ", u32 p" + std::to_string(i);
+      Sym s; s.cxx = "p" + std::to_string(i);
+      sc.push_back({d->params[i], s});
+    }
+    sig += ")";
+    const bool save = init_mode;
+    init_mode = false;
+    const std::string body = ex(d->body, sc);
+    init_mode = save;
+    fn_protos.push_back(sig + ";");
+    fn_bodies.push_back(sig + " {\n  Ar& A = *c.A; (void)A;\n  return " + body + ";\n}\n");
+    return fn;
+  }
+
+  std::string let_defs(const NP& e, Scope& sc) {   // C++ lambdas of a LET's definitions
+    std::string out;
+    for (auto& d : e->defs) {
+      if (!d->body) unsup(*e, "LET definition " + d->name + " (" + d->error + ")");
+      Sym s; s.kind = Sym::LetOp; s.def = d; s.cxx = fresh("L");
+      s.scope = std::make_shared<Scope>(sc);   // recursion is outside the subset
+      Scope inner = sc;
+      std::string params;
+      for (size_t i = 0; i < d->params.size(); ++i) {
+        const std::string pn = fresh("q");
+        params += (i ? ", u32 " : "u32 ") + pn;
+        Sym ps; ps.cxx = pn;
+        inner.push_back({d->params[i], ps});
+      }
+      out += "auto " + s.cxx + " = [&](" + params + ") -> u32 { return " + ex(d->body, inner) + "; };\n";
+      sc.push_back({d->name, s});
+    }
+    return out;
+  }
+
+  std::string set_loop(const std::string& set, const std::string& elem, const std::string& body, bool restore_top) {
+    const std::string S = fresh("S"), i = fresh("i"), n = fresh("n"), st = fresh("t");
+    return "{ const u32 " + S + " = " + set + ";\n if (tg(A, " + S + ") != T_SET) A.err |= E_TYPE; else { u32 " + elem +
+           " = first(" + S + ");\n for (u32 " + i + " = 0, " + n + " = count(A, " + S + "); " + i + " < " + n + "; ++" + i +
+           ", " + elem + " = nextv(A, " + elem + ")) {\n" + (restore_top ? " const u32 " + st + " = A.top;\n" : "") + body +
+           (restore_top ? " A.top = " + st + ";\n" : "") + " } } }\n";
+  }
+
+  // nested loops over binds; `inner` is generated with the bound names in scope
+  std::string bind_loops(const std::vector<Bind>& bs, size_t bi, size_t ni, Scope& sc, bool restore,
+                         const std::function<std::string(Scope&)>& inner) {
+    if (bi == bs.size()) return inner(sc);
+    const Bind& b = bs[bi];
+    // the set of a multi-name bind is evaluated once
+    if (ni == 0 && b.names.size() > 1) {
+      const std::string sv = fresh("B");
+      Scope s2 = sc;
+      Sym ss; ss.cxx = sv;
+      s2.push_back({"\x01set" + std::to_string(bi), ss});
+      return "{ const u32 " + sv + " = " + ex(b.set, sc) + ";\n" + bind_loops_named(bs, bi, 0, s2, restore, inner, sv) + "}\n";
+    }
+    return bind_loops_named(bs, bi, ni, sc, restore, inner, ex(b.set, sc));
+  }
+  std::string bind_loops_named(const std::vector<Bind>& bs, size_t bi, size_t ni, Scope& sc, bool restore,
+                               const std::function<std::string(Scope&)>& inner, const std::string& setx) {
+    const Bind& b = bs[bi];
+    const std::string el = fresh("e");
+    Scope s2 = sc;
+    Sym s; s.cxx = el;
+    s2.push_back({b.names[ni], s});
+    std::string body;
+    if (ni + 1 < b.names.size()) body = bind_loops_named(bs, bi, ni + 1, s2, restore, inner, setx);
+    else body = bind_loops(bs, bi + 1, 0, s2, restore, inner);
+    return set_loop(setx, el, body, restore);
+  }
+
+  // ---- expressions: a C++ expression yielding a value handle
+  std::string ex(const NP& e, Scope& sc) {
+    const Node& n = *e;
+    switch (n.k) {
+      case K::Num: return "mk_int(A, " + std::to_string(n.n) + "LL)";
+      case K::Str: return "mk_atom(A, " + std::to_string(str_atom(n.s)) + "u)";
+      case K::Bool: return n.n ? "2u" : "0u";
+      case K::At: {
+        const Sym* s = find(sc, "@");
+        if (!s) unsup(n, "@ outside EXCEPT");
+        return s->cxx;
+      }
+      case K::Ident: return ident(n, sc, {});
+      case K::OpApp: {
+        std::vector<std::string> args;
+        for (auto& a : n.a) args.push_back(ex(a, sc));
+        return ident(n, sc, args);
+      }
+      case K::Prime: {
+        if (n.a[0]->k != K::Ident || !var_idx.count(n.a[0]->s)) unsup(n, "priming a non-variable expression");
+        const std::string X = std::to_string(var_idx[n.a[0]->s]);
+        return "(((c.asg >> " + X + ") & 1ull) ? c.nxt[" + X + "] : (A.err |= E_ASSIGN, 0u))";
+      }
+      case K::Unary: {
+        const std::string x = ex(n.a[0], sc);
+        if (n.s == "~") return "mk_bool(!truth(A, " + x + "))";
+        if (n.s == "-") return "mk_int(A, -ival(A, " + x + "))";
+        if (n.s == "DOMAIN") return "dom(A, " + x + ")";
+        if (n.s == "SUBSET") return "powerset(A, " + x + ")";
+        if (n.s == "UNION") return "union_all(A, " + x + ")";
+        unsup(n, "operator " + n.s);
+      }
+      case K::Binary: return binary(n, sc);
+      case K::And: case K::Or: {
+        std::string o = "mk_bool(";
+        for (size_t i = 0; i < n.a.size(); ++i) o += (i ? (n.k == K::And ? " && " : " || ") : "") + std::string("truth(A, ") + ex(n.a[i], sc) + ")";
+        return o + ")";
+      }
+      case K::If:
+        return "(truth(A, " + ex(n.a[0], sc) + ") ? " + ex(n.a[1], sc) + " : " + ex(n.a[2], sc) + ")";
+      case K::Case: {
+        std::string o, close;
+        for (size_t i = 0; i < n.a.size(); i += 2) {
+          if (!n.a[i]) { o += ex(n.a[i + 1], sc); close += ""; goto done; }
+          o += "(truth(A, " + ex(n.a[i], sc) + ") ? " + ex(n.a[i + 1], sc) + " : ";
+          close += ")";
+        }
+        o += "(A.err |= E_DOMAIN, 0u)";
+      done:
+        return o + close;
+      }
+      case K::Let: {
+        Scope s2 = sc;
+        const std::string defs = let_defs(e, s2);
+        return "[&]() -> u32 {\n" + defs + "return " + ex(n.a[0], s2) + ";\n}()";
+      }
+      case K::Forall: case K::Exists: {
+        const bool all = n.k == K::Forall;
+        Scope s2 = sc;
+        const std::string loops = bind_loops(n.binds, 0, 0, s2, true, [&](Scope& s3) {
+          return std::string(" if (") + (all ? "!" : "") + "truth(A, " + ex(n.a[0], s3) + ")) return " + (all ? "0u" : "2u") + ";\n";
+        });
+        return "[&]() -> u32 {\n" + loops + " return " + (all ? "2u" : "0u") + ";\n}()";
+      }
+      case K::Choose: {
+        Scope s2 = sc;
+        const std::string loops = bind_loops(n.binds, 0, 0, s2, true, [&](Scope& s3) {
+          return " if (truth(A, " + ex(n.a[0], s3) + ")) return " + find(s3, n.binds[0].names[0])->cxx + ";\n";
+        });
+        return "[&]() -> u32 {\n" + loops + " A.err |= E_CHOOSE; return 0u;\n}()";
+      }
+      case K::SetEnum: {
+        if (n.a.empty()) return "set_end(A, A.htop)";
+        const std::string m = fresh("m");
+        std::string o = "[&]() -> u32 { const u32 " + m + " = A.htop;\n";
+        for (auto& a : n.a) o += " hpush(A, " + ex(a, sc) + ");\n";
+        return o + " return set_end(A, " + m + ");\n}()";
+      }
+      case K::Tuple: {
+        const std::string m = fresh("m");
+        std::string o = "[&]() -> u32 { const u32 " + m + " = A.htop;\n";
+        for (auto& a : n.a) o += " hpush(A, " + ex(a, sc) + ");\n";
+        return o + " return seq_end(A, " + m + ");\n}()";
+      }
+      case K::SetFilter: case K::SetMap: {
+        const std::string m = fresh("m");
+        Scope s2 = sc;
+        const bool filt = n.k == K::SetFilter;
+        const std::string loops = bind_loops(n.binds, 0, 0, s2, false, [&](Scope& s3) {
+          if (filt) return " if (truth(A, " + ex(n.a[0], s3) + ")) hpush(A, " + find(s3, n.binds[0].names[0])->cxx + ");\n";
+          return " hpush(A, " + ex(n.a[0], s3) + ");\n";
+        });
+        return "[&]() -> u32 { const u32 " + m + " = A.htop;\n" + loops + " return set_end(A, " + m + ");\n}()";
+      }
+      case K::FunCons: {
+        const std::string m = fresh("m");
+        Scope s2 = sc;
+        const std::string loops = bind_loops(n.binds, 0, 0, s2, false, [&](Scope& s3) {
+          std::vector<std::string> names;
+          for (auto& b : n.binds) for (auto& nm : b.names) names.push_back(find(s3, nm)->cxx);
+          std::string key = names[0];
+          if (names.size() > 1) {
+            const std::string km = fresh("m");
+            key = "[&]() -> u32 { const u32 " + km + " = A.htop;";
+            for (auto& x : names) key += " hpush(A, " + x + ");";
+            key += " return seq_end(A, " + km + "); }()";
+          }
+          const std::string kv = fresh("k");
+          return " { const u32 " + kv + " = " + key + "; const u32 v_ = " + ex(n.a[0], s3) + "; hpush(A, " + kv + "); hpush(A, v_); }\n";
+        });
+        return "[&]() -> u32 { const u32 " + m + " = A.htop;\n" + loops + " return fun_end(A, " + m + ");\n}()";
+      }
+      case K::FunApp: return "apply(A, " + ex(n.a[0], sc) + ", " + ex(n.a[1], sc) + ")";
+      case K::Dot: return "apply(A, " + ex(n.a[0], sc) + ", mk_atom(A, " + std::to_string(str_atom(n.s)) + "u))";
+      case K::Record: {
+        const std::string m = fresh("m");
+        std::string o = "[&]() -> u32 { const u32 " + m + " = A.htop;\n";
+        for (size_t i = 0; i < n.fields.size(); ++i) {
+          const std::string kv = fresh("k");
+          o += " { const u32 " + kv + " = mk_atom(A, " + std::to_string(str_atom(n.fields[i])) + "u); const u32 v_ = " +
+               ex(n.a[i], sc) + "; hpush(A, " + kv + "); hpush(A, v_); }\n";
+        }
+        return o + " return fun_end(A, " + m + ");\n}()";
+      }
+      case K::Except: {
+        const std::string F = fresh("F");
+        std::string o = "[&]() -> u32 { u32 " + F + " = " + ex(n.a[0], sc) + ";\n";
+        for (auto& u : n.ups) o += except_update(F, u, 0, sc, F);
+        return o + " return " + F + ";\n}()";
+      }
+      default: break;
+    }
+    unsup(n, "this expression form");
+  }
+
+  // [F EXCEPT !p1..pk = rhs]: F_new = except(F, p1, [F[p1] EXCEPT !p2..pk = rhs]); keys outside the domain leave F unchanged
+  std::string except_update(const std::string& F, const Update& u, size_t i, Scope& sc, const std::string& target) {
+    const PathStep& st = u.path[i];
+    const std::string key = fresh("x"), old = fresh("o");
+    std::string o = "{ const u32 " + key + " = " + (st.field ? "mk_atom(A, " + std::to_string(str_atom(st.name)) + "u)" : ex(st.idx, sc)) +
+                    ";\n const u32 " + old + " = lookup(A, " + F + ", " + key + ");\n if (" + old + ") {\n";
+    if (i + 1 == u.path.size()) {
+      Scope s2 = sc;
+      Sym at; at.cxx = old;
+      s2.push_back({"@", at});
+      o += " " + target + " = except(A, " + F + ", " + key + ", " + ex(u.rhs, s2) + ");\n";
+    } else {
+      const std::string sub = fresh("F");
+      o += " u32 " + sub + " = " + old + ";\n" + except_update(old, u, i + 1, sc, sub) + " " + target + " = except(A, " + F + ", " +
+           key + ", " + sub + ");\n";
+    }
+    return o + " } }\n";
+  }
+
+  std::string binary(const Node& n, Scope& sc) {
+    const std::string& op = n.s;
+    const NP& l = n.a[0];
+    const NP& r = n.a[1];
+    if (op == "\\in" || op == "\\notin") {
+      const std::string neg = op == "\\notin" ? "!" : "";
+      if (r->k == K::Ident && !find(sc, r->s) && !global(r->s)) {
+        if (r->s == "Nat") return "[&]() -> u32 { const u32 x_ = " + ex(l, sc) + "; return mk_bool(" + neg + "(tg(A, x_) == T_INT && ival(A, x_) >= 0)); }()";
+        if (r->s == "Int") return "mk_bool(" + neg + "(tg(A, " + ex(l, sc) + ") == T_INT))";
+      }
+      if (r->k == K::Unary && r->s == "DOMAIN") return "mk_bool(" + neg + "in_dom(A, " + ex(r->a[0], sc) + ", " + ex(l, sc) + "))";
+      return "mk_bool(" + neg + "set_in(A, " + ex(l, sc) + ", " + ex(r, sc) + "))";
+    }
+    if (op == "=>") return "mk_bool(!truth(A, " + ex(l, sc) + ") || truth(A, " + ex(r, sc) + "))";
+    if (op == "<=>") return "mk_bool(truth(A, " + ex(l, sc) + ") == truth(A, " + ex(r, sc) + "))";
+    const std::string a = ex(l, sc), b = ex(r, sc);
+    if (op == "=") return "mk_bool(eqv(A, " + a + ", " + b + "))";
+    if (op == "/=") return "mk_bool(!eqv(A, " + a + ", " + b + "))";
+    if (op == "<" || op == ">" || op == "<=" || op == ">=") return "mk_bool(ival(A, " + a + ") " + op + " ival(A, " + b + "))";
+    if (op == "+" || op == "-" || op == "*") return "mk_int(A, ival(A, " + a + ") " + op + " ival(A, " + b + "))";
+    if (op == "\\div") return "[&]() -> u32 { const i64 x_ = ival(A, " + a + "), y_ = ival(A, " + b + "); if (y_ <= 0) { A.err |= E_ARITH; return 0u; } i64 q_ = x_ / y_; if ((x_ % y_) < 0) --q_; return mk_int(A, q_); }()";
+    if (op == "%") return "[&]() -> u32 { const i64 x_ = ival(A, " + a + "), y_ = ival(A, " + b + "); if (y_ <= 0) { A.err |= E_ARITH; return 0u; } i64 m_ = x_ % y_; if (m_ < 0) m_ += y_; return mk_int(A, m_); }()";
+    if (op == "..") return "range(A, ival(A, " + a + "), ival(A, " + b + "))";
+    if (op == "\\cup") return "set_union(A, " + a + ", " + b + ")";
+    if (op == "\\cap") return "set_cap(A, " + a + ", " + b + ")";
+    if (op == "\\") return "set_minus(A, " + a + ", " + b + ")";
+    if (op == "\\subseteq") return "mk_bool(set_subseteq(A, " + a + ", " + b + "))";
+    if (op == ":>") return "colon_gt(A, " + a + ", " + b + ")";
+    if (op == "@@") return "atat(A, " + a + ", " + b + ")";
+    if (op == "\\o") return "concat(A, " + a + ", " + b + ")";
+    if (auto d = global(op)) {   // user-defined infix operator
+      const std::string fn = op_function(d, n);
+      return fn + "(c, " + a + ", " + b + ")";
+    }
+    unsup(n, "operator " + op);
+  }
+
+  std::string ident(const Node& n, Scope& sc, const std::vector<std::string>& args) {
+    const std::string& nm = n.s;
+    if (const Sym* s = find(sc, nm)) {
+      if (s->kind == Sym::Val) {
+        if (!args.empty()) unsup(n, "applying a value as an operator");
+        return s->cxx;
+      }
+      std::string o = s->cxx + "(";
+      for (size_t i = 0; i < args.size(); ++i) o += (i ? ", " : "") + args[i];
+      return o + ")";
+    }
+    if (auto d = global(nm)) {
+      if (d->params.size() != args.size()) unsup(n, "operator " + nm + " with " + std::to_string(args.size()) + " arguments");
+      std::string o = op_function(d, n) + "(c";
+      for (auto& a : args) o += ", " + a;
+      return o + ")";
+    }
+    if (var_idx.count(nm)) {
+      if (!args.empty()) unsup(n, "applying a variable");
+      const std::string X = std::to_string(var_idx[nm]);
+      if (init_mode) return "(((c.asg >> " + X + ") & 1ull) ? c.nxt[" + X + "] : (A.err |= E_ASSIGN, 0u))";
+      return "c.cur[" + X + "]";
+    }
+    if (const_idx.count(nm)) {
+      if (!args.empty()) unsup(n, "operator constants");
+      return "c.k[" + std::to_string(const_idx[nm]) + "]";
+    }
+    // standard modules
+    auto need = [&](size_t k) { if (args.size() != k) unsup(n, nm + " with " + std::to_string(args.size()) + " arguments"); };
+    if (nm == "Len") { need(1); return "mk_int(A, fun_len(A, " + args[0] + "))"; }
+    if (nm == "Append") { need(2); return "append(A, " + args[0] + ", " + args[1] + ")"; }
+    if (nm == "SubSeq") { need(3); return "subseq(A, " + args[0] + ", ival(A, " + args[1] + "), ival(A, " + args[2] + "))"; }
+    if (nm == "Head") { need(1); return "head(A, " + args[0] + ")"; }
+    if (nm == "Tail") { need(1); return "tail(A, " + args[0] + ")"; }
+    if (nm == "Cardinality") { need(1); return "mk_int(A, set_card(A, " + args[0] + "))"; }
+    if (nm == "IsFiniteSet") { need(1); return "2u"; }
+    if (nm == "Print" || nm == "PrintT") { return args.back(); }
+    if (nm == "Assert") { need(2); return "(truth(A, " + args[0] + ") ? 2u : (A.err |= E_DOMAIN, 0u))"; }
+    if (nm == "BOOLEAN") { need(0); return "[&]() -> u32 { const u32 m_ = A.htop; hpush(A, 0u); hpush(A, 2u); return set_end(A, m_); }()"; }
+    unsup(n, "identifier " + nm);
+  }
+
+  // ---- actions: statements that run `k` once per way the formula is satisfied
+  std::string wrap(const std::string& k, std::string& decl) {
+    if (k.size() < 160) return k;
+    const std::string name = fresh("K");
+    decl += "auto " + name + " = [&]() {\n" + k + "};\n";
+    return name + "();\n";
+  }
+
+  std::string assign(int X, const std::string& v, const std::string& k) {
+    const std::string x = std::to_string(X), vv = fresh("v"), fr = fresh("f");
+    return "{ const u32 " + vv + " = " + v + ";\n const bool " + fr + " = !((c.asg >> " + x + ") & 1ull);\n if (" + fr + ") { c.nxt[" + x +
+           "] = " + vv + "; c.asg |= 1ull << " + x + "; }\n if (" + fr + " || eqv(A, c.nxt[" + x + "], " + vv + ")) {\n" + k + "}\n if (" +
+           fr + ") c.asg &= ~(1ull << " + x + ");\n}\n";
+  }
+
+  int target_var(const NP& e) {   // the variable an `x' = ..` (Next) or `x = ..` (Init) determines, or -1
+    if (!init_mode && e->k == K::Prime && e->a[0]->k == K::Ident && var_idx.count(e->a[0]->s)) return var_idx[e->a[0]->s];
+    if (init_mode && e->k == K::Ident && var_idx.count(e->s)) return var_idx[e->s];
+    return -1;
+  }
+
+  void unchanged_vars(const NP& e, std::vector<int>& out, int depth = 0) {
+    if (depth > 16) unsup(*e, "UNCHANGED nesting");
+    if (e->k == K::Tuple) { for (auto& x : e->a) unchanged_vars(x, out, depth + 1); return; }
+    if (e->k == K::Ident) {
+      if (var_idx.count(e->s)) { out.push_back(var_idx[e->s]); return; }
+      if (auto d = global(e->s)) { if (d->params.empty() && d->body) { unchanged_vars(d->body, out, depth + 1); return; } }
+    }
+    unsup(*e, "UNCHANGED of a non-variable");
+  }
+
+  std::string act(const NP& e, Scope& sc, const std::string& k, bool split, int label) {
+    const Node& n = *e;
+    switch (n.k) {
+      case K::And: {
+        std::function<std::string(size_t)> chain = [&](size_t i) -> std::string {
+          if (i == n.a.size()) return k;
+          return act(n.a[i], sc, chain(i + 1), false, label);
+        };
+        return chain(0);
+      }
+      case K::Or: {
+        std::string decl;
+        const std::string kk = wrap(k, decl);
+        std::string o = "{\n" + decl;
+        for (auto& b : n.a) {
+          const std::string sa = fresh("a"), st = fresh("t");
+          o += "{ const unsigned long long " + sa + " = c.asg; const u32 " + st + " = A.top;\n";
+          if (split) o += " c.act = " + std::to_string(label) + ";\n";
+          o += act(b, sc, kk, split, label) + " c.asg = " + sa + "; A.top = " + st + "; }\n";
+        }
+        return o + "}\n";
+      }
+      case K::Exists: {
+        Scope s2 = sc;
+        return bind_loops(n.binds, 0, 0, s2, true, [&](Scope& s3) {
+          return std::string(split ? " c.act = " + std::to_string(label) + ";\n" : "") + act(n.a[0], s3, k, split, label);
+        });
+      }
+      case K::Let: {
+        Scope s2 = sc;
+        const std::string defs = let_defs(e, s2);
+        return "{\n" + defs + act(n.a[0], s2, k, split, label) + "}\n";
+      }
+      case K::If: {
+        std::string decl;
+        const std::string kk = wrap(k, decl);
+        return "{\n" + decl + "if (truth(A, " + ex(n.a[0], sc) + ")) {\n" + act(n.a[1], sc, kk, false, label) + "} else {\n" +
+               act(n.a[2], sc, kk, false, label) + "}\n}\n";
+      }
+      case K::Case: {
+        std::string decl;
+        const std::string kk = wrap(k, decl);
+        std::string o = "{\n" + decl;
+        bool other = false;
+        for (size_t i = 0; i < n.a.size(); i += 2) {
+          if (!n.a[i]) { o += (i ? "else {\n" : "{\n") + act(n.a[i + 1], sc, kk, false, label) + "}\n"; other = true; break; }
+          o += std::string(i ? "else " : "") + "if (truth(A, " + ex(n.a[i], sc) + ")) {\n" + act(n.a[i + 1], sc, kk, false, label) + "}\n";
+        }
+        if (!other) o += "else A.err |= E_DOMAIN;\n";
+        return o + "}\n";
+      }
+      case K::Unchanged: {
+        std::vector<int> vs;
+        unchanged_vars(n.a[0], vs);
+        std::string o = k;
+        for (size_t i = vs.size(); i-- > 0;) o = assign(vs[i], "c.cur[" + std::to_string(vs[i]) + "]", o);
+        return o;
+      }
+      case K::Binary: {
+        if (n.s == "=") {
+          const int X = target_var(n.a[0]);
+          if (X >= 0) return assign(X, ex(n.a[1], sc), k);
+        }
+        if (n.s == "\\in") {
+          const int X = target_var(n.a[0]);
+          if (X >= 0) {
+            const std::string el = fresh("e");
+            return set_loop(ex(n.a[1], sc), el, assign(X, el, k), true);
+          }
+        }
+        break;
+      }
+      case K::Ident: case K::OpApp: {
+        if (find(sc, n.s)) {
+          const Sym* s = find(sc, n.s);
+          if (s->kind == Sym::LetOp && (init_mode || is_action_body(s->def))) return inline_op(n, sc, *s->def, *s->scope, k, split, label, false);
+          break;
+        }
+        if (auto d = global(n.s)) {
+          body_of(d, n);
+          const bool action = is_action(d);
+          if (action || init_mode) return inline_op(n, sc, *d, Scope(), k, split, split && action ? action_id(d->name) : label, split && action);
+        }
+        break;
+      }
+      case K::Temporal: case K::Enabled: unsup(n, "a temporal formula in an action");
+      default: break;
+    }
+    return "if (truth(A, " + ex(e, sc) + ")) {\n" + k + "}\n";
+  }
+
+  bool is_action_body(const std::shared_ptr<Def>& d) { std::set<std::string> v; return has_action(d->body, v); }
+
+  std::string inline_op(const Node& n, Scope& sc, const Def& d, const Scope& defscope, const std::string& k, bool split, int label, bool set_label) {
+    if (n.a.size() != d.params.size()) unsup(n, "operator " + d.name + " with " + std::to_string(n.a.size()) + " arguments");
+    std::string o = "{\n";
+    Scope s2 = defscope;
+    for (size_t i = 0; i < d.params.size(); ++i) {
+      const std::string pn = fresh("p");
+      o += " const u32 " + pn + " = " + ex(n.a[i], sc) + ";\n";
+      Sym s; s.cxx = pn;
+      s2.push_back({d.params[i], s});
+    }
+    if (set_label) o += " c.act = " + std::to_string(label) + ";\n";
+    return o + act(d.body, s2, k, split, label) + "}\n";
+  }
+
+  std::string cval(const CVal& v) {
+    switch (v.kind) {
+      case CVal::Int: return "mk_int(A, " + std::to_string(v.i) + "LL)";
+      case CVal::Str: return "mk_atom(A, " + std::to_string(str_atom(v.s)) + "u)";
+      case CVal::MV: return "mk_atom(A, " + std::to_string(mv_atom(v.s)) + "u)";
+      case CVal::Bool: return v.i ? "2u" : "0u";
+      case CVal::Set: {
+        std::string o = "[&]() -> u32 { const u32 m_ = A.htop;";
+        for (auto& e : v.elems) o += " hpush(A, " + cval(e) + ");";
+        return o + " return set_end(A, m_); }()";
+      }
+    }
+    return "0u";
+  }
+
+  std::shared_ptr<Def> cfg_def(const std::string& name, const char* what) {
+    auto d = global(name);
+    if (!d) throw CfgError(MC_E_UNSUPPORTED, std::string("cfg ") + what + " " + name + " is not defined in the module");
+    if (!d->body) throw CfgError(MC_E_UNSUPPORTED, std::string("cfg ") + what + " " + name + " does not parse: " + d->error);
+    return d;
+  }
+};
+
+}  // namespace
+
+Generated generate(const Program& prog, const CfgFile& cfg) {
+  Gen g(prog, cfg);
+  Generated out;
+  out.variables = prog.variables;
+  if (prog.variables.size() > 64) throw CfgError(MC_E_UNSUPPORTED, "more than 64 state variables");
+  if (!cfg.symmetry.empty() || !cfg.view.empty())
+    throw CfgError(MC_E_UNSUPPORTED, "SYMMETRY / VIEW on the generated path (the hand-compiled tlc_membership path has them)");
+  if (!cfg.action_constraints.empty()) throw CfgError(MC_E_UNSUPPORTED, "ACTION_CONSTRAINTS on the generated path");
+  std::ostringstream consts;
+  for (size_t i = 0; i < prog.constants.size(); ++i) {
+    const std::string& c = prog.constants[i];
+    if (!cfg.has(c)) throw CfgError(MC_E_PARSE, "constant " + c + " has no value in the cfg");
+    consts << "  c.k[" << i << "] = " << g.cval(cfg.get(c)) << ";\n";
+  }
+  out.init_name = cfg.init.empty() ? "Init" : cfg.init;
+  out.next_name = cfg.next.empty() ? "Next" : cfg.next;
+  auto initd = g.cfg_def(out.init_name, "INIT");
+  auto nextd = g.cfg_def(out.next_name, "NEXT");
+  if (!initd->params.empty() || !nextd->params.empty()) throw CfgError(MC_E_UNSUPPORTED, "INIT / NEXT with parameters");
+  const std::string full = prog.variables.size() == 64 ? "~0ull" : "((1ull << " + std::to_string(prog.variables.size()) + ") - 1ull)";
+
+  Scope sc;
+  g.init_mode = true;
+  const std::string init_body = g.act(initd->body, sc, "if (c.asg == " + full + ") em(c); else A.err |= E_ASSIGN;\n", false, 0);
+  g.init_mode = false;
+  const int next_label = g.action_id(out.next_name);
+  const std::string next_body = g.act(nextd->body, sc, "if (c.asg == " + full + ") em(c); else A.err |= E_ASSIGN;\n", true, next_label);
+  std::string cons = "TLV_HD bool constraints(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
+  for (auto& n : cfg.constraints) {
+    auto d = g.cfg_def(n, "CONSTRAINT");
+    Scope s0;
+    cons += "  if (!truth(A, " + g.ex(d->body, s0) + ")) return false;\n";
+    out.constraints.push_back(n);
+  }
+  cons += "  return true;\n}\n";
+  std::string invs = "TLV_HD int invariants(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
+  for (size_t i = 0; i < cfg.invariants.size(); ++i) {
+    auto d = g.cfg_def(cfg.invariants[i], "INVARIANT");
+    Scope s0;
+    invs += "  if (!truth(A, " + g.ex(d->body, s0) + ")) return " + std::to_string(i) + ";\n";
+    out.invariants.push_back(cfg.invariants[i]);
+  }
+  invs += "  return -1;\n}\n";
+
+  std::ostringstream s;
+  s << "namespace tlg {\nusing namespace tlv;\n";
+  s << "enum : int { NV = " << prog.variables.size() << ", NK = " << prog.constants.size() << ", NACT = " << g.actions.size()
+    << ", NINV = " << cfg.invariants.size() << " };\n";
+  s << "struct Cx { Ar* A; u32 k[" << (prog.constants.empty() ? 1 : prog.constants.size()) << "]; u32 cur[" << std::max<size_t>(1, prog.variables.size())
+    << "]; u32 nxt[" << std::max<size_t>(1, prog.variables.size()) << "]; unsigned long long asg; int act; };\n";
+  for (auto& p : g.fn_protos) s << p << "\n";
+  s << "TLV_HD void init_consts(Cx& c) {\n  Ar& A = *c.A; (void)A;\n" << consts.str() << "}\n";
+  for (auto& b : g.fn_bodies) s << b;
+  s << "template <class EM> TLV_HD void init_states(Cx& c, EM& em) {\n  Ar& A = *c.A; (void)A;\n  c.asg = 0; c.act = 0;\n" << init_body << "}\n";
+  s << "template <class EM> TLV_HD void next_states(Cx& c, EM& em) {\n  Ar& A = *c.A; (void)A;\n  c.asg = 0; c.act = " << next_label << ";\n" << next_body << "}\n";
+  s << cons << invs << "}  // namespace tlg\n";
+  out.source = s.str();
+  out.actions = g.actions;
+  out.atoms = g.atoms;
+  return out;
+}
+
+std::string compose_source(const Generated& g, const std::string& tlv_text, const std::string& tail) {
+  std::ostringstream s;
+  s << "// generated by raftmc's TLA+ front end\n" << tlv_text << "\n" << g.source << "\n";
+  s << "namespace tlg {\n";
+  s << "static const char* const kActionNames[] = {";
+  for (auto& a : g.actions) s << cstr(a) << ", ";
+  s << "nullptr};\nstatic const char* const kInvariantNames[] = {";
+  for (auto& a : g.invariants) s << cstr(a) << ", ";
+  s << "nullptr};\nstatic const char* const kVarNames[] = {";
+  for (auto& a : g.variables) s << cstr(a) << ", ";
+  s << "nullptr};\nstatic const char* const kAtomNames[] = {";
+  for (auto& a : g.atoms) s << cstr(a) << ", ";
+  s << "nullptr};\n}  // namespace tlg\n";
+  s << tail;
+  return s.str();
+}
+
+}  // namespace tlagen
+}  // namespace rmc

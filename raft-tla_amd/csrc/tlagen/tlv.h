@@ -1,0 +1,367 @@
+// tlv.h — TLA+ values for the generated path (host and device, no headers needed).
+//
+// The SANY-subset front end (tla_front.cpp) compiles a module's Init / Next / constraints /
+// invariants into C++ over this library; the same text is compiled by hiprtc for gfx950 (the
+// BFS kernels in tlagen_kernels.h) and by a host compiler for the CPU-side semantics tests.
+//
+// A value is a canonical word string in a per-thread arena, addressed by its word offset:
+//   word 0: tag (3 bits) | total words << 3
+//   BOOL [h, b]   INT [h, v ^ 0x80000000]   ATOM [h, id] (model values and strings, interned)
+//   SEQ  [h, n, e1 .. en]                   a function whose domain is 1..n (tuples, records
+//                                           never: their domain is a set of atoms)
+//   FUN  [h, n, k1 v1 .. kn vn]             keys strictly increasing, domain not 1..n
+//   SET  [h, n, e1 .. en]                   elements strictly increasing
+// Equal TLA+ values have equal word strings (TLC's value equality: <<a, b>> = [i \in 1..2 |->
+// ..], [x \in {} |-> e] = <<>>, 1 :> v = <<v>>), so a state's words are its canonical key and
+// the fingerprint is a hash of the words.  The order (word-lexicographic) is a total order
+// used to normalise sets and function domains; on integers it is the numeric order.
+//
+// Errors (TLC's evaluation errors: a function applied outside its domain, a bad sequence index,
+// CHOOSE with no witness, a type error, arena overflow) set bits in Ar::err and return a valid
+// dummy value, so evaluation never faults; the engine reports the error for the parent state.
+#pragma once
+#ifndef TLV_HD
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+#define TLV_HD __host__ __device__ inline
+#else
+#define TLV_HD inline
+#endif
+#endif
+
+namespace tlv {
+typedef unsigned int u32;
+typedef unsigned long long u64;
+typedef long long i64;
+
+enum : u32 { T_BOOL = 1, T_INT = 2, T_ATOM = 3, T_SEQ = 4, T_FUN = 5, T_SET = 6 };
+enum : u32 {
+  E_OVF = 1u,        // arena or handle stack full (capacity, not a spec error)
+  E_DOMAIN = 2u,     // f[x] with x outside DOMAIN f, r.fld missing
+  E_TYPE = 4u,       // operand of the wrong kind
+  E_CHOOSE = 8u,     // CHOOSE without a witness
+  E_SEQ = 16u,       // SubSeq / Head / Tail / index out of range
+  E_ASSIGN = 32u,    // x' read before it is determined
+  E_ARITH = 64u,     // integer overflow / division by zero
+  E_UNSUP = 128u     // construct outside the compiled subset reached at run time
+};
+
+struct Ar {
+  u32* w;       // values grow up from 4 (0: FALSE, 2: TRUE)
+  u32 top, cap;
+  u32* hs;      // handle stack (builders)
+  u32 htop, hcap;
+  u32 err;
+};
+
+TLV_HD u32 hdr(u32 tag, u32 n) { return tag | (n << 3); }
+TLV_HD u32 tg(const Ar& a, u32 v) { return a.w[v] & 7u; }
+TLV_HD u32 sz(const Ar& a, u32 v) { return a.w[v] >> 3; }
+TLV_HD void init(Ar& a, u32* w, u32 cap, u32* hs, u32 hcap) {
+  a.w = w; a.cap = cap; a.hs = hs; a.hcap = hcap; a.htop = 0; a.err = 0;
+  w[0] = hdr(T_BOOL, 2); w[1] = 0; w[2] = hdr(T_BOOL, 2); w[3] = 1; a.top = 4;
+}
+TLV_HD u32 alloc(Ar& a, u32 n) {
+  if (a.err & E_OVF) return 0;
+  if (a.top + n > a.cap) { a.err |= E_OVF; return 0; }
+  const u32 r = a.top; a.top += n; return r;
+}
+TLV_HD void hpush(Ar& a, u32 h) { if (a.htop < a.hcap) a.hs[a.htop++] = h; else a.err |= E_OVF; }
+TLV_HD u32 copy_in(Ar& a, const u32* src) {   // a value from outside the arena (state store)
+  const u32 n = src[0] >> 3, r = alloc(a, n);
+  if (a.err & E_OVF) return 0;
+  for (u32 q = 0; q < n; ++q) a.w[r + q] = src[q];
+  return r;
+}
+
+// ---- scalars
+TLV_HD u32 mk_bool(bool b) { return b ? 2u : 0u; }
+TLV_HD u32 mk_int(Ar& a, i64 x) {
+  if (x > 2147483647LL || x < -2147483648LL) { a.err |= E_ARITH; x = 0; }
+  const u32 r = alloc(a, 2);
+  if (a.err & E_OVF) return 0;
+  a.w[r] = hdr(T_INT, 2); a.w[r + 1] = (u32)(int)x ^ 0x80000000u; return r;
+}
+TLV_HD u32 mk_atom(Ar& a, u32 id) {
+  const u32 r = alloc(a, 2);
+  if (a.err & E_OVF) return 0;
+  a.w[r] = hdr(T_ATOM, 2); a.w[r + 1] = id; return r;
+}
+TLV_HD i64 ival(Ar& a, u32 v) {
+  if (tg(a, v) != T_INT) { a.err |= E_TYPE; return 0; }
+  return (i64)(int)(a.w[v + 1] ^ 0x80000000u);
+}
+TLV_HD bool truth(Ar& a, u32 v) {
+  if (tg(a, v) != T_BOOL) { a.err |= E_TYPE; return false; }
+  return a.w[v + 1] != 0;
+}
+
+// ---- order / equality (word-lexicographic; the header holds tag and size)
+TLV_HD int cmpv(const Ar& a, u32 x, u32 y) {
+  if (x == y) return 0;
+  const u32 n = sz(a, x) < sz(a, y) ? sz(a, x) : sz(a, y);
+  for (u32 q = 0; q < n; ++q) {
+    const u32 p = a.w[x + q], r = a.w[y + q];
+    if (p != r) return p < r ? -1 : 1;
+  }
+  return 0;   // equal headers imply equal sizes
+}
+TLV_HD bool eqv(const Ar& a, u32 x, u32 y) {
+  if (x == y) return true;
+  const u32 n = sz(a, x);
+  if (a.w[x] != a.w[y]) return false;
+  for (u32 q = 1; q < n; ++q) if (a.w[x + q] != a.w[y + q]) return false;
+  return true;
+}
+
+// ---- element walk: first element (SET/SEQ) or key (FUN) of a collection, next value
+TLV_HD u32 count(const Ar& a, u32 v) { return a.w[v + 1]; }
+TLV_HD u32 first(u32 v) { return v + 2; }
+TLV_HD u32 nextv(const Ar& a, u32 e) { return e + sz(a, e); }
+TLV_HD bool is_coll(const Ar& a, u32 v) { const u32 t = tg(a, v); return t == T_SEQ || t == T_FUN || t == T_SET; }
+
+// ---- builders: push element handles, then end
+TLV_HD void sort_handles(Ar& a, u32 mark, u32 stride) {   // insertion sort of stride-groups by their first handle
+  for (u32 i = mark + stride; i < a.htop; i += stride) {
+    for (u32 j = i; j > mark && cmpv(a, a.hs[j - stride], a.hs[j]) > 0; j -= stride)
+      for (u32 s = 0; s < stride; ++s) { const u32 t = a.hs[j - stride + s]; a.hs[j - stride + s] = a.hs[j + s]; a.hs[j + s] = t; }
+  }
+}
+TLV_HD u32 write_coll(Ar& a, u32 tag, u32 mark, u32 stride, u32 take_from, bool dedup) {
+  // writes the stride-groups hs[mark..htop) (only handles take_from.. of each group) as one value
+  u32 n = 0, words = 2;
+  for (u32 i = mark; i < a.htop; i += stride) {
+    if (dedup && i > mark && eqv(a, a.hs[i - stride], a.hs[i])) continue;
+    ++n;
+    for (u32 s = take_from; s < stride; ++s) words += sz(a, a.hs[i + s]);
+  }
+  const u32 r = alloc(a, words);
+  if (a.err & E_OVF) { a.htop = mark; return 0; }
+  a.w[r] = hdr(tag, words); a.w[r + 1] = n;
+  u32 o = r + 2;
+  for (u32 i = mark; i < a.htop; i += stride) {
+    if (dedup && i > mark && eqv(a, a.hs[i - stride], a.hs[i])) continue;
+    for (u32 s = take_from; s < stride; ++s) {
+      const u32 h = a.hs[i + s], m = sz(a, h);
+      for (u32 q = 0; q < m; ++q) a.w[o + q] = a.w[h + q];
+      o += m;
+    }
+  }
+  a.htop = mark;
+  return r;
+}
+TLV_HD u32 set_end(Ar& a, u32 mark) { sort_handles(a, mark, 1); return write_coll(a, T_SET, mark, 1, 0, true); }
+TLV_HD u32 seq_end(Ar& a, u32 mark) { return write_coll(a, T_SEQ, mark, 1, 0, false); }
+// function from (key, value) handle pairs; duplicate keys keep the first pair (callers never
+// produce two values for one key: a constructor's domain is a set)
+TLV_HD u32 fun_end(Ar& a, u32 mark) {
+  sort_handles(a, mark, 2);
+  u32 w = mark;   // drop later duplicates of a key (stable sort keeps insertion order of ties)
+  for (u32 i = mark; i < a.htop; i += 2) {
+    if (w > mark && eqv(a, a.hs[w - 2], a.hs[i])) continue;
+    a.hs[w] = a.hs[i]; a.hs[w + 1] = a.hs[i + 1]; w += 2;
+  }
+  a.htop = w;
+  bool seq = true;
+  i64 k = 1;
+  for (u32 i = mark; i < a.htop; i += 2, ++k) {
+    const u32 h = a.hs[i];
+    if (tg(a, h) != T_INT || (i64)(int)(a.w[h + 1] ^ 0x80000000u) != k) { seq = false; break; }
+  }
+  return seq ? write_coll(a, T_SEQ, mark, 2, 1, false) : write_coll(a, T_FUN, mark, 2, 0, false);
+}
+
+// ---- sets
+TLV_HD bool set_in(Ar& a, u32 x, u32 s) {
+  if (tg(a, s) != T_SET) { a.err |= E_TYPE; return false; }
+  u32 e = first(s);
+  for (u32 i = 0, n = count(a, s); i < n; ++i, e = nextv(a, e)) {
+    const int c = cmpv(a, e, x);
+    if (c == 0) return true;
+    if (c > 0) return false;   // sorted
+  }
+  return false;
+}
+TLV_HD u32 set_card(Ar& a, u32 s) {
+  if (tg(a, s) != T_SET) { a.err |= E_TYPE; return 0; }
+  return count(a, s);
+}
+TLV_HD u32 set_union(Ar& a, u32 x, u32 y) {
+  if (tg(a, x) != T_SET || tg(a, y) != T_SET) { a.err |= E_TYPE; return x; }
+  const u32 mark = a.htop;
+  u32 e = first(x);
+  for (u32 i = 0, n = count(a, x); i < n; ++i, e = nextv(a, e)) hpush(a, e);
+  e = first(y);
+  for (u32 i = 0, n = count(a, y); i < n; ++i, e = nextv(a, e)) hpush(a, e);
+  return set_end(a, mark);
+}
+TLV_HD u32 set_filter_in(Ar& a, u32 x, u32 y, bool keep_in) {   // x \cap y (keep_in) or x \ y
+  if (tg(a, x) != T_SET || tg(a, y) != T_SET) { a.err |= E_TYPE; return x; }
+  const u32 mark = a.htop;
+  u32 e = first(x);
+  for (u32 i = 0, n = count(a, x); i < n; ++i, e = nextv(a, e))
+    if (set_in(a, e, y) == keep_in) hpush(a, e);
+  return write_coll(a, T_SET, mark, 1, 0, false);   // a subsequence of a sorted set
+}
+TLV_HD u32 set_cap(Ar& a, u32 x, u32 y) { return set_filter_in(a, x, y, true); }
+TLV_HD u32 set_minus(Ar& a, u32 x, u32 y) { return set_filter_in(a, x, y, false); }
+TLV_HD bool set_subseteq(Ar& a, u32 x, u32 y) {
+  if (tg(a, x) != T_SET || tg(a, y) != T_SET) { a.err |= E_TYPE; return false; }
+  u32 e = first(x);
+  for (u32 i = 0, n = count(a, x); i < n; ++i, e = nextv(a, e)) if (!set_in(a, e, y)) return false;
+  return true;
+}
+TLV_HD u32 range(Ar& a, i64 lo, i64 hi) {
+  const u32 mark = a.htop;
+  for (i64 k = lo; k <= hi; ++k) hpush(a, mk_int(a, k));
+  return write_coll(a, T_SET, mark, 1, 0, false);
+}
+TLV_HD u32 powerset(Ar& a, u32 s) {
+  if (tg(a, s) != T_SET) { a.err |= E_TYPE; return s; }
+  const u32 n = count(a, s);
+  if (n > 16) { a.err |= E_UNSUP; return s; }
+  const u32 outer = a.htop;
+  for (u32 m = 0; m < (1u << n); ++m) {
+    const u32 mark = a.htop;
+    u32 e = first(s);
+    for (u32 i = 0; i < n; ++i, e = nextv(a, e)) if ((m >> i) & 1u) hpush(a, e);
+    const u32 sub = write_coll(a, T_SET, mark, 1, 0, false);
+    hpush(a, sub);
+  }
+  return set_end(a, outer);
+}
+TLV_HD u32 union_all(Ar& a, u32 s) {   // UNION s
+  if (tg(a, s) != T_SET) { a.err |= E_TYPE; return s; }
+  const u32 mark = a.htop;
+  u32 e = first(s);
+  for (u32 i = 0, n = count(a, s); i < n; ++i, e = nextv(a, e)) {
+    if (tg(a, e) != T_SET) { a.err |= E_TYPE; continue; }
+    u32 f = first(e);
+    for (u32 j = 0, m = count(a, e); j < m; ++j, f = nextv(a, f)) hpush(a, f);
+  }
+  return set_end(a, mark);
+}
+
+// ---- functions, records, sequences
+TLV_HD u32 dom(Ar& a, u32 f) {
+  const u32 t = tg(a, f);
+  if (t == T_SEQ) return range(a, 1, count(a, f));
+  if (t != T_FUN) { a.err |= E_TYPE; return f; }
+  const u32 mark = a.htop;
+  u32 e = first(f);
+  for (u32 i = 0, n = count(a, f); i < n; ++i) { hpush(a, e); e = nextv(a, e); e = nextv(a, e); }
+  return write_coll(a, T_SET, mark, 1, 0, false);
+}
+// pointer to f[x] or 0 if x is outside DOMAIN f (no error flagged)
+TLV_HD u32 lookup(Ar& a, u32 f, u32 x) {
+  const u32 t = tg(a, f);
+  if (t == T_SEQ) {
+    if (tg(a, x) != T_INT) return 0;
+    const i64 k = ival(a, x);
+    if (k < 1 || k > (i64)count(a, f)) return 0;
+    u32 e = first(f);
+    for (i64 i = 1; i < k; ++i) e = nextv(a, e);
+    return e;
+  }
+  if (t != T_FUN) { a.err |= E_TYPE; return 0; }
+  u32 e = first(f);
+  for (u32 i = 0, n = count(a, f); i < n; ++i) {
+    const u32 v = nextv(a, e);
+    if (eqv(a, e, x)) return v;
+    e = nextv(a, v);
+  }
+  return 0;
+}
+TLV_HD bool in_dom(Ar& a, u32 f, u32 x) { return lookup(a, f, x) != 0; }
+TLV_HD u32 apply(Ar& a, u32 f, u32 x) {
+  const u32 r = lookup(a, f, x);
+  if (!r) { a.err |= E_DOMAIN; return 0; }
+  return r;
+}
+TLV_HD u32 fun_len(Ar& a, u32 f) {   // Len
+  if (tg(a, f) != T_SEQ) { a.err |= E_TYPE; return 0; }
+  return count(a, f);
+}
+// [f EXCEPT ![x] = v]; x outside DOMAIN f leaves f unchanged (TLC)
+TLV_HD u32 except(Ar& a, u32 f, u32 x, u32 v) {
+  const u32 t = tg(a, f);
+  if (t != T_SEQ && t != T_FUN) { a.err |= E_TYPE; return f; }
+  const u32 at = lookup(a, f, x);
+  if (!at) return f;
+  const u32 old = sz(a, at), nw = sz(a, v), total = sz(a, f) - old + nw;
+  const u32 r = alloc(a, total);
+  if (a.err & E_OVF) return 0;
+  u32 o = r;
+  for (u32 q = f; q < at; ++q) a.w[o++] = a.w[q];
+  for (u32 q = 0; q < nw; ++q) a.w[o++] = a.w[v + q];
+  for (u32 q = at + old; q < f + sz(a, f); ++q) a.w[o++] = a.w[q];
+  a.w[r] = hdr(t, total);
+  return r;
+}
+TLV_HD u32 colon_gt(Ar& a, u32 k, u32 v) {   // k :> v
+  const u32 mark = a.htop;
+  hpush(a, k); hpush(a, v);
+  return fun_end(a, mark);
+}
+TLV_HD void push_pairs(Ar& a, u32 f) {
+  const u32 t = tg(a, f);
+  if (t == T_SEQ) {
+    u32 e = first(f);
+    for (u32 i = 0, n = count(a, f); i < n; ++i, e = nextv(a, e)) { hpush(a, mk_int(a, (i64)i + 1)); hpush(a, e); }
+  } else if (t == T_FUN) {
+    u32 e = first(f);
+    for (u32 i = 0, n = count(a, f); i < n; ++i) { const u32 v = nextv(a, e); hpush(a, e); hpush(a, v); e = nextv(a, v); }
+  } else a.err |= E_TYPE;
+}
+TLV_HD u32 atat(Ar& a, u32 f, u32 g) {   // f @@ g: f's pairs, then g's keys not in DOMAIN f
+  const u32 mark = a.htop;
+  push_pairs(a, f);
+  push_pairs(a, g);
+  return fun_end(a, mark);   // stable: f's pair wins a shared key
+}
+TLV_HD u32 append(Ar& a, u32 s, u32 e) {
+  if (tg(a, s) != T_SEQ) { a.err |= E_TYPE; return s; }
+  const u32 n = sz(a, s), m = sz(a, e), r = alloc(a, n + m);
+  if (a.err & E_OVF) return 0;
+  for (u32 q = 0; q < n; ++q) a.w[r + q] = a.w[s + q];
+  for (u32 q = 0; q < m; ++q) a.w[r + n + q] = a.w[e + q];
+  a.w[r] = hdr(T_SEQ, n + m); a.w[r + 1] = count(a, s) + 1;
+  return r;
+}
+TLV_HD u32 concat(Ar& a, u32 s, u32 t) {   // s \o t
+  if (tg(a, s) != T_SEQ || tg(a, t) != T_SEQ) { a.err |= E_TYPE; return s; }
+  const u32 n = sz(a, s), m = sz(a, t) - 2, r = alloc(a, n + m);
+  if (a.err & E_OVF) return 0;
+  for (u32 q = 0; q < n; ++q) a.w[r + q] = a.w[s + q];
+  for (u32 q = 0; q < m; ++q) a.w[r + n + q] = a.w[t + 2 + q];
+  a.w[r] = hdr(T_SEQ, n + m); a.w[r + 1] = count(a, s) + count(a, t);
+  return r;
+}
+TLV_HD u32 subseq(Ar& a, u32 s, i64 m, i64 n) {   // SubSeq(s, m, n)
+  if (tg(a, s) != T_SEQ) { a.err |= E_TYPE; return s; }
+  const u32 mark = a.htop;
+  if (m > n) return seq_end(a, mark);
+  if (m < 1 || n > (i64)count(a, s)) { a.err |= E_SEQ; return seq_end(a, mark); }
+  u32 e = first(s);
+  for (i64 i = 1; i <= n; ++i, e = nextv(a, e)) if (i >= m) hpush(a, e);
+  return seq_end(a, mark);
+}
+TLV_HD u32 head(Ar& a, u32 s) {
+  if (tg(a, s) != T_SEQ || count(a, s) == 0) { a.err |= E_SEQ; return 0; }
+  return first(s);
+}
+TLV_HD u32 tail(Ar& a, u32 s) {
+  if (tg(a, s) != T_SEQ || count(a, s) == 0) { a.err |= E_SEQ; return s; }
+  return subseq(a, s, 2, count(a, s));
+}
+
+// ---- state words and fingerprint
+TLV_HD u64 fmix(u64 h) { h ^= h >> 33; h *= 0xff51afd7ed558ccdULL; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ULL; h ^= h >> 33; return h; }
+TLV_HD u64 fp_words(const u32* w, u32 n, u64 seed) {
+  u64 h = seed ^ ((u64)n * 0x9e3779b97f4a7c15ULL);
+  u32 q = 0;
+  for (; q + 1 < n; q += 2) h = fmix(h ^ (((u64)w[q + 1] << 32) | w[q])) + 0x9e3779b97f4a7c15ULL;
+  if (q < n) h = fmix(h ^ (u64)w[q] ^ 0x5555555500000000ULL);
+  h = fmix(h);
+  return h ? h : 1ULL;   // 0 marks an empty seen-set slot
+}
+}  // namespace tlv
