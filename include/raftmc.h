@@ -92,8 +92,20 @@ typedef struct mc_opts {
   int32_t same_device;        /* n_gpus > 1 only: 1 = every rank on `device` (the ranks exchange through
                                  an in-process loopback of device copies): the multi-GPU level loop on
                                  a one-GPU machine (tests); 0 = one device per rank (default)        */
-  int32_t reserved[6];
+  int32_t frontend;           /* MC_FRONTEND_*: which compiled form of the module mc_open uses          */
+  int32_t reserved[5];
 } mc_opts;
+
+/* mc_opts.frontend.  AUTO: the hand-compiled kernels for thirdparty/raft_original.tla and
+ * tlc_membership/raft.tla (and their configs/ wrappers), the generated path for any other module.
+ * GENERATED: the SANY-subset front end for any module (csrc/tlagen: parse, generate C++ over
+ * tlv.h, hiprtc to a gfx950 code object cached by source hash; a path ending in .gen.hip is taken
+ * as an already generated source); single GPU, TLC -workers N semantics (every count exact, the
+ * kept parents first-come), no SYMMETRY / VIEW / ACTION_CONSTRAINTS.  HAND: the hand-compiled
+ * families only (MC_E_UNSUPPORTED otherwise). */
+#define MC_FRONTEND_AUTO 0
+#define MC_FRONTEND_GENERATED 1
+#define MC_FRONTEND_HAND 2
 
 typedef struct mc_summary_t {
   int64_t generated;          /* "states generated" (initial states included)             */

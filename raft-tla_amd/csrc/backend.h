@@ -92,5 +92,7 @@ struct Backend {
 
 Backend* make_orig_backend(const CfgFile& cfg);   // throws CfgError
 Backend* make_memb_backend(const CfgFile& cfg);   // throws CfgError
+// the generated path (csrc/tlagen): any module in the front end's subset, or a .gen.hip source
+Backend* make_tlagen_backend(const std::string& tla_path, const CfgFile& cfg);   // throws CfgError
 
 }  // namespace rmc

@@ -120,11 +120,20 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
   c->ro.block_size = o->block_size ? o->block_size : 256;
   c->ro.workers = o->workers;
   try {
-    std::string fam = rmc::detect_spec_family(rmc::read_text_file(tla_path));
+    if (o->frontend < MC_FRONTEND_AUTO || o->frontend > MC_FRONTEND_HAND) throw rmc::CfgError(MC_E_INVALID, "bad mc_opts.frontend");
+    std::string fam;
+    const std::string tla_text = rmc::read_text_file(tla_path);
+    if (o->frontend == MC_FRONTEND_GENERATED) fam = "tlagen";
+    else {
+      try { fam = rmc::detect_spec_family(tla_text); }
+      catch (const rmc::CfgError&) { if (o->frontend == MC_FRONTEND_HAND) throw; fam = "tlagen"; }
+    }
     rmc::CfgFile cfg = rmc::parse_cfg_text(rmc::read_text_file(cfg_path));
+    if (fam == "tlagen" && c->n_gpus > 1) throw rmc::CfgError(MC_E_UNSUPPORTED, "the generated path runs on one GPU (n_gpus = 1)");
     auto make = [&]() -> rmc::Backend* {
       if (fam == "raft_original") return rmc::make_orig_backend(cfg);
       if (fam == "tlc_membership") return rmc::make_memb_backend(cfg);
+      if (fam == "tlagen") return rmc::make_tlagen_backend(tla_path, cfg);
       throw rmc::CfgError(MC_E_UNSUPPORTED, "spec family '" + fam + "' has no GPU backend in this build");
     };
     c->be.reset(make());

@@ -35,6 +35,10 @@ int main(int argc, char** argv) {
     else if (k == "-depth") o.max_depth = std::atoll(val());
     else if (k == "-device") o.device = std::atoi(val());
     else if (k == "-gpus") o.n_gpus = std::atoi(val());
+    else if (k == "-frontend") {   // "auto" (default), "generated" (the SANY-subset front end for any module), "hand"
+      const std::string v = val();
+      o.frontend = v == "generated" ? MC_FRONTEND_GENERATED : v == "hand" ? MC_FRONTEND_HAND : MC_FRONTEND_AUTO;
+    }
     else if (k == "-fptable") o.fp_table_bytes = std::strtoull(val(), nullptr, 10);
     else if (k == "-store") o.state_store_bytes = std::strtoull(val(), nullptr, 10);
     else if (k == "-seed") o.seed = std::strtoull(val(), nullptr, 0);

@@ -1,0 +1,63 @@
+"""Build step: generated sources and gfx950 code objects for the repo's generated-path test
+specs, so the GPU box (which has no /root/reference) runs them without the front end or hiprtc.
+
+For each (name, module, cfg): `_build/tlagen <module> <cfg> --kernels` writes
+_build/tlagen_co/<name>.gen.hip (skipped when the module's base file is absent and the source
+already exists), and hipcc --genco compiles it to _build/tlagen_co/<key>.hsaco, where <key> is the
+library's cache key (FNV-1a 64 of the source and the hiprtc options, tlagen_backend.cpp)."""
+import concurrent.futures
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(os.path.dirname(HERE))
+ROOT = os.path.dirname(PKG)
+OUT = os.path.join(PKG, "_build", "tlagen_co")
+OPTS = ["--offload-arch=gfx950", "-O2", "-std=c++17"]
+REF = os.environ.get("RAFTMC_REFERENCE", "/root/reference")
+
+SPECS = [(n, "configs/raft_original_mc.tla", "configs/%s.cfg" % n)
+         for n in ("c1", "parity_single", "parity_pair", "parity_trio", "c2", "c2_noleader")]
+SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing.cfg")]
+
+
+def key_of(src):
+    h = 1469598103934665603
+    for b in (src + "".join("\n" + o for o in OPTS)).encode():
+        h = ((h ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return "%016x" % h
+
+
+def one(spec):
+    name, mod, cfg = spec
+    gen = os.path.join(OUT, name + ".gen.hip")
+    tool = os.path.join(PKG, "_build", "tlagen")
+    r = subprocess.run([tool, os.path.join(ROOT, mod), os.path.join(ROOT, cfg), "-I", REF, "--kernels", "-o", gen + ".tmp"],
+                       capture_output=True, text=True)
+    if r.returncode == 0:
+        if not os.path.exists(gen) or open(gen).read() != open(gen + ".tmp").read():
+            os.replace(gen + ".tmp", gen)
+        else:
+            os.remove(gen + ".tmp")
+    elif not os.path.exists(gen):
+        return name, "skipped (%s)" % r.stderr.strip()[:200]
+    src = open(gen).read()
+    co = os.path.join(OUT, key_of(src) + ".hsaco")
+    if not os.path.exists(co):
+        c = subprocess.run(["/opt/rocm/bin/hipcc", "--genco", *OPTS, "-o", co + ".tmp", "-x", "hip", gen], capture_output=True, text=True)
+        if c.returncode != 0:
+            raise RuntimeError("hipcc %s: %s" % (name, c.stderr[-2000:]))
+        os.replace(co + ".tmp", co)
+    return name, key_of(src)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        for name, res in ex.map(one, SPECS):
+            print("tlagen prebuild %s: %s" % (name, res))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

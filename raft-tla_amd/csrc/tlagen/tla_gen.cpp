@@ -116,7 +116,7 @@ struct Gen {
     std::string fn = "op_" + std::to_string(op_fn.size()) + "_";
     for (char ch : d->name) fn += std::isalnum((unsigned char)ch) ? ch : '_';
     op_fn[d->name] = fn;
-    std::string sig = "TLV_HD u32 " + fn + "(Cx& c";
+    std::string sig = "TLV_NI u32 " + fn + "(Cx& c";
     Scope sc;
     for (size_t i = 0; i < d->params.size(); ++i) {
       sig += ", u32 p" + std::to_string(i);
@@ -426,7 +426,7 @@ struct Gen {
   std::string wrap(const std::string& k, std::string& decl) {
     if (k.size() < 160) return k;
     const std::string name = fresh("K");
-    decl += "auto " + name + " = [&]() {\n" + k + "};\n";
+    decl += "auto " + name + " = [&]() TLG_NOINLINE {\n" + k + "};\n";
     return name + "();\n";
   }
 
@@ -471,7 +471,11 @@ struct Gen {
           const std::string sa = fresh("a"), st = fresh("t");
           o += "{ const unsigned long long " + sa + " = c.asg; const u32 " + st + " = A.top;\n";
           if (split) o += " c.act = " + std::to_string(label) + ";\n";
-          o += act(b, sc, kk, split, label) + " c.asg = " + sa + "; A.top = " + st + "; }\n";
+          std::string body = act(b, sc, kk, split, label);
+          // a large branch becomes a function of its own: short branches and fewer live registers
+          // in the expand kernel (one giant body needs long jumps and spills)
+          if (body.size() > 1500) body = "[&]() TLG_NOINLINE {\n" + body + "}();\n";
+          o += body + " c.asg = " + sa + "; A.top = " + st + "; }\n";
         }
         return o + "}\n";
       }
@@ -612,7 +616,7 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
   g.init_mode = false;
   const int next_label = g.action_id(out.next_name);
   const std::string next_body = g.act(nextd->body, sc, "if (c.asg == " + full + ") em(c); else A.err |= E_ASSIGN;\n", true, next_label);
-  std::string cons = "TLV_HD bool constraints(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
+  std::string cons = "TLV_NI bool constraints(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
   for (auto& n : cfg.constraints) {
     auto d = g.cfg_def(n, "CONSTRAINT");
     Scope s0;
@@ -620,7 +624,7 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
     out.constraints.push_back(n);
   }
   cons += "  return true;\n}\n";
-  std::string invs = "TLV_HD int invariants(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
+  std::string invs = "TLV_NI int invariants(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
   for (size_t i = 0; i < cfg.invariants.size(); ++i) {
     auto d = g.cfg_def(cfg.invariants[i], "INVARIANT");
     Scope s0;
@@ -630,12 +634,14 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
   invs += "  return -1;\n}\n";
 
   std::ostringstream s;
+  s << "#ifndef TLG_NOINLINE\n#define TLG_NOINLINE __attribute__((noinline))\n#endif\n";
   s << "namespace tlg {\nusing namespace tlv;\n";
   s << "enum : int { NV = " << prog.variables.size() << ", NK = " << prog.constants.size() << ", NACT = " << g.actions.size()
     << ", NINV = " << cfg.invariants.size() << " };\n";
   s << "struct Cx { Ar* A; u32 k[" << (prog.constants.empty() ? 1 : prog.constants.size()) << "]; u32 cur[" << std::max<size_t>(1, prog.variables.size())
     << "]; u32 nxt[" << std::max<size_t>(1, prog.variables.size()) << "]; unsigned long long asg; int act; };\n";
   for (auto& p : g.fn_protos) s << p << "\n";
+  s << "TLV_NI bool constraints(Cx& c);\nTLV_NI int invariants(Cx& c);\n";
   s << "TLV_HD void init_consts(Cx& c) {\n  Ar& A = *c.A; (void)A;\n" << consts.str() << "}\n";
   for (auto& b : g.fn_bodies) s << b;
   s << "template <class EM> TLV_HD void init_states(Cx& c, EM& em) {\n  Ar& A = *c.A; (void)A;\n  c.asg = 0; c.act = 0;\n" << init_body << "}\n";
@@ -649,7 +655,12 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
 
 std::string compose_source(const Generated& g, const std::string& tlv_text, const std::string& tail) {
   std::ostringstream s;
-  s << "// generated by raftmc's TLA+ front end\n" << tlv_text << "\n" << g.source << "\n";
+  s << "// generated by raftmc's TLA+ front end\n";
+  for (auto& v : g.variables) s << "//@var " << v << "\n";
+  for (auto& a : g.actions) s << "//@action " << a << "\n";
+  for (auto& a : g.invariants) s << "//@invariant " << a << "\n";
+  for (auto& a : g.atoms) s << "//@atom " << a << "\n";
+  s << tlv_text << "\n" << g.source << "\n";
   s << "namespace tlg {\n";
   s << "static const char* const kActionNames[] = {";
   for (auto& a : g.actions) s << cstr(a) << ", ";

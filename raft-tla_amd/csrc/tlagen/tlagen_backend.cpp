@@ -1,0 +1,404 @@
+// tlagen_backend.cpp — the generated path behind the C ABI (mc_opts.frontend, SURVEY.md §8(f)
+// rank 3): a module + cfg outside the hand-compiled families (or any module, on request) is
+// parsed by the SANY-subset front end, compiled to C++ over tlv.h together with the BFS kernels
+// of tlagen_kernels.h, turned into a gfx950 code object by hiprtc (cached by source hash next
+// to the library, or prebuilt by the build for the repo's own test specs), and run level by
+// level from here.  The same module text gives the same counts as the hand-compiled kernels
+// (tests/test_tlagen.py, tests/test_gpu_tlagen.py).
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+#include <sys/stat.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <sstream>
+
+#include "../../../include/raftmc.h"
+#include "../backend.h"
+#include "tla_gen.h"
+#include "tlv_text.h"
+
+namespace rmc {
+
+namespace {
+
+using u32 = unsigned int;
+using u64 = unsigned long long;
+
+// counters of tlagen_kernels.h
+enum { C_GEN = 0, C_GIN = 1, C_ERR = 2, C_CAP = 3, C_FLAG = 4, C_KIND = 5, C_SID = 6, C_INV = 7, C_EACT = 8, C_EWORDS = 9, C_ACT = 16 };
+
+struct KArgs {   // tlk::Args, field for field
+  u32* words; u64* words_used; u64 words_cap;
+  u64* offs; u64* parent; u32* act; u64 states_cap;
+  u64* n_states;
+  u64* table; u64 table_mask;
+  u32* arena; u32 acap;
+  u32* hstack; u32 hcap;
+  u64* ctr;
+  u32* evbuf; u32 evcap;
+  u64 first, count;
+  u64 seed;
+  int inv_oom, deadlock;
+};
+
+std::string read_all(const std::string& p) {
+  std::ifstream f(p, std::ios::binary);
+  if (!f) return "";
+  std::stringstream ss; ss << f.rdbuf();
+  return ss.str();
+}
+u64 fnv64(const std::string& s) {
+  u64 h = 1469598103934665603ull;
+  for (unsigned char ch : s) { h ^= ch; h *= 1099511628211ull; }
+  return h;
+}
+std::string hex(u64 v) { char b[17]; std::snprintf(b, sizeof b, "%016llx", v); return b; }
+std::string dir_of(const std::string& p) { const size_t s = p.rfind('/'); return s == std::string::npos ? "." : p.substr(0, s); }
+
+std::string lib_dir() {
+  Dl_info info;
+  if (dladdr((void*)&lib_dir, &info) && info.dli_fname) return dir_of(info.dli_fname);
+  return ".";
+}
+
+const char* kOpts[] = {"--offload-arch=gfx950", "-O2", "-std=c++17"};
+
+#define HIPOK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { err = std::string(#x) + ": " + hipGetErrorString(e_); return MC_E_NO_DEVICE; } } while (0)
+
+struct Meta {
+  std::vector<std::string> vars, actions, invariants, atoms;
+};
+
+// the generated source names its variables, actions, invariants and atoms in "//@" lines
+Meta parse_meta(const std::string& src) {
+  Meta m;
+  std::istringstream in(src);
+  std::string line;
+  while (std::getline(in, line)) {
+    if (line.rfind("//@", 0) != 0) { if (!line.empty() && line[0] != '/') break; continue; }
+    const size_t sp = line.find(' ');
+    const std::string kind = line.substr(3, sp - 3), val = sp == std::string::npos ? "" : line.substr(sp + 1);
+    if (kind == "var") m.vars.push_back(val);
+    else if (kind == "action") m.actions.push_back(val);
+    else if (kind == "invariant") m.invariants.push_back(val);
+    else if (kind == "atom") m.atoms.push_back(val);
+  }
+  return m;
+}
+
+struct Printer {
+  const Meta& m;
+  std::string v(const u32* w) const {
+    const u32 tag = w[0] & 7u, n = w[1];
+    switch (tag) {
+      case 1: return w[1] ? "TRUE" : "FALSE";
+      case 2: return std::to_string((long long)(int)(w[1] ^ 0x80000000u));
+      case 3: return w[1] < m.atoms.size() ? m.atoms[w[1]] : "?";
+      case 4: case 6: {
+        std::string o = tag == 4 ? "<<" : "{";
+        const u32* e = w + 2;
+        for (u32 i = 0; i < n; ++i) { o += (i ? ", " : "") + v(e); e += e[0] >> 3; }
+        return o + (tag == 4 ? ">>" : "}");
+      }
+      case 5: {
+        bool rec = true;
+        const u32* e = w + 2;
+        for (u32 i = 0; i < n; ++i) {
+          if ((e[0] & 7u) != 3 || e[1] >= m.atoms.size() || m.atoms[e[1]].empty() || m.atoms[e[1]][0] != '"') rec = false;
+          e += e[0] >> 3; e += e[0] >> 3;
+        }
+        std::string o = rec ? "[" : "(";
+        e = w + 2;
+        for (u32 i = 0; i < n; ++i) {
+          const u32* val = e + (e[0] >> 3);
+          if (rec) { const std::string& k = m.atoms[e[1]]; o += (i ? ", " : "") + k.substr(1, k.size() - 2) + " |-> " + v(val); }
+          else o += (i ? " @@ " : "") + v(e) + " :> " + v(val);
+          e = val + (val[0] >> 3);
+        }
+        return o + (rec ? "]" : ")");
+      }
+    }
+    return "?";
+  }
+  std::string state(const u32* w) const {
+    std::string o;
+    for (size_t i = 0; i < m.vars.size(); ++i) {
+      o += (i ? "\n" : "") + std::string("/\\ ") + m.vars[i] + " = " + v(w);
+      w += w[0] >> 3;
+    }
+    return o;
+  }
+  static u32 words_of(const u32* w, size_t nv) { u32 n = 0; for (size_t i = 0; i < nv; ++i) { n += w[0] >> 3; w += w[0] >> 3; } return n; }
+};
+
+struct TlagenBackend : Backend {
+  std::string src, key, src_origin;
+  Meta meta;
+  RunResult last;
+  // device state kept after run() for dump_states / traces
+  u32* d_words = nullptr; u64* d_offs = nullptr; u64 n_stored = 0, words_stored = 0;
+  int dev = 0;
+
+  TlagenBackend(const std::string& tla_path, const CfgFile& cfg) {
+    if (tla_path.size() > 8 && tla_path.compare(tla_path.size() - 8, 8, ".gen.hip") == 0) {
+      src = read_all(tla_path);
+      if (src.empty()) throw CfgError(MC_E_IO, "cannot read " + tla_path);
+      src_origin = "pregenerated " + tla_path;
+    } else {
+      std::vector<std::string> dirs;
+      if (const char* e = std::getenv("RAFTMC_TLA_PATH")) {
+        std::string s = e;
+        size_t a = 0;
+        while (a <= s.size()) { size_t b = s.find(':', a); if (b == std::string::npos) b = s.size(); if (b > a) dirs.push_back(s.substr(a, b - a)); a = b + 1; }
+      }
+      tlagen::Program prog;
+      try { prog = tlagen::load_program(tla_path, dirs); }
+      catch (const tlagen::ParseError& e) { throw CfgError(MC_E_PARSE, e.what()); }
+      tlagen::Generated g = tlagen::generate(prog, cfg);
+      src = tlagen::compose_source(g, kTlvText, kTlgKernelsText);
+      src_origin = "front end: " + tla_path;
+    }
+    meta = parse_meta(src);
+    if (meta.vars.empty()) throw CfgError(MC_E_PARSE, "generated source without metadata");
+    std::string k = src;
+    for (const char* o : kOpts) k += std::string("\n") + o;
+    key = hex(fnv64(k));
+  }
+  ~TlagenBackend() override { release(); }
+  void release() {
+    if (d_words) (void)hipFree(d_words);
+    if (d_offs) (void)hipFree(d_offs);
+    d_words = nullptr; d_offs = nullptr;
+  }
+
+  std::string family() const override { return "tlagen"; }
+  std::string describe_json() const override {
+    std::string o = "{\"family\": \"tlagen\", \"origin\": \"" + src_origin + "\", \"code_object\": \"" + key + "\", \"variables\": [";
+    for (size_t i = 0; i < meta.vars.size(); ++i) o += (i ? ", \"" : "\"") + meta.vars[i] + "\"";
+    o += "], \"actions\": [";
+    for (size_t i = 0; i < meta.actions.size(); ++i) o += (i ? ", \"" : "\"") + meta.actions[i] + "\"";
+    return o + "]}";
+  }
+
+  // code object: cache file, else hiprtc
+  int code_object(std::string& image, std::string& err) {
+    std::vector<std::string> dirs;
+    if (const char* e = std::getenv("RAFTMC_TLAGEN_CACHE")) dirs.push_back(e);
+    dirs.push_back(lib_dir() + "/tlagen_co");
+    for (auto& d : dirs) {
+      image = read_all(d + "/" + key + ".hsaco");
+      if (!image.empty()) return 0;
+    }
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "tlagen.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) { err = "hiprtcCreateProgram failed"; return MC_E_NO_DEVICE; }
+    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, kOpts);
+    if (rc != HIPRTC_SUCCESS) {
+      size_t n = 0; hiprtcGetProgramLogSize(prog, &n);
+      std::string log(n, '\0'); if (n) hiprtcGetProgramLog(prog, &log[0]);
+      hiprtcDestroyProgram(&prog);
+      err = "hiprtc: " + log.substr(0, 4000);
+      return MC_E_UNSUPPORTED;
+    }
+    size_t n = 0; hiprtcGetCodeSize(prog, &n);
+    image.assign(n, '\0'); hiprtcGetCode(prog, &image[0]);
+    hiprtcDestroyProgram(&prog);
+    for (auto& d : dirs) {   // best effort: keep it for the next open
+      ::mkdir(d.c_str(), 0755);
+      std::ofstream f(d + "/" + key + ".hsaco", std::ios::binary);
+      if (f) { f.write(image.data(), (std::streamsize)image.size()); break; }
+    }
+    return 0;
+  }
+
+  int run(const RunOpts& o, RunResult& r, std::string& err) override {
+    const auto t_start = std::chrono::steady_clock::now();
+    // every count is order independent; with -workers 1 the kept parents (traces) are still first-come
+    dev = o.device;
+    HIPOK(hipSetDevice(dev));
+    std::string image;
+    if (int rc = code_object(image, err)) return rc;
+    hipModule_t mod;
+    HIPOK(hipModuleLoadData(&mod, image.data()));
+    hipFunction_t f_init, f_expand;
+    HIPOK(hipModuleGetFunction(&f_init, mod, "tlg_init_k"));
+    HIPOK(hipModuleGetFunction(&f_expand, mod, "tlg_expand_k"));
+    release();
+    // HBM layout: store words + per-state offsets/parents/actions, seen-set, lanes' arenas
+    const u64 store = o.state_store_bytes ? o.state_store_bytes : (16ull << 30);
+    const u64 words_cap = store / 2 / 4, states_cap = store / 2 / 20;
+    u64 tbytes = o.fp_table_bytes ? o.fp_table_bytes : (2ull << 30);
+    u64 slots = 1; while (slots * 2 * 8 <= tbytes) slots *= 2;
+    const u32 acap = 16384, hcap = 4096, evcap = 65536;
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const u64 lanes = (u64)ncu * 4 * 64;   // 4 waves of 64 per CU
+    u64 *d_parent = nullptr, *d_table = nullptr, *d_ctr = nullptr;
+    u32 *d_act = nullptr, *d_arena = nullptr, *d_hs = nullptr, *d_ev = nullptr;
+    auto freeall = [&]() {
+      for (void* p : {(void*)d_parent, (void*)d_table, (void*)d_ctr, (void*)d_act, (void*)d_arena, (void*)d_hs, (void*)d_ev}) if (p) (void)hipFree(p);
+      (void)hipModuleUnload(mod);
+    };
+    const int nact = (int)meta.actions.size();
+    const size_t nctr = C_ACT + 2 * (size_t)nact + 4;   // + n_states, words_used
+    if (hipMalloc(&d_words, words_cap * 4) || hipMalloc(&d_offs, states_cap * 8) || hipMalloc(&d_parent, states_cap * 8) ||
+        hipMalloc(&d_act, states_cap * 4) || hipMalloc(&d_table, slots * 8) || hipMalloc(&d_ctr, nctr * 8) ||
+        hipMalloc(&d_arena, lanes * acap * 4) || hipMalloc(&d_hs, lanes * hcap * 4) || hipMalloc(&d_ev, evcap * 4)) {
+      freeall(); release();
+      err = "device allocation failed";
+      return MC_E_OOM;
+    }
+    HIPOK(hipMemset(d_table, 0, slots * 8));
+    HIPOK(hipMemset(d_ctr, 0, nctr * 8));
+    KArgs a{};
+    a.words = d_words; a.words_used = d_ctr + nctr - 1; a.words_cap = words_cap;
+    a.offs = d_offs; a.parent = d_parent; a.act = d_act; a.states_cap = states_cap;
+    a.n_states = d_ctr + nctr - 2;
+    a.table = d_table; a.table_mask = slots - 1;
+    a.arena = d_arena; a.acap = acap; a.hstack = d_hs; a.hcap = hcap;
+    a.ctr = d_ctr; a.evbuf = d_ev; a.evcap = evcap;
+    a.seed = o.seed ? o.seed : 0x2545f4914f6cdd1dull;
+    a.inv_oom = o.inv_out_of_model ? 1 : 0;
+    a.deadlock = o.check_deadlock ? 1 : 0;
+    std::vector<u64> h(nctr);
+    hipEvent_t e0, e1;
+    HIPOK(hipEventCreate(&e0)); HIPOK(hipEventCreate(&e1));
+    auto launch = [&](hipFunction_t f, u64 blocks) -> int {
+      void* params[] = {&a};
+      HIPOK(hipEventRecord(e0, 0));
+      HIPOK(hipModuleLaunchKernel(f, (unsigned)blocks, 1, 1, 64, 1, 1, 0, 0, params, nullptr));
+      HIPOK(hipEventRecord(e1, 0));
+      HIPOK(hipEventSynchronize(e1));
+      float ms = 0; (void)hipEventElapsedTime(&ms, e0, e1);
+      r.seconds_kernels += ms / 1e3;
+      r.levels.empty() ? void() : void(r.levels.back().kernel_ms += ms);
+      HIPOK(hipMemcpy(h.data(), d_ctr, nctr * 8, hipMemcpyDeviceToHost));
+      return 0;
+    };
+    r = RunResult();
+    r.action_names = meta.actions;
+    if (int rc = launch(f_init, 1)) { freeall(); return rc; }
+    u64 first = 0, count = h[nctr - 2], gen_prev = h[C_GEN];
+    r.generated = (int64_t)h[C_GEN];
+    if (count) { r.depth = 1; r.levels.push_back({(int64_t)count, (int64_t)h[C_GEN], 0}); }
+    const u64 grid = lanes / 64;
+    while (count && !h[C_FLAG] && !h[C_CAP]) {
+      if (o.max_depth && r.depth >= o.max_depth) { r.verdict = MC_VERDICT_DEPTH_LIMIT; r.left_on_queue = (int64_t)count; break; }
+      a.first = first; a.count = count;
+      r.levels.push_back({0, 0, 0});
+      if (int rc = launch(f_expand, grid)) { freeall(); return rc; }
+      ++r.n_launches;
+      const u64 total = h[nctr - 2];
+      const u64 fresh = total - (first + count);
+      r.levels.back().states = (int64_t)fresh;
+      r.levels.back().generated = (int64_t)(h[C_GEN] - gen_prev);
+      gen_prev = h[C_GEN];
+      first += count; count = fresh;
+      if (fresh) ++r.depth; else r.levels.pop_back();
+    }
+    n_stored = std::min<u64>(h[nctr - 2], states_cap);
+    words_stored = std::min<u64>(h[nctr - 1], words_cap);
+    r.generated = (int64_t)h[C_GEN];
+    r.generated_in_model = (int64_t)h[C_GIN];
+    r.distinct = (int64_t)n_stored;
+    r.act_generated.resize(nact); r.act_distinct.resize(nact);
+    for (int k = 0; k < nact; ++k) { r.act_generated[k] = (int64_t)h[C_ACT + k]; r.act_distinct[k] = (int64_t)h[C_ACT + nact + k]; }
+    if (h[C_CAP]) {
+      r.verdict = MC_VERDICT_CAPACITY_OVERFLOW;
+      r.error = (h[C_CAP] & 4) ? "lane arena too small for one state's successors" : (h[C_CAP] & 2) ? "seen-set full" : "state store full";
+    } else if (h[C_FLAG]) {
+      const u64 kind = h[C_KIND], sid = h[C_SID];
+      Printer pr{meta};
+      std::vector<u64> path;
+      if (sid != ~0ull) chase(sid, path, d_parent, err);
+      for (size_t i = path.size(); i-- > 0;) trace_step(path[i], d_parent, d_act, pr, r);
+      if (kind == 1 || kind == 2) {
+        r.verdict = MC_VERDICT_INVARIANT_VIOLATION;
+        r.violated = h[C_INV] < meta.invariants.size() ? meta.invariants[h[C_INV]] : "?";
+        if (kind == 2) {   // the violating successor is outside the constraints: printed from the event buffer
+          std::vector<u32> w(h[C_EWORDS]);
+          (void)hipMemcpy(w.data(), d_ev, w.size() * 4, hipMemcpyDeviceToHost);
+          const u64 ak = h[C_EACT];
+          r.trace.push_back({ak < meta.actions.size() ? meta.actions[ak] : "?", pr.state(w.data())});
+        }
+      } else if (kind == 3) {
+        r.verdict = MC_VERDICT_EVAL_ERROR;
+        r.error = "evaluation error (tlv error bits " + std::to_string(h[C_INV]) + ") while computing the successors of the last state";
+      } else {
+        r.verdict = MC_VERDICT_DEADLOCK;
+      }
+      r.left_on_queue = (int64_t)count;
+    }
+    r.seed = a.seed;
+    r.state_bytes = 0;
+    (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+    freeall();
+    r.seconds_total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    last = r;
+    return 0;
+  }
+
+  void chase(u64 sid, std::vector<u64>& path, u64* d_parent, std::string& err) {
+    (void)err;
+    while (sid != ~0ull && path.size() < 100000) {
+      path.push_back(sid);
+      u64 p = ~0ull;
+      (void)hipMemcpy(&p, d_parent + sid, 8, hipMemcpyDeviceToHost);
+      sid = p;
+    }
+  }
+  void trace_step(u64 sid, u64* d_parent, u32* d_act, const Printer& pr, RunResult& r) {
+    u64 off = 0, par = 0;
+    u32 act = 0;
+    (void)hipMemcpy(&off, d_offs + sid, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&par, d_parent + sid, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&act, d_act + sid, 4, hipMemcpyDeviceToHost);
+    std::vector<u32> w(std::min<u64>(1u << 20, words_stored - off));
+    (void)hipMemcpy(w.data(), d_words + off, w.size() * 4, hipMemcpyDeviceToHost);
+    r.trace.push_back({par == ~0ull ? "Initial predicate" : act < meta.actions.size() ? meta.actions[act] : "?", pr.state(w.data())});
+  }
+
+  int dump_states(const std::string& path, std::string& err) override {
+    if (!d_words) { err = "no run"; return MC_E_STATE; }
+    std::vector<u32> w(words_stored);
+    std::vector<u64> off(n_stored);
+    HIPOK(hipMemcpy(w.data(), d_words, w.size() * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(off.data(), d_offs, off.size() * 8, hipMemcpyDeviceToHost));
+    FILE* f = std::fopen(path.c_str(), "w");
+    if (!f) { err = "cannot write " + path; return MC_E_IO; }
+    Printer pr{meta};
+    for (u64 i = 0; i < n_stored; ++i) {
+      std::string s = pr.state(w.data() + off[i]);
+      for (char& ch : s) if (ch == '\n') ch = ' ';
+      std::fprintf(f, "%s\n", s.c_str());
+    }
+    std::fclose(f);
+    return 0;
+  }
+
+  // single-GPU only: the sharded entry points are the hand-compiled families'
+  int shard_open(const RunOpts&, int, int, std::string& err) override { err = "the generated path runs on one GPU"; return MC_E_UNSUPPORTED; }
+  int shard_record_bytes(int) const override { return 0; }
+  int shard_frontier(int64_t*, int64_t*) const override { return MC_E_UNSUPPORTED; }
+  int shard_generate(int64_t, int64_t, int64_t*, std::string& err) override { err = "unsupported"; return MC_E_UNSUPPORTED; }
+  int shard_fill(int, void*, const int64_t*, std::string& err) override { err = "unsupported"; return MC_E_UNSUPPORTED; }
+  int shard_dedup(const void*, const int64_t*, int64_t*, std::string& err) override { err = "unsupported"; return MC_E_UNSUPPORTED; }
+  int shard_materialize(const void*, const int64_t*, std::string& err) override { err = "unsupported"; return MC_E_UNSUPPORTED; }
+  int shard_store(const void*, int64_t, std::string& err) override { err = "unsupported"; return MC_E_UNSUPPORTED; }
+  int shard_level_stats(int64_t*, std::string& err) override { err = "unsupported"; return MC_E_UNSUPPORTED; }
+  int shard_level_commit(const int64_t*, int*, std::string& err) override { err = "unsupported"; return MC_E_UNSUPPORTED; }
+  int shard_read_state(uint64_t, std::string&, uint64_t*, std::string& err) const override { err = "unsupported"; return MC_E_UNSUPPORTED; }
+  int shard_violation(uint64_t*, std::string&, std::string&) const override { return MC_E_UNSUPPORTED; }
+  const RunResult* shard_result() const override { return &last; }
+};
+
+}  // namespace
+
+Backend* make_tlagen_backend(const std::string& tla_path, const CfgFile& cfg) { return new TlagenBackend(tla_path, cfg); }
+
+}  // namespace rmc

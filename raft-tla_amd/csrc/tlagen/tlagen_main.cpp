@@ -1,7 +1,7 @@
 // tlagen — the front end as a command: parse a TLA+ module (+ the modules it EXTENDS) and a TLC
 // cfg, and print the generated C++ (tlv.h + namespace tlg) that the GPU path compiles.
 //
-//   tlagen SPEC.tla CFG.cfg [-I DIR]... [-o OUT] [--parse-only]
+//   tlagen SPEC.tla CFG.cfg [-I DIR]... [-o OUT] [--parse-only] [--kernels]
 //
 // --parse-only parses every definition of every module and reports the ones outside the subset
 // (what SANY's parse of the module would reject is a parse error here too).
@@ -18,12 +18,13 @@ int main(int argc, char** argv) {
   using namespace rmc;
   std::string spec, cfgp, out;
   std::vector<std::string> dirs;
-  bool parse_only = false;
+  bool parse_only = false, kernels = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     if (a == "-I" && i + 1 < argc) dirs.push_back(argv[++i]);
     else if (a == "-o" && i + 1 < argc) out = argv[++i];
     else if (a == "--parse-only") parse_only = true;
+    else if (a == "--kernels") kernels = true;
     else if (spec.empty()) spec = a;
     else cfgp = a;
   }
@@ -48,7 +49,7 @@ int main(int argc, char** argv) {
     }
     CfgFile cfg = parse_cfg_text(read_text_file(cfgp));
     tlagen::Generated g = tlagen::generate(prog, cfg);
-    const std::string src = tlagen::compose_source(g, kTlvText, "");
+    const std::string src = tlagen::compose_source(g, kTlvText, kernels ? kTlgKernelsText : "");
     if (out.empty()) std::cout << src;
     else { std::ofstream f(out); f << src; }
     return 0;

@@ -23,8 +23,10 @@
 #ifndef TLV_HD
 #if defined(__HIPCC__) || defined(__HIPCC_RTC__)
 #define TLV_HD __host__ __device__ inline
+#define TLV_NI __host__ __device__ __attribute__((noinline))   // large routines: one copy, not one per use
 #else
 #define TLV_HD inline
+#define TLV_NI static __attribute__((noinline))
 #endif
 #endif
 
@@ -66,7 +68,7 @@ TLV_HD u32 alloc(Ar& a, u32 n) {
   const u32 r = a.top; a.top += n; return r;
 }
 TLV_HD void hpush(Ar& a, u32 h) { if (a.htop < a.hcap) a.hs[a.htop++] = h; else a.err |= E_OVF; }
-TLV_HD u32 copy_in(Ar& a, const u32* src) {   // a value from outside the arena (state store)
+TLV_NI u32 copy_in(Ar& a, const u32* src) {   // a value from outside the arena (state store)
   const u32 n = src[0] >> 3, r = alloc(a, n);
   if (a.err & E_OVF) return 0;
   for (u32 q = 0; q < n; ++q) a.w[r + q] = src[q];
@@ -96,7 +98,7 @@ TLV_HD bool truth(Ar& a, u32 v) {
 }
 
 // ---- order / equality (word-lexicographic; the header holds tag and size)
-TLV_HD int cmpv(const Ar& a, u32 x, u32 y) {
+TLV_NI int cmpv(const Ar& a, u32 x, u32 y) {
   if (x == y) return 0;
   const u32 n = sz(a, x) < sz(a, y) ? sz(a, x) : sz(a, y);
   for (u32 q = 0; q < n; ++q) {
@@ -120,13 +122,13 @@ TLV_HD u32 nextv(const Ar& a, u32 e) { return e + sz(a, e); }
 TLV_HD bool is_coll(const Ar& a, u32 v) { const u32 t = tg(a, v); return t == T_SEQ || t == T_FUN || t == T_SET; }
 
 // ---- builders: push element handles, then end
-TLV_HD void sort_handles(Ar& a, u32 mark, u32 stride) {   // insertion sort of stride-groups by their first handle
+TLV_NI void sort_handles(Ar& a, u32 mark, u32 stride) {   // insertion sort of stride-groups by their first handle
   for (u32 i = mark + stride; i < a.htop; i += stride) {
     for (u32 j = i; j > mark && cmpv(a, a.hs[j - stride], a.hs[j]) > 0; j -= stride)
       for (u32 s = 0; s < stride; ++s) { const u32 t = a.hs[j - stride + s]; a.hs[j - stride + s] = a.hs[j + s]; a.hs[j + s] = t; }
   }
 }
-TLV_HD u32 write_coll(Ar& a, u32 tag, u32 mark, u32 stride, u32 take_from, bool dedup) {
+TLV_NI u32 write_coll(Ar& a, u32 tag, u32 mark, u32 stride, u32 take_from, bool dedup) {
   // writes the stride-groups hs[mark..htop) (only handles take_from.. of each group) as one value
   u32 n = 0, words = 2;
   for (u32 i = mark; i < a.htop; i += stride) {
@@ -153,7 +155,7 @@ TLV_HD u32 set_end(Ar& a, u32 mark) { sort_handles(a, mark, 1); return write_col
 TLV_HD u32 seq_end(Ar& a, u32 mark) { return write_coll(a, T_SEQ, mark, 1, 0, false); }
 // function from (key, value) handle pairs; duplicate keys keep the first pair (callers never
 // produce two values for one key: a constructor's domain is a set)
-TLV_HD u32 fun_end(Ar& a, u32 mark) {
+TLV_NI u32 fun_end(Ar& a, u32 mark) {
   sort_handles(a, mark, 2);
   u32 w = mark;   // drop later duplicates of a key (stable sort keeps insertion order of ties)
   for (u32 i = mark; i < a.htop; i += 2) {
@@ -171,7 +173,7 @@ TLV_HD u32 fun_end(Ar& a, u32 mark) {
 }
 
 // ---- sets
-TLV_HD bool set_in(Ar& a, u32 x, u32 s) {
+TLV_NI bool set_in(Ar& a, u32 x, u32 s) {
   if (tg(a, s) != T_SET) { a.err |= E_TYPE; return false; }
   u32 e = first(s);
   for (u32 i = 0, n = count(a, s); i < n; ++i, e = nextv(a, e)) {
@@ -185,7 +187,7 @@ TLV_HD u32 set_card(Ar& a, u32 s) {
   if (tg(a, s) != T_SET) { a.err |= E_TYPE; return 0; }
   return count(a, s);
 }
-TLV_HD u32 set_union(Ar& a, u32 x, u32 y) {
+TLV_NI u32 set_union(Ar& a, u32 x, u32 y) {
   if (tg(a, x) != T_SET || tg(a, y) != T_SET) { a.err |= E_TYPE; return x; }
   const u32 mark = a.htop;
   u32 e = first(x);
@@ -194,7 +196,7 @@ TLV_HD u32 set_union(Ar& a, u32 x, u32 y) {
   for (u32 i = 0, n = count(a, y); i < n; ++i, e = nextv(a, e)) hpush(a, e);
   return set_end(a, mark);
 }
-TLV_HD u32 set_filter_in(Ar& a, u32 x, u32 y, bool keep_in) {   // x \cap y (keep_in) or x \ y
+TLV_NI u32 set_filter_in(Ar& a, u32 x, u32 y, bool keep_in) {   // x \cap y (keep_in) or x \ y
   if (tg(a, x) != T_SET || tg(a, y) != T_SET) { a.err |= E_TYPE; return x; }
   const u32 mark = a.htop;
   u32 e = first(x);
@@ -204,18 +206,18 @@ TLV_HD u32 set_filter_in(Ar& a, u32 x, u32 y, bool keep_in) {   // x \cap y (kee
 }
 TLV_HD u32 set_cap(Ar& a, u32 x, u32 y) { return set_filter_in(a, x, y, true); }
 TLV_HD u32 set_minus(Ar& a, u32 x, u32 y) { return set_filter_in(a, x, y, false); }
-TLV_HD bool set_subseteq(Ar& a, u32 x, u32 y) {
+TLV_NI bool set_subseteq(Ar& a, u32 x, u32 y) {
   if (tg(a, x) != T_SET || tg(a, y) != T_SET) { a.err |= E_TYPE; return false; }
   u32 e = first(x);
   for (u32 i = 0, n = count(a, x); i < n; ++i, e = nextv(a, e)) if (!set_in(a, e, y)) return false;
   return true;
 }
-TLV_HD u32 range(Ar& a, i64 lo, i64 hi) {
+TLV_NI u32 range(Ar& a, i64 lo, i64 hi) {
   const u32 mark = a.htop;
   for (i64 k = lo; k <= hi; ++k) hpush(a, mk_int(a, k));
   return write_coll(a, T_SET, mark, 1, 0, false);
 }
-TLV_HD u32 powerset(Ar& a, u32 s) {
+TLV_NI u32 powerset(Ar& a, u32 s) {
   if (tg(a, s) != T_SET) { a.err |= E_TYPE; return s; }
   const u32 n = count(a, s);
   if (n > 16) { a.err |= E_UNSUP; return s; }
@@ -229,7 +231,7 @@ TLV_HD u32 powerset(Ar& a, u32 s) {
   }
   return set_end(a, outer);
 }
-TLV_HD u32 union_all(Ar& a, u32 s) {   // UNION s
+TLV_NI u32 union_all(Ar& a, u32 s) {   // UNION s
   if (tg(a, s) != T_SET) { a.err |= E_TYPE; return s; }
   const u32 mark = a.htop;
   u32 e = first(s);
@@ -242,7 +244,7 @@ TLV_HD u32 union_all(Ar& a, u32 s) {   // UNION s
 }
 
 // ---- functions, records, sequences
-TLV_HD u32 dom(Ar& a, u32 f) {
+TLV_NI u32 dom(Ar& a, u32 f) {
   const u32 t = tg(a, f);
   if (t == T_SEQ) return range(a, 1, count(a, f));
   if (t != T_FUN) { a.err |= E_TYPE; return f; }
@@ -252,7 +254,7 @@ TLV_HD u32 dom(Ar& a, u32 f) {
   return write_coll(a, T_SET, mark, 1, 0, false);
 }
 // pointer to f[x] or 0 if x is outside DOMAIN f (no error flagged)
-TLV_HD u32 lookup(Ar& a, u32 f, u32 x) {
+TLV_NI u32 lookup(Ar& a, u32 f, u32 x) {
   const u32 t = tg(a, f);
   if (t == T_SEQ) {
     if (tg(a, x) != T_INT) return 0;
@@ -282,7 +284,7 @@ TLV_HD u32 fun_len(Ar& a, u32 f) {   // Len
   return count(a, f);
 }
 // [f EXCEPT ![x] = v]; x outside DOMAIN f leaves f unchanged (TLC)
-TLV_HD u32 except(Ar& a, u32 f, u32 x, u32 v) {
+TLV_NI u32 except(Ar& a, u32 f, u32 x, u32 v) {
   const u32 t = tg(a, f);
   if (t != T_SEQ && t != T_FUN) { a.err |= E_TYPE; return f; }
   const u32 at = lookup(a, f, x);
@@ -302,7 +304,7 @@ TLV_HD u32 colon_gt(Ar& a, u32 k, u32 v) {   // k :> v
   hpush(a, k); hpush(a, v);
   return fun_end(a, mark);
 }
-TLV_HD void push_pairs(Ar& a, u32 f) {
+TLV_NI void push_pairs(Ar& a, u32 f) {
   const u32 t = tg(a, f);
   if (t == T_SEQ) {
     u32 e = first(f);
@@ -312,13 +314,13 @@ TLV_HD void push_pairs(Ar& a, u32 f) {
     for (u32 i = 0, n = count(a, f); i < n; ++i) { const u32 v = nextv(a, e); hpush(a, e); hpush(a, v); e = nextv(a, v); }
   } else a.err |= E_TYPE;
 }
-TLV_HD u32 atat(Ar& a, u32 f, u32 g) {   // f @@ g: f's pairs, then g's keys not in DOMAIN f
+TLV_NI u32 atat(Ar& a, u32 f, u32 g) {   // f @@ g: f's pairs, then g's keys not in DOMAIN f
   const u32 mark = a.htop;
   push_pairs(a, f);
   push_pairs(a, g);
   return fun_end(a, mark);   // stable: f's pair wins a shared key
 }
-TLV_HD u32 append(Ar& a, u32 s, u32 e) {
+TLV_NI u32 append(Ar& a, u32 s, u32 e) {
   if (tg(a, s) != T_SEQ) { a.err |= E_TYPE; return s; }
   const u32 n = sz(a, s), m = sz(a, e), r = alloc(a, n + m);
   if (a.err & E_OVF) return 0;
@@ -327,7 +329,7 @@ TLV_HD u32 append(Ar& a, u32 s, u32 e) {
   a.w[r] = hdr(T_SEQ, n + m); a.w[r + 1] = count(a, s) + 1;
   return r;
 }
-TLV_HD u32 concat(Ar& a, u32 s, u32 t) {   // s \o t
+TLV_NI u32 concat(Ar& a, u32 s, u32 t) {   // s \o t
   if (tg(a, s) != T_SEQ || tg(a, t) != T_SEQ) { a.err |= E_TYPE; return s; }
   const u32 n = sz(a, s), m = sz(a, t) - 2, r = alloc(a, n + m);
   if (a.err & E_OVF) return 0;
@@ -336,7 +338,7 @@ TLV_HD u32 concat(Ar& a, u32 s, u32 t) {   // s \o t
   a.w[r] = hdr(T_SEQ, n + m); a.w[r + 1] = count(a, s) + count(a, t);
   return r;
 }
-TLV_HD u32 subseq(Ar& a, u32 s, i64 m, i64 n) {   // SubSeq(s, m, n)
+TLV_NI u32 subseq(Ar& a, u32 s, i64 m, i64 n) {   // SubSeq(s, m, n)
   if (tg(a, s) != T_SEQ) { a.err |= E_TYPE; return s; }
   const u32 mark = a.htop;
   if (m > n) return seq_end(a, mark);
@@ -356,7 +358,7 @@ TLV_HD u32 tail(Ar& a, u32 s) {
 
 // ---- state words and fingerprint
 TLV_HD u64 fmix(u64 h) { h ^= h >> 33; h *= 0xff51afd7ed558ccdULL; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ULL; h ^= h >> 33; return h; }
-TLV_HD u64 fp_words(const u32* w, u32 n, u64 seed) {
+TLV_NI u64 fp_words(const u32* w, u32 n, u64 seed) {
   u64 h = seed ^ ((u64)n * 0x9e3779b97f4a7c15ULL);
   u32 q = 0;
   for (; q + 1 < n; q += 2) h = fmix(h ^ (((u64)w[q + 1] << 32) | w[q])) + 0x9e3779b97f4a7c15ULL;

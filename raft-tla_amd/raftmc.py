@@ -38,8 +38,8 @@ class McOpts(ctypes.Structure):
                 ("workers", ctypes.c_int32), ("fp_table_bytes", ctypes.c_uint64),
                 ("state_store_bytes", ctypes.c_uint64), ("max_depth", ctypes.c_int64), ("seed", ctypes.c_uint64),
                 ("tlc_compat_flags", ctypes.c_uint32), ("check_deadlock", ctypes.c_int32),
-                ("block_size", ctypes.c_int32), ("same_device", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 6)]
+                ("block_size", ctypes.c_int32), ("same_device", ctypes.c_int32), ("frontend", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 5)]
 
 
 class McSummary(ctypes.Structure):
@@ -70,9 +70,12 @@ def source_hash():
     hdr = os.path.join(os.path.dirname(here), "include", "raftmc.h")
     if not (os.path.isdir(csrc) and os.path.exists(hdr)):
         return None
-    names = sorted(f for f in os.listdir(csrc) if f.endswith((".h", ".cpp", ".hip")))
+    names = [os.path.join("csrc", f) for f in os.listdir(csrc) if f.endswith((".h", ".cpp", ".hip"))]
+    tg = os.path.join(csrc, "tlagen")   # the front end (tlv_text.h is derived from its sources)
+    if os.path.isdir(tg):
+        names += [os.path.join("csrc", "tlagen", f) for f in os.listdir(tg) if f.endswith((".h", ".cpp")) and f != "tlv_text.h"]
     h = hashlib.sha256()
-    for f in [os.path.join("csrc", n) for n in names]:
+    for f in sorted(names):
         with open(os.path.join(here, f), "rb") as fh:
             h.update(fh.read())
     with open(hdr, "rb") as fh:
@@ -141,10 +144,12 @@ class ModelChecker:
     # sym_tlc: SYMMETRY as TLC applies it (the default, MC_COMPAT_SYM_TLC); False = the orbit mode
     def __init__(self, spec, config=None, workers=1, deadlock=True, device=0, max_depth=0,
                  fp_table_bytes=0, state_store_bytes=0, seed=0, inv_out_of_model=True, sym_tlc=True, n_gpus=1,
-                 same_device=False):
+                 same_device=False, frontend="auto"):
         """n_gpus > 1: one search over the GPUs device .. device + n_gpus - 1 (owner-partitioned
         fingerprints, one host thread per GPU inside the library, in-process RCCL); same_device: all
-        those ranks on `device` (the multi-GPU level loop on a one-GPU machine)."""
+        those ranks on `device` (the multi-GPU level loop on a one-GPU machine).  frontend: "auto"
+        (hand-compiled kernels for the two Raft families, the generated path otherwise),
+        "generated" (the SANY-subset front end for any module, or a .gen.hip source), "hand"."""
         self.lib = load_library()
         if config is None:
             config = spec[:-4] + ".cfg" if spec.endswith(".tla") else spec + ".cfg"
@@ -152,6 +157,7 @@ class ModelChecker:
         self.lib.mc_default_opts(ctypes.byref(o))
         o.device, o.workers, o.max_depth = device, workers, max_depth
         o.n_gpus, o.same_device = n_gpus, 1 if same_device else 0
+        o.frontend = {"auto": 0, "generated": 1, "hand": 2}[frontend]
         o.fp_table_bytes, o.state_store_bytes, o.seed = fp_table_bytes, state_store_bytes, seed
         o.check_deadlock = 1 if deadlock else 0
         o.tlc_compat_flags = (MC_COMPAT_INV_OUT_OF_MODEL if inv_out_of_model else 0) | (MC_COMPAT_SYM_TLC if sym_tlc else 0)

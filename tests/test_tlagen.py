@@ -1,0 +1,102 @@
+"""The SANY-subset front end (raft-tla_amd/csrc/tlagen) on the CPU:
+it parses every module of the reference, and the C++ it generates — the code the GPU path
+compiles for gfx950 — reproduces the oracle's counts when run by a plain host BFS
+(tests/native/tlagen_host_bfs.cpp): thirdparty/raft_original.tla, unmodified, through the
+generated path gives C1's and the parity configs' generated / distinct / depth / level sizes
+(tests/golden/orig_parity.json); the repo's own TokenRing.tla matches an independent Python
+restatement (tests/tlagen_models.py)."""
+import json
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+from oracle_util import CONFIGS, GOLDEN, ORIG_MC
+from tlagen_models import token_ring
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOOL = os.path.join(ROOT, "raft-tla_amd", "_build", "tlagen")
+REF = "/root/reference"
+RING = os.path.join(CONFIGS, "tlagen", "TokenRing.tla")
+
+needs_tool = pytest.mark.skipif(not os.path.exists(TOOL), reason="raft-tla_amd/_build/tlagen not built")
+needs_ref = pytest.mark.skipif(not os.path.isdir(REF), reason="the reference checkout is not present")
+
+
+def generate(spec, cfg):
+    fd, out = tempfile.mkstemp(suffix=".gen.h")
+    os.close(fd)
+    r = subprocess.run([TOOL, spec, cfg, "-I", REF, "-o", out], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return out
+
+
+def host_bfs(gen, *args):
+    exe = gen + ".bin"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-w", '-DTLG_FILE="%s"' % gen, "-o", exe,
+                    os.path.join(ROOT, "tests", "native", "tlagen_host_bfs.cpp")], check=True)
+    out = subprocess.run([exe, *args], capture_output=True, text=True, check=True).stdout
+    os.unlink(exe)
+    os.unlink(gen)
+    return json.loads(out)
+
+
+@needs_tool
+@needs_ref
+@pytest.mark.parametrize("module,defs,unparsed", [
+    ("thirdparty/raft_original.tla", 38, 0), ("thirdparty/raft_dricketts.tla", 63, 0),
+    ("thirdparty/raft_membership.tla", 46, 0), ("tlc_membership/raft.tla", 166, 1),
+    ("apalache_no_membership/raft.tla", 103, 1), ("apalache_membership_broken/raft.tla", 75, 1)])
+def test_parses_reference_modules(module, defs, unparsed):
+    """Every definition of every reference module (and the modules they EXTEND) parses; the one
+    exception is SequencesExt's Remove, a LAMBDA (outside the subset, reported, never used)."""
+    r = subprocess.run([TOOL, os.path.join(REF, module), "--parse-only"], capture_output=True, text=True)
+    summary = json.loads(r.stdout.strip().splitlines()[-1])
+    assert (summary["definitions"], summary["unparsed"]) == (defs, unparsed), r.stdout
+    if unparsed:
+        assert "SequencesExt: Remove" in r.stdout and "LAMBDA" not in "".join(
+            l for l in r.stdout.splitlines() if not l.startswith("SequencesExt: Remove"))
+
+
+@needs_tool
+@needs_ref
+@pytest.mark.parametrize("name", ["c1", "parity_single", "parity_pair", "parity_trio"])
+def test_raft_original_generated_matches_oracle(name):
+    g = json.load(open(os.path.join(GOLDEN, "orig_parity.json")))[name]
+    r = host_bfs(generate(ORIG_MC, os.path.join(CONFIGS, name + ".cfg")))
+    assert r["verdict"] == "OK" and r["err"] == 0
+    assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == (g["generated"], g["distinct"], g["depth"], g["levels"])
+    # raft_original's Next is a conjunction: TLC does not split it, so it is one action
+    assert list(r["actions"]) == ["Next"]
+
+
+@needs_tool
+def test_token_ring_matches_python_model():
+    want = token_ring()
+    r = host_bfs(generate(RING, os.path.join(CONFIGS, "tlagen", "TokenRing.cfg")))
+    assert r["verdict"] == "OK" and r["err"] == 0
+    for k in ("generated", "distinct", "depth", "levels"):
+        assert r[k] == want[k], k
+    for a, v in want["actions"].items():
+        assert r["actions"][a] == v, a
+
+
+@needs_tool
+def test_token_ring_violation_depth():
+    want = token_ring(stop_when_all_full=True)
+    r = host_bfs(generate(RING, os.path.join(CONFIGS, "tlagen", "TokenRing_full.cfg")))
+    assert (r["verdict"], r["violated"], r["depth"]) == ("INVARIANT_VIOLATION", "NotAllFull", want["depth"])
+
+
+@needs_tool
+def test_unsupported_construct_fails_loudly(tmp_path):
+    """A definition outside the subset that the cfg reaches is an error naming it (never a silent
+    fallback); an unreached one is not."""
+    (tmp_path / "Lam.tla").write_text(
+        "---- MODULE Lam ----\nEXTENDS Naturals, Sequences\nVARIABLE x\n"
+        "Keep(s) == SelectSeq(s, LAMBDA t : t > 0)\nInit == x = <<1, 2>>\nNext == x' = Keep(x)\n"
+        "Unused == SelectSeq(x, LAMBDA t : t)\n====\n")
+    (tmp_path / "Lam.cfg").write_text("INIT Init\nNEXT Next\n")
+    r = subprocess.run([TOOL, str(tmp_path / "Lam.tla"), str(tmp_path / "Lam.cfg")], capture_output=True, text=True)
+    assert r.returncode == 1 and "Keep" in r.stderr and "does not parse" in r.stderr
