@@ -231,7 +231,8 @@ struct TlagenBackend : Backend {
     release();
     // HBM layout: store words + per-state offsets/parents/actions, seen-set, lanes' arenas
     const u64 store = o.state_store_bytes ? o.state_store_bytes : (16ull << 30);
-    const u64 words_cap = store / 2 / 4, states_cap = store / 2 / 20;
+    // canonical words dominate (C2: ~350-450 words per state); 20 B per state for offsets, parents, actions
+    const u64 states_cap = store / 7 / 20, words_cap = (store - states_cap * 20) / 4;
     u64 tbytes = o.fp_table_bytes ? o.fp_table_bytes : (2ull << 30);
     u64 slots = 1; while (slots * 2 * 8 <= tbytes) slots *= 2;
     const u32 acap = 16384, hcap = 4096, evcap = 65536;

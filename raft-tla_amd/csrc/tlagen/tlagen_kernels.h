@@ -158,6 +158,7 @@ extern "C" __global__ void __launch_bounds__(64) tlg_init_k(tlk::Args a) {
   tlk::lane_init(a, A, c, em, 0);
   em.parent = ~0ull;
   tlg::init_states(c, em);
+  for (int k = 0; k < (tlg::NACT > 0 ? tlg::NACT : 1); ++k) { em.act_gen[k] = 0; em.act_dist[k] = 0; }   // initial states are no action's
   if (A.err) {
     if (A.err & tlv::E_OVF) atomicOr(&a.ctr[tlk::C_CAP], 4ull);
     else if (tlk::claim(a)) { a.ctr[tlk::C_KIND] = 3; a.ctr[tlk::C_SID] = ~0ull; a.ctr[tlk::C_INV] = A.err; }

@@ -117,8 +117,11 @@ int main(int argc, char** argv) {
     if (!next.empty()) { ++depth; levels.push_back((long long)next.size()); }
     frontier.swap(next);
   }
+  size_t nwords = 0;
+  for (auto& w : seen) nwords += w.size();
   std::printf("{\"verdict\": \"%s\", \"violated\": \"%s\", \"generated\": %lld, \"distinct\": %zu, \"depth\": %d, \"err\": %u, "
-              "\"levels\": [", verdict.c_str(), violated.c_str(), generated, seen.size(), depth, err);
+              "\"words_per_state\": %.1f, \"levels\": [", verdict.c_str(), violated.c_str(), generated, seen.size(), depth, err,
+              seen.empty() ? 0.0 : (double)nwords / seen.size());
   for (size_t q = 0; q < levels.size(); ++q) std::printf("%s%lld", q ? ", " : "", levels[q]);
   std::printf("], \"actions\": {");
   for (int k = 0; k < tlg::NACT; ++k) std::printf("%s\"%s\": [%lld, %lld]", k ? ", " : "", tlg::kActionNames[k], gen_act[k], dist_act[k]);

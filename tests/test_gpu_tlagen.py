@@ -45,7 +45,7 @@ def test_generated_c2_full_size(raftmc):
     """BASELINE configs[1] through the generated path: the oracle's full-size C2 counts."""
     o = json.load(open(os.path.join(GOLDEN, "c2_oracle.json")))
     with raftmc.ModelChecker(gen_source("c2"), os.path.join(CONFIGS, "c2.cfg"), frontend="generated", workers=0,
-                             fp_table_bytes=1 << 30, state_store_bytes=64 << 30) as mc:
+                             fp_table_bytes=1 << 30, state_store_bytes=200 << 30) as mc:
         r = mc.run()
     assert r.verdict == "OK", r.error
     assert (r.generated, r.distinct, r.depth) == (o["generated"], o["distinct"], o["depth"])
@@ -58,7 +58,7 @@ def test_generated_violation_depth(raftmc):
     the trace ends in a state with a leader."""
     g = json.load(open(os.path.join(GOLDEN, "orig_events.json")))["c2_noleader"]
     with raftmc.ModelChecker(gen_source("c2_noleader"), os.path.join(CONFIGS, "c2_noleader.cfg"), frontend="generated",
-                             workers=0, **SMALL) as mc:
+                             workers=0, fp_table_bytes=1 << 28, state_store_bytes=16 << 30) as mc:
         r = mc.run()
     assert (r.verdict, r.violated, r.depth) == ("INVARIANT_VIOLATION", "NoLeader", g["depth"])
     assert r.trace_text.count("/\\ state = ") == g["depth"]
@@ -67,7 +67,8 @@ def test_generated_violation_depth(raftmc):
 
 def test_token_ring_front_end_on_gpu(raftmc):
     """The repo's TokenRing.tla through the whole front end on the box (auto: not a hand-compiled
-    family): counts and per-action counts of the Python model."""
+    family): counts and per-action generated counts of the Python model (per-action distinct
+    counts depend on which producer reaches a state first: first-come here, as with TLC -workers N)."""
     want = token_ring()
     with raftmc.ModelChecker(RING, os.path.join(CONFIGS, "tlagen", "TokenRing.cfg"), workers=0, **SMALL) as mc:
         r = mc.run()
@@ -75,7 +76,8 @@ def test_token_ring_front_end_on_gpu(raftmc):
     assert (r.generated, r.distinct, r.depth) == (want["generated"], want["distinct"], want["depth"])
     assert [lv[0] for lv in r.levels] == want["levels"]
     for a, v in want["actions"].items():
-        assert r.actions[a] == v, a
+        assert r.actions[a][0] == v[0], a
+    assert sum(v[1] for v in r.actions.values()) == want["distinct"] - 1
 
 
 def test_token_ring_violation_trace(raftmc):
