@@ -44,6 +44,9 @@ struct Gen {
   std::map<std::string, std::string> op_fn;       // global op -> C++ function name
   std::vector<std::string> fn_protos, fn_bodies;
   std::map<std::string, int> level_memo;          // 0 pure, 1 action
+  std::map<std::string, int> free_memo;           // 1: the definition reads no state variable
+  std::map<std::string, int> cache_slot;          // state-free 0-arity definitions: c.k slot
+  std::vector<std::string> cache_init;            // their evaluation, in dependency order
   int uid = 0;
   bool init_mode = false;
 
@@ -107,6 +110,33 @@ struct Gen {
     return r;
   }
   bool is_action(const std::shared_ptr<Def>& d) { std::set<std::string> v; return d->body && is_action(d, v); }
+
+  // a definition that reads no state variable (transitively) has one value per model: it is
+  // evaluated once per lane (init_consts) instead of at every use (raft's Quorum: SUBSET Server)
+  bool reads_state(const NP& e, std::set<std::string>& visiting) {
+    if (!e) return false;
+    if (e->k == K::Prime || e->k == K::Unchanged || e->k == K::Enabled || e->k == K::Temporal) return true;
+    if (e->k == K::Ident || e->k == K::OpApp || e->k == K::Binary) {
+      if (var_idx.count(e->s)) return true;
+      auto d = global(e->s);
+      if (d && (!d->body || !state_free(d, visiting))) return true;
+    }
+    for (auto& c : e->a) if (reads_state(c, visiting)) return true;
+    for (auto& b : e->binds) if (reads_state(b.set, visiting)) return true;
+    for (auto& u : e->ups) { if (reads_state(u.rhs, visiting)) return true; for (auto& st : u.path) if (reads_state(st.idx, visiting)) return true; }
+    for (auto& d : e->defs) if (reads_state(d->body, visiting)) return true;
+    return false;
+  }
+  bool state_free(const std::shared_ptr<Def>& d, std::set<std::string>& visiting) {
+    auto it = free_memo.find(d->name);
+    if (it != free_memo.end()) return it->second != 0;
+    if (visiting.count(d->name)) return false;
+    visiting.insert(d->name);
+    const bool r = d->body && !reads_state(d->body, visiting);
+    visiting.erase(d->name);
+    free_memo[d->name] = r;
+    return r;
+  }
 
   // ---- a global operator as a C++ function (emitted once)
   std::string op_function(const std::shared_ptr<Def>& d, const Node& at) {
@@ -203,6 +233,8 @@ struct Gen {
       }
       case K::Ident: return ident(n, sc, {});
       case K::OpApp: {
+        if (n.s == "Cardinality" && n.a.size() == 1 && n.a[0]->k == K::Unary && n.a[0]->s == "DOMAIN" && !find(sc, n.s) && !global(n.s))
+          return "mk_int(A, coll_card(A, " + ex(n.a[0]->a[0], sc) + "))";
         std::vector<std::string> args;
         for (auto& a : n.a) args.push_back(ex(a, sc));
         return ident(n, sc, args);
@@ -354,6 +386,10 @@ struct Gen {
         if (r->s == "Int") return "mk_bool(" + neg + "(tg(A, " + ex(l, sc) + ") == T_INT))";
       }
       if (r->k == K::Unary && r->s == "DOMAIN") return "mk_bool(" + neg + "in_dom(A, " + ex(r->a[0], sc) + ", " + ex(l, sc) + "))";
+      if (r->k == K::Binary && r->s == "..")
+        return "[&]() -> u32 { const u32 x_ = " + ex(l, sc) + "; const i64 lo_ = ival(A, " + ex(r->a[0], sc) + "), hi_ = ival(A, " +
+               ex(r->a[1], sc) + "); if (tg(A, x_) != T_INT) return mk_bool(" + (neg.empty() ? "false" : "true") +
+               "); const i64 v_ = ival(A, x_); return mk_bool(" + neg + "(v_ >= lo_ && v_ <= hi_)); }()";
       return "mk_bool(" + neg + "set_in(A, " + ex(l, sc) + ", " + ex(r, sc) + "))";
     }
     if (op == "=>") return "mk_bool(!truth(A, " + ex(l, sc) + ") || truth(A, " + ex(r, sc) + "))";
@@ -393,6 +429,16 @@ struct Gen {
     }
     if (auto d = global(nm)) {
       if (d->params.size() != args.size()) unsup(n, "operator " + nm + " with " + std::to_string(args.size()) + " arguments");
+      std::set<std::string> v;
+      if (d->params.empty() && state_free(d, v)) {
+        auto it = cache_slot.find(nm);
+        if (it != cache_slot.end()) return "c.k[" + std::to_string(it->second) + "]";
+        const std::string fn = op_function(d, n);   // dependencies get their slots first
+        const int slot = (int)(P.constants.size() + cache_slot.size());
+        cache_slot[nm] = slot;
+        cache_init.push_back("  c.k[" + std::to_string(slot) + "] = " + fn + "(c);\n");
+        return "c.k[" + std::to_string(slot) + "]";
+      }
       std::string o = op_function(d, n) + "(c";
       for (auto& a : args) o += ", " + a;
       return o + ")";
@@ -638,12 +684,14 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
   s << "namespace tlg {\nusing namespace tlv;\n";
   s << "enum : int { NV = " << prog.variables.size() << ", NK = " << prog.constants.size() << ", NACT = " << g.actions.size()
     << ", NINV = " << cfg.invariants.size() << " };\n";
-  s << "struct Cx { Ar* A; u32 k[" << (prog.constants.empty() ? 1 : prog.constants.size()) << "]; u32 cur[" << std::max<size_t>(1, prog.variables.size())
+  s << "struct Cx { Ar* A; u32 k[" << std::max<size_t>(1, prog.constants.size() + g.cache_slot.size()) << "]; u32 cur[" << std::max<size_t>(1, prog.variables.size())
     << "]; u32 nxt[" << std::max<size_t>(1, prog.variables.size()) << "]; unsigned long long asg; int act; };\n";
   for (auto& p : g.fn_protos) s << p << "\n";
   s << "TLV_NI bool constraints(Cx& c);\nTLV_NI int invariants(Cx& c);\n";
-  s << "TLV_HD void init_consts(Cx& c) {\n  Ar& A = *c.A; (void)A;\n" << consts.str() << "}\n";
   for (auto& b : g.fn_bodies) s << b;
+  s << "TLV_HD void init_consts(Cx& c) {\n  Ar& A = *c.A; (void)A;\n" << consts.str();
+  for (auto& ci : g.cache_init) s << ci;
+  s << "}\n";
   s << "template <class EM> TLV_HD void init_states(Cx& c, EM& em) {\n  Ar& A = *c.A; (void)A;\n  c.asg = 0; c.act = 0;\n" << init_body << "}\n";
   s << "template <class EM> TLV_HD void next_states(Cx& c, EM& em) {\n  Ar& A = *c.A; (void)A;\n  c.asg = 0; c.act = " << next_label << ";\n" << next_body << "}\n";
   s << cons << invs << "}  // namespace tlg\n";

@@ -238,7 +238,9 @@ struct TlagenBackend : Backend {
     const u32 acap = 16384, hcap = 4096, evcap = 65536;
     int ncu = 256;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const u64 lanes = (u64)ncu * 4 * 64;   // 4 waves of 64 per CU
+    int waves = 8;   // per CU: 2 per SIMD (the expand kernel holds ~250 VGPRs)
+    if (const char* e = std::getenv("RAFTMC_TLAGEN_WAVES")) waves = std::max(1, std::atoi(e));
+    const u64 lanes = (u64)ncu * waves * 64;
     u64 *d_parent = nullptr, *d_table = nullptr, *d_ctr = nullptr;
     u32 *d_act = nullptr, *d_arena = nullptr, *d_hs = nullptr, *d_ev = nullptr;
     auto freeall = [&]() {

@@ -187,14 +187,24 @@ TLV_HD u32 set_card(Ar& a, u32 s) {
   if (tg(a, s) != T_SET) { a.err |= E_TYPE; return 0; }
   return count(a, s);
 }
-TLV_NI u32 set_union(Ar& a, u32 x, u32 y) {
+TLV_NI u32 set_union(Ar& a, u32 x, u32 y) {   // linear merge of two sorted sets
   if (tg(a, x) != T_SET || tg(a, y) != T_SET) { a.err |= E_TYPE; return x; }
+  if (count(a, y) == 0) return x;
+  if (count(a, x) == 0) return y;
   const u32 mark = a.htop;
-  u32 e = first(x);
-  for (u32 i = 0, n = count(a, x); i < n; ++i, e = nextv(a, e)) hpush(a, e);
-  e = first(y);
-  for (u32 i = 0, n = count(a, y); i < n; ++i, e = nextv(a, e)) hpush(a, e);
-  return set_end(a, mark);
+  u32 e = first(x), f = first(y), i = 0, j = 0;
+  const u32 n = count(a, x), m = count(a, y);
+  while (i < n || j < m) {
+    int c = i == n ? 1 : j == m ? -1 : cmpv(a, e, f);
+    if (c <= 0) { hpush(a, e); e = nextv(a, e); ++i; if (c == 0) { f = nextv(a, f); ++j; } }
+    else { hpush(a, f); f = nextv(a, f); ++j; }
+  }
+  return write_coll(a, T_SET, mark, 1, 0, false);
+}
+TLV_HD u32 coll_card(Ar& a, u32 f) {   // Cardinality(DOMAIN f) without building the domain
+  const u32 t = tg(a, f);
+  if (t != T_SEQ && t != T_FUN) { a.err |= E_TYPE; return 0; }
+  return count(a, f);
 }
 TLV_NI u32 set_filter_in(Ar& a, u32 x, u32 y, bool keep_in) {   // x \cap y (keep_in) or x \ y
   if (tg(a, x) != T_SET || tg(a, y) != T_SET) { a.err |= E_TYPE; return x; }

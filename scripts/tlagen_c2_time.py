@@ -1,0 +1,19 @@
+"""Time the generated path on full-size C2 (raft_original.tla through the SANY-subset front end,
+prebuilt source) on the GPU box; one JSON line per lane configuration."""
+import importlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+rm = importlib.import_module("raft-tla_amd")
+src = os.path.join(ROOT, "raft-tla_amd", "_build", "tlagen_co", "c2.gen.hip")
+for waves in sys.argv[1:] or ["8"]:
+    os.environ["RAFTMC_TLAGEN_WAVES"] = waves
+    with rm.ModelChecker(src, os.path.join(ROOT, "configs", "c2.cfg"), frontend="generated", workers=0,
+                         fp_table_bytes=1 << 30, state_store_bytes=200 << 30) as mc:
+        r = mc.run()
+    print(json.dumps({"workload": "C2 via the generated path", "waves_per_cu": int(waves), "verdict": r.verdict,
+                      "distinct": r.distinct, "generated": r.generated, "depth": r.depth, "run_s": round(r.seconds, 3),
+                      "kernel_s": round(r.kernel_seconds, 3), "distinct_per_s": r.distinct / r.seconds}), flush=True)
