@@ -248,7 +248,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": tj.get("hbm_bytes_per_launch") if tj else None,
                          "kernel": kname, "algo_bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_s * 1e3,
                          "pipeline_frac": res.algo_bytes / per_step / 1e9 / HBM_PEAK_GBS,
-                         "bytes": "SURVEY.md 8(d): F*S + G_in*8 + D*(16+S) of the run / launches of the dominant kernel"},
+                         "bytes": "SURVEY.md 8(d): F*S + G_in*8 + D*(16+S) of the run / launches of the dominant kernel",
+                         "timed": "HIP events around the kernel's launch pair orig_generate + orig_generate_lead (the "
+                                  "leader-work pass over the same parents): rocprofv3 lists them as two kernels whose "
+                                  "averages add up to avg_launch_ms" if kname == "orig_generate" else "HIP events around the kernel"},
             "kernels": {k: {"ms": v["ms"], "launches": v["launches"],
                             "algo_GBps": v["algo_bytes"] / max(v["ms"], 1e-9) / 1e6} for k, v in kernels.items()},
         }
