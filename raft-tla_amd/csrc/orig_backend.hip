@@ -198,6 +198,9 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
       W t;
       const int act = S::apply(s, k, t, err);
 #ifdef RMC_EXP_DOUBLE_APPLY
+#ifdef RMC_EXP_DOUBLE_HI
+      if (k >= RMC_EXP_DOUBLE_LO && k < RMC_EXP_DOUBLE_HI)   // only the instances [LO, HI)
+#endif
       {   // cost-attribution experiment: apply a second time on a laundered copy (same result)
         W s2 = s, t2;
         exp_launder<S>(s2);
