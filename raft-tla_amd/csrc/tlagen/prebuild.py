@@ -19,7 +19,10 @@ REF = os.environ.get("RAFTMC_REFERENCE", "/root/reference")
 
 SPECS = [(n, "configs/raft_original_mc.tla", "configs/%s.cfg" % n)
          for n in ("c1", "parity_single", "parity_pair", "parity_trio", "c2", "c2_noleader")]
-SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing.cfg")]
+SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing.cfg"),
+          ("toy_ring_full", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing_full.cfg"),
+          ("countdown", "configs/tlagen/Countdown.tla", "configs/tlagen/Countdown.cfg"),
+          ("countdown_evalerr", "configs/tlagen/Countdown.tla", "configs/tlagen/Countdown_evalerr.cfg")]
 
 
 def key_of(src):

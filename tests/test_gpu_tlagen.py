@@ -87,3 +87,15 @@ def test_token_ring_violation_trace(raftmc):
     assert (r.verdict, r.violated, r.depth) == ("INVARIANT_VIOLATION", "NotAllFull", want["depth"])
     last = r.trace_text.split("/\\ logs = ")[-1].splitlines()[0]
     assert last.count("val |->") == 6, last
+
+
+@pytest.mark.parametrize("cfg,verdict,depth,code", [("Countdown", "DEADLOCK", 4, 11), ("Countdown_evalerr", "EVAL_ERROR", 3, 75)])
+def test_generated_deadlock_and_eval_error(raftmc, cfg, verdict, depth, code):
+    """TLC's deadlock and evaluation-error reports from the generated kernels: verdict, TLC's exit
+    code, and the trace to the state whose successors could not be computed (or did not exist)."""
+    with raftmc.ModelChecker(os.path.join(CONFIGS, "tlagen", "Countdown.tla"), os.path.join(CONFIGS, "tlagen", cfg + ".cfg"),
+                             workers=0, **SMALL) as mc:
+        r = mc.run()
+    assert (r.verdict, r.depth, r.distinct, r.exit_code) == (verdict, depth, depth, code)
+    assert r.trace_text.count("/\\ x = ") == depth
+    assert "/\\ x = %d" % (0 if verdict == "DEADLOCK" else 1) in r.trace_text.split("State %d:" % depth)[1]

@@ -100,3 +100,12 @@ def test_unsupported_construct_fails_loudly(tmp_path):
     (tmp_path / "Lam.cfg").write_text("INIT Init\nNEXT Next\n")
     r = subprocess.run([TOOL, str(tmp_path / "Lam.tla"), str(tmp_path / "Lam.cfg")], capture_output=True, text=True)
     assert r.returncode == 1 and "Keep" in r.stderr and "does not parse" in r.stderr
+
+
+@needs_tool
+@pytest.mark.parametrize("cfg,verdict,depth", [("Countdown", "DEADLOCK", 4), ("Countdown_evalerr", "EVAL_ERROR", 3)])
+def test_countdown_verdicts(cfg, verdict, depth):
+    """TLC's other verdict classes on the generated path: a state without successors (deadlock,
+    checked by default) and a sequence read past its end while computing successors."""
+    r = host_bfs(generate(os.path.join(CONFIGS, "tlagen", "Countdown.tla"), os.path.join(CONFIGS, "tlagen", cfg + ".cfg")))
+    assert (r["verdict"], r["depth"], r["distinct"]) == (verdict, depth, depth)
