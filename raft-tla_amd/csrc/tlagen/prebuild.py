@@ -22,7 +22,9 @@ SPECS = [(n, "configs/raft_original_mc.tla", "configs/%s.cfg" % n)
 SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing.cfg"),
           ("toy_ring_full", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing_full.cfg"),
           ("countdown", "configs/tlagen/Countdown.tla", "configs/tlagen/Countdown.cfg"),
-          ("countdown_evalerr", "configs/tlagen/Countdown.tla", "configs/tlagen/Countdown_evalerr.cfg")]
+          ("countdown_evalerr", "configs/tlagen/Countdown.tla", "configs/tlagen/Countdown_evalerr.cfg"),
+          ("ricketts_c1", "configs/ricketts_mc.tla", "configs/ricketts_c1.cfg"),
+          ("ricketts_noleader", "configs/ricketts_mc.tla", "configs/ricketts_noleader.cfg")]
 
 
 def key_of(src):

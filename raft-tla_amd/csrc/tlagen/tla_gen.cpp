@@ -409,10 +409,11 @@ struct Gen {
     if (op == ":>") return "colon_gt(A, " + a + ", " + b + ")";
     if (op == "@@") return "atat(A, " + a + ", " + b + ")";
     if (op == "\\o") return "concat(A, " + a + ", " + b + ")";
-    if (auto d = global(op)) {   // user-defined infix operator
+    if (auto d = global(op)) {   // user-defined infix operator (TypedBags defines its own (+))
       const std::string fn = op_function(d, n);
       return fn + "(c, " + a + ", " + b + ")";
     }
+    if (op == "(+)" || op == "(-)") return "bag_op(A, " + a + ", " + b + ", " + (op == "(+)" ? "true" : "false") + ")";   // Bags
     unsup(n, "operator " + op);
   }
 
@@ -464,6 +465,14 @@ struct Gen {
     if (nm == "IsFiniteSet") { need(1); return "2u"; }
     if (nm == "Print" || nm == "PrintT") { return args.back(); }
     if (nm == "Assert") { need(2); return "(truth(A, " + args[0] + ") ? 2u : (A.err |= E_DOMAIN, 0u))"; }
+    // Bags
+    if (nm == "EmptyBag") { need(0); return "seq_end(A, A.htop)"; }
+    if (nm == "SetToBag") { need(1); return "set_to_bag(A, " + args[0] + ")"; }
+    if (nm == "BagToSet") { need(1); return "dom(A, " + args[0] + ")"; }
+    if (nm == "BagIn") { need(2); return "mk_bool(in_dom(A, " + args[1] + ", " + args[0] + "))"; }
+    if (nm == "CopiesIn") { need(2); return "[&]() -> u32 { const u32 o_ = lookup(A, " + args[1] + ", " + args[0] + "); return o_ ? o_ : mk_int(A, 0); }()"; }
+    if (nm == "BagCardinality") { need(1); return "mk_int(A, bag_card(A, " + args[0] + "))"; }
+    if (nm == "IsABag") { need(1); return "2u"; }
     if (nm == "BOOLEAN") { need(0); return "[&]() -> u32 { const u32 m_ = A.htop; hpush(A, 0u); hpush(A, 2u); return set_end(A, m_); }()"; }
     unsup(n, "identifier " + nm);
   }

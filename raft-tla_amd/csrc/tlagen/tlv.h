@@ -330,6 +330,52 @@ TLV_NI u32 atat(Ar& a, u32 f, u32 g) {   // f @@ g: f's pairs, then g's keys not
   push_pairs(a, g);
   return fun_end(a, mark);   // stable: f's pair wins a shared key
 }
+// ---- the standard Bags module (a bag: a function from elements to positive counts)
+TLV_NI u32 set_to_bag(Ar& a, u32 s) {   // SetToBag(S) == [e \in S |-> 1]
+  if (tg(a, s) != T_SET) { a.err |= E_TYPE; return s; }
+  const u32 mark = a.htop;
+  u32 e = first(s);
+  for (u32 i = 0, n = count(a, s); i < n; ++i, e = nextv(a, e)) { hpush(a, e); hpush(a, mk_int(a, 1)); }
+  return fun_end(a, mark);
+}
+TLV_NI u32 bag_op(Ar& a, u32 x, u32 y, bool add) {   // B1 (+) B2, B1 (-) B2 (counts <= 0 leave the domain)
+  const u32 tx = tg(a, x), ty = tg(a, y);
+  if ((tx != T_SEQ && tx != T_FUN) || (ty != T_SEQ && ty != T_FUN)) { a.err |= E_TYPE; return x; }
+  const u32 pm = a.htop;
+  push_pairs(a, x);
+  const u32 px = a.htop;
+  push_pairs(a, y);
+  const u32 py = a.htop;
+  const u32 mark = a.htop;
+  for (u32 i = pm; i < px; i += 2) {
+    const u32 k = a.hs[i];
+    i64 c = ival(a, a.hs[i + 1]);
+    const u32 o = lookup(a, y, k);
+    if (o) c += add ? ival(a, o) : -ival(a, o);
+    if (c > 0) { hpush(a, k); hpush(a, mk_int(a, c)); }
+  }
+  if (add)
+    for (u32 i = px; i < py; i += 2)
+      if (!lookup(a, x, a.hs[i])) { hpush(a, a.hs[i]); hpush(a, a.hs[i + 1]); }
+  // move the result pairs down over the operands' pairs, then build
+  u32 w = pm;
+  for (u32 i = mark; i < a.htop; ++i) a.hs[w++] = a.hs[i];
+  a.htop = w;
+  return fun_end(a, pm);
+}
+TLV_NI i64 bag_card(Ar& a, u32 b) {   // BagCardinality
+  const u32 t = tg(a, b);
+  if (t != T_SEQ && t != T_FUN) { a.err |= E_TYPE; return 0; }
+  i64 s = 0;
+  u32 e = first(b);
+  for (u32 i = 0, n = count(a, b); i < n; ++i) {
+    if (t == T_FUN) e = nextv(a, e);   // skip the key
+    s += ival(a, e);
+    e = nextv(a, e);
+  }
+  return s;
+}
+
 TLV_NI u32 append(Ar& a, u32 s, u32 e) {
   if (tg(a, s) != T_SEQ) { a.err |= E_TYPE; return s; }
   const u32 n = sz(a, s), m = sz(a, e), r = alloc(a, n + m);

@@ -99,3 +99,19 @@ def test_generated_deadlock_and_eval_error(raftmc, cfg, verdict, depth, code):
     assert (r.verdict, r.depth, r.distinct, r.exit_code) == (verdict, depth, depth, code)
     assert r.trace_text.count("/\\ x = ") == depth
     assert "/\\ x = %d" % (0 if verdict == "DEADLOCK" else 1) in r.trace_text.split("State %d:" % depth)[1]
+
+
+def test_ricketts_on_gpu(raftmc):
+    """thirdparty/raft_dricketts.tla (Bags module, TLAPS-only in the reference) through the generated
+    path to depth 12: the host build's counts (tests/test_tlagen.py, parity unpinned), and NoLeader's
+    depth."""
+    from test_tlagen import RICKETTS_D12
+    with raftmc.ModelChecker(gen_source("ricketts_c1"), os.path.join(CONFIGS, "ricketts_c1.cfg"), frontend="generated",
+                             workers=0, max_depth=12, **SMALL) as mc:
+        r = mc.run()
+    assert r.verdict == "DEPTH_LIMIT", r.error
+    assert (r.generated, r.distinct, [lv[0] for lv in r.levels]) == (RICKETTS_D12["generated"], RICKETTS_D12["distinct"], RICKETTS_D12["levels"])
+    with raftmc.ModelChecker(gen_source("ricketts_noleader"), os.path.join(CONFIGS, "ricketts_noleader.cfg"), frontend="generated",
+                             workers=0, **SMALL) as mc:
+        r = mc.run()
+    assert (r.verdict, r.violated, r.depth) == ("INVARIANT_VIOLATION", "NoLeader", 10)

@@ -109,3 +109,28 @@ def test_countdown_verdicts(cfg, verdict, depth):
     checked by default) and a sequence read past its end while computing successors."""
     r = host_bfs(generate(os.path.join(CONFIGS, "tlagen", "Countdown.tla"), os.path.join(CONFIGS, "tlagen", cfg + ".cfg")))
     assert (r["verdict"], r["depth"], r["distinct"]) == (verdict, depth, depth)
+
+
+# Ricketts' spec (thirdparty/raft_dricketts.tla, TLAPS-proved, no TLC cfg in the reference) on the
+# generated path through configs/ricketts_mc.tla: the oracle has no restatement of it, so these
+# counts are the host build's of the generated code ("parity unpinned"); the GPU test holds the
+# GPU kernels to the same numbers.
+RICKETTS_D12 = dict(generated=538450, distinct=68004, levels=[1, 3, 15, 61, 195, 483, 985, 2181, 5019, 9747, 16557, 32757])
+
+
+@needs_tool
+@needs_ref
+def test_ricketts_depth_limited():
+    r = host_bfs(generate(os.path.join(CONFIGS, "ricketts_mc.tla"), os.path.join(CONFIGS, "ricketts_c1.cfg")), "--max-depth", "12")
+    assert (r["verdict"], r["err"]) == ("DEPTH_LIMIT", 0)
+    assert {k: r[k] for k in RICKETTS_D12} == RICKETTS_D12
+    # Ricketts' Next is a disjunction: TLC splits it into its actions; inside Receive, UpdateTerm(i, j, m)
+    # is a disjunct of its own, `m.mtype = .. /\ Handle..(i, j, m)` is a conjunction (named Receive)
+    assert {"Restart", "Timeout", "RequestVote", "BecomeLeader", "Receive", "UpdateTerm", "DropMessage"} <= set(r["actions"])
+
+
+@needs_tool
+@needs_ref
+def test_ricketts_noleader():
+    r = host_bfs(generate(os.path.join(CONFIGS, "ricketts_mc.tla"), os.path.join(CONFIGS, "ricketts_noleader.cfg")))
+    assert (r["verdict"], r["violated"], r["depth"]) == ("INVARIANT_VIOLATION", "NoLeader", 10)
