@@ -68,6 +68,7 @@ struct Em {
 
   __device__ __attribute__((noinline)) void operator()(tlg::Cx& c) {
     Ar& A = *c.A;
+    if (A.err) return;   // computed after an evaluation error: not a successor (the parent reports the error)
     const u32 t0 = A.top;
     u32 n = 0;
     for (int i = 0; i < tlg::NV; ++i) n += sz(A, c.nxt[i]);
