@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <chrono>
 #include <cstdio>
@@ -208,10 +209,15 @@ struct TlagenBackend : Backend {
     size_t n = 0; hiprtcGetCodeSize(prog, &n);
     image.assign(n, '\0'); hiprtcGetCode(prog, &image[0]);
     hiprtcDestroyProgram(&prog);
-    for (auto& d : dirs) {   // best effort: keep it for the next open
+    for (auto& d : dirs) {   // best effort: keep it for the next open (written aside, then renamed)
       ::mkdir(d.c_str(), 0755);
-      std::ofstream f(d + "/" + key + ".hsaco", std::ios::binary);
-      if (f) { f.write(image.data(), (std::streamsize)image.size()); break; }
+      const std::string path = d + "/" + key + ".hsaco", tmp = path + ".tmp" + std::to_string((long)::getpid());
+      std::ofstream f(tmp, std::ios::binary);
+      if (!f) continue;
+      f.write(image.data(), (std::streamsize)image.size());
+      f.close();
+      if (f && std::rename(tmp.c_str(), path.c_str()) == 0) break;
+      std::remove(tmp.c_str());
     }
     return 0;
   }
@@ -219,15 +225,29 @@ struct TlagenBackend : Backend {
   int run(const RunOpts& o, RunResult& r, std::string& err) override {
     const auto t_start = std::chrono::steady_clock::now();
     // every count is order independent; with -workers 1 the kept parents (traces) are still first-come
+    if (!o.checkpoint_path.empty() || !o.recover_path.empty()) {
+      err = "checkpoint / recover are not implemented on the generated path";
+      return MC_E_UNSUPPORTED;
+    }
     dev = o.device;
     HIPOK(hipSetDevice(dev));
     std::string image;
     if (int rc = code_object(image, err)) return rc;
-    hipModule_t mod;
-    HIPOK(hipModuleLoadData(&mod, image.data()));
+    struct Scratch {   // everything but the store (kept for traces / dump_states) is freed on every return
+      hipModule_t mod = nullptr;
+      std::vector<void*> bufs;
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      ~Scratch() {
+        for (void* p : bufs) if (p) (void)hipFree(p);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        if (mod) (void)hipModuleUnload(mod);
+      }
+    } sc;
+    HIPOK(hipModuleLoadData(&sc.mod, image.data()));
     hipFunction_t f_init, f_expand;
-    HIPOK(hipModuleGetFunction(&f_init, mod, "tlg_init_k"));
-    HIPOK(hipModuleGetFunction(&f_expand, mod, "tlg_expand_k"));
+    HIPOK(hipModuleGetFunction(&f_init, sc.mod, "tlg_init_k"));
+    HIPOK(hipModuleGetFunction(&f_expand, sc.mod, "tlg_expand_k"));
     release();
     // HBM layout: store words + per-state offsets/parents/actions, seen-set, lanes' arenas
     const u64 store = o.state_store_bytes ? o.state_store_bytes : (16ull << 30);
@@ -243,19 +263,17 @@ struct TlagenBackend : Backend {
     const u64 lanes = (u64)ncu * waves * 64;
     u64 *d_parent = nullptr, *d_table = nullptr, *d_ctr = nullptr;
     u32 *d_act = nullptr, *d_arena = nullptr, *d_hs = nullptr, *d_ev = nullptr;
-    auto freeall = [&]() {
-      for (void* p : {(void*)d_parent, (void*)d_table, (void*)d_ctr, (void*)d_act, (void*)d_arena, (void*)d_hs, (void*)d_ev}) if (p) (void)hipFree(p);
-      (void)hipModuleUnload(mod);
-    };
     const int nact = (int)meta.actions.size();
     const size_t nctr = C_ACT + 2 * (size_t)nact + 4;   // + n_states, words_used
     if (hipMalloc(&d_words, words_cap * 4) || hipMalloc(&d_offs, states_cap * 8) || hipMalloc(&d_parent, states_cap * 8) ||
         hipMalloc(&d_act, states_cap * 4) || hipMalloc(&d_table, slots * 8) || hipMalloc(&d_ctr, nctr * 8) ||
         hipMalloc(&d_arena, lanes * acap * 4) || hipMalloc(&d_hs, lanes * hcap * 4) || hipMalloc(&d_ev, evcap * 4)) {
-      freeall(); release();
+      sc.bufs = {d_parent, d_table, d_ctr, d_act, d_arena, d_hs, d_ev};
+      release();
       err = "device allocation failed";
       return MC_E_OOM;
     }
+    sc.bufs = {d_parent, d_table, d_ctr, d_act, d_arena, d_hs, d_ev};
     HIPOK(hipMemset(d_table, 0, slots * 8));
     HIPOK(hipMemset(d_ctr, 0, nctr * 8));
     KArgs a{};
@@ -269,8 +287,8 @@ struct TlagenBackend : Backend {
     a.inv_oom = o.inv_out_of_model ? 1 : 0;
     a.deadlock = o.check_deadlock ? 1 : 0;
     std::vector<u64> h(nctr);
-    hipEvent_t e0, e1;
-    HIPOK(hipEventCreate(&e0)); HIPOK(hipEventCreate(&e1));
+    HIPOK(hipEventCreate(&sc.e0)); HIPOK(hipEventCreate(&sc.e1));
+    hipEvent_t e0 = sc.e0, e1 = sc.e1;
     auto launch = [&](hipFunction_t f, u64 blocks) -> int {
       void* params[] = {&a};
       HIPOK(hipEventRecord(e0, 0));
@@ -285,7 +303,7 @@ struct TlagenBackend : Backend {
     };
     r = RunResult();
     r.action_names = meta.actions;
-    if (int rc = launch(f_init, 1)) { freeall(); return rc; }
+    if (int rc = launch(f_init, 1)) return rc;
     u64 first = 0, count = h[nctr - 2], gen_prev = h[C_GEN];
     r.generated = (int64_t)h[C_GEN];
     if (count) { r.depth = 1; r.levels.push_back({(int64_t)count, (int64_t)h[C_GEN], 0}); }
@@ -294,7 +312,7 @@ struct TlagenBackend : Backend {
       if (o.max_depth && r.depth >= o.max_depth) { r.verdict = MC_VERDICT_DEPTH_LIMIT; r.left_on_queue = (int64_t)count; break; }
       a.first = first; a.count = count;
       r.levels.push_back({0, 0, 0});
-      if (int rc = launch(f_expand, grid)) { freeall(); return rc; }
+      if (int rc = launch(f_expand, grid)) return rc;
       ++r.n_launches;
       const u64 total = h[nctr - 2];
       const u64 fresh = total - (first + count);
@@ -339,8 +357,6 @@ struct TlagenBackend : Backend {
     }
     r.seed = a.seed;
     r.state_bytes = 0;
-    (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
-    freeall();
     r.seconds_total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
     last = r;
     return 0;
