@@ -300,6 +300,10 @@ def tlc_main(argv):
             kw["max_depth"] = int(next(it))
         elif a == "-gpus":
             kw["n_gpus"] = int(next(it))
+        elif a == "-frontend":                   # raftmc: auto (default) | generated | hand
+            kw["frontend"] = next(it)
+            if kw["frontend"] not in ("auto", "generated", "hand"):
+                raise ValueError("-frontend auto|generated|hand")
         elif a == "-symmetry":                   # raftmc: tlc (TLC's rule, default) | orbit
             v = next(it)
             if v not in ("tlc", "orbit"):
