@@ -20,7 +20,9 @@ region; each with its own barrier-bracketed max-over-ranks timing):
   scale_workload  C5v2 to depth 12 (configs/c5v2.cfg: BASELINE configs[4]'s 5-server model,
                   482M distinct states), the workload large enough for a 1/2/4/8-GPU curve
   variants        C2 with MaxMsgDomain = 6 (configs/c2_md6.cfg): AppendEntries responses and
-                  commits fire, which C2 as frozen (5 messages) never reaches
+                  commits fire, which C2 as frozen (5 messages) never reaches; at N=1 also C2
+                  through the generated path (the front end's code for the
+                  unmodified raft_original.tla, one run)
 
 The JSON line adds:
   roofline      dominant kernel (the one with the most HIP-event time): SURVEY.md
@@ -193,6 +195,22 @@ def main():
         except Exception as e:   # noqa: BLE001 - the headline stands on its own
             return {"workload": workload_name(cfg, max_depth), "error": str(e)[:300]}
 
+    def generated_c2():
+        """C2 through the generated path (the SANY-subset front end's code for the unmodified
+        thirdparty/raft_original.tla, prebuilt by build(): DESIGN.md §8), one timed run"""
+        src = os.path.join(ROOT, "raft-tla_amd", "_build", "tlagen_co", "c2.gen.hip")
+        try:
+            with mod.ModelChecker(src, os.path.join(ROOT, "configs", "c2.cfg"), frontend="generated", workers=0, device=local,
+                                  fp_table_bytes=1 << 30, state_store_bytes=200 << 30) as mc:
+                t0 = time.perf_counter()
+                r = mc.run()
+                t = time.perf_counter() - t0
+            return {"workload": "C2 via the generated path (front end + generic kernels)", "value": r.distinct / t,
+                    "unit": "distinct states/s", "ms_per_step": t * 1e3, "steps": 1, "distinct_per_run": r.distinct,
+                    "generated_per_run": r.generated, "depth": r.depth, "verdict": r.verdict}
+        except Exception as e:   # noqa: BLE001
+            return {"workload": "C2 via the generated path", "error": str(e)[:300]}
+
     extra = {}
     if not args.no_extra:
         # C5v2 to depth 12: 482M states of 160 B + 8 B parent pointers = 81 GB, and the host spill's
@@ -200,6 +218,8 @@ def main():
         # completed levels to host memory every run, 1.04 s instead of 0.23 s)
         extra["scale_workload"] = side(os.path.join(ROOT, "configs", "c5v2.cfg"), 12, 128, 16, 2)
         extra["variants"] = {"c2_md6": side(os.path.join(ROOT, "configs", "c2_md6.cfg"), 0, 64, 8, 2)}
+        if world == 1:
+            extra["variants"]["c2_generated"] = generated_c2()
 
     if rank == 0:
         total_distinct = float(res.distinct)    # the sharded result is global (every rank reports the model's counts)
