@@ -59,9 +59,14 @@ def one(spec):
 
 def main():
     os.makedirs(OUT, exist_ok=True)
+    keys = set()
     with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
         for name, res in ex.map(one, SPECS):
             print("tlagen prebuild %s: %s" % (name, res))
+            keys.add(res)
+    for f in os.listdir(OUT):   # code objects of sources no longer generated (they travel to the GPU box)
+        if f.endswith(".hsaco") and f[:-6] not in keys:
+            os.remove(os.path.join(OUT, f))
 
 
 if __name__ == "__main__":
