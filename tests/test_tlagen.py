@@ -134,3 +134,25 @@ def test_ricketts_depth_limited():
 def test_ricketts_noleader():
     r = host_bfs(generate(os.path.join(CONFIGS, "ricketts_mc.tla"), os.path.join(CONFIGS, "ricketts_noleader.cfg")))
     assert (r["verdict"], r["violated"], r["depth"]) == ("INVARIANT_VIOLATION", "NoLeader", 10)
+
+
+@needs_tool
+def test_generated_source_is_deterministic():
+    """The code-object cache is keyed by the generated source: generating twice gives the same text,
+    and the build's prebuilt TokenRing code object is the one the library looks up (the GPU box runs
+    the front end on TokenRing.tla itself and must hit it)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("prebuild", os.path.join(ROOT, "raft-tla_amd", "csrc", "tlagen", "prebuild.py"))
+    pb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(pb)
+    outs = []
+    for _ in range(2):
+        fd, out = tempfile.mkstemp(suffix=".gen.hip")
+        os.close(fd)
+        subprocess.run([TOOL, RING, os.path.join(CONFIGS, "tlagen", "TokenRing.cfg"), "--kernels", "-o", out], check=True)
+        outs.append(open(out).read())
+        os.unlink(out)
+    assert outs[0] == outs[1]
+    co = os.path.join(pb.OUT, pb.key_of(outs[0]) + ".hsaco")
+    if os.path.isdir(pb.OUT):
+        assert os.path.exists(co), co
