@@ -154,7 +154,14 @@ struct FifoShardLoop {
       if (int e = be.shard_level_stats(st, err)) return e;
       int64_t news[8];
       if (int e = allgather(st[0], news, err)) return e;
+      const int64_t my_flags = st[3];
       if (int e = allreduce(st, NST, flag_max, err)) return e;
+      if (st[3]) {   // some rank raised an error: the bitwise OR of every rank's flags, not the max
+        int64_t fl[8];
+        if (int e = allgather(my_flags, fl, err)) return e;
+        st[3] = 0;
+        for (int r = 0; r < W; ++r) st[3] |= fl[r];
+      }
       if (st[4]) {   // the level's first event in key order stops the search
         int64_t ev[NST];
         if (int e = be.shard_event_stats(st, ev, err)) return e;

@@ -230,6 +230,20 @@ int run_multi(mc_ctx* c) {
   rmc::LoopbackWorld world(W);
   std::vector<int> rcs(W, MC_OK);
   std::vector<std::string> errs(W);
+  // A rank that leaves the loop early (shard_open failed, a rank-local capacity error, a transfer
+  // error) must not leave its peers blocked in the next collective: the loopback world releases
+  // every rendezvous, and on RCCL every local communicator is aborted (ncclCommAbort stops the
+  // peers' pending send/recv/all-reduce kernels; an aborted communicator is never reused).
+  std::mutex abort_mu;
+  bool comms_aborted = false;
+  auto abort_all = [&]() {
+    world.abort();
+    if (!use_rccl) return;
+    std::lock_guard<std::mutex> lk(abort_mu);
+    if (comms_aborted) return;
+    comms_aborted = true;
+    for (ncclComm_t x : c->local_comms) if (x) (void)rmc::rccl().CommAbort(x);
+  };
   auto rank_main = [&](int r) {
     rmc::Backend* be = c->rank_backend(r);
     rmc::RunOpts o = c->ro;
@@ -240,15 +254,19 @@ int run_multi(mc_ctx* c) {
       if (use_rccl) { rmc::RcclTransport t(c->local_comms[r]); rc = be->shard_run_native(t, e); }
       else { rmc::LoopbackTransport t(world, r); rc = be->shard_run_native(t, e); }
     }
-    if (rc) world.abort();
+    if (rc) abort_all();
     rcs[r] = rc; errs[r] = e;
   };
   std::vector<std::thread> th;
   for (int r = 1; r < W; ++r) th.emplace_back(rank_main, r);
   rank_main(0);
   for (auto& x : th) x.join();
-  for (int r = 0; r < W; ++r)
-    if (rcs[r]) { c->last_error = "rank " + std::to_string(r) + ": " + errs[r]; return rcs[r]; }
+  if (comms_aborted) c->local_comms.clear();   // aborted: the next run builds fresh communicators
+  // report the rank that failed first in its own right (not a peer released by the abort)
+  for (int pass = 0; pass < 2; ++pass)
+    for (int r = 0; r < W; ++r)
+      if (rcs[r] && (pass == 1 || errs[r].find("another rank left") == std::string::npos))
+        { c->last_error = "rank " + std::to_string(r) + ": " + errs[r]; return rcs[r]; }
   c->res = *c->be->shard_result();                 // every rank holds the global counts
   for (int r = 0; r < W && c->res.violated.empty(); ++r) c->res.violated = c->rank_backend(r)->shard_result()->violated;
   // the counterexample: the lowest rank holding the stop's head, then the parent chain by owner
@@ -409,6 +427,14 @@ int mc_dump_states(const mc_ctx* c, const char* path) {
   if (!c || !path) return MC_E_INVALID;
   if (!c->ran) return MC_E_STATE;
   std::string err;
+  if (c->n_gpus > 1) {
+    // every rank's partition of the state space: one file per rank, path.rank<r> (as shard.py writes)
+    for (int r = 0; r < c->n_gpus; ++r) {
+      const int rc = const_cast<mc_ctx*>(c)->rank_backend(r)->dump_states(std::string(path) + ".rank" + std::to_string(r), err);
+      if (rc) { const_cast<mc_ctx*>(c)->last_error = "rank " + std::to_string(r) + ": " + err; return rc; }
+    }
+    return MC_OK;
+  }
   int rc = c->be->dump_states(path, err);
   if (rc) const_cast<mc_ctx*>(c)->last_error = err;
   return rc;

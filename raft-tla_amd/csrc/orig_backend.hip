@@ -2243,16 +2243,22 @@ class OrigGpu : public Backend {
     sres_.kernels[k].launches++;                                               \
   } while (0)
     auto allreduce_level = [&](int64_t* g, int64_t next_chunks, int64_t& chunks_out) -> int {
-      // g: local stats in, global stats out; MAX slots: [3,6) flags, [6] chunk rounds of the next level
+      // g: local stats in, global stats out; MAX slots: [3,6) flags, [6] chunk rounds of the next
+      // level, [8, 8+32) one slot per bit of the error word (max per bit = bitwise OR over ranks:
+      // two ranks' different capacity errors are both reported)
+      static_assert(8 + 32 <= MC_SHARD_NSTAT, "max slots");
       for (int k = 0; k < MC_SHARD_NSTAT; ++k) h_sum[k] = g[k];
       for (int k = 0; k < MC_SHARD_NSTAT; ++k) h_max[k] = 0;
       h_max[3] = g[3]; h_max[4] = g[4]; h_max[5] = g[5]; h_max[6] = next_chunks;
+      for (int b = 0; b < 32; ++b) h_max[8 + b] = (g[3] >> b) & 1;
       HIPCHK(hipMemcpyAsync(d_sum, h_sum, 2 * MC_SHARD_NSTAT * 8, hipMemcpyHostToDevice, stream_));
-      if (W > 1 && T.allreduce(d_sum, MC_SHARD_NSTAT, d_max, 8, stream_, err)) return MC_E_NO_DEVICE;
+      if (W > 1 && T.allreduce(d_sum, MC_SHARD_NSTAT, d_max, 8 + 32, stream_, err)) return MC_E_NO_DEVICE;
       HIPCHK(hipMemcpyAsync(h_sum, d_sum, 2 * MC_SHARD_NSTAT * 8, hipMemcpyDeviceToHost, stream_));
       HIPCHK(hipStreamSynchronize(stream_));
       for (int k = 0; k < MC_SHARD_NSTAT; ++k) g[k] = h_sum[k];
-      g[3] = h_max[3]; g[4] = h_max[4]; g[5] = h_max[5];
+      g[3] = 0;
+      for (int b = 0; b < 32; ++b) g[3] |= (h_max[8 + b] ? 1ll : 0ll) << b;
+      g[4] = h_max[4]; g[5] = h_max[5];
       chunks_out = h_max[6];
       return 0;
     };

@@ -17,6 +17,7 @@ struct RcclApi {
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;   // one process, one rank per device
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;     // releases peers blocked in this comm's kernels
   ncclResult_t (*GroupStart)() = nullptr;
   ncclResult_t (*GroupEnd)() = nullptr;
   ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
@@ -38,6 +39,7 @@ struct RcclApi {
     RMC_SYM(CommInitRank, "ncclCommInitRank");
     RMC_SYM(CommInitAll, "ncclCommInitAll");
     RMC_SYM(CommDestroy, "ncclCommDestroy");
+    RMC_SYM(CommAbort, "ncclCommAbort");
     RMC_SYM(GroupStart, "ncclGroupStart");
     RMC_SYM(GroupEnd, "ncclGroupEnd");
     RMC_SYM(Send, "ncclSend");

@@ -652,6 +652,8 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
   if (!cfg.symmetry.empty() || !cfg.view.empty())
     throw CfgError(MC_E_UNSUPPORTED, "SYMMETRY / VIEW on the generated path (the hand-compiled tlc_membership path has them)");
   if (!cfg.action_constraints.empty()) throw CfgError(MC_E_UNSUPPORTED, "ACTION_CONSTRAINTS on the generated path");
+  // a model with temporal properties must not report "No error has been found" without checking them
+  if (!cfg.properties.empty()) throw CfgError(MC_E_UNSUPPORTED, "temporal PROPERTIES are not supported");
   std::ostringstream consts;
   for (size_t i = 0; i < prog.constants.size(); ++i) {
     const std::string& c = prog.constants[i];

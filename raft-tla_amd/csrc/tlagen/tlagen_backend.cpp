@@ -37,7 +37,7 @@ enum { C_GEN = 0, C_GIN = 1, C_ERR = 2, C_CAP = 3, C_FLAG = 4, C_KIND = 5, C_SID
 struct KArgs {   // tlk::Args, field for field
   u32* words; u64* words_used; u64 words_cap;
   u64* offs; u64* parent; u32* act; u64 states_cap;
-  u64* n_states;
+  u64* n_states; u64* n_committed;
   u64* table; u64 table_mask;
   u32* arena; u32 acap;
   u32* hstack; u32 hcap;
@@ -144,6 +144,7 @@ struct TlagenBackend : Backend {
   RunResult last;
   // device state kept after run() for dump_states / traces
   u32* d_words = nullptr; u64* d_offs = nullptr; u64 n_stored = 0, words_stored = 0;
+  bool store_complete = true;   // false after a store overflow (ids handed out without words)
   int dev = 0;
 
   TlagenBackend(const std::string& tla_path, const CfgFile& cfg) {
@@ -280,6 +281,7 @@ struct TlagenBackend : Backend {
     a.words = d_words; a.words_used = d_ctr + nctr - 1; a.words_cap = words_cap;
     a.offs = d_offs; a.parent = d_parent; a.act = d_act; a.states_cap = states_cap;
     a.n_states = d_ctr + nctr - 2;
+    a.n_committed = d_ctr + nctr - 3;
     a.table = d_table; a.table_mask = slots - 1;
     a.arena = d_arena; a.acap = acap; a.hstack = d_hs; a.hcap = hcap;
     a.ctr = d_ctr; a.evbuf = d_ev; a.evcap = evcap;
@@ -322,7 +324,10 @@ struct TlagenBackend : Backend {
       first += count; count = fresh;
       if (fresh) ++r.depth; else r.levels.pop_back();
     }
-    n_stored = std::min<u64>(h[nctr - 2], states_cap);
+    // on a store overflow some ids were handed out without their words: only the committed states
+    // are stored (and ids are no longer dense, so traces and dumps are refused below)
+    store_complete = h[nctr - 3] == h[nctr - 2];
+    n_stored = store_complete ? h[nctr - 2] : h[nctr - 3];
     words_stored = std::min<u64>(h[nctr - 1], words_cap);
     r.generated = (int64_t)h[C_GEN];
     r.generated_in_model = (int64_t)h[C_GIN];
@@ -384,6 +389,7 @@ struct TlagenBackend : Backend {
 
   int dump_states(const std::string& path, std::string& err) override {
     if (!d_words) { err = "no run"; return MC_E_STATE; }
+    if (!store_complete) { err = "the state store overflowed: the stored states are incomplete"; return MC_E_STATE; }
     std::vector<u32> w(words_stored);
     std::vector<u64> off(n_stored);
     HIPOK(hipMemcpy(w.data(), d_words, w.size() * 4, hipMemcpyDeviceToHost));

@@ -43,7 +43,8 @@ struct Args {
   unsigned long long* parent;       // per state id: parent id (~0 for initial states)
   u32* act;                         // per state id: action that produced it
   unsigned long long states_cap;
-  unsigned long long* n_states;
+  unsigned long long* n_states;     // state ids handed out (may pass states_cap on overflow)
+  unsigned long long* n_committed;  // states whose words, offset, parent and action were written
   unsigned long long* table;        // seen-set of fingerprints (0 = empty)
   unsigned long long table_mask;
   u32* arena;                       // per lane: acap words
@@ -112,6 +113,7 @@ struct Em {
           a->offs[sid] = wp;
           a->parent[sid] = parent;
           a->act[sid] = (u32)c.act;
+          atomicAdd(a->n_committed, 1ull);
           const int bad = tlg::invariants(d);
           if (bad >= 0 && claim(*a)) {
             a->ctr[C_KIND] = 1; a->ctr[C_SID] = sid; a->ctr[C_INV] = (unsigned long long)bad;

@@ -202,7 +202,15 @@ class Exchanger:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
         t[FLAG_SLICE] = m
-        return t.tolist()
+        out = t.tolist()
+        if out[FLAG_SLICE.start]:
+            # error flags are a bit set: report the OR over ranks, not the largest word
+            # (every rank sees the same max, so every rank takes this extra all-gather)
+            acc = 0
+            for f in self.allgather(st[FLAG_SLICE.start]):
+                acc |= f
+            out[FLAG_SLICE.start] = acc
+        return out
 
     def allreduce_sum(self, st):
         if self.world == 1:

@@ -103,6 +103,16 @@ def test_unsupported_construct_fails_loudly(tmp_path):
 
 
 @needs_tool
+def test_temporal_properties_refused(tmp_path):
+    """A cfg with PROPERTY/PROPERTIES is refused on the generated path (as on the hand-compiled
+    ones): the search checks safety only and must not report a liveness property as checked."""
+    cfg = open(os.path.join(CONFIGS, "tlagen", "TokenRing.cfg")).read() + "\nPROPERTY Liveness\n"
+    (tmp_path / "ring.cfg").write_text(cfg)
+    r = subprocess.run([TOOL, RING, str(tmp_path / "ring.cfg")], capture_output=True, text=True)
+    assert r.returncode != 0 and "PROPERTIES" in r.stderr, (r.returncode, r.stderr)
+
+
+@needs_tool
 @pytest.mark.parametrize("cfg,verdict,depth", [("Countdown", "DEADLOCK", 4), ("Countdown_evalerr", "EVAL_ERROR", 3)])
 def test_countdown_verdicts(cfg, verdict, depth):
     """TLC's other verdict classes on the generated path: a state without successors (deadlock,
