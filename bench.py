@@ -36,7 +36,9 @@ The JSON line adds:
                 figures only when the summary names the same kernel AND workload; pipeline_frac =
                 the same bytes over the whole step time (every kernel and the host between them)
   dedup_set     the BASELINE metric's second half: dedup-set GB/s (G_in*8 + D*16) / (merge +
-                probe kernel time) and seen-set probes/s (G_in / that time)
+                probe kernel time), seen-set probes/s (the device's probe count / that time:
+                successors the same workgroup produced twice probe once) and the transaction-level
+                figure (probes * 64 B / that time, against the 8 TB/s peak)
   cpu_baseline  the builder's multithreaded C++ CPU BFS (oracle/cpu_bfs.cpp: TLC-style workers, a
                 lock-free fingerprint set, the product's packed successor function and invariants;
                 "port") with threads = the host cores of this job, on the whole C2 (bounded by
@@ -278,9 +280,17 @@ def main():
         if fifo is not None:
             line["tlc_workers_1"] = fifo
         if ded_s > 0:
+            # probes: the device's count of fingerprints that reached the seen-set (a successor that the
+            # same 256 parents produced before is filtered in LDS and never probes); the transaction-level
+            # figure prices each probe at one 64-B HBM line (8 TB/s / 64 B = 125 G/s)
+            probes = res.seen_set_probes
             line["dedup_set"] = {"GBps": (res.generated_in_model * 8 + res.distinct * 16) / ded_s / 1e9,
-                                 "probes_per_s": res.generated_in_model / ded_s, "ms": ded_s * 1e3,
-                                 "bytes": "G_in*8 + D*16 (SURVEY.md 8(d) dedup-set metric) / (merge + probe kernel time)"}
+                                 "probes_per_s": probes / ded_s, "probes_per_run": probes,
+                                 "successors_per_s": res.generated_in_model / ded_s,
+                                 "transaction_GBps": probes * 64 / ded_s / 1e9,
+                                 "transaction_frac": probes * 64 / ded_s / 1e9 / HBM_PEAK_GBS, "ms": ded_s * 1e3,
+                                 "bytes": "G_in*8 + D*16 (SURVEY.md 8(d) dedup-set metric) / (merge + probe kernel time); "
+                                          "transaction: probes * 64 B / the same time"}
         # VALU issue fraction of the dominant kernel: PMC instruction count per launch from profiles/, live
         # launch time; MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 VALU instruction issues in 2 cycles
         vj = pmc_summary(args.valu_json)

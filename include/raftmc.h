@@ -125,6 +125,8 @@ typedef struct mc_summary_t {
   int32_t n_launches;          /* expand-kernel launches (BFS levels expanded)          */
   char violated[64];          /* property name for INVARIANT_VIOLATION                     */
   char spec[32];              /* "raft_original" | "tlc_membership"                        */
+  int64_t seen_set_probes;    /* fingerprints that probed the seen-set (device counter; the
+                                 successors a workgroup's parents produce twice probe once)   */
 } mc_summary_t;
 
 /* Fill opts with defaults. */

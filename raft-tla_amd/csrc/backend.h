@@ -50,6 +50,7 @@ struct RunResult {
   // algorithmic byte accounting of the expand kernel
   double algo_bytes = 0;                 // F*S + G_in*8 + D*(8+8+S) summed over levels
   int64_t generated_in_model = 0;
+  int64_t seen_set_probes = 0;           // fingerprints that probed the seen-set (after workgroup-local dedup)
   int state_bytes = 0;
   int n_launches = 0;
   std::vector<KernelStat> kernels;       // per-kernel HIP-event time and algorithmic bytes

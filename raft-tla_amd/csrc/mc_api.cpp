@@ -318,6 +318,7 @@ int mc_summary(const mc_ctx* c, mc_summary_t* s) {
   s->seconds_total = r.seconds_total; s->seconds_kernels = r.seconds_kernels; s->fp_seed = r.seed;
   s->algo_bytes = r.algo_bytes; s->generated_in_model = r.generated_in_model; s->state_bytes = r.state_bytes;
   s->n_launches = r.n_launches;
+  s->seen_set_probes = r.seen_set_probes;
   std::snprintf(s->violated, sizeof s->violated, "%s", r.violated.c_str());
   std::snprintf(s->spec, sizeof s->spec, "%s", c->be->family().c_str());
   return MC_OK;

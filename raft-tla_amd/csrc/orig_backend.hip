@@ -61,6 +61,7 @@ namespace rmc {
 enum {
   K_NEW = 0, K_GEN_IN = 1, K_ERR = 2, K_EVENT = 3, K_ERRGID = 4, K_INS = 5, K_CHUNK_NEW = 6, K_LEVEL_NEW = 7,
   K_ACT = 8, K_PROF = K_ACT + 2 * OA_NACT,   // K_PROF: phase timers (RAFTMC_PROF, slots 0..5)
+  K_PROBES = K_PROF + 6,                       // seen-set probes issued (fingerprints that reached the table)
   K_LEAD = K_PROF + 7,                         // the chunk's leader-work parents (orig_generate_lead)
   K_NCTR = K_PROF + 8
 };
@@ -592,6 +593,7 @@ __global__ void __launch_bounds__(BS) orig_probe(DedupArgs a) {
   const ulonglong2* in = a.urec + (u64)blockIdx.x * a.region;
   u32 err = 0;
   const u64 t0 = a.prof ? wall_clock64() : 0;
+  if (threadIdx.x == 0 && n) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)n);
 #pragma unroll 1
   for (u32 i0 = 0; i0 < n; i0 += DEDUP_PER * BS) {
     u64 fp[DEDUP_PER], nk[DEDUP_PER], pos[DEDUP_PER];
@@ -699,6 +701,7 @@ __global__ void __launch_bounds__(BS) orig_probe_plain(DedupArgs a) {
   const ulonglong2* in = a.urec + (u64)blockIdx.x * a.region;
   const u64 pgid0 = a.gid0 + (u64)blockIdx.x * BS;   // global id of this workgroup's first parent
   u32 err = 0;
+  if (threadIdx.x == 0 && n) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)n);
 #pragma unroll 1
   for (u32 i0 = 0; i0 < n; i0 += DEDUP_PER * BS) {
     u64 fp[DEDUP_PER], key[DEDUP_PER], pos[DEDUP_PER];
@@ -757,6 +760,7 @@ __global__ void __launch_bounds__(BS) orig_dedup_plain(DedupArgs a) {
   const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
   const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
   u32 err = 0;
+  u64 probes = 0;   // wave-uniform
 #pragma unroll 1
   for (u32 i0 = 0; i0 < n; i0 += DEDUP_PER * BS) {
     u64 fp[DEDUP_PER], key[DEDUP_PER], pos[DEDUP_PER];
@@ -768,13 +772,109 @@ __global__ void __launch_bounds__(BS) orig_dedup_plain(DedupArgs a) {
       key[j] = i < n ? (u64)keys[at] : 0ull;     // local key lane << 8 | instance
     }
 #pragma unroll
-    for (int j = 0; j < DEDUP_PER; ++j)
+    for (int j = 0; j < DEDUP_PER; ++j) {
       if (fp[j] && !lds_first(lfp, fp[j])) fp[j] = 0ull;   // produced by this workgroup's parents before
+      probes += (u64)__popcll(__ballot(fp[j] != 0ull));
+    }
     const u32 ins = probe_batch<DEDUP_PER, false, 1>(a.table, a.table_mask, fp, key, pos, err);
 #pragma unroll
     for (int j = 0; j < DEDUP_PER; ++j)
       if ((ins >> j) & 1u) atomicOr(&win[(key[j] >> 8) * WW + ((key[j] & 255) >> 6)], 1ull << (key[j] & 63));
   }
+  if (__lane_id() == 0 && probes) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)probes);
+  __syncthreads();
+  u64 wm[WW];
+  u32 mine = 0;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) { wm[q] = win[threadIdx.x * WW + q]; mine += (u32)__popcll(wm[q]); }
+  u32 total = 0;
+  const u32 off = block_excl_scan(mine, wave_tot, &total);
+  if (threadIdx.x == 0) base_sh = total ? atomicAdd(&a.ctr[K_CHUNK_NEW], (unsigned long long)total) : 0ull;
+  __syncthreads();
+  u64 o = base_sh + off;
+  const u64 pg = a.gid0 + (u64)blockIdx.x * BS + threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) {
+    u64 m = wm[q];
+    while (m) {
+      const int k = q * 64 + __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      a.newpos[o++] = (pg << 8) | (u64)k;
+    }
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+}
+
+// The same, with full probe lanes: about half of the records repeat a successor of the same 256
+// parents, so probing straight after the LDS filter leaves half of every probe batch empty (the
+// probes in flight per thread that hide the HBM latency are really ~4 of 8).  Here each wave
+// pushes its filter survivors into its own LDS queue (ballot + mbcnt, no atomics) and probes only
+// full batches of 64 * DEDUP_PER fingerprints; the partial rest goes out at the end.  The wave's
+// actual probes are counted into ctr[K_PROBES] (the probes/s the bench reports).
+constexpr int DQ_P = 4;                                  // records loaded per lane per round
+constexpr int DQ_CAP = 64 * (DEDUP_PER + DQ_P);          // per-wave queue entries
+template <int WW>
+__global__ void __launch_bounds__(BS) orig_dedup_queue(DedupArgs a) {
+  __shared__ unsigned long long lfp[LDS_FP_SLOTS];
+  __shared__ u32 wave_tot[BS / 64];
+  __shared__ unsigned long long base_sh;
+  __shared__ unsigned long long win[BS * WW];
+  __shared__ unsigned long long qfp[BS / 64][DQ_CAP];
+  __shared__ unsigned short qkey[BS / 64][DQ_CAP];
+  for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lfp[t] = 0ull;
+  for (int t = threadIdx.x; t < BS * WW; t += BS) win[t] = 0ull;
+  __syncthreads();
+  const WaveRegions wr(a.rcnt + 4 * blockIdx.x, a.region / 4);
+  const u32 n = wr.n;
+  const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
+  const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
+  const int lane = __lane_id(), wv = threadIdx.x >> 6;
+  unsigned long long* qf = qfp[wv];
+  unsigned short* qk = qkey[wv];
+  u32 qn = 0;            // wave-uniform queue length
+  u64 probes = 0;        // wave-uniform
+  u32 err = 0;
+  // probe the top `take` (<= 64 * DEDUP_PER) queue entries, DEDUP_PER per lane
+  auto drain = [&](u32 take) {
+    u64 fp[DEDUP_PER], key[DEDUP_PER], pos[DEDUP_PER];
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j) {
+      const u32 q = (u32)j * 64 + (u32)lane;
+      fp[j] = q < take ? (u64)qf[qn - take + q] : 0ull;
+      key[j] = q < take ? (u64)qk[qn - take + q] : 0ull;
+    }
+    const u32 ins = probe_batch<DEDUP_PER, false, 1>(a.table, a.table_mask, fp, key, pos, err);
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j)
+      if ((ins >> j) & 1u) atomicOr(&win[(key[j] >> 8) * WW + ((key[j] & 255) >> 6)], 1ull << (key[j] & 63));
+    probes += take;
+    qn -= take;
+    __builtin_amdgcn_wave_barrier();   // the next pushes reuse these queue entries
+  };
+#pragma unroll 1
+  for (u32 i0 = 0; i0 < n; i0 += DQ_P * BS) {
+#pragma unroll
+    for (int j = 0; j < DQ_P; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      const u64 at = wr.at(i);
+      const u64 fp = i < n ? fps[at] : 0ull;
+      const unsigned short k = i < n ? keys[at] : (unsigned short)0;
+      const bool keep = fp && lds_first(lfp, fp);   // else produced by this workgroup's parents before
+      const u64 m = __ballot(keep);
+      if (keep) {
+        const u32 slot = qn + (u32)__popcll(m & ((1ull << lane) - 1ull));
+        qf[slot] = (unsigned long long)fp;
+        qk[slot] = k;
+      }
+      qn += (u32)__popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();   // the queue writes of every lane before the reads below
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    while (qn >= 64u * DEDUP_PER) drain(64u * DEDUP_PER);
+  }
+  if (qn) drain(qn);
+  if (lane == 0 && probes) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)probes);
   __syncthreads();
   u64 wm[WW];
   u32 mine = 0;
@@ -1532,8 +1632,10 @@ class OrigGpu : public Backend {
             hipLaunchKernelGGL(orig_merge_plain, dim3(nblk), dim3(BS), 0, stream_, d);
             HIPCHK(hipGetLastError());
             hipLaunchKernelGGL((orig_probe_plain<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
-          } else {
+          } else if (dedup_nocompact_) {
             hipLaunchKernelGGL((orig_dedup_plain<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
+          } else {
+            hipLaunchKernelGGL((orig_dedup_queue<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
           }
         }
         HIPCHK(hipGetLastError());
@@ -1644,8 +1746,11 @@ class OrigGpu : public Backend {
           os << " state store full (raise state_store_bytes): " << cap_ << " state slots, " << base_
              << " states on the host, level ends at " << level_end << ", " << nnew << " new;";
         if (e & OE_TABLE_FULL) os << " fingerprint table full (raise fp_table_bytes);";
+        // the summary counts the completed levels (their sizes sum to it, and the depth is theirs);
+        // whatever part of the interrupted level reached the store is not a level of the search
+        os << " the summary counts the " << level_end << " states of the " << r.depth << " completed levels;";
         r.error = os.str();
-        total_ = std::min<u64>(next_write, base_ + cap_);
+        total_ = level_end;
         r.distinct = (int64_t)total_;
         break;
       }
@@ -1653,6 +1758,7 @@ class OrigGpu : public Backend {
       for (int k = 0; k < OA_NACT; ++k) { r.act_generated[k] += (int64_t)c[K_ACT + k]; r.act_distinct[k] += (int64_t)c[K_ACT + OA_NACT + k]; gen += (int64_t)c[K_ACT + k]; }
       r.generated += gen;
       r.generated_in_model += (int64_t)G_in;
+      r.seen_set_probes += (int64_t)c[K_PROBES];
       r.algo_bytes += (double)level_count * S_B + (double)G_in * 8 + (double)nnew * (16 + S_B);
       total_ += nnew;
       r.distinct = (int64_t)total_;
@@ -2412,8 +2518,9 @@ class OrigGpu : public Backend {
   u64 fill_counts_route_[8] = {0};
   u64 sviol_parent_ = 0; u32 sviol_bad_ = 0; std::string sviol_act_, sviol_text_;
   u64 sh_event_ = ~0ull;
-  bool last_fifo_ = true;
-  const bool split_plain_ = std::getenv("RAFTMC_SPLIT_PLAIN") != nullptr;   // experiment: merge + probe kernels   // seen-set layout of the last single-GPU run (16-B keyed / 8-B entries)
+  bool last_fifo_ = true;   // seen-set layout of the last single-GPU run (16-B keyed / 8-B entries)
+  const bool split_plain_ = std::getenv("RAFTMC_SPLIT_PLAIN") != nullptr;          // experiment: merge + probe kernels
+  const bool dedup_nocompact_ = std::getenv("RAFTMC_DEDUP_NOCOMPACT") != nullptr;  // experiment: probe right after the filter
   // RAFTMC_PROF=1: per-phase wall-clock ticks (100 MHz) of orig_dedup, summed over workgroups
   const bool prof_ = std::getenv("RAFTMC_PROF") != nullptr;
   const bool progress_ = std::getenv("RAFTMC_PROGRESS") != nullptr;

@@ -15,8 +15,8 @@ namespace tlagen {
 namespace {
 
 struct Sym {
-  enum Kind { Val, LetOp } kind = Val;
-  std::string cxx;                 // Val: handle expression; LetOp: lambda name
+  enum Kind { Val, LetOp, RecFn } kind = Val;
+  std::string cxx;                 // Val: handle expression; LetOp: lambda name; RecFn: how to call it (see rec_call)
   std::shared_ptr<Def> def;        // LetOp
   std::shared_ptr<std::vector<std::pair<std::string, Sym>>> scope;   // LetOp: scope at its definition
 };
@@ -163,10 +163,75 @@ struct Gen {
     return fn;
   }
 
+  // ---- recursive function definitions  f[x \in S] == e  whose body applies f (TypedBags' Sum:
+  // LET DSum[S \in SUBSET DOMAIN f] == .. DSum[S \ {elt}] ..).  TLC evaluates them lazily, one
+  // application at a time (never the whole function over S); so does the generated code: the
+  // definition becomes a recursive C++ function of the argument, which checks that the argument
+  // lies in the domain (TLC's error otherwise) and evaluates e with x bound to it.
+  static bool mentions(const NP& e, const std::string& name) {
+    if (!e) return false;
+    if ((e->k == K::Ident || e->k == K::OpApp) && e->s == name) return true;
+    for (auto& c : e->a) if (mentions(c, name)) return true;
+    for (auto& b : e->binds) if (mentions(b.set, name)) return true;
+    for (auto& u : e->ups) { if (mentions(u.rhs, name)) return true; for (auto& s : u.path) if (mentions(s.idx, name)) return true; }
+    for (auto& d : e->defs) if (d->name != name && mentions(d->body, name)) return true;
+    return false;
+  }
+  static bool recursive_fun(const Def& d) {
+    return d.params.empty() && d.body && d.body->k == K::FunCons && mentions(d.body->a[0], d.name);
+  }
+  // the body of the recursive function as a C++ statement block over the argument `arg`: domain
+  // check, then the value of e; `sc` must already map the function's name to its RecFn symbol
+  std::string rec_body(const Def& d, Scope& sc, const std::string& arg) {
+    const Node& fc = *d.body;
+    if (fc.binds.size() != 1 || fc.binds[0].names.size() != 1) unsup(fc, "recursive function " + d.name + " of more than one argument");
+    Scope inner = sc;
+    Sym x; x.cxx = arg;
+    inner.push_back({fc.binds[0].names[0], x});
+    auto in = std::make_shared<Node>(fc);   // arg \in S, by the membership rules of binary()
+    in->k = K::Binary; in->s = "\\in"; in->binds.clear();
+    auto id = std::make_shared<Node>(fc);
+    id->k = K::Ident; id->s = fc.binds[0].names[0]; id->a.clear(); id->binds.clear();
+    in->a = {id, fc.binds[0].set};
+    return "if (!truth(A, " + ex(in, inner) + ")) { A.err |= E_DOMAIN; return 0u; }\n return " + ex(fc.a[0], inner) + ";\n";
+  }
+  std::string rec_call(const Sym& s, const std::string& arg) {
+    return s.cxx + "(" + s.cxx + ", " + arg + ")";   // a generic lambda that receives itself
+  }
+
+  std::string rec_fun_function(const std::shared_ptr<Def>& d, const Node& at) {   // a global one, emitted once
+    auto it = op_fn.find(d->name);
+    if (it != op_fn.end()) return it->second;
+    body_of(d, at);
+    std::string fn = "rf_" + std::to_string(op_fn.size()) + "_";
+    for (char ch : d->name) fn += std::isalnum((unsigned char)ch) ? ch : '_';
+    op_fn[d->name] = fn;
+    const std::string sig = "TLV_NI u32 " + fn + "(Cx& c, u32 a0)";
+    fn_protos.push_back(sig + ";");
+    const bool save = init_mode;
+    init_mode = false;
+    Scope sc;
+    const std::string body = rec_body(*d, sc, "a0");
+    init_mode = save;
+    fn_bodies.push_back(sig + " {\n  Ar& A = *c.A; (void)A;\n  " + body + "}\n");
+    return fn;
+  }
+
   std::string let_defs(const NP& e, Scope& sc) {   // C++ lambdas of a LET's definitions
     std::string out;
     for (auto& d : e->defs) {
       if (!d->body) unsup(*e, "LET definition " + d->name + " (" + d->error + ")");
+      if (recursive_fun(*d)) {
+        Sym s; s.kind = Sym::RecFn; s.def = d; s.cxx = fresh("R");
+        sc.push_back({d->name, s});
+        Scope inner = sc;
+        // inside its own body the function calls itself through the lambda's first parameter
+        Sym self = s; self.cxx = fresh("self");
+        inner.push_back({d->name, self});
+        const std::string arg = fresh("a");
+        out += "auto " + s.cxx + " = [&](auto& " + self.cxx + ", u32 " + arg + ") -> u32 {\n " + rec_body(*d, inner, arg) + "};\n";
+        continue;
+      }
       Sym s; s.kind = Sym::LetOp; s.def = d; s.cxx = fresh("L");
       s.scope = std::make_shared<Scope>(sc);   // recursion is outside the subset
       Scope inner = sc;
@@ -333,7 +398,14 @@ struct Gen {
         });
         return "[&]() -> u32 { const u32 " + m + " = A.htop;\n" + loops + " return fun_end(A, " + m + ");\n}()";
       }
-      case K::FunApp: return "apply(A, " + ex(n.a[0], sc) + ", " + ex(n.a[1], sc) + ")";
+      case K::FunApp: {
+        if (n.a[0]->k == K::Ident) {
+          const Sym* s = find(sc, n.a[0]->s);
+          if (s && s->kind == Sym::RecFn) return rec_call(*s, ex(n.a[1], sc));
+          if (!s) if (auto d = global(n.a[0]->s)) if (recursive_fun(*d)) return rec_fun_function(d, n) + "(c, " + ex(n.a[1], sc) + ")";
+        }
+        return "apply(A, " + ex(n.a[0], sc) + ", " + ex(n.a[1], sc) + ")";
+      }
       case K::Dot: return "apply(A, " + ex(n.a[0], sc) + ", mk_atom(A, " + std::to_string(str_atom(n.s)) + "u))";
       case K::Record: {
         const std::string m = fresh("m");
@@ -386,6 +458,9 @@ struct Gen {
         if (r->s == "Int") return "mk_bool(" + neg + "(tg(A, " + ex(l, sc) + ") == T_INT))";
       }
       if (r->k == K::Unary && r->s == "DOMAIN") return "mk_bool(" + neg + "in_dom(A, " + ex(r->a[0], sc) + ", " + ex(l, sc) + "))";
+      if (r->k == K::Unary && r->s == "SUBSET")   // x \in SUBSET S  <=>  x is a set and x \subseteq S (no 2^|S| powerset)
+        return "[&]() -> u32 { const u32 x_ = " + ex(l, sc) + "; return mk_bool(" + neg + "(tg(A, x_) == T_SET && set_subseteq(A, x_, " +
+               ex(r->a[0], sc) + "))); }()";
       if (r->k == K::Binary && r->s == "..")
         return "[&]() -> u32 { const u32 x_ = " + ex(l, sc) + "; const i64 lo_ = ival(A, " + ex(r->a[0], sc) + "), hi_ = ival(A, " +
                ex(r->a[1], sc) + "); if (tg(A, x_) != T_INT) return mk_bool(" + (neg.empty() ? "false" : "true") +
@@ -420,6 +495,7 @@ struct Gen {
   std::string ident(const Node& n, Scope& sc, const std::vector<std::string>& args) {
     const std::string& nm = n.s;
     if (const Sym* s = find(sc, nm)) {
+      if (s->kind == Sym::RecFn) unsup(n, "a recursive function (" + nm + ") used other than by application");
       if (s->kind == Sym::Val) {
         if (!args.empty()) unsup(n, "applying a value as an operator");
         return s->cxx;
@@ -429,6 +505,7 @@ struct Gen {
       return o + ")";
     }
     if (auto d = global(nm)) {
+      if (recursive_fun(*d)) unsup(n, "a recursive function (" + nm + ") used other than by application");
       if (d->params.size() != args.size()) unsup(n, "operator " + nm + " with " + std::to_string(args.size()) + " arguments");
       std::set<std::string> v;
       if (d->params.empty() && state_free(d, v)) {

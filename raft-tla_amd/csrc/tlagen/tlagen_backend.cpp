@@ -355,6 +355,10 @@ struct TlagenBackend : Backend {
       } else if (kind == 3) {
         r.verdict = MC_VERDICT_EVAL_ERROR;
         r.error = "evaluation error (tlv error bits " + std::to_string(h[C_INV]) + ") while computing the successors of the last state";
+      } else if (kind == 5) {   // TLC: "Evaluating invariant X failed." with the behavior up to the state
+        r.verdict = MC_VERDICT_EVAL_ERROR;
+        r.violated = h[C_INV] < meta.invariants.size() ? meta.invariants[h[C_INV]] : "?";
+        r.error = "Evaluating invariant " + r.violated + " failed.";
       } else {
         r.verdict = MC_VERDICT_DEADLOCK;
       }

@@ -27,7 +27,9 @@ enum : u32 {
   C_ERR = 2,       // OR of arena error bits of failed lanes
   C_CAP = 3,       // store / seen-set capacity exhausted
   C_FLAG = 4,      // event claimed (0/1)
-  C_KIND = 5,      // event kind: 1 violation (stored state), 2 violation (out-of-model successor), 3 eval error, 4 deadlock
+  C_KIND = 5,      // event kind: 1 violation (stored state), 2 violation (out-of-model successor), 3 eval error (computing
+                   // the successors of C_SID, a constraint or an out-of-model invariant), 4 deadlock, 5 eval error of an
+                   // invariant on the stored state C_SID (C_INV: the invariant)
   C_SID = 6,       // event state id (kind 1: the violating state; 2: its parent; 3/4: the state being expanded)
   C_INV = 7,       // kind 1/2: invariant index; kind 3: error bits
   C_EACT = 8,      // kind 2: action of the violating successor
@@ -86,6 +88,11 @@ struct Em {
     tlg::Cx d = c;
     for (int i = 0; i < tlg::NV; ++i) d.cur[i] = c.nxt[i];
     const bool im = tlg::constraints(d);
+    if (A.err) {   // a constraint could not be evaluated on this successor: TLC's evaluation error
+      if (!(A.err & E_OVF) && claim(*a)) { a->ctr[C_KIND] = 3; a->ctr[C_SID] = parent; a->ctr[C_INV] = A.err; }
+      A.top = t0;
+      return;
+    }
     if (im) {
       ++gin;
       const unsigned long long fp = fp_words(A.w + w0, n, a->seed);
@@ -115,14 +122,18 @@ struct Em {
           a->act[sid] = (u32)c.act;
           atomicAdd(a->n_committed, 1ull);
           const int bad = tlg::invariants(d);
-          if (bad >= 0 && claim(*a)) {
+          if (A.err) {   // an invariant could not be evaluated on the new state: TLC's evaluation error
+            if (!(A.err & E_OVF) && claim(*a)) { a->ctr[C_KIND] = 5; a->ctr[C_SID] = sid; a->ctr[C_INV] = (unsigned long long)bad; }
+          } else if (bad >= 0 && claim(*a)) {
             a->ctr[C_KIND] = 1; a->ctr[C_SID] = sid; a->ctr[C_INV] = (unsigned long long)bad;
           }
         }
       }
     } else if (a->inv_oom) {
       const int bad = tlg::invariants(d);
-      if (bad >= 0 && claim(*a)) {
+      if (A.err) {   // evaluation error of an invariant on an out-of-model successor
+        if (!(A.err & E_OVF) && claim(*a)) { a->ctr[C_KIND] = 3; a->ctr[C_SID] = parent; a->ctr[C_INV] = A.err; }
+      } else if (bad >= 0 && claim(*a)) {
         a->ctr[C_KIND] = 2; a->ctr[C_SID] = parent; a->ctr[C_INV] = (unsigned long long)bad;
         a->ctr[C_EACT] = (unsigned long long)c.act;
         const u32 m = n < a->evcap ? n : a->evcap;

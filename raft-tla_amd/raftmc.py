@@ -49,7 +49,7 @@ class McSummary(ctypes.Structure):
                 ("seconds_total", ctypes.c_double), ("seconds_kernels", ctypes.c_double),
                 ("fp_seed", ctypes.c_uint64), ("algo_bytes", ctypes.c_double),
                 ("generated_in_model", ctypes.c_int64), ("state_bytes", ctypes.c_int32), ("n_launches", ctypes.c_int32),
-                ("violated", ctypes.c_char * 64), ("spec", ctypes.c_char * 32)]
+                ("violated", ctypes.c_char * 64), ("spec", ctypes.c_char * 32), ("seen_set_probes", ctypes.c_int64)]
 
 
 class RaftMCError(RuntimeError):
@@ -252,6 +252,7 @@ class ModelChecker:
                       collision_prob_observed=s.collision_prob_observed,
                       seconds=s.seconds_total, kernel_seconds=s.seconds_kernels, fp_seed=s.fp_seed,
                       algo_bytes=s.algo_bytes, generated_in_model=s.generated_in_model,
+                      seen_set_probes=s.seen_set_probes,
                       state_bytes=s.state_bytes, n_launches=s.n_launches,
                       trace_text=self._text(self.lib.mc_trace), report=self._text(self.lib.mc_report),
                       error=self.lib.mc_last_error(self.h).decode(),

@@ -20,7 +20,7 @@ struct WordsHash {
   size_t operator()(const std::vector<u32>& w) const { return (size_t)tlv::fp_words(w.data(), (u32)w.size(), 7); }
 };
 
-struct Succ { std::vector<u32> w; int act; bool im; };
+struct Succ { std::vector<u32> w; int act; bool im, cerr; };
 
 struct Emit {
   std::vector<Succ>* out;
@@ -30,7 +30,10 @@ struct Emit {
     tlg::Cx d = c;
     for (int i = 0; i < tlg::NV; ++i) d.cur[i] = c.nxt[i];
     Succ s;
+    const u32 e0 = A.err;
     s.im = tlg::constraints(d);
+    s.cerr = A.err != e0;   // a constraint could not be evaluated: TLC's evaluation error
+    A.err = e0;
     for (int i = 0; i < tlg::NV; ++i) { const u32 h = c.nxt[i]; s.w.insert(s.w.end(), A.w + h, A.w + h + tlv::sz(A, h)); }
     s.act = c.act;
     out->push_back(std::move(s));
@@ -65,11 +68,18 @@ int main(int argc, char** argv) {
   std::string verdict = "OK", violated;
   int depth = 0;
   unsigned err = 0;
+  // invariant index that fails, -1 if all hold; an evaluation error sets `inv_err` (TLC's
+  // "Evaluating invariant X failed": an EVAL_ERROR verdict, not a violation)
+  bool inv_err = false;
   auto check = [&](const std::vector<u32>& w) -> int {
-    A.top = floor; load(c, w);
+    A.top = floor; A.err = 0; load(c, w);
     const int bad = tlg::invariants(c);
-    err |= A.err;
+    if (A.err) { err |= A.err; inv_err = true; }
     return bad;
+  };
+  auto report = [&](int bad) {
+    if (inv_err) { verdict = "EVAL_ERROR"; violated = tlg::kInvariantNames[bad]; }
+    else { verdict = "INVARIANT_VIOLATION"; violated = tlg::kInvariantNames[bad]; }
   };
   {
     std::vector<Succ> init;
@@ -83,7 +93,7 @@ int main(int argc, char** argv) {
       if (!tlg::constraints(c)) continue;
       if (!seen.insert(s.w).second) continue;
       const int bad = check(s.w);
-      if (bad >= 0) { verdict = "INVARIANT_VIOLATION"; violated = tlg::kInvariantNames[bad]; }
+      if (bad >= 0) report(bad);
       frontier.push_back(s.w);
     }
     if (!frontier.empty()) { depth = 1; levels.push_back((long long)frontier.size()); }
@@ -102,6 +112,7 @@ int main(int argc, char** argv) {
       generated += (long long)succ.size();
       if (succ.empty() && deadlock) { verdict = "DEADLOCK"; break; }
       for (auto& s : succ) {
+        if (s.cerr) { verdict = "EVAL_ERROR"; break; }
         gen_act[s.act]++;
         bool isnew = false;
         if (s.im) {
@@ -110,7 +121,7 @@ int main(int argc, char** argv) {
         }
         if (isnew || !s.im) {
           const int bad = check(s.w);
-          if (bad >= 0) { verdict = "INVARIANT_VIOLATION"; violated = tlg::kInvariantNames[bad]; break; }
+          if (bad >= 0) { report(bad); break; }
         }
       }
     }

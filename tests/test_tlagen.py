@@ -13,7 +13,7 @@ import tempfile
 import pytest
 
 from oracle_util import CONFIGS, GOLDEN, ORIG_MC
-from tlagen_models import token_ring
+from tlagen_models import rec_fun, token_ring
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TOOL = os.path.join(ROOT, "raft-tla_amd", "_build", "tlagen")
@@ -100,6 +100,53 @@ def test_unsupported_construct_fails_loudly(tmp_path):
     (tmp_path / "Lam.cfg").write_text("INIT Init\nNEXT Next\n")
     r = subprocess.run([TOOL, str(tmp_path / "Lam.tla"), str(tmp_path / "Lam.cfg")], capture_output=True, text=True)
     assert r.returncode == 1 and "Keep" in r.stderr and "does not parse" in r.stderr
+
+
+REC = os.path.join(CONFIGS, "tlagen", "RecFun.tla")
+
+
+@needs_tool
+def test_recursive_function_definitions():
+    """Recursive function definitions (TypedBags' Sum, tlc_membership/TypedBags.tla:73-83: a LET
+    DSum[S \\in SUBSET DOMAIN f] that applies itself) evaluated lazily like TLC, one application at
+    a time: the counts of configs/tlagen/RecFun.tla equal an independent Python restatement."""
+    want = rec_fun()
+    r = host_bfs(generate(REC, os.path.join(CONFIGS, "tlagen", "RecFun.cfg")))
+    assert r["verdict"] == "OK" and r["err"] == 0
+    assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == (want["generated"], want["distinct"], want["depth"], want["levels"])
+
+
+@needs_tool
+@pytest.mark.parametrize("cfg,inv", [("RecFun_fact", "FactNot24"), ("RecFun_sum", "SumNot7")])
+def test_recursive_function_violations(cfg, inv):
+    want = rec_fun(inv)
+    r = host_bfs(generate(REC, os.path.join(CONFIGS, "tlagen", cfg + ".cfg")))
+    assert (r["verdict"], r["violated"], r["depth"]) == ("INVARIANT_VIOLATION", inv, want["depth"])
+
+
+@needs_tool
+def test_invariant_evaluation_error():
+    """An invariant that cannot be evaluated (Fact applied outside its domain 0..6) is TLC's
+    "Evaluating invariant X failed" — an EVAL_ERROR verdict, not a violation."""
+    r = host_bfs(generate(REC, os.path.join(CONFIGS, "tlagen", "RecFun_dom.cfg")))
+    assert (r["verdict"], r["violated"], r["depth"]) == ("EVAL_ERROR", "OutOfDomain", 7)
+
+
+# apalache_no_membership/raft.tla with its shipped raft.cfg (TLC syntax): the first spec of SURVEY.md
+# 8(f) rank 3 that needs recursive function definitions (TypedBags' Sum via BagCardinality in
+# BoundedInFlightMessages).  No oracle restates this spec: the counts are the host build's of the
+# generated code ("parity unpinned"); the GPU test holds the kernels to the same numbers.
+APALACHE_D9 = dict(generated=141083, distinct=60955, levels=[1, 2, 6, 28, 120, 520, 2310, 10388, 47580])
+
+
+@needs_tool
+@needs_ref
+def test_apalache_no_membership_shipped_cfg():
+    spec = os.path.join(REF, "apalache_no_membership", "raft.tla")
+    r = host_bfs(generate(spec, os.path.join(REF, "apalache_no_membership", "raft.cfg")), "--max-depth", "9")
+    assert (r["verdict"], r["err"]) == ("DEPTH_LIMIT", 0)
+    assert {k: r[k] for k in APALACHE_D9} == APALACHE_D9
+    assert sum(r["levels"]) == r["distinct"]
 
 
 @needs_tool

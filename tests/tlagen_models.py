@@ -52,3 +52,46 @@ def token_ring(max_depth=0, stop_when_all_full=False):
         frontier = nxt
     return dict(verdict="OK", generated=generated, distinct=len(seen), depth=depth, levels=levels,
                 actions={k: [gen[k], dist[k]] for k in gen})
+
+
+FACT = {n: (1 if n == 0 else None) for n in range(7)}
+for _n in range(1, 7):
+    FACT[_n] = _n * FACT[_n - 1]
+
+
+def rec_fun(invariant=None):
+    """BFS over configs/tlagen/RecFun.tla (x, bag): Next = tick \\/ \\E k : decrement.  `invariant`:
+    None, "FactNot24" or "SumNot7"; returns the run's counts, or the violation depth."""
+    init = (0, (0, 0, 0))
+    seen = {init}
+    frontier = [init]
+    levels = [1]
+    generated = 1
+    depth = 1
+    bad = {None: lambda s: False, "FactNot24": lambda s: FACT[s[0]] == 24, "SumNot7": lambda s: sum(s[1]) == 7}[invariant]
+    while frontier:
+        nxt = []
+        for (x, bag) in frontier:
+            succs = []
+            nb = list(bag)
+            if sum(bag) < 9:
+                nb[x % 3] += 1
+            succs.append(((x + 1) % 7, tuple(nb)))
+            if sum(bag) > 0:
+                for k in range(3):
+                    if bag[k] > 0:
+                        b2 = list(bag)
+                        b2[k] -= 1
+                        succs.append((x, tuple(b2)))
+            for s in succs:
+                generated += 1
+                if s not in seen:
+                    seen.add(s)
+                    nxt.append(s)
+                    if bad(s):
+                        return dict(verdict="INVARIANT_VIOLATION", depth=depth + 1)
+        if nxt:
+            depth += 1
+            levels.append(len(nxt))
+        frontier = nxt
+    return dict(verdict="OK", generated=generated, distinct=len(seen), depth=depth, levels=levels)
