@@ -57,6 +57,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 TLA = os.path.join(ROOT, "configs", "raft_original_mc.tla")
+TLA_MEMB = os.path.join(ROOT, "configs", "raft_membership_mc.tla")
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -135,12 +136,12 @@ def main():
     mod = importlib.import_module("raft-tla_amd")
     shard = importlib.import_module("raft-tla_amd.shard") if world > 1 else None
 
-    def checker(cfg, max_depth, store, table, workers):
+    def checker(cfg, max_depth, store, table, workers, tla=TLA):
         if world > 1:
             # owner-partitioned fingerprints, 3 RCCL all-to-alls per level chunk (raft-tla_amd/shard.py)
-            return shard.ShardedChecker(TLA, cfg, rank, world, device_index=local, seed=0x5EED, fp_table_bytes=table,
+            return shard.ShardedChecker(tla, cfg, rank, world, device_index=local, seed=0x5EED, fp_table_bytes=table,
                                         state_store_bytes=store, max_depth=max_depth)
-        return mod.ModelChecker(TLA, cfg, device=local, seed=0x5EED, fp_table_bytes=table, state_store_bytes=store,
+        return mod.ModelChecker(tla, cfg, device=local, seed=0x5EED, fp_table_bytes=table, state_store_bytes=store,
                                 workers=workers, max_depth=max_depth)
 
     def barrier_sync():
@@ -157,9 +158,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t[0])
 
-    def measure(cfg, max_depth, steps, warmup, store, table, workers):
+    def measure(cfg, max_depth, steps, warmup, store, table, workers, tla=TLA):
         """W untimed runs, then K timed runs bracketed by barrier + device sync; max over ranks"""
-        mc = checker(cfg, max_depth, store, table, workers)
+        mc = checker(cfg, max_depth, store, table, workers, tla)
         try:
             for _ in range(warmup):
                 mc.run()
@@ -177,6 +178,16 @@ def main():
 
     res, per_step = measure(args.config, args.max_depth, args.steps, args.warmup, args.state_store_bytes,
                             args.fp_table_bytes, args.workers)
+    # the seen-set probes of one run, counted by the instrumented dedup kernel in a run of its own
+    # (RAFTMC_COUNT_PROBES; the timed runs use the uninstrumented one)
+    probes_per_run = None
+    if world == 1 and args.workers != 1:
+        os.environ["RAFTMC_COUNT_PROBES"] = "1"
+        try:
+            with checker(args.config, args.max_depth, args.state_store_bytes, args.fp_table_bytes, args.workers) as mc:
+                probes_per_run = mc.run().seen_set_probes
+        finally:
+            del os.environ["RAFTMC_COUNT_PROBES"]
     # TLC -workers 1 (FIFO order) on the same model, outside the timed region: its cost is reported
     fifo = None
     if world == 1 and args.workers != 1 and args.fifo_steps > 0:
@@ -185,17 +196,27 @@ def main():
                 "generated_per_run": r1.generated, "kernels_ms": {k: v["ms"] for k, v in r1.kernels.items() if v["launches"]}}
         assert (r1.distinct, r1.generated, r1.depth) == (res.distinct, res.generated, res.depth)
 
-    def side(cfg, max_depth, store_gib, table_gib, steps):
+    def side(cfg, max_depth, store_gib, table_gib, steps, tla=TLA, workers=None):
         """a second workload at the same N through the same path; its failure is reported, not fatal"""
+        name = workload_name(cfg, max_depth) if tla == TLA else "tlc_membership/raft.tla + configs/%s%s" % (
+            os.path.basename(cfg), " to depth %d" % max_depth if max_depth else "")
         try:
             store = int(store_gib * (1 << 30) / world * (1.3 if world > 1 else 1.0))
-            r, t = measure(cfg, max_depth, steps, 1, store, int(table_gib * (1 << 30)), args.workers)
-            return {"workload": workload_name(cfg, max_depth), "value": r.distinct / t, "unit": "distinct states/s",
-                    "ms_per_step": t * 1e3, "steps": steps, "distinct_per_run": r.distinct, "generated_per_run": r.generated,
-                    "depth": r.depth, "verdict": r.verdict,
-                    "kernels_ms": {k: v["ms"] for k, v in r.kernels.items() if v["launches"]}}
+            r, t = measure(cfg, max_depth, steps, 1, store, int(table_gib * (1 << 30)), args.workers if workers is None else workers, tla)
+            out = {"workload": name, "value": r.distinct / t, "unit": "distinct states/s",
+                   "ms_per_step": t * 1e3, "steps": steps, "distinct_per_run": r.distinct, "generated_per_run": r.generated,
+                   "depth": r.depth, "verdict": r.verdict,
+                   "kernels_ms": {k: v["ms"] for k, v in r.kernels.items() if v["launches"]}}
+            ks = {k: v for k, v in r.kernels.items() if v["launches"]}
+            if ks and r.algo_bytes:   # the dominant kernel against the HBM roofline, SURVEY.md 8(d) bytes
+                kname, kst = max(ks.items(), key=lambda kv: kv[1]["ms"])
+                avg_s = kst["ms"] / kst["launches"] / 1e3
+                ach = r.algo_bytes / kst["launches"] / avg_s / 1e9
+                out["roofline"] = {"bound": "hbm", "kernel": kname, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": ach / HBM_PEAK_GBS, "avg_launch_ms": avg_s * 1e3}
+            return out
         except Exception as e:   # noqa: BLE001 - the headline stands on its own
-            return {"workload": workload_name(cfg, max_depth), "error": str(e)[:300]}
+            return {"workload": name, "error": str(e)[:300]}
 
     def generated_c2():
         """C2 through the generated path (the SANY-subset front end's code for the unmodified
@@ -219,6 +240,11 @@ def main():
         # 1.5x margin on the next level must not trigger: 128 GiB at N=1 (a 96 GiB store spilled the
         # completed levels to host memory every run, 1.04 s instead of 0.23 s)
         extra["scale_workload"] = side(os.path.join(ROOT, "configs", "c5v2.cfg"), 12, 128, 16, 2)
+        # the membership model (C3 without the invariant it violates at depth 21), depth-bounded: TLC's
+        # FIFO first-found order under VIEW and SYMMETRY in TLC's rule; at N > 1 the FIFO-ranked sharded
+        # level loop (csrc/fifo_shard_loop.h), so the scaling curve covers both spec families
+        extra["scale_workload_membership"] = side(os.path.join(ROOT, "configs", "memb_four_scale.cfg"), 20, 64, 8, 2,
+                                                  tla=TLA_MEMB, workers=1)
         extra["variants"] = {"c2_md6": side(os.path.join(ROOT, "configs", "c2_md6.cfg"), 0, 64, 8, 2)}
         if world == 1:
             extra["variants"]["c2_generated"] = generated_c2()
@@ -283,14 +309,15 @@ def main():
             # probes: the device's count of fingerprints that reached the seen-set (a successor that the
             # same 256 parents produced before is filtered in LDS and never probes); the transaction-level
             # figure prices each probe at one 64-B HBM line (8 TB/s / 64 B = 125 G/s)
-            probes = res.seen_set_probes
+            probes = probes_per_run or 0
             line["dedup_set"] = {"GBps": (res.generated_in_model * 8 + res.distinct * 16) / ded_s / 1e9,
                                  "probes_per_s": probes / ded_s, "probes_per_run": probes,
                                  "successors_per_s": res.generated_in_model / ded_s,
                                  "transaction_GBps": probes * 64 / ded_s / 1e9,
                                  "transaction_frac": probes * 64 / ded_s / 1e9 / HBM_PEAK_GBS, "ms": ded_s * 1e3,
                                  "bytes": "G_in*8 + D*16 (SURVEY.md 8(d) dedup-set metric) / (merge + probe kernel time); "
-                                          "transaction: probes * 64 B / the same time"}
+                                          "transaction: probes * 64 B / the same time; probes_per_run counted in an extra "
+                                          "run by the instrumented dedup kernel (RAFTMC_COUNT_PROBES), rates over the timed runs' time"}
         # VALU issue fraction of the dominant kernel: PMC instruction count per launch from profiles/, live
         # launch time; MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 VALU instruction issues in 2 cycles
         vj = pmc_summary(args.valu_json)

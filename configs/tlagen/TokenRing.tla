@@ -12,6 +12,7 @@ VARIABLES token, logs, sent, history
 
 vars == <<token, logs, sent, history>>
 static == <<logs, sent>>
+tokenlogs == <<token, logs>>   \* a VIEW that leaves out sent and history (TokenRing_view.cfg)
 
 Min(S) == CHOOSE x \in S : \A y \in S : x <= y
 Max(S) == CHOOSE x \in S : \A y \in S : x >= y

@@ -1546,6 +1546,48 @@ struct Memb {
     }
     return best;
   }
+  // The least permuted code of one message over all permutations, without trying them: with no
+  // ConfigEntry renamed (ce false) only its server-valued fields change, so the least code renames
+  // them in order of significance -- the most significant to server 0, the next different one to 1,
+  // the next to 2.  *lab: the servers of those fields and their labels (server | label << 4, per
+  // field, most significant first), for cand_of.
+  RMC_HD static u64 canon_code(u64 c, u32& lab) {
+    const u64 dp = mdesc_packed(mcls(c));
+    const int od = (int)(dp & 127), os = (int)((dp >> 7) & 127), ov = (int)((dp >> 21) & 127);
+    const int sd = CODEB - od - SB, ss = CODEB - os - SB, sv = CODEB - ov - SB;
+    const bool has_v = ov != 0;
+    // the fields (shift, server), most significant (largest shift) first: a 3-element sorting
+    // network of selects (lanes hold different message classes: no divergent branches); a class
+    // without a third server field gets shift -1 there, which sorts last
+    int h0 = sd, h1 = ss, h2 = has_v ? sv : -1;
+    int f0 = (int)((c >> sd) & lomask(SB)), f1 = (int)((c >> ss) & lomask(SB)), f2 = has_v ? (int)((c >> sv) & lomask(SB)) : 0;
+    auto cswap = [](int& ha, int& fa, int& hb, int& fb) {
+      const bool sw = hb > ha;
+      const int th = sw ? hb : ha, tf = sw ? fb : fa;
+      hb = sw ? ha : hb; fb = sw ? fa : fb; ha = th; fa = tf;
+    };
+    cswap(h0, f0, h1, f1); cswap(h1, f1, h2, f2); cswap(h0, f0, h1, f1);
+    const int l0 = 0, l1 = f1 == f0 ? 0 : 1;
+    const int l2 = f2 == f0 ? l0 : f2 == f1 ? l1 : l1 + 1;
+    u64 x = c & ~(lomask(SB) << sd) & ~(lomask(SB) << ss);
+    if (has_v) x &= ~(lomask(SB) << sv);
+    x |= (u64)l0 << h0 | (u64)l1 << h1;
+    if (h2 >= 0) x |= (u64)l2 << h2;
+    lab = (u32)(f0 | l0 << 4) | (u32)(f1 | l1 << 4) << 8 | (h2 >= 0 ? ((u32)(f2 | l2 << 4) | 0x80u) << 16 : 0u);
+    return x;
+  }
+  // the permutations that rename the fields as canon_code's labels say
+  RMC_HD static u32 cand_of(u32 lab) {
+    u32 m = 0;
+#pragma unroll 1
+    for (int p = 0; p < NPERM; ++p) {
+      const u32 pi = perm_of(p);
+      bool ok = pi_of(pi, (int)(lab & 15u)) == (int)((lab >> 4) & 15u) && pi_of(pi, (int)((lab >> 8) & 15u)) == (int)((lab >> 12) & 15u);
+      if ((lab >> 23) & 1u) ok = ok && pi_of(pi, (int)((lab >> 16) & 15u)) == (int)((lab >> 20) & 7u);
+      m |= ok ? 1u << p : 0u;
+    }
+    return m;
+  }
   // the permutation TLC picks: least permuted variable tuple, variable by variable
   RMC_HD static u32 tlc_min_perm(const Work& t, const BagRef& bag, int len, bool ce, u32 cfgt) {
     u32 cand = (u32)lomask(NPERM);
@@ -1553,8 +1595,23 @@ struct Memb {
     // for all — then the domain elements ascending, then the counts in domain order)
     u64 last = 0;
     bool have_last = false;
+    int j0 = 0;
+#ifndef RMC_TLC_NO_CANON
+    if (!ce && len > 0) {
+      // the first (least) permuted message in closed form: the least canonical code over the
+      // messages, and the permutations that give some message of that code its canonical labels
+      // (instead of the least permuted code under each of the N! permutations)
+      u64 best = ~0ull;
 #pragma unroll 1
-    for (int j = 0; j == 0 || (j < len && !single(cand)); ++j) {   // (one pass even for an empty bag)
+      for (int q = 0; q < len; ++q) { u32 lab; const u64 cc = canon_code(mcode(bag[q]), lab); best = cc < best ? cc : best; }
+      u32 cm = 0;
+#pragma unroll 1
+      for (int q = 0; q < len; ++q) { u32 lab; if (canon_code(mcode(bag[q]), lab) == best) cm |= cand_of(lab); }
+      cand = cm; last = best; have_last = true; j0 = 1;
+    }
+#endif
+#pragma unroll 1
+    for (int j = j0; j == 0 || (j < len && !single(cand)); ++j) {   // (one pass even for an empty bag)
       cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); });
       last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
       have_last = true;

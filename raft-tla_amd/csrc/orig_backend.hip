@@ -180,22 +180,80 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
   // a wave with one leader lane would pay all of [LEAD_LO, LEAD_HI) for it (measured: a third of
   // this kernel's time for 0.7% of C2's successors)
   const bool lead = active && S::leader_work(s);
+#ifndef RMC_GEN_BINNED
+  // A wave-uniform loop over the instances: k is a scalar, so the instance decode and the bag slot
+  // selects are scalar work, and the successor's pack + fingerprint + record append run once per
+  // slot for all lanes.  (RMC_GEN_BINNED below bins each lane's enabled instances by family
+  // instead -- SURVEY.md §7 hard part 8 -- and measured 19.5 vs 14.5 ms of orig_generate per C2 run
+  // on MI355X, round 4: the per-lane instance index turns the decode and selects into vector work
+  // and the saved iterations do not pay for it.)
 #pragma unroll 1
-  for (int k = 0; k < S::NI; ++k) {
+  for (int kk = 0; kk < S::NI; ++kk) {
 #ifndef RMC_DBG_NO_SKIP
-    if (k == S::LEAD_LO) k = S::LEAD_HI;      // wave-uniform
+    if (kk == S::LEAD_LO) kk = S::LEAD_HI;      // wave-uniform
 #endif
 #ifdef RMC_EXP_SKIP_HI
-    if (k >= RMC_EXP_SKIP_LO && k < RMC_EXP_SKIP_HI) continue;   // cost-attribution experiment only
+    if (kk >= RMC_EXP_SKIP_LO && kk < RMC_EXP_SKIP_HI) continue;   // cost-attribution experiment only
 #endif
+    const int k = kk;
+#else
+  // Experiment (see above): instances binned by family (SURVEY.md §7 hard part 8): the lane's enabled instances of one
+  // family, one per iteration, every lane at once -- the lanes of an iteration share one handler,
+  // and the wave iterates as often as its busiest lane has instances of the family instead of once
+  // per instance slot.  Families: Restart, Timeout, RequestVote, Receive per message class
+  // (UpdateTerm, then one handler per message type), DuplicateMessage/DropMessage (those out of the
+  // model counted at once, below).  Successor records carry their instance, so the order they are
+  // produced in is immaterial (the seen-set keeps minimum keys, events are minima over keys).
+  constexpr int NFAM = 4 + S::RECV_CLASSES;
+  u32 fm_to = 0, fm_rv = 0, fm_dd = 0, fm_rc[S::RECV_CLASSES];
+#pragma unroll
+  for (int c = 0; c < S::RECV_CLASSES; ++c) fm_rc[c] = 0u;
+  if (active) {
+    fm_to = S::timeout_mask(s);
+    fm_rv = S::request_vote_mask(s);
+#pragma unroll
+    for (int q = 0; q < S::MK; ++q) {
+      const int cls = S::recv_class(s, q);
+#pragma unroll
+      for (int c = 0; c < S::RECV_CLASSES; ++c) fm_rc[c] |= (cls == c ? 1u : 0u) << q;
+    }
+    u32 ndup = 0, ndrop = 0;
+#pragma unroll
+    for (int q = 0; q < 2 * S::MK; ++q) {
+      if (s.bag.v[q < S::MK ? q : q - S::MK] == S::BEMPTY) continue;
+      if (S::quick_out_of_model(s, S::I_DUP + q, a.rt) >= 0) { if (q < S::MK) ++ndup; else ++ndrop; }
+      else fm_dd |= 1u << q;
+    }
+    nsucc += ndup + ndrop;
+    if (ndup) atomicAdd(&lds_cnt[OA_DuplicateMessage], ndup);
+    if (ndrop) atomicAdd(&lds_cnt[OA_DropMessage], ndrop);
+  }
+  // family f (wave-uniform): this lane's mask and the family's first instance
+  auto fam_mask = [&](int f) -> u32 {
+    u32 m = f == 0 ? (active ? (u32)lomask(S::N) : 0u) : f == 1 ? fm_to : f == 2 ? fm_rv : f == NFAM - 1 ? fm_dd : 0u;
+#pragma unroll
+    for (int c = 0; c < S::RECV_CLASSES; ++c) m = f == 3 + c ? fm_rc[c] : m;
+    return m;
+  };
+  auto fam_base = [&](int f) -> int { return f == 0 ? 0 : f == 1 ? S::N : f == 2 ? 2 * S::N : f == NFAM - 1 ? S::I_DUP : S::I_RECV; };
+  int fam = 0;
+  u32 fmask = fam_mask(0);
+#pragma unroll 1
+  for (;;) {
+    while (fam < NFAM && !__ballot(fmask != 0u)) { ++fam; fmask = fam < NFAM ? fam_mask(fam) : 0u; }   // wave-uniform
+    if (fam == NFAM) break;
+    int k = -1;   // none for this lane in this iteration (it still takes part in the wave's ballots)
+    if (fmask) { k = fam_base(fam) + __builtin_ctz(fmask); fmask &= fmask - 1u; }
+#endif
+    const bool on = active && k >= 0;
     u64 fp = 0;
     bool have = false;
     int cnt_act = -1;   // this lane's successor action (RMC_GEN_WAVE_COUNTS: counted per wave)
-    const int qa = active ? S::quick_out_of_model(s, k, a.rt) : -1;
+    const int qa = on ? S::quick_out_of_model(s, k, a.rt) : -1;
     if (qa >= 0) {      // generated, out of the model, no invariant to check: counted only
       ++nsucc;
       atomicAdd(&lds_cnt[qa], 1u);
-    } else if (active) {
+    } else if (on) {
       W t;
       const int act = S::apply(s, k, t, err);
 #ifdef RMC_EXP_DOUBLE_APPLY
@@ -745,8 +803,11 @@ __global__ void __launch_bounds__(BS) orig_probe_plain(DedupArgs a) {
 // Fused variant for TLC -workers N (what the pipeline runs): records through a first-come LDS
 // filter (plain LDS loads and stores, 32 KB: a race can only let a duplicate through to the
 // seen-set, never drop a state), the survivors probe the 8-B seen-set DEDUP_PER at a time, and
-// the new states' producers go out parent-major as in orig_probe_plain.
-template <int WW>
+// the new states' producers go out parent-major as in orig_probe_plain.  COUNT: also count the
+// fingerprints that reach the seen-set (ctr[K_PROBES], one atomic per workgroup) -- a separate
+// instantiation, because even one extra same-address atomic per wave costs ~3 ms of C2's
+// 11 ms here (round 4, measured), so timed runs leave it off (RAFTMC_COUNT_PROBES).
+template <int WW, bool COUNT>
 __global__ void __launch_bounds__(BS) orig_dedup_plain(DedupArgs a) {
   __shared__ unsigned long long lfp[LDS_FP_SLOTS];
   __shared__ u32 wave_tot[BS / 64];
@@ -760,7 +821,7 @@ __global__ void __launch_bounds__(BS) orig_dedup_plain(DedupArgs a) {
   const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
   const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
   u32 err = 0;
-  u64 probes = 0;   // wave-uniform
+  u32 probes = 0;   // this lane's (summed over the wave at the end)
 #pragma unroll 1
   for (u32 i0 = 0; i0 < n; i0 += DEDUP_PER * BS) {
     u64 fp[DEDUP_PER], key[DEDUP_PER], pos[DEDUP_PER];
@@ -772,17 +833,40 @@ __global__ void __launch_bounds__(BS) orig_dedup_plain(DedupArgs a) {
       key[j] = i < n ? (u64)keys[at] : 0ull;     // local key lane << 8 | instance
     }
 #pragma unroll
-    for (int j = 0; j < DEDUP_PER; ++j) {
+    for (int j = 0; j < DEDUP_PER; ++j)
       if (fp[j] && !lds_first(lfp, fp[j])) fp[j] = 0ull;   // produced by this workgroup's parents before
-      probes += (u64)__popcll(__ballot(fp[j] != 0ull));
+    if constexpr (COUNT) {
+#pragma unroll
+      for (int j = 0; j < DEDUP_PER; ++j) probes += fp[j] ? 1u : 0u;
     }
     const u32 ins = probe_batch<DEDUP_PER, false, 1>(a.table, a.table_mask, fp, key, pos, err);
+#ifdef RMC_EXP_DOUBLE_PROBE
+    {   // cost attribution only: the same probes again (now all present: lookups, no CAS)
+      u64 pos2[DEDUP_PER];
+      u32 e2 = 0;
+      if (probe_batch<DEDUP_PER, false, 1>(a.table, a.table_mask, fp, key, pos2, e2)) err |= OE_TABLE_FULL;
+    }
+#endif
 #pragma unroll
     for (int j = 0; j < DEDUP_PER; ++j)
       if ((ins >> j) & 1u) atomicOr(&win[(key[j] >> 8) * WW + ((key[j] & 255) >> 6)], 1ull << (key[j] & 63));
   }
-  if (__lane_id() == 0 && probes) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)probes);
+  __shared__ u32 wave_probes[BS / 64];
+  if constexpr (COUNT) {
+    u32 wp = probes;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) wp += __shfl_xor(wp, d);
+    if (__lane_id() == 0) wave_probes[threadIdx.x >> 6] = wp;
+  }
   __syncthreads();
+  if constexpr (COUNT) {
+    if (threadIdx.x == 0) {
+      u32 t = 0;
+#pragma unroll
+      for (int w = 0; w < BS / 64; ++w) t += wave_probes[w];
+      if (t) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)t);
+    }
+  }
   u64 wm[WW];
   u32 mine = 0;
 #pragma unroll
@@ -1545,6 +1629,9 @@ class OrigGpu : public Backend {
     // TLC -workers 1: single-worker FIFO order (16-B {fp, ~key} entries); -workers N: 8-B entries
     const bool fifo = o.workers == 1;
     last_fifo_ = fifo;
+    // RAFTMC_COUNT_PROBES: count the seen-set probes of the -workers N pipeline (an instrumented
+    // kernel; read per run, so a caller can count in a run of its own outside a timed region)
+    const bool count_probes = std::getenv("RAFTMC_COUNT_PROBES") != nullptr;
     const u64 tmask = fifo ? table_mask_ : 2 * (table_mask_ + 1) - 1;
     ctr_clean_ = false;
 
@@ -1632,10 +1719,12 @@ class OrigGpu : public Backend {
             hipLaunchKernelGGL(orig_merge_plain, dim3(nblk), dim3(BS), 0, stream_, d);
             HIPCHK(hipGetLastError());
             hipLaunchKernelGGL((orig_probe_plain<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
-          } else if (dedup_nocompact_) {
-            hipLaunchKernelGGL((orig_dedup_plain<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
-          } else {
+          } else if (dedup_queue_) {
             hipLaunchKernelGGL((orig_dedup_queue<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
+          } else if (count_probes) {
+            hipLaunchKernelGGL((orig_dedup_plain<WW, true>), dim3(nblk), dim3(BS), 0, stream_, d);
+          } else {
+            hipLaunchKernelGGL((orig_dedup_plain<WW, false>), dim3(nblk), dim3(BS), 0, stream_, d);
           }
         }
         HIPCHK(hipGetLastError());
@@ -2520,7 +2609,7 @@ class OrigGpu : public Backend {
   u64 sh_event_ = ~0ull;
   bool last_fifo_ = true;   // seen-set layout of the last single-GPU run (16-B keyed / 8-B entries)
   const bool split_plain_ = std::getenv("RAFTMC_SPLIT_PLAIN") != nullptr;          // experiment: merge + probe kernels
-  const bool dedup_nocompact_ = std::getenv("RAFTMC_DEDUP_NOCOMPACT") != nullptr;  // experiment: probe right after the filter
+  const bool dedup_queue_ = std::getenv("RAFTMC_DEDUP_QUEUE") != nullptr;   // experiment: full-lane probes from per-wave LDS queues
   // RAFTMC_PROF=1: per-phase wall-clock ticks (100 MHz) of orig_dedup, summed over workgroups
   const bool prof_ = std::getenv("RAFTMC_PROF") != nullptr;
   const bool progress_ = std::getenv("RAFTMC_PROGRESS") != nullptr;

@@ -328,6 +328,34 @@ struct Orig {
     return any;
   }
 
+  // ---------------------------------------------------------------- instance families (generate's binning)
+  // Which instances of a family can be enabled in s, as a bit mask over the family's instances: a
+  // superset of those apply() enables (apply decides).  The generate kernel runs a family's set
+  // bits one per iteration on every lane at once, so the lanes of an iteration share one handler
+  // (SURVEY.md §7 hard part 8) and a lane with nothing left of a family costs no iterations.
+  RMC_HD static u32 timeout_mask(const Work& s) {   // Timeout(i) :177-186: a Follower or Candidate
+    u32 m = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) { const int st = g_st(s, i); m |= (st == (int)F || st == (int)C) ? 1u << i : 0u; }
+    return m;
+  }
+  RMC_HD static u32 request_vote_mask(const Work& s) {   // RequestVote(i, j) :189-198: i a Candidate, j not responded
+    u32 m = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (g_st(s, i) == (int)C) m |= ((~row_bits(s.vresp, i)) & (u32)lomask(N)) << (i * N);
+    return m;
+  }
+  // Receive(m) of bag slot km: -1 empty slot, 0 UpdateTerm (m.mterm > currentTerm[m.mdest], which
+  // excludes every handler), else 1 + the message type (each type its own handler, :283-402)
+  RMC_HD static int recv_class(const Work& s, int km) {
+    const BE ent = sel(s.bag, km);
+    if (ent == BEMPTY) return -1;
+    const MC m = ecode_of(ent);
+    return mterm(m) > g_term(s, mdst(m)) ? 0 : 1 + mtype(m);
+  }
+  static constexpr int RECV_CLASSES = 5;
+
   // DuplicateMessage(m) / DropMessage(m) change one message count and nothing else (:442-449): the
   // successor is out of the model iff BoundedMessages puts that count outside [MinMsgCount,
   // MaxMsgCount], and no invariant reads the bag (inv_frame).  Returns the action when instance k

@@ -24,7 +24,14 @@ SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing
           ("countdown", "configs/tlagen/Countdown.tla", "configs/tlagen/Countdown.cfg"),
           ("countdown_evalerr", "configs/tlagen/Countdown.tla", "configs/tlagen/Countdown_evalerr.cfg"),
           ("ricketts_c1", "configs/ricketts_mc.tla", "configs/ricketts_c1.cfg"),
-          ("ricketts_noleader", "configs/ricketts_mc.tla", "configs/ricketts_noleader.cfg")]
+          ("ricketts_noleader", "configs/ricketts_mc.tla", "configs/ricketts_noleader.cfg"),
+          ("toy_ring_view", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing_view.cfg"),
+          ("rec_fun", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun.cfg"),
+          ("rec_fun_fact", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_fact.cfg"),
+          ("rec_fun_sum", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_sum.cfg"),
+          ("rec_fun_dom", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_dom.cfg"),
+          # the reference's Apalache spec with its own shipped cfg (TLC syntax): recursive Sum
+          ("apalache_nm", REF + "/apalache_no_membership/raft.tla", REF + "/apalache_no_membership/raft.cfg")]
 
 
 def key_of(src):
@@ -38,7 +45,7 @@ def one(spec):
     name, mod, cfg = spec
     gen = os.path.join(OUT, name + ".gen.hip")
     tool = os.path.join(PKG, "_build", "tlagen")
-    r = subprocess.run([tool, os.path.join(ROOT, mod), os.path.join(ROOT, cfg), "-I", REF, "--kernels", "-o", gen + ".tmp"],
+    r = subprocess.run([tool, os.path.join(ROOT, mod), os.path.join(ROOT, cfg), "-I", REF, "--kernels", "-o", gen + ".tmp"],   # (absolute paths stay)
                        capture_output=True, text=True)
     if r.returncode == 0:
         if not os.path.exists(gen) or open(gen).read() != open(gen + ".tmp").read():

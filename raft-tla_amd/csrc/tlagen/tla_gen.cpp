@@ -1,6 +1,7 @@
 // tla_gen.cpp — TLA+ (SANY subset) to C++ over tlv.h; see tla_gen.h for the semantics.
 #include "tla_gen.h"
 
+#include <algorithm>
 #include <cctype>
 #include <functional>
 #include <map>
@@ -726,8 +727,8 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
   Generated out;
   out.variables = prog.variables;
   if (prog.variables.size() > 64) throw CfgError(MC_E_UNSUPPORTED, "more than 64 state variables");
-  if (!cfg.symmetry.empty() || !cfg.view.empty())
-    throw CfgError(MC_E_UNSUPPORTED, "SYMMETRY / VIEW on the generated path (the hand-compiled tlc_membership path has them)");
+  if (!cfg.symmetry.empty())
+    throw CfgError(MC_E_UNSUPPORTED, "SYMMETRY on the generated path (the hand-compiled tlc_membership path has it)");
   if (!cfg.action_constraints.empty()) throw CfgError(MC_E_UNSUPPORTED, "ACTION_CONSTRAINTS on the generated path");
   // a model with temporal properties must not report "No error has been found" without checking them
   if (!cfg.properties.empty()) throw CfgError(MC_E_UNSUPPORTED, "temporal PROPERTIES are not supported");
@@ -766,23 +767,50 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
     out.invariants.push_back(cfg.invariants[i]);
   }
   invs += "  return -1;\n}\n";
+  // TLC's VIEW: states are told apart (fingerprinted) by the value of this expression; the state
+  // kept for a view class is the first found (TLC's single-worker FIFO order, tlagen_kernels.h)
+  std::string view = "TLV_NI u32 view(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
+  if (!cfg.view.empty()) {
+    auto d = g.cfg_def(cfg.view, "VIEW");
+    if (!d->params.empty()) throw CfgError(MC_E_UNSUPPORTED, "VIEW " + cfg.view + " with parameters");
+    Scope s0;
+    view += "  return " + g.ex(d->body, s0) + ";\n}\n";
+  } else {
+    view += "  return 0u;\n}\n";
+  }
 
   std::ostringstream s;
   s << "#ifndef TLG_NOINLINE\n#define TLG_NOINLINE __attribute__((noinline))\n#endif\n";
   s << "namespace tlg {\nusing namespace tlv;\n";
   s << "enum : int { NV = " << prog.variables.size() << ", NK = " << prog.constants.size() << ", NACT = " << g.actions.size()
-    << ", NINV = " << cfg.invariants.size() << " };\n";
+    << ", NINV = " << cfg.invariants.size() << ", HAS_VIEW = " << (cfg.view.empty() ? 0 : 1) << " };\n";
   s << "struct Cx { Ar* A; u32 k[" << std::max<size_t>(1, prog.constants.size() + g.cache_slot.size()) << "]; u32 cur[" << std::max<size_t>(1, prog.variables.size())
     << "]; u32 nxt[" << std::max<size_t>(1, prog.variables.size()) << "]; unsigned long long asg; int act; };\n";
   for (auto& p : g.fn_protos) s << p << "\n";
-  s << "TLV_NI bool constraints(Cx& c);\nTLV_NI int invariants(Cx& c);\n";
+  s << "TLV_NI bool constraints(Cx& c);\nTLV_NI int invariants(Cx& c);\nTLV_NI u32 view(Cx& c);\n";
   for (auto& b : g.fn_bodies) s << b;
-  s << "TLV_HD void init_consts(Cx& c) {\n  Ar& A = *c.A; (void)A;\n" << consts.str();
+  // atoms in TLC's order (tlv ocmp): strings by text, model values by name (s1 < s2 < ..., the
+  // declaration order of the cfg's model values), model values after strings
+  {
+    std::vector<std::pair<std::pair<int, std::string>, size_t>> ord;
+    for (size_t i = 0; i < g.atoms.size(); ++i) {
+      const std::string& t = g.atoms[i];
+      const bool str = !t.empty() && t[0] == '"';
+      ord.push_back({{str ? 0 : 1, str ? t.substr(1, t.size() - 2) : t}, i});
+    }
+    std::sort(ord.begin(), ord.end());
+    std::vector<unsigned> key(g.atoms.size());
+    for (size_t r = 0; r < ord.size(); ++r) key[ord[r].second] = (unsigned)r | (ord[r].first.first ? (1u << 30) : 0u);
+    s << "TLV_CONST u32 kAtomKey[] = {";
+    for (size_t i = 0; i < key.size(); ++i) s << (i ? ", " : "") << key[i] << "u";
+    s << (key.empty() ? "0u" : "") << "};\n";
+  }
+  s << "TLV_HD void init_consts(Cx& c) {\n  Ar& A = *c.A; (void)A;\n  A.akey = kAtomKey; A.nakey = " << g.atoms.size() << ";\n" << consts.str();
   for (auto& ci : g.cache_init) s << ci;
   s << "}\n";
   s << "template <class EM> TLV_HD void init_states(Cx& c, EM& em) {\n  Ar& A = *c.A; (void)A;\n  c.asg = 0; c.act = 0;\n" << init_body << "}\n";
   s << "template <class EM> TLV_HD void next_states(Cx& c, EM& em) {\n  Ar& A = *c.A; (void)A;\n  c.asg = 0; c.act = " << next_label << ";\n" << next_body << "}\n";
-  s << cons << invs << "}  // namespace tlg\n";
+  s << cons << invs << view << "}  // namespace tlg\n";
   out.source = s.str();
   out.actions = g.actions;
   out.atoms = g.atoms;

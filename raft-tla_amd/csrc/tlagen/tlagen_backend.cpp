@@ -11,6 +11,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -26,13 +27,17 @@
 
 namespace rmc {
 
+int tlagen_sort_keys(const unsigned long long* keys_in, unsigned long long* keys_out, unsigned long long n, int bits,
+                     void** tmp, size_t* tmp_bytes, hipStream_t s);   // tlagen_sort.hip
+
 namespace {
 
 using u32 = unsigned int;
 using u64 = unsigned long long;
 
 // counters of tlagen_kernels.h
-enum { C_GEN = 0, C_GIN = 1, C_ERR = 2, C_CAP = 3, C_FLAG = 4, C_KIND = 5, C_SID = 6, C_INV = 7, C_EACT = 8, C_EWORDS = 9, C_ACT = 16 };
+enum { C_GEN = 0, C_GIN = 1, C_ERR = 2, C_CAP = 3, C_FLAG = 4, C_KIND = 5, C_SID = 6, C_INV = 7, C_EACT = 8, C_EWORDS = 9,
+       C_EV = 10, C_EVINV = 11, C_NEWPOS = 12, C_ACT = 16 };
 
 struct KArgs {   // tlk::Args, field for field
   u32* words; u64* words_used; u64 words_cap;
@@ -46,6 +51,12 @@ struct KArgs {   // tlk::Args, field for field
   u64 first, count;
   u64 seed;
   int inv_oom, deadlock;
+  int fifo;
+  u64* newpos; u64 newpos_cap;
+  const u64* wkeys; u64 n_w;
+  u64 level_end;
+  u64 stop_rank, stop_ord;
+  int stop_kind;
 };
 
 std::string read_all(const std::string& p) {
@@ -93,6 +104,9 @@ Meta parse_meta(const std::string& src) {
   return m;
 }
 
+// TLA+ text of a value, with the library's canonical print rule (the hand-compiled decoders' and
+// the oracle's, oracle/tla.h show): records print their fields alphabetically, set elements and
+// function pairs sorted by their text, so traces and state dumps compare as text
 struct Printer {
   const Meta& m;
   std::string v(const u32* w) const {
@@ -102,9 +116,12 @@ struct Printer {
       case 2: return std::to_string((long long)(int)(w[1] ^ 0x80000000u));
       case 3: return w[1] < m.atoms.size() ? m.atoms[w[1]] : "?";
       case 4: case 6: {
-        std::string o = tag == 4 ? "<<" : "{";
+        std::vector<std::string> el;
         const u32* e = w + 2;
-        for (u32 i = 0; i < n; ++i) { o += (i ? ", " : "") + v(e); e += e[0] >> 3; }
+        for (u32 i = 0; i < n; ++i) { el.push_back(v(e)); e += e[0] >> 3; }
+        if (tag == 6) std::sort(el.begin(), el.end());
+        std::string o = tag == 4 ? "<<" : "{";
+        for (u32 i = 0; i < n; ++i) o += (i ? ", " : "") + el[i];
         return o + (tag == 4 ? ">>" : "}");
       }
       case 5: {
@@ -114,14 +131,17 @@ struct Printer {
           if ((e[0] & 7u) != 3 || e[1] >= m.atoms.size() || m.atoms[e[1]].empty() || m.atoms[e[1]][0] != '"') rec = false;
           e += e[0] >> 3; e += e[0] >> 3;
         }
-        std::string o = rec ? "[" : "(";
+        std::vector<std::pair<std::string, std::string>> fs;
         e = w + 2;
         for (u32 i = 0; i < n; ++i) {
           const u32* val = e + (e[0] >> 3);
-          if (rec) { const std::string& k = m.atoms[e[1]]; o += (i ? ", " : "") + k.substr(1, k.size() - 2) + " |-> " + v(val); }
-          else o += (i ? " @@ " : "") + v(e) + " :> " + v(val);
+          if (rec) { const std::string& k = m.atoms[e[1]]; fs.push_back({k.substr(1, k.size() - 2), v(val)}); }
+          else fs.push_back({v(e), v(val)});
           e = val + (val[0] >> 3);
         }
+        std::sort(fs.begin(), fs.end());
+        std::string o = rec ? "[" : "(";
+        for (u32 i = 0; i < n; ++i) o += (i ? (rec ? ", " : " @@ ") : "") + fs[i].first + (rec ? " |-> " : " :> ") + fs[i].second;
         return o + (rec ? "]" : ")");
       }
     }
@@ -224,12 +244,37 @@ struct TlagenBackend : Backend {
   }
 
   int run(const RunOpts& o, RunResult& r, std::string& err) override {
+    // a lane arena too small for one state's successors: searched again with 4x the arena per lane
+    // on a quarter of the lanes (the same HBM), up to 64x (C2: 16K words; the Apalache spec's
+    // states are ~1.4K words and need more)
+    for (arena_scale = 1;; arena_scale *= 4) {
+      bool again = false;
+      int rc = run_once(o, r, err, again);
+      if (rc == 0 && again) {
+        // TLC -workers N found an event: TLC's counterexample and stop point are the single-worker
+        // search's, so the model is searched again in FIFO order (as the hand-compiled paths do)
+        RunOpts o1 = o;
+        o1.workers = 1;
+        rc = run_once(o1, r, err, again);
+      }
+      if (rc != 0 || !arena_overflow || arena_scale >= 64) return rc;
+    }
+  }
+  u32 arena_scale = 1;
+  bool arena_overflow = false;
+
+  int run_once(const RunOpts& o, RunResult& r, std::string& err, bool& again) {
+    again = false;
+    arena_overflow = false;
     const auto t_start = std::chrono::steady_clock::now();
-    // every count is order independent; with -workers 1 the kept parents (traces) are still first-come
     if (!o.checkpoint_path.empty() || !o.recover_path.empty()) {
       err = "checkpoint / recover are not implemented on the generated path";
       return MC_E_UNSUPPORTED;
     }
+    // TLC -workers 1: the single-worker FIFO order (two passes per level, tlagen_kernels.h); any
+    // other -workers: first-come insertion, every count TLC prints is order independent, and an
+    // event is searched again in FIFO order for TLC's counterexample and stop point
+    const bool fifo = o.workers == 1;
     dev = o.device;
     HIPOK(hipSetDevice(dev));
     std::string image;
@@ -237,45 +282,57 @@ struct TlagenBackend : Backend {
     struct Scratch {   // everything but the store (kept for traces / dump_states) is freed on every return
       hipModule_t mod = nullptr;
       std::vector<void*> bufs;
+      void* sort_tmp = nullptr;
       hipEvent_t e0 = nullptr, e1 = nullptr;
       ~Scratch() {
         for (void* p : bufs) if (p) (void)hipFree(p);
+        if (sort_tmp) (void)hipFree(sort_tmp);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         if (mod) (void)hipModuleUnload(mod);
       }
     } sc;
+    size_t sort_bytes = 0;
     HIPOK(hipModuleLoadData(&sc.mod, image.data()));
-    hipFunction_t f_init, f_expand;
+    hipFunction_t f_init, f_expand, f_keys, f_mat, f_stop;
     HIPOK(hipModuleGetFunction(&f_init, sc.mod, "tlg_init_k"));
     HIPOK(hipModuleGetFunction(&f_expand, sc.mod, "tlg_expand_k"));
+    HIPOK(hipModuleGetFunction(&f_keys, sc.mod, "tlg_keys_k"));
+    HIPOK(hipModuleGetFunction(&f_mat, sc.mod, "tlg_mat_k"));
+    HIPOK(hipModuleGetFunction(&f_stop, sc.mod, "tlg_stop_k"));
     release();
-    // HBM layout: store words + per-state offsets/parents/actions, seen-set, lanes' arenas
+    // HBM layout: store words + per-state offsets/parents/actions, seen-set, lanes' arenas (+ FIFO:
+    // the level's inserted entries and their keys, unsorted and sorted)
     const u64 store = o.state_store_bytes ? o.state_store_bytes : (16ull << 30);
-    // canonical words dominate (C2: ~350-450 words per state); 20 B per state for offsets, parents, actions
-    const u64 states_cap = store / 7 / 20, words_cap = (store - states_cap * 20) / 4;
+    // canonical words dominate (C2: ~350-450 words per state); 20 B per state for offsets, parents,
+    // actions (+ 24 B of per-level key arrays in FIFO order)
+    const u64 per_state = fifo ? 44 : 20;
+    const u64 states_cap = store / 7 / per_state, words_cap = (store - states_cap * per_state) / 4;
+    const u64 entry = fifo ? 16 : 8;
     u64 tbytes = o.fp_table_bytes ? o.fp_table_bytes : (2ull << 30);
-    u64 slots = 1; while (slots * 2 * 8 <= tbytes) slots *= 2;
-    const u32 acap = 16384, hcap = 4096, evcap = 65536;
+    u64 slots = 1; while (slots * 2 * entry <= tbytes) slots *= 2;
+    const u32 acap = 16384 * arena_scale, hcap = 4096 * arena_scale, evcap = 65536 * arena_scale;
     int ncu = 256;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     int waves = 8;   // per CU: 2 per SIMD (the expand kernel holds ~250 VGPRs)
     if (const char* e = std::getenv("RAFTMC_TLAGEN_WAVES")) waves = std::max(1, std::atoi(e));
-    const u64 lanes = (u64)ncu * waves * 64;
-    u64 *d_parent = nullptr, *d_table = nullptr, *d_ctr = nullptr;
+    const u64 lanes = std::max<u64>(64, (u64)ncu * waves * 64 / arena_scale);
+    u64 *d_parent = nullptr, *d_table = nullptr, *d_ctr = nullptr, *d_newpos = nullptr, *d_keys = nullptr, *d_sorted = nullptr;
     u32 *d_act = nullptr, *d_arena = nullptr, *d_hs = nullptr, *d_ev = nullptr;
     const int nact = (int)meta.actions.size();
-    const size_t nctr = C_ACT + 2 * (size_t)nact + 4;   // + n_states, words_used
-    if (hipMalloc(&d_words, words_cap * 4) || hipMalloc(&d_offs, states_cap * 8) || hipMalloc(&d_parent, states_cap * 8) ||
-        hipMalloc(&d_act, states_cap * 4) || hipMalloc(&d_table, slots * 8) || hipMalloc(&d_ctr, nctr * 8) ||
-        hipMalloc(&d_arena, lanes * acap * 4) || hipMalloc(&d_hs, lanes * hcap * 4) || hipMalloc(&d_ev, evcap * 4)) {
-      sc.bufs = {d_parent, d_table, d_ctr, d_act, d_arena, d_hs, d_ev};
+    const size_t nctr = C_ACT + 2 * (size_t)nact + 4;   // + n_committed, n_states, words_used
+    const u64 kcap = fifo ? std::min<u64>(states_cap, slots) : 1;
+    bool oom = hipMalloc(&d_words, words_cap * 4) || hipMalloc(&d_offs, states_cap * 8) || hipMalloc(&d_parent, states_cap * 8) ||
+               hipMalloc(&d_act, states_cap * 4) || hipMalloc(&d_table, slots * entry) || hipMalloc(&d_ctr, nctr * 8) ||
+               hipMalloc(&d_arena, lanes * acap * 4) || hipMalloc(&d_hs, lanes * hcap * 4) || hipMalloc(&d_ev, evcap * 4);
+    if (!oom && fifo) oom = hipMalloc(&d_newpos, kcap * 8) || hipMalloc(&d_keys, kcap * 8) || hipMalloc(&d_sorted, kcap * 8);
+    sc.bufs = {d_parent, d_table, d_ctr, d_act, d_arena, d_hs, d_ev, d_newpos, d_keys, d_sorted};
+    if (oom) {
       release();
       err = "device allocation failed";
       return MC_E_OOM;
     }
-    sc.bufs = {d_parent, d_table, d_ctr, d_act, d_arena, d_hs, d_ev};
-    HIPOK(hipMemset(d_table, 0, slots * 8));
+    HIPOK(hipMemset(d_table, 0, slots * entry));
     HIPOK(hipMemset(d_ctr, 0, nctr * 8));
     KArgs a{};
     a.words = d_words; a.words_used = d_ctr + nctr - 1; a.words_cap = words_cap;
@@ -288,13 +345,15 @@ struct TlagenBackend : Backend {
     a.seed = o.seed ? o.seed : 0x2545f4914f6cdd1dull;
     a.inv_oom = o.inv_out_of_model ? 1 : 0;
     a.deadlock = o.check_deadlock ? 1 : 0;
+    a.fifo = fifo ? 1 : 0;
+    a.newpos = d_newpos; a.newpos_cap = kcap;
     std::vector<u64> h(nctr);
     HIPOK(hipEventCreate(&sc.e0)); HIPOK(hipEventCreate(&sc.e1));
     hipEvent_t e0 = sc.e0, e1 = sc.e1;
-    auto launch = [&](hipFunction_t f, u64 blocks) -> int {
-      void* params[] = {&a};
+    // every kernel but tlg_keys_k takes the Args block (tlk::Args)
+    auto launch_with = [&](hipFunction_t f, u64 blocks, unsigned bs, void** params) -> int {
       HIPOK(hipEventRecord(e0, 0));
-      HIPOK(hipModuleLaunchKernel(f, (unsigned)blocks, 1, 1, 64, 1, 1, 0, 0, params, nullptr));
+      HIPOK(hipModuleLaunchKernel(f, (unsigned)blocks, 1, 1, bs, 1, 1, 0, 0, params, nullptr));
       HIPOK(hipEventRecord(e1, 0));
       HIPOK(hipEventSynchronize(e1));
       float ms = 0; (void)hipEventElapsedTime(&ms, e0, e1);
@@ -303,27 +362,64 @@ struct TlagenBackend : Backend {
       HIPOK(hipMemcpy(h.data(), d_ctr, nctr * 8, hipMemcpyDeviceToHost));
       return 0;
     };
+    auto launch = [&](hipFunction_t f, u64 blocks, unsigned bs) -> int {
+      void* params[] = {&a};
+      return launch_with(f, blocks, bs, params);
+    };
+    auto set_ctr = [&](u32 k, u64 v) -> int { HIPOK(hipMemcpy(d_ctr + k, &v, 8, hipMemcpyHostToDevice)); return 0; };
     r = RunResult();
     r.action_names = meta.actions;
-    if (int rc = launch(f_init, 1)) return rc;
+    if (int rc = launch(f_init, 1, 64)) return rc;
     u64 first = 0, count = h[nctr - 2], gen_prev = h[C_GEN];
     r.generated = (int64_t)h[C_GEN];
     if (count) { r.depth = 1; r.levels.push_back({(int64_t)count, (int64_t)h[C_GEN], 0}); }
     const u64 grid = lanes / 64;
+    u64 fifo_ev = ~0ull;                              // FIFO: the stop point's event word
+    std::vector<int64_t> prior_gen(nact, 0), prior_dist(nact, 0);
+    int64_t prior_generated = 0;
     while (count && !h[C_FLAG] && !h[C_CAP]) {
       if (o.max_depth && r.depth >= o.max_depth) { r.verdict = MC_VERDICT_DEPTH_LIMIT; r.left_on_queue = (int64_t)count; break; }
       a.first = first; a.count = count;
       r.levels.push_back({0, 0, 0});
-      if (int rc = launch(f_expand, grid)) return rc;
+      u64 fresh = 0;
+      if (!fifo) {
+        if (int rc = launch(f_expand, grid, 64)) return rc;
+        fresh = h[nctr - 2] - (first + count);
+      } else {
+        prior_generated = (int64_t)h[C_GEN];
+        for (int k = 0; k < nact; ++k) { prior_gen[k] = (int64_t)h[C_ACT + k]; prior_dist[k] = (int64_t)h[C_ACT + nact + k]; }
+        if (set_ctr(C_EV, ~0ull) || set_ctr(C_NEWPOS, 0)) return MC_E_NO_DEVICE;
+        a.wkeys = nullptr; a.n_w = 0; a.level_end = first + count;
+        if (int rc = launch(f_expand, grid, 64)) return rc;   // pass 1: keys into the seen-set
+        if (h[C_CAP]) { r.levels.pop_back(); break; }
+        const u64 nw = h[C_NEWPOS];
+        const u64 level_end = first + count;
+        if (nw) {
+          {   // tlg_keys_k(table, newpos, n, keys)
+            const u64* kt = d_table; const u64* kn = d_newpos; u64 kcount = nw; u64* kk = d_keys;
+            void* kp[] = {(void*)&kt, (void*)&kn, (void*)&kcount, (void*)&kk};
+            if (int rc = launch_with(f_keys, std::min<u64>(4096, (nw + 255) / 256), 256, kp)) return rc;
+          }
+          if (tlagen_sort_keys(d_keys, d_sorted, nw, 64, &sc.sort_tmp, &sort_bytes, 0)) { err = "radix sort of the level's keys failed"; return MC_E_NO_DEVICE; }
+          a.wkeys = d_sorted; a.n_w = nw; a.level_end = level_end;
+          if (int rc = launch(f_mat, grid, 64)) return rc;     // pass 2: the winners, in key order
+          const u64 total = level_end + nw;
+          if (hipMemcpy(d_ctr + nctr - 2, &total, 8, hipMemcpyHostToDevice) != hipSuccess) { err = "counter write failed"; return MC_E_NO_DEVICE; }
+          h[nctr - 2] = total;
+        }
+        fresh = nw;
+        // the level is not complete at a stop: only completed levels are reported (as TLC does)
+        if (h[C_CAP]) { r.levels.pop_back(); break; }
+        if (h[C_EV] != ~0ull) { fifo_ev = h[C_EV]; r.levels.pop_back(); break; }
+      }
       ++r.n_launches;
-      const u64 total = h[nctr - 2];
-      const u64 fresh = total - (first + count);
       r.levels.back().states = (int64_t)fresh;
       r.levels.back().generated = (int64_t)(h[C_GEN] - gen_prev);
       gen_prev = h[C_GEN];
       first += count; count = fresh;
       if (fresh) ++r.depth; else r.levels.pop_back();
     }
+    if (!fifo && h[C_FLAG] && !h[C_CAP]) { again = true; return 0; }   // (searched again in FIFO order by run())
     // on a store overflow some ids were handed out without their words: only the committed states
     // are stored (and ids are no longer dense, so traces and dumps are refused below)
     store_complete = h[nctr - 3] == h[nctr - 2];
@@ -334,18 +430,27 @@ struct TlagenBackend : Backend {
     r.distinct = (int64_t)n_stored;
     r.act_generated.resize(nact); r.act_distinct.resize(nact);
     for (int k = 0; k < nact; ++k) { r.act_generated[k] = (int64_t)h[C_ACT + k]; r.act_distinct[k] = (int64_t)h[C_ACT + nact + k]; }
-    if (h[C_CAP]) {
-      r.verdict = MC_VERDICT_CAPACITY_OVERFLOW;
-      r.error = (h[C_CAP] & 4) ? "lane arena too small for one state's successors" : (h[C_CAP] & 2) ? "seen-set full" : "state store full";
-    } else if (h[C_FLAG]) {
-      const u64 kind = h[C_KIND], sid = h[C_SID];
-      Printer pr{meta};
+    Printer pr{meta};
+    auto trace_to = [&](u64 sid) {
       std::vector<u64> path;
       if (sid != ~0ull) chase(sid, path, d_parent, err);
       for (size_t i = path.size(); i-- > 0;) trace_step(path[i], d_parent, d_act, pr, r);
+    };
+    auto inv_name = [&](u64 i) { return i < meta.invariants.size() ? meta.invariants[i] : std::string("?"); };
+    if (h[C_CAP]) {
+      arena_overflow = (h[C_CAP] & 4) != 0;
+      r.verdict = MC_VERDICT_CAPACITY_OVERFLOW;
+      r.error = (h[C_CAP] & 4) ? "lane arena too small for one state's successors" : (h[C_CAP] & 2) ? "seen-set full"
+              : (h[C_CAP] & 8) ? "a state has more than 2^24 successors" : "state store full";
+    } else if (fifo_ev != ~0ull) {
+      if (int rc = fifo_stop(a, fifo_ev, first, count, f_stop, grid, launch, h, nctr, prior_generated, prior_gen, prior_dist,
+                             trace_to, inv_name, r, err)) return rc;
+    } else if (h[C_FLAG]) {   // an event among the initial states (one lane, Init's order: TLC's)
+      const u64 kind = h[C_KIND], sid = h[C_SID];
+      trace_to(sid);
       if (kind == 1 || kind == 2) {
         r.verdict = MC_VERDICT_INVARIANT_VIOLATION;
-        r.violated = h[C_INV] < meta.invariants.size() ? meta.invariants[h[C_INV]] : "?";
+        r.violated = inv_name(h[C_INV]);
         if (kind == 2) {   // the violating successor is outside the constraints: printed from the event buffer
           std::vector<u32> w(h[C_EWORDS]);
           (void)hipMemcpy(w.data(), d_ev, w.size() * 4, hipMemcpyDeviceToHost);
@@ -354,10 +459,10 @@ struct TlagenBackend : Backend {
         }
       } else if (kind == 3) {
         r.verdict = MC_VERDICT_EVAL_ERROR;
-        r.error = "evaluation error (tlv error bits " + std::to_string(h[C_INV]) + ") while computing the successors of the last state";
+        r.error = "evaluation error (tlv error bits " + std::to_string(h[C_INV]) + ") while computing the initial states";
       } else if (kind == 5) {   // TLC: "Evaluating invariant X failed." with the behavior up to the state
         r.verdict = MC_VERDICT_EVAL_ERROR;
-        r.violated = h[C_INV] < meta.invariants.size() ? meta.invariants[h[C_INV]] : "?";
+        r.violated = inv_name(h[C_INV]);
         r.error = "Evaluating invariant " + r.violated + " failed.";
       } else {
         r.verdict = MC_VERDICT_DEADLOCK;
@@ -368,6 +473,93 @@ struct TlagenBackend : Backend {
     r.state_bytes = 0;
     r.seconds_total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
     last = r;
+    return 0;
+  }
+
+  // TLC's report at the FIFO stop point: the level's first event in key order (tlagen_kernels.h
+  // C_EV), its counters (generated = successor lists of the parents up to the event's; distinct =
+  // the new states before it in key order, the violating one included; left on queue = the rest of
+  // the level's parents plus the new states so far) and the counterexample
+  template <class Launch, class TraceTo, class InvName>
+  int fifo_stop(KArgs& a, u64 ev, u64 first, u64 count, hipFunction_t f_stop, u64 grid, Launch& launch, std::vector<u64>& h,
+                size_t nctr, int64_t prior_generated, const std::vector<int64_t>& prior_gen, const std::vector<int64_t>& prior_dist,
+                TraceTo& trace_to, InvName& inv_name, RunResult& r, std::string& err) {
+    const u64 key = ev >> 3, kind = ev & 7, rank = key >> 24, ord = key & ((1ull << 24) - 1);
+    const int nact = (int)meta.actions.size();
+    const u64 level_end = first + count, nw = a.n_w;
+    const bool new_state = kind == 3 || kind == 5;   // EV_INV_ERROR_NEW / EV_VIOLATION_NEW
+    // the winners before the event in key order (binary search over the sorted keys)
+    u64 lo = 0, hi = a.wkeys ? nw : 0;
+    while (lo < hi) {
+      const u64 mid = (lo + hi) / 2;
+      u64 kk = 0;
+      HIPOK(hipMemcpy(&kk, a.wkeys + mid, 8, hipMemcpyDeviceToHost));
+      if (kk < key || (kk == key && new_state)) lo = mid + 1; else hi = mid;
+    }
+    const u64 before = lo;
+    // generated counts: re-derived over the parents [0, rank] (and the event successor captured)
+    for (size_t k = 0; k < nctr - 3; ++k) if (k == C_GEN || (k >= C_ACT && k < (size_t)C_ACT + nact)) h[k] = 0;
+    HIPOK(hipMemcpy(a.ctr, h.data(), (nctr - 3) * 8, hipMemcpyHostToDevice));
+    a.stop_rank = rank; a.stop_ord = ord; a.stop_kind = (int)kind;
+    if (int rc = launch(f_stop, std::min<u64>(grid, (rank + 64) / 64), 64)) return rc;
+    r.generated = prior_generated + (int64_t)h[C_GEN];
+    for (int k = 0; k < nact; ++k) r.act_generated[k] = prior_gen[k] + (int64_t)h[C_ACT + k];
+    std::vector<u32> acts(before);
+    if (before) HIPOK(hipMemcpy(acts.data(), a.act + level_end, before * 4, hipMemcpyDeviceToHost));
+    for (int k = 0; k < nact; ++k) r.act_distinct[k] = prior_dist[k];
+    for (u32 x : acts) if (x < (u32)nact) ++r.act_distinct[x];
+    r.distinct = (int64_t)(level_end + before);
+    r.left_on_queue = (int64_t)(count - rank - 1 + before);
+    n_stored = level_end + before;
+    const u64 parent_sid = first + rank;
+    auto successor = [&]() {   // the event's successor, captured by tlg_stop_k
+      std::vector<u32> w(h[C_EWORDS]);
+      if (w.empty()) { err = "the stop point's successor was not re-derived"; return; }
+      (void)hipMemcpy(w.data(), a.evbuf, w.size() * 4, hipMemcpyDeviceToHost);
+      const u64 ak = h[C_EACT];
+      Printer pr{meta};
+      r.trace.push_back({ak < meta.actions.size() ? meta.actions[ak] : "?", pr.state(w.data())});
+    };
+    switch (kind) {
+      case 0:   // EV_NEXT_ERROR
+        r.verdict = MC_VERDICT_EVAL_ERROR;
+        r.error = "evaluation error while computing the successors of the last state";
+        trace_to(parent_sid);
+        break;
+      case 1:   // EV_DEADLOCK
+        r.verdict = MC_VERDICT_DEADLOCK;
+        trace_to(parent_sid);
+        break;
+      case 2:   // EV_INV_ERROR_OOM: a constraint / VIEW / invariant could not be evaluated on a successor
+        r.verdict = MC_VERDICT_EVAL_ERROR;
+        r.violated = inv_name(h[C_EVINV]);
+        r.error = "evaluation error on a successor of the last state (a constraint, the VIEW or invariant " + r.violated + ")";
+        trace_to(parent_sid);
+        successor();
+        r.depth += 1;
+        break;
+      case 3:   // EV_INV_ERROR_NEW
+        r.verdict = MC_VERDICT_EVAL_ERROR;
+        r.violated = inv_name(h[C_EVINV]);
+        r.error = "Evaluating invariant " + r.violated + " failed.";
+        trace_to(level_end + before - 1);
+        r.depth += 1;
+        break;
+      case 4:   // EV_VIOLATION_OOM
+        r.verdict = MC_VERDICT_INVARIANT_VIOLATION;
+        r.violated = inv_name(h[C_EVINV]);
+        trace_to(parent_sid);
+        successor();
+        r.depth += 1;
+        break;
+      default:  // EV_VIOLATION_NEW
+        r.verdict = MC_VERDICT_INVARIANT_VIOLATION;
+        r.violated = inv_name(h[C_EVINV]);
+        trace_to(level_end + before - 1);
+        r.depth += 1;
+        break;
+    }
+    (void)err;
     return 0;
   }
 

@@ -13,8 +13,9 @@
 //   SET  [h, n, e1 .. en]                   elements strictly increasing
 // Equal TLA+ values have equal word strings (TLC's value equality: <<a, b>> = [i \in 1..2 |->
 // ..], [x \in {} |-> e] = <<>>, 1 :> v = <<v>>), so a state's words are its canonical key and
-// the fingerprint is a hash of the words.  The order (word-lexicographic) is a total order
-// used to normalise sets and function domains; on integers it is the numeric order.
+// the fingerprint is a hash of the words.  Sets and function domains are kept sorted in TLC's
+// value order (ocmp below: the order TLC enumerates `\E x \in S`, CHOOSE and DOMAIN in, so the
+// successors come out in TLC's order); any total order would give canonical words.
 //
 // Errors (TLC's evaluation errors: a function applied outside its domain, a bad sequence index,
 // CHOOSE with no witness, a type error, arena overflow) set bits in Ar::err and return a valid
@@ -27,6 +28,13 @@
 #else
 #define TLV_HD inline
 #define TLV_NI static __attribute__((noinline))
+#endif
+#endif
+#ifndef TLV_CONST
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+#define TLV_CONST __device__ constexpr
+#else
+#define TLV_CONST constexpr
 #endif
 #endif
 
@@ -53,13 +61,16 @@ struct Ar {
   u32* hs;      // handle stack (builders)
   u32 htop, hcap;
   u32 err;
+  const u32* akey;   // per atom id: AK_MV bit for model values, then its rank in TLC's order (generated)
+  u32 nakey;
 };
+enum : u32 { AK_MV = 1u << 30 };
 
 TLV_HD u32 hdr(u32 tag, u32 n) { return tag | (n << 3); }
 TLV_HD u32 tg(const Ar& a, u32 v) { return a.w[v] & 7u; }
 TLV_HD u32 sz(const Ar& a, u32 v) { return a.w[v] >> 3; }
 TLV_HD void init(Ar& a, u32* w, u32 cap, u32* hs, u32 hcap) {
-  a.w = w; a.cap = cap; a.hs = hs; a.hcap = hcap; a.htop = 0; a.err = 0;
+  a.w = w; a.cap = cap; a.hs = hs; a.hcap = hcap; a.htop = 0; a.err = 0; a.akey = nullptr; a.nakey = 0;
   w[0] = hdr(T_BOOL, 2); w[1] = 0; w[2] = hdr(T_BOOL, 2); w[3] = 1; a.top = 4;
 }
 TLV_HD u32 alloc(Ar& a, u32 n) {
@@ -121,10 +132,72 @@ TLV_HD u32 first(u32 v) { return v + 2; }
 TLV_HD u32 nextv(const Ar& a, u32 e) { return e + sz(a, e); }
 TLV_HD bool is_coll(const Ar& a, u32 v) { const u32 t = tg(a, v); return t == T_SEQ || t == T_FUN || t == T_SET; }
 
+// TLC's value order (the oracle's cmp, oracle/tla.h:150, as TLC's Value.compareTo is recalled,
+// SURVEY.md [ext]): kinds BOOLEAN < integers < strings < model values < sequences < sets <
+// functions (records are functions); integers numerically, strings by text and model values by
+// declaration (the atom's rank, a.akey), sequences and sets by length then element by element,
+// functions by domain size, then the domain elements, then the values.  Iterative (an explicit
+// stack of the collections being compared): no recursion on the device.
+TLV_HD u32 orank(const Ar& a, u32 v) {
+  const u32 t = tg(a, v);
+  if (t == T_BOOL) return 0;
+  if (t == T_INT) return 1;
+  if (t == T_ATOM) { const u32 id = a.w[v + 1]; return (a.akey && id < a.nakey && (a.akey[id] & AK_MV)) ? 3 : 2; }
+  return t == T_SEQ ? 4 : t == T_SET ? 5 : 6;
+}
+TLV_NI int ocmp(const Ar& a, u32 x, u32 y) {
+  struct Fr { u32 x, y, x0, y0, left, n, fun; };   // fun: 0 SEQ/SET, 1 FUN keys, 2 FUN values
+  Fr st[24];
+  int sp = -1;
+  u32 cx = x, cy = y;
+  for (;;) {
+    if (cx != cy) {
+      const u32 rx = orank(a, cx), ry = orank(a, cy);
+      if (rx != ry) return rx < ry ? -1 : 1;
+      const u32 t = tg(a, cx);
+      if (t == T_BOOL || t == T_INT) {
+        const u32 p = a.w[cx + 1], q = a.w[cy + 1];
+        if (p != q) return p < q ? -1 : 1;   // biased integers compare as unsigned words
+      } else if (t == T_ATOM) {
+        const u32 i = a.w[cx + 1], j = a.w[cy + 1];
+        const u32 p = (a.akey && i < a.nakey) ? a.akey[i] : i, q = (a.akey && j < a.nakey) ? a.akey[j] : j;
+        if (p != q) return p < q ? -1 : 1;
+      } else {
+        const u32 n = count(a, cx), m = count(a, cy);
+        if (n != m) return n < m ? -1 : 1;
+        if (n > 0) {
+          if (sp + 1 >= 24) return cmpv(a, cx, cy);   // (nesting deeper than any spec value: word order)
+          st[++sp] = Fr{first(cx), first(cy), first(cx), first(cy), n, n, t == T_FUN ? 1u : 0u};
+          cx = first(cx); cy = first(cy);
+          continue;
+        }
+      }
+    }
+    // the pair is equal: the next pair of the innermost collection still being compared
+    for (;;) {
+      if (sp < 0) return 0;
+      Fr& f = st[sp];
+      if (--f.left > 0) {
+        f.x = nextv(a, f.x); f.y = nextv(a, f.y);
+        if (f.fun) { f.x = nextv(a, f.x); f.y = nextv(a, f.y); }   // over the value (or the key)
+        cx = f.x; cy = f.y;
+        break;
+      }
+      if (f.fun == 1) {   // the domains are equal: now the values, in domain order
+        f.fun = 2; f.left = f.n;
+        f.x = nextv(a, f.x0); f.y = nextv(a, f.y0);
+        cx = f.x; cy = f.y;
+        break;
+      }
+      --sp;
+    }
+  }
+}
+
 // ---- builders: push element handles, then end
 TLV_NI void sort_handles(Ar& a, u32 mark, u32 stride) {   // insertion sort of stride-groups by their first handle
   for (u32 i = mark + stride; i < a.htop; i += stride) {
-    for (u32 j = i; j > mark && cmpv(a, a.hs[j - stride], a.hs[j]) > 0; j -= stride)
+    for (u32 j = i; j > mark && ocmp(a, a.hs[j - stride], a.hs[j]) > 0; j -= stride)
       for (u32 s = 0; s < stride; ++s) { const u32 t = a.hs[j - stride + s]; a.hs[j - stride + s] = a.hs[j + s]; a.hs[j + s] = t; }
   }
 }
@@ -177,7 +250,7 @@ TLV_NI bool set_in(Ar& a, u32 x, u32 s) {
   if (tg(a, s) != T_SET) { a.err |= E_TYPE; return false; }
   u32 e = first(s);
   for (u32 i = 0, n = count(a, s); i < n; ++i, e = nextv(a, e)) {
-    const int c = cmpv(a, e, x);
+    const int c = ocmp(a, e, x);
     if (c == 0) return true;
     if (c > 0) return false;   // sorted
   }
@@ -195,7 +268,7 @@ TLV_NI u32 set_union(Ar& a, u32 x, u32 y) {   // linear merge of two sorted sets
   u32 e = first(x), f = first(y), i = 0, j = 0;
   const u32 n = count(a, x), m = count(a, y);
   while (i < n || j < m) {
-    int c = i == n ? 1 : j == m ? -1 : cmpv(a, e, f);
+    int c = i == n ? 1 : j == m ? -1 : ocmp(a, e, f);
     if (c <= 0) { hpush(a, e); e = nextv(a, e); ++i; if (c == 0) { f = nextv(a, f); ++j; } }
     else { hpush(a, f); f = nextv(a, f); ++j; }
   }

@@ -73,7 +73,7 @@ def source_hash():
     names = [os.path.join("csrc", f) for f in os.listdir(csrc) if f.endswith((".h", ".cpp", ".hip"))]
     tg = os.path.join(csrc, "tlagen")   # the front end (tlv_text.h is derived from its sources)
     if os.path.isdir(tg):
-        names += [os.path.join("csrc", "tlagen", f) for f in os.listdir(tg) if f.endswith((".h", ".cpp")) and f != "tlv_text.h"]
+        names += [os.path.join("csrc", "tlagen", f) for f in os.listdir(tg) if f.endswith((".h", ".cpp", ".hip")) and f != "tlv_text.h"]
     h = hashlib.sha256()
     for f in sorted(names):
         with open(os.path.join(here, f), "rb") as fh:

@@ -15,7 +15,7 @@ $H $F --offload-arch=gfx950 -munsafe-fp-atomics -DRMC_QUICK_BUILD $DEFS -I$C -c 
 $H -shared --offload-arch=gfx950 -o "$OUT/libraftmc.so" "$OUT/orig_backend.o" $ROOT/raft-tla_amd/_build/memb_backend.o \
    $ROOT/raft-tla_amd/_build/mc_api.o $ROOT/raft-tla_amd/_build/model.o $ROOT/raft-tla_amd/_build/orig_model.o \
    $ROOT/raft-tla_amd/_build/memb_model.o $ROOT/raft-tla_amd/_build/tla_value.o \
-   $ROOT/raft-tla_amd/_build/tla_parse.o $ROOT/raft-tla_amd/_build/tla_gen.o $ROOT/raft-tla_amd/_build/tlagen_backend.o \
+   $ROOT/raft-tla_amd/_build/tla_parse.o $ROOT/raft-tla_amd/_build/tla_gen.o $ROOT/raft-tla_amd/_build/tlagen_backend.o $ROOT/raft-tla_amd/_build/tlagen_sort.o \
    -ldl -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 rm -f "$OUT/orig_backend.o"
 echo "$OUT/libraftmc.so"

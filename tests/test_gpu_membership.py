@@ -8,8 +8,9 @@ match: per-action DISTINCT counts, the history counters of every kept state
 (they are part of the dumped text) and the counterexample trace, state by
 state.  The punctuated-search cases (CommitWhenConcurrentLeaders_unique,
 MajorityOfClusterRestarts_constraint) take the reference's golden history
-traces from the committed fixtures.  The oracle runs SYMMETRY in orbit ("view") mode, which is what the
-GPU implements.
+traces from the committed fixtures.  SYMMETRY runs in both modes, on the GPU as in the oracle:
+TLC's rule (least permuted full state, then VIEW: the drop-in default, fixtures prefixed "tlc:")
+and the orbit of the VIEW ("view").
 """
 import hashlib
 import json

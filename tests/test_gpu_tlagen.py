@@ -115,3 +115,82 @@ def test_ricketts_on_gpu(raftmc):
                              workers=0, **SMALL) as mc:
         r = mc.run()
     assert (r.verdict, r.violated, r.depth) == ("INVARIANT_VIOLATION", "NoLeader", 10)
+
+
+def test_generated_fifo_trace_equals_oracle(raftmc):
+    """TLC's single-worker FIFO order on the generated path (workers=1: two passes per level, the
+    minimum (parent rank, successor ordinal) key kept per fingerprint, tlagen_kernels.h): the
+    NoLeader counterexample of the unmodified raft_original.tla equals the oracle's state by state
+    (tests/golden/orig_events.json), and so do TLC's counters at the stop point.  raft_original's
+    Next is one conjunction, so every step is the action "Next" (the oracle names the handler)."""
+    from test_gpu import trace_states
+    g = json.load(open(os.path.join(GOLDEN, "orig_events.json")))["c2_noleader"]
+    for workers in (1, 0):   # -workers N: the event is searched again in FIFO order
+        with raftmc.ModelChecker(gen_source("c2_noleader"), os.path.join(CONFIGS, "c2_noleader.cfg"), frontend="generated",
+                                 workers=workers, fp_table_bytes=1 << 28, state_store_bytes=16 << 30) as mc:
+            r = mc.run()
+        assert (r.verdict, r.violated, r.depth, r.exit_code) == ("INVARIANT_VIOLATION", "NoLeader", g["depth"], 12), r.error
+        assert (r.generated, r.distinct, r.left_on_queue) == (g["generated"], g["distinct"], g["left_on_queue"])
+        assert [lv[0] for lv in r.levels] == g["levels"]
+        assert [s for _, s in trace_states(r)] == [t["state"] for t in g["trace"]]
+
+
+@pytest.mark.parametrize("workers", [1, 0])
+def test_generated_parity_both_orders(raftmc, workers):
+    """raft_original has no VIEW: the FIFO two-pass search and the -workers N one give the oracle's
+    counts (parity_pair, tests/golden/orig_parity.json), and the FIFO one its per-level sizes."""
+    g = json.load(open(os.path.join(GOLDEN, "orig_parity.json")))["parity_pair"]
+    with raftmc.ModelChecker(gen_source("parity_pair"), os.path.join(CONFIGS, "parity_pair.cfg"), frontend="generated",
+                             workers=workers, **SMALL) as mc:
+        r = mc.run()
+    assert r.verdict == "OK", r.error
+    assert (r.generated, r.distinct, r.depth, [lv[0] for lv in r.levels]) == (g["generated"], g["distinct"], g["depth"], g["levels"])
+
+
+def test_view_fifo_on_gpu(raftmc):
+    """TLC's VIEW on the GPU in TLC's FIFO order (TokenRing_view.cfg): counts, levels and per-action
+    generated AND distinct counts of the Python restatement -- which state of a view class is kept
+    (the first found) decides its successors."""
+    want = token_ring(view=True)
+    with raftmc.ModelChecker(gen_source("toy_ring_view"), os.path.join(CONFIGS, "tlagen", "TokenRing_view.cfg"),
+                             frontend="generated", workers=1, **SMALL) as mc:
+        r = mc.run()
+    assert r.verdict == "OK", r.error
+    assert (r.generated, r.distinct, r.depth, [lv[0] for lv in r.levels]) == (want["generated"], want["distinct"], want["depth"], want["levels"])
+    for a, v in want["actions"].items():
+        assert r.actions[a] == v, a
+
+
+@pytest.mark.parametrize("workers", [1, 0])
+def test_recursive_functions_on_gpu(raftmc, workers):
+    """Recursive function definitions evaluated on the device (TypedBags' Sum form; RecFun.tla):
+    the Python restatement's counts, its violation depths, and TLC's evaluation error for an
+    invariant applied outside the function's domain."""
+    from tlagen_models import rec_fun
+    rec = os.path.join(CONFIGS, "tlagen", "RecFun.cfg")
+    want = rec_fun()
+    with raftmc.ModelChecker(gen_source("rec_fun"), rec, frontend="generated", workers=workers, **SMALL) as mc:
+        r = mc.run()
+    assert r.verdict == "OK", r.error
+    assert (r.generated, r.distinct, r.depth, [lv[0] for lv in r.levels]) == (want["generated"], want["distinct"], want["depth"], want["levels"])
+    for name, inv in (("rec_fun_fact", "FactNot24"), ("rec_fun_sum", "SumNot7")):
+        with raftmc.ModelChecker(gen_source(name), os.path.join(CONFIGS, "tlagen", name.replace("rec_fun", "RecFun") + ".cfg"),
+                                 frontend="generated", workers=workers, **SMALL) as mc:
+            r = mc.run()
+        assert (r.verdict, r.violated, r.depth) == ("INVARIANT_VIOLATION", inv, rec_fun(inv)["depth"])
+    with raftmc.ModelChecker(gen_source("rec_fun_dom"), os.path.join(CONFIGS, "tlagen", "RecFun_dom.cfg"), frontend="generated",
+                             workers=workers, **SMALL) as mc:
+        r = mc.run()
+    assert (r.verdict, r.violated, r.depth, r.exit_code) == ("EVAL_ERROR", "OutOfDomain", 7, 75)
+
+
+def test_apalache_no_membership_on_gpu(raftmc):
+    """apalache_no_membership/raft.tla with its shipped raft.cfg (recursive Sum in the constraints):
+    the host build's counts to depth 9 (tests/test_tlagen.py; parity unpinned), both search orders."""
+    from test_tlagen import APALACHE_D9
+    for workers in (1, 0):
+        with raftmc.ModelChecker(gen_source("apalache_nm"), os.path.join(ROOT, "configs", "apalache_nm.cfg"), frontend="generated",
+                                 workers=workers, max_depth=9, **SMALL) as mc:
+            r = mc.run()
+        assert r.verdict == "DEPTH_LIMIT", r.error
+        assert {"generated": r.generated, "distinct": r.distinct, "levels": [lv[0] for lv in r.levels]} == APALACHE_D9

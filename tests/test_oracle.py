@@ -130,8 +130,11 @@ def test_oracle_validates_gpu_counterexamples(cfg):
     """Counterexamples the GPU finds beyond the oracle's BFS reach (tests/golden/gpu_traces/): the
     LogMatching violation of the dynamic-membership model (InitServer = {s1, s2} grows to three
     servers), the known-false VotesGrantedInv_false / LeaderCompleteness_false (positive controls of
-    the invariant kernels, raft.tla:1038-1046, :1079-1083) and BoundedTrace under
-    CommitWhenConcurrentLeaders_constraint (raft.tla:1182-1186).  The oracle replays each state by
+    the invariant kernels, raft.tla:1038-1046, :1079-1083), BoundedTrace under
+    CommitWhenConcurrentLeaders_constraint (raft.tla:1182-1186) and the scenario
+    NewlyJoinedBecomeLeader (raft.tla:1258-1266: a server added by AddNewServer later becomes leader;
+    depth 21 on the growing cluster InitServer = {s1}, Server = {s1, s2}, whose stop-point counters
+    the oracle's lean BFS also reached: "oracle_pin").  The oracle replays each state by
     state through its own Init, Next, constraints and invariants: valid, and the last state violates
     the named property."""
     from oracle_util import MEMB_MC, run_oracle
@@ -140,6 +143,9 @@ def test_oracle_validates_gpu_counterexamples(cfg):
                    os.path.join(GOLDEN, "gpu_traces", cfg + ".txt"))
     assert r["valid"] and r["length"] == g["depth"] and r["violated"] == g["violated"], r
     assert r["actions"].split(",") == g["actions"][1:]
+    if "oracle_pin" in g:   # the oracle's own lean-mode BFS reached the stop point (make_gpu_trace_pin.py)
+        assert {k: g["oracle_pin"][k] for k in ("verdict", "violated", "depth", "distinct", "generated", "left_on_queue")} == \
+            {k: g[k] for k in ("verdict", "violated", "depth", "distinct", "generated", "left_on_queue")}
 
 
 @pytest.mark.parametrize("name", ["parity_pair", "parity_trio", "c2_noleader"])

@@ -83,6 +83,21 @@ def test_token_ring_matches_python_model():
 
 
 @needs_tool
+def test_token_ring_view_fifo():
+    """TLC's VIEW (configs/tlagen/TokenRing_view.cfg: VIEW <<token, logs>>): states are told apart
+    by the view and the kept one is the first found in TLC's single-worker FIFO order -- its
+    history decides its own successors, so every count is FIFO-sensitive; the host BFS (sequential:
+    FIFO) equals the Python restatement."""
+    want = token_ring(view=True)
+    r = host_bfs(generate(RING, os.path.join(CONFIGS, "tlagen", "TokenRing_view.cfg")))
+    assert r["verdict"] == "OK" and r["err"] == 0
+    for k in ("generated", "distinct", "depth", "levels"):
+        assert r[k] == want[k], k
+    for a, v in want["actions"].items():
+        assert r["actions"][a] == v, a
+
+
+@needs_tool
 def test_token_ring_violation_depth():
     want = token_ring(stop_when_all_full=True)
     r = host_bfs(generate(RING, os.path.join(CONFIGS, "tlagen", "TokenRing_full.cfg")))
@@ -114,6 +129,19 @@ def test_recursive_function_definitions():
     r = host_bfs(generate(REC, os.path.join(CONFIGS, "tlagen", "RecFun.cfg")))
     assert r["verdict"] == "OK" and r["err"] == 0
     assert (r["generated"], r["distinct"], r["depth"], r["levels"]) == (want["generated"], want["distinct"], want["depth"], want["levels"])
+
+
+@needs_tool
+@needs_ref
+def test_generated_fifo_trace_equals_oracle():
+    """The generated code enumerates successors in TLC's order (sets and function domains in TLC's
+    value order, tlv.h ocmp; Next's disjuncts and bound variables in text order): a sequential FIFO
+    BFS over it (TLC -workers 1) finds the oracle's NoLeader counterexample state by state, with
+    TLC's counters at the stop point (tests/golden/orig_events.json, c2_noleader)."""
+    g = json.load(open(os.path.join(GOLDEN, "orig_events.json")))["c2_noleader"]
+    r = host_bfs(generate(ORIG_MC, os.path.join(CONFIGS, "c2_noleader.cfg")), "--trace")
+    assert (r["verdict"], r["violated"], r["distinct"]) == ("INVARIANT_VIOLATION", "NoLeader", g["distinct"])
+    assert r["trace"] == [t["state"] for t in g["trace"]]
 
 
 @needs_tool

@@ -11,10 +11,15 @@ def _succ(p):   # Succ(p): CASE p = Max(Proc) -> Min(Proc) [] OTHER -> Min({q \i
     return min(PROC) if p == max(PROC) else min(q for q in PROC if q > p)
 
 
-def token_ring(max_depth=0, stop_when_all_full=False):
-    """BFS over (token, logs, sent, passes, crashes); returns the run's counts."""
+def token_ring(max_depth=0, stop_when_all_full=False, view=False):
+    """BFS over (token, logs, sent, passes, crashes); returns the run's counts.  view: TLC's
+    `VIEW tokenlogs` (configs/tlagen/TokenRing_view.cfg) in TLC's single-worker FIFO
+    order -- states are told apart by their view <<token, logs>>, and the one kept per view is the
+    first found (parents in queue order, successors in Next's enumeration order), whose history
+    (crashes) decides its own Lose successors."""
     init = (min(PROC), ((),) * len(PROC), frozenset(), 0, 0)
-    seen = {init}
+    key = (lambda s: (s[0], s[1])) if view else (lambda s: s)
+    seen = {key(init)}
     frontier = [init]
     levels = [1]
     gen = {"Write": 0, "Pass": 0, "Lose": 0}
@@ -40,8 +45,8 @@ def token_ring(max_depth=0, stop_when_all_full=False):
             for act, s in succs:
                 generated += 1
                 gen[act] += 1
-                if s not in seen:
-                    seen.add(s)
+                if key(s) not in seen:
+                    seen.add(key(s))
                     dist[act] += 1
                     nxt.append(s)
                     if stop_when_all_full and all(len(l) == MAX_LOG for l in s[1]):
