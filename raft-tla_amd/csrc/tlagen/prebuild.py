@@ -30,6 +30,10 @@ SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing
           ("rec_fun_fact", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_fact.cfg"),
           ("rec_fun_sum", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_sum.cfg"),
           ("rec_fun_dom", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_dom.cfg"),
+          # the unmodified tlc_membership/raft.tla with VIEW vars and SYMMETRY perms (TLC's rule)
+          ("memb_nosym_gen", "configs/raft_membership_mc.tla", "configs/memb_nosym.cfg"),
+          ("memb_shipped_gen", "configs/raft_membership_mc.tla", "configs/membership_shipped.cfg"),
+          ("memb_two_gen", "configs/raft_membership_mc.tla", "configs/memb_two.cfg"),
           # the reference's Apalache spec with its own shipped cfg (TLC syntax): recursive Sum
           ("apalache_nm", REF + "/apalache_no_membership/raft.tla", REF + "/apalache_no_membership/raft.cfg")]
 

@@ -541,6 +541,7 @@ struct Gen {
     if (nm == "Tail") { need(1); return "tail(A, " + args[0] + ")"; }
     if (nm == "Cardinality") { need(1); return "mk_int(A, set_card(A, " + args[0] + "))"; }
     if (nm == "IsFiniteSet") { need(1); return "2u"; }
+    if (nm == "Permutations") { need(1); return "permutations(A, " + args[0] + ")"; }   // TLC module (SYMMETRY sets)
     if (nm == "Print" || nm == "PrintT") { return args.back(); }
     if (nm == "Assert") { need(2); return "(truth(A, " + args[0] + ") ? 2u : (A.err |= E_DOMAIN, 0u))"; }
     // Bags
@@ -722,13 +723,38 @@ struct Gen {
 
 }  // namespace
 
+// What TLC fingerprints for a state (VIEW / SYMMETRY): under SYMMETRY the least state over the
+// permutations, variables compared in declaration order in TLC's value order (tlv ocmp; TLC's rule
+// as the oracle's --sym tlc restates it), then the VIEW of it, or the tuple of its variables.  One
+// value handle; its words are what is fingerprinted (and the host BFS's seen-set key).
+static const char* const kCanonView = R"(TLV_NI u32 canon_view(Cx& d) {
+  Ar& A = *d.A;
+  Cx e = d;
+  if (HAS_SYMMETRY) {
+    const u32 ps = symmetry(d);
+    if (tg(A, ps) != T_SET) { A.err |= E_TYPE; return 0u; }
+    u32 pe = first(ps);
+    for (u32 q = 0, n = count(A, ps); q < n; ++q, pe = nextv(A, pe)) {
+      int c = q == 0 ? -1 : 0;   // the first permutation sets the least state so far
+      for (int i = 0; i < NV; ++i) {
+        const u32 r = perm_value(A, d.cur[i], pe);
+        if (c == 0) { c = ocmp(A, r, e.cur[i]); if (c > 0) break; }
+        if (c < 0) e.cur[i] = r;
+      }
+    }
+  }
+  if (HAS_VIEW) return view(e);
+  const u32 m = A.htop;
+  for (int i = 0; i < NV; ++i) hpush(A, e.cur[i]);
+  return seq_end(A, m);
+}
+)";
+
 Generated generate(const Program& prog, const CfgFile& cfg) {
   Gen g(prog, cfg);
   Generated out;
   out.variables = prog.variables;
   if (prog.variables.size() > 64) throw CfgError(MC_E_UNSUPPORTED, "more than 64 state variables");
-  if (!cfg.symmetry.empty())
-    throw CfgError(MC_E_UNSUPPORTED, "SYMMETRY on the generated path (the hand-compiled tlc_membership path has it)");
   if (!cfg.action_constraints.empty()) throw CfgError(MC_E_UNSUPPORTED, "ACTION_CONSTRAINTS on the generated path");
   // a model with temporal properties must not report "No error has been found" without checking them
   if (!cfg.properties.empty()) throw CfgError(MC_E_UNSUPPORTED, "temporal PROPERTIES are not supported");
@@ -767,6 +793,19 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
     out.invariants.push_back(cfg.invariants[i]);
   }
   invs += "  return -1;\n}\n";
+  // TLC's SYMMETRY: the set of permutations (of model values) under which states are identified; the
+  // kernels fingerprint the least permuted state in TLC's order (tlagen_kernels.h canonical)
+  std::string symm = "TLV_NI u32 symmetry(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
+  if (!cfg.symmetry.empty()) {
+    auto d = g.cfg_def(cfg.symmetry, "SYMMETRY");
+    if (!d->params.empty()) throw CfgError(MC_E_UNSUPPORTED, "SYMMETRY " + cfg.symmetry + " with parameters");
+    Node idn;
+    idn.k = K::Ident; idn.s = cfg.symmetry; idn.line = d->line; idn.module = d->module;
+    Scope s0;
+    symm += "  return " + g.ident(idn, s0, {}) + ";\n}\n";
+  } else {
+    symm += "  return 0u;\n}\n";
+  }
   // TLC's VIEW: states are told apart (fingerprinted) by the value of this expression; the state
   // kept for a view class is the first found (TLC's single-worker FIFO order, tlagen_kernels.h)
   std::string view = "TLV_NI u32 view(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
@@ -783,11 +822,12 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
   s << "#ifndef TLG_NOINLINE\n#define TLG_NOINLINE __attribute__((noinline))\n#endif\n";
   s << "namespace tlg {\nusing namespace tlv;\n";
   s << "enum : int { NV = " << prog.variables.size() << ", NK = " << prog.constants.size() << ", NACT = " << g.actions.size()
-    << ", NINV = " << cfg.invariants.size() << ", HAS_VIEW = " << (cfg.view.empty() ? 0 : 1) << " };\n";
+    << ", NINV = " << cfg.invariants.size() << ", HAS_VIEW = " << (cfg.view.empty() ? 0 : 1)
+    << ", HAS_SYMMETRY = " << (cfg.symmetry.empty() ? 0 : 1) << " };\n";
   s << "struct Cx { Ar* A; u32 k[" << std::max<size_t>(1, prog.constants.size() + g.cache_slot.size()) << "]; u32 cur[" << std::max<size_t>(1, prog.variables.size())
     << "]; u32 nxt[" << std::max<size_t>(1, prog.variables.size()) << "]; unsigned long long asg; int act; };\n";
   for (auto& p : g.fn_protos) s << p << "\n";
-  s << "TLV_NI bool constraints(Cx& c);\nTLV_NI int invariants(Cx& c);\nTLV_NI u32 view(Cx& c);\n";
+  s << "TLV_NI bool constraints(Cx& c);\nTLV_NI int invariants(Cx& c);\nTLV_NI u32 view(Cx& c);\nTLV_NI u32 symmetry(Cx& c);\n";
   for (auto& b : g.fn_bodies) s << b;
   // atoms in TLC's order (tlv ocmp): strings by text, model values by name (s1 < s2 < ..., the
   // declaration order of the cfg's model values), model values after strings
@@ -810,7 +850,7 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
   s << "}\n";
   s << "template <class EM> TLV_HD void init_states(Cx& c, EM& em) {\n  Ar& A = *c.A; (void)A;\n  c.asg = 0; c.act = 0;\n" << init_body << "}\n";
   s << "template <class EM> TLV_HD void next_states(Cx& c, EM& em) {\n  Ar& A = *c.A; (void)A;\n  c.asg = 0; c.act = " << next_label << ";\n" << next_body << "}\n";
-  s << cons << invs << view << "}  // namespace tlg\n";
+  s << cons << invs << view << symm << kCanonView << "}  // namespace tlg\n";
   out.source = s.str();
   out.actions = g.actions;
   out.atoms = g.atoms;

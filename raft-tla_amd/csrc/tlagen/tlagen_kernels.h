@@ -171,8 +171,8 @@ struct Em {
     if (im) {
       ++gin;
       unsigned long long fp;
-      if (tlg::HAS_VIEW) {   // TLC's VIEW: the fingerprint of the view of the state
-        const u32 vh = tlg::view(d);
+      if (tlg::HAS_VIEW || tlg::HAS_SYMMETRY) {   // TLC's VIEW / SYMMETRY: the fingerprint of what tells states apart
+        const u32 vh = tlg::canon_view(d);
         if (A.err) { error_event(A, key, keyed); A.top = t0; return; }
         fp = fp_words(A.w + vh, sz(A, vh), a->seed);
       } else {

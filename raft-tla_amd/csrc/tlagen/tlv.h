@@ -403,6 +403,52 @@ TLV_NI u32 atat(Ar& a, u32 f, u32 g) {   // f @@ g: f's pairs, then g's keys not
   push_pairs(a, g);
   return fun_end(a, mark);   // stable: f's pair wins a shared key
 }
+// ---- TLC's SYMMETRY: Permutations(S) and the renaming of a value by one permutation
+// Permutations(S) (the TLC module): every bijection S -> S, as functions; |S| <= 6 (720 of them)
+TLV_NI u32 permutations(Ar& a, u32 s) {
+  if (tg(a, s) != T_SET) { a.err |= E_TYPE; return s; }
+  const u32 n = count(a, s);
+  if (n > 6) { a.err |= E_UNSUP; return s; }
+  u32 el[6];
+  u32 e = first(s);
+  for (u32 i = 0; i < n; ++i, e = nextv(a, e)) el[i] = e;
+  u32 idx[6];
+  for (u32 i = 0; i < n; ++i) idx[i] = i;
+  const u32 outer = a.htop;
+  for (;;) {   // lexicographic enumeration of index permutations
+    const u32 mark = a.htop;
+    for (u32 i = 0; i < n; ++i) { hpush(a, el[i]); hpush(a, el[idx[i]]); }
+    hpush(a, fun_end(a, mark));
+    int k = (int)n - 2;
+    while (k >= 0 && idx[k] > idx[k + 1]) --k;
+    if (k < 0) break;
+    int l = (int)n - 1;
+    while (idx[l] < idx[k]) --l;
+    u32 t = idx[k]; idx[k] = idx[l]; idx[l] = t;
+    for (int x = k + 1, y = (int)n - 1; x < y; ++x, --y) { t = idx[x]; idx[x] = idx[y]; idx[y] = t; }
+  }
+  return set_end(a, outer);
+}
+// v with every atom in DOMAIN pi renamed to pi[atom] (sets and function domains re-sorted); a
+// value that contains no renamed atom comes back as the same handle (nothing is rebuilt)
+TLV_NI u32 perm_value(Ar& a, u32 v, u32 pi) {
+  const u32 t = tg(a, v);
+  if (t == T_BOOL || t == T_INT) return v;
+  if (t == T_ATOM) { const u32 r = lookup(a, pi, v); return r ? r : v; }
+  const u32 n = count(a, v), mark = a.htop;
+  bool changed = false;
+  u32 e = first(v);
+  for (u32 i = 0; i < n * (t == T_FUN ? 2u : 1u); ++i, e = nextv(a, e)) {
+    const u32 r = perm_value(a, e, pi);
+    changed |= r != e;
+    hpush(a, r);
+  }
+  if (!changed) { a.htop = mark; return v; }
+  if (t == T_SET) return set_end(a, mark);
+  if (t == T_FUN) return fun_end(a, mark);
+  return seq_end(a, mark);
+}
+
 // ---- the standard Bags module (a bag: a function from elements to positive counts)
 TLV_NI u32 set_to_bag(Ar& a, u32 s) {   // SetToBag(S) == [e \in S |-> 1]
   if (tg(a, s) != T_SET) { a.err |= E_TYPE; return s; }

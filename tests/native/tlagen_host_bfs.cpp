@@ -38,8 +38,8 @@ struct Emit {
     s.cerr = A.err != e0;   // a constraint could not be evaluated: TLC's evaluation error
     A.err = e0;
     for (int i = 0; i < tlg::NV; ++i) { const u32 h = c.nxt[i]; s.w.insert(s.w.end(), A.w + h, A.w + h + tlv::sz(A, h)); }
-    if (tlg::HAS_VIEW && s.im && !s.cerr) {   // TLC's VIEW: states are told apart by the view's value
-      const u32 vh = tlg::view(d);
+    if ((tlg::HAS_VIEW || tlg::HAS_SYMMETRY) && s.im && !s.cerr) {   // TLC's VIEW / SYMMETRY: states told apart by canon_view
+      const u32 vh = tlg::canon_view(d);
       s.key.assign(A.w + vh, A.w + vh + tlv::sz(A, vh));
       if (A.err != e0) { s.cerr = true; A.err = e0; }
     } else {

@@ -194,3 +194,22 @@ def test_apalache_no_membership_on_gpu(raftmc):
             r = mc.run()
         assert r.verdict == "DEPTH_LIMIT", r.error
         assert {"generated": r.generated, "distinct": r.distinct, "levels": [lv[0] for lv in r.levels]} == APALACHE_D9
+
+
+@pytest.mark.parametrize("case,gen", [("memb_nosym@13", "memb_nosym_gen"), ("tlc:membership_shipped@16", "memb_shipped_gen"),
+                                      ("tlc:memb_two@16", "memb_two_gen")])
+def test_generated_membership_on_gpu(raftmc, case, gen):
+    """The unmodified tlc_membership/raft.tla through the generated path on the GPU, TLC's semantics in
+    full (VIEW vars; SYMMETRY perms by TLC's rule; the single-worker FIFO order that decides which
+    state of a view class is kept): the oracle's counts, level sizes and per-action distinct counts
+    (tests/golden/memb_parity.json; "generated" as tests/test_tlagen.py explains)."""
+    from test_tlagen import memb_actions_as_generated
+    g = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))[case]
+    with raftmc.ModelChecker(gen_source(gen), os.path.join(CONFIGS, g["cfg"] + ".cfg"), frontend="generated", workers=1,
+                             deadlock=False, max_depth=g["max_depth"], **SMALL) as mc:
+        r = mc.run()
+    assert r.verdict in ("DEPTH_LIMIT", "OK"), r.error
+    assert (r.distinct, r.depth, [lv[0] for lv in r.levels]) == (g["distinct"], g["depth"], g["levels"])
+    want = memb_actions_as_generated(g["actions"])
+    assert {k: v[1] for k, v in r.actions.items() if v[0]} == {k: v[1] for k, v in want.items()}
+    assert 0 <= r.generated - g["generated"] <= g["actions"]["HandleCheckOldConfig"][0]

@@ -144,6 +144,55 @@ def test_generated_fifo_trace_equals_oracle():
     assert r["trace"] == [t["state"] for t in g["trace"]]
 
 
+# the hand-compiled path's action names for what the unmodified spec's ReceiveDirect disjunction
+# holds (tlc_membership/raft.tla:842-863): the generated path splits actions where TLC does
+# (disjunctions, \E, operator definitions), and `m.mtype = X /\ HandleX(..)` is a conjunction
+RECEIVE_DIRECT = ("HandleRequestVoteRequest", "HandleRequestVoteResponse", "DropStaleResponse", "HandleAppendEntriesRequest",
+                  "HandleAppendEntriesResponse", "HandleCatchupRequest", "HandleCatchupResponse", "HandleCheckOldConfig")
+
+
+# NextUnreliable's disjuncts `\E m \in DOMAIN messages : /\ messages[m] = 1 /\ DuplicateMessage(m)`
+# (and DropMessage, raft.tla:924-932) are conjunctions under the \E: actions named NextUnreliable
+UNRELIABLE = ("DuplicateMessage", "DropMessage")
+
+
+def memb_actions_as_generated(acts):
+    out = {k: v for k, v in acts.items() if k not in RECEIVE_DIRECT + UNRELIABLE and v[0]}
+    for name, group in (("ReceiveDirect", RECEIVE_DIRECT), ("NextUnreliable", UNRELIABLE)):
+        g = [sum(acts.get(k, [0, 0])[i] for k in group) for i in (0, 1)]
+        if g[0]:
+            out[name] = g
+    return out
+
+
+@needs_tool
+@needs_ref
+@pytest.mark.parametrize("case", ["memb_nosym@13", "tlc:membership_shipped@16", "tlc:memb_two@16"])
+def test_generated_membership_matches_oracle(case):
+    """The unmodified tlc_membership/raft.tla (through configs/raft_membership_mc.tla) on the generated
+    path with TLC's semantics in full -- VIEW vars, SYMMETRY perms by TLC's rule (the least permuted
+    state in TLC's value order, then its VIEW: tla_gen.cpp canon_view), the single-worker FIFO order
+    that decides which state of a view class is kept -- against the oracle's fixtures
+    (tests/golden/memb_parity.json): counts, level sizes and per-action generated AND distinct
+    counts (the handlers inside ReceiveDirect summed under that name)."""
+    g = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))[case]
+    r = host_bfs(generate(os.path.join(CONFIGS, "raft_membership_mc.tla"), os.path.join(CONFIGS, g["cfg"] + ".cfg")),
+                 "--max-depth", str(g["max_depth"]), "--no-deadlock")
+    assert r["err"] == 0 and r["verdict"] in ("DEPTH_LIMIT", "OK"), r["verdict"]
+    assert (r["distinct"], r["depth"], r["levels"]) == (g["distinct"], g["depth"], g["levels"])
+    want = memb_actions_as_generated(g["actions"])
+    got = {k: v for k, v in r["actions"].items() if v[0]}
+    assert {k: v[1] for k, v in got.items()} == {k: v[1] for k, v in want.items()}   # distinct: FIFO-sensitive
+    # generated: the front end enumerates every true disjunct of an infix \/ inside an action, as
+    # TLC's getNextStates does for a disjunction (DESIGN.md §8), so HandleCheckOldConfig's guard
+    # `state[i] /= Leader \/ m.mterm = currentTerm[i]` (raft.tla:796) yields its Discard successor
+    # twice when both hold; the oracle evaluates that guard as one boolean.  Only that handler differs.
+    extra = r["generated"] - g["generated"]
+    assert 0 <= extra <= g["actions"]["HandleCheckOldConfig"][0]
+    assert {k: v[0] for k, v in got.items() if k != "ReceiveDirect"} == {k: v[0] for k, v in want.items() if k != "ReceiveDirect"}
+    assert got.get("ReceiveDirect", [0, 0])[0] - want.get("ReceiveDirect", [0, 0])[0] == extra
+
+
 @needs_tool
 @pytest.mark.parametrize("cfg,inv", [("RecFun_fact", "FactNot24"), ("RecFun_sum", "SumNot7")])
 def test_recursive_function_violations(cfg, inv):
