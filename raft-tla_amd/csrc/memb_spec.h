@@ -1484,13 +1484,77 @@ struct Memb {
     u64 best = ~0ull;
     u32 out = 0;
 #pragma unroll 1
-    for (int p = 0; p < NPERM; ++p)
-      if ((cand >> p) & 1u) {
-        const u64 k = key(p, perm_of(p));
-        out = k < best ? (1u << p) : k == best ? (out | 1u << p) : out;
-        best = k < best ? k : best;
-      }
+    for (u32 m = cand; m; m &= m - 1u) {   // the candidates only (a lane's trip count is |cand|)
+      const int p = __builtin_ctz(m);
+      const u64 k = key(p, perm_of(p));
+      out = k < best ? (1u << p) : k == best ? (out | 1u << p) : out;
+      best = k < best ? k : best;
+    }
     return out;
+  }
+  // pi^-1 packed like pi (2 bits per server): pinv(pi, s) == pi_of(inv_of(pi), s)
+  RMC_HD static u32 inv_of(u32 pi) {
+    u32 r = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r |= (u32)i << (2 * pi_of(pi, i));
+    return r;
+  }
+  // TLC's order over the variables after the messages, in as few integer keys as fit: a run of
+  // consecutive keys of known widths packed most significant first into one u64 orders the run
+  // exactly as comparing key by key does, so one keep_min settles a whole run (a wave's trip count
+  // is the number of runs, not of keys).
+  static constexpr int RTB = 2 + 3;   // server[x] = [restarted (<= MaxRestarts = 2), timeout (3 bits)]
+  static constexpr int SCAL_BITS = RKB + N * (RTB + TB + 2 + VB);
+  static constexpr int LOG_BITS = IB + MAXLOG * EW;
+  static constexpr int CV_BITS = N * IB + 2 * N * 4;
+  static constexpr int NM_BITS = N * N * IB;
+  static_assert(SCAL_BITS <= 64 && LOG_BITS <= 64 && CV_BITS <= 64 && NM_BITS <= 64, "fused TLC keys fit 64 bits");
+  // history (the rank of the permuted global sequence, then server[x] of the server mapped to x),
+  // currentTerm, state ("Candidate" < "Follower" < "Leader"), votedFor (Nil = 0 sorts first)
+  RMC_HD static u64 key_scalars(const Work& t, int p, u32 pi) {
+    const u32 iv = inv_of(pi);
+    u64 k = hrank(t, p);
+#pragma unroll
+    for (int x = 0; x < N; ++x) { const int i = pi_of(iv, x); k = k << RTB | (u64)restarted(t, i) << 3 | (u64)timeouts(t, i); }
+#pragma unroll
+    for (int x = 0; x < N; ++x) k = k << TB | (u64)g_term(t, pi_of(iv, x));
+#pragma unroll
+    for (int x = 0; x < N; ++x) { const int st = g_st(t, pi_of(iv, x)); k = k << 2 | (u64)(st == (int)C ? 0 : st == (int)F ? 1 : 2); }
+#pragma unroll
+    for (int x = 0; x < N; ++x) { const int v = g_voted(t, pi_of(iv, x)); k = k << VB | (u64)(v == N ? 0 : 1 + pi_of(pi, v)); }
+    return k;
+  }
+  // log[x]: length, then the entries (config entries renamed), 0 past the end
+  RMC_HD static u64 key_log(const Work& t, int x, u32 pi, u32 cfgt) {
+    const LogV l = getlog(t, pinv(pi, x));
+    const int n = llen(l);
+    u64 k = (u64)n;
+#pragma unroll
+    for (int pos = 0; pos < MAXLOG; ++pos) k = k << EW | (pos < n ? (u64)pentry(lent(l, pos), pi, cfgt) : 0ull);
+    return k;
+  }
+  // commitIndex, votesResponded, votesGranted (sets: cardinality, then elements: m2r)
+  RMC_HD static u64 key_cv(const Work& t, u32 pi) {
+    const u32 iv = inv_of(pi);
+    u64 k = 0;
+#pragma unroll
+    for (int x = 0; x < N; ++x) k = k << IB | (u64)g_commit(t, pi_of(iv, x));
+#pragma unroll
+    for (int x = 0; x < N; ++x) k = k << 4 | (u64)m2r(pmask(g_vr(t, pi_of(iv, x)), pi));
+#pragma unroll
+    for (int x = 0; x < N; ++x) k = k << 4 | (u64)m2r(pmask(g_vg(t, pi_of(iv, x)), pi));
+    return k;
+  }
+  // nextIndex (match: matchIndex)
+  RMC_HD static u64 key_nm(const Work& t, u32 pi, bool match) {
+    const u32 iv = inv_of(pi);
+    u64 k = 0;
+#pragma unroll
+    for (int z = 0; z < N * N; ++z) {
+      const int i = pi_of(iv, z / N), j = pi_of(iv, z % N);
+      k = k << IB | (u64)(match ? g_match(t, i, j) : g_next(t, i, j));
+    }
+    return k;
   }
   // 64-bit hash of the permuted state pi(t) as far as TLC's order sees it: its VIEW (view_hash1), the
   // rank of its permuted history["global"] and its per-server [restarted, timeout] records
@@ -1634,48 +1698,17 @@ struct Memb {
       });
       last = code; have_last = true;
     }
-    // history: [global, hadNum* (invariant), server]: the rank of the permuted global sequence,
-    // then server[x] = [restarted, timeout] of the server mapped to x
-    if (!single(cand)) cand = keep_min(cand, [&](int p, u32) { return (u64)hrank(t, p); });
+    // history: [global, hadNum* (invariant), server], currentTerm, state, votedFor, log, commitIndex,
+    // votesResponded, votesGranted, nextIndex, matchIndex — each a function over the servers, in
+    // the fused runs of key_scalars / key_log / key_cv / key_nm
+    if (!single(cand)) cand = keep_min(cand, [&](int p, u32 pi) { return key_scalars(t, p, pi); });
 #pragma unroll 1
     for (int x = 0; x < N && !single(cand); ++x)
-      cand = keep_min(cand, [&](int, u32 pi) { const int i = pinv(pi, x); return (u64)restarted(t, i) << 8 | (u64)timeouts(t, i); });
-    // currentTerm, state ("Candidate" < "Follower" < "Leader"), votedFor (Nil = 0 sorts before
-    // the servers), log (length, then entries), commitIndex, votesResponded, votesGranted (sets:
-    // cardinality, then elements), nextIndex, matchIndex — each a function over the servers
+      cand = keep_min(cand, [&](int, u32 pi) { return key_log(t, x, pi, cfgt); });
+    if (!single(cand)) cand = keep_min(cand, [&](int, u32 pi) { return key_cv(t, pi); });
 #pragma unroll 1
-    for (int x = 0; x < N && !single(cand); ++x)
-      cand = keep_min(cand, [&](int, u32 pi) { return (u64)g_term(t, pinv(pi, x)); });
-#pragma unroll 1
-    for (int x = 0; x < N && !single(cand); ++x)
-      cand = keep_min(cand, [&](int, u32 pi) { const int st = g_st(t, pinv(pi, x)); return (u64)(st == (int)C ? 0 : st == (int)F ? 1 : 2); });
-#pragma unroll 1
-    for (int x = 0; x < N && !single(cand); ++x)
-      cand = keep_min(cand, [&](int, u32 pi) { const int v = g_voted(t, pinv(pi, x)); return (u64)(v == N ? 0 : 1 + pi_of(pi, v)); });
-#pragma unroll 1
-    for (int x = 0; x < N && !single(cand); ++x)
-#pragma unroll 1
-      for (int pos = -1; pos < MAXLOG && !single(cand); ++pos)
-        cand = keep_min(cand, [&](int, u32 pi) {
-          const LogV l = getlog(t, pinv(pi, x));
-          if (pos < 0) return (u64)llen(l);
-          return pos < llen(l) ? (u64)pentry(lent(l, pos), pi, cfgt) : (u64)0;
-        });
-#pragma unroll 1
-    for (int x = 0; x < N && !single(cand); ++x)
-      cand = keep_min(cand, [&](int, u32 pi) { return (u64)g_commit(t, pinv(pi, x)); });
-#pragma unroll 1
-    for (int x = 0; x < 2 * N && !single(cand); ++x)
-      cand = keep_min(cand, [&](int, u32 pi) {
-        const int i = pinv(pi, x < N ? x : x - N);
-        return (u64)m2r(pmask(x < N ? g_vr(t, i) : g_vg(t, i), pi));
-      });
-#pragma unroll 1
-    for (int xy = 0; xy < 2 * N * N && !single(cand); ++xy)
-      cand = keep_min(cand, [&](int, u32 pi) {
-        const int z = xy < N * N ? xy : xy - N * N, i = pinv(pi, z / N), j = pinv(pi, z % N);
-        return (u64)(xy < N * N ? g_next(t, i, j) : g_match(t, i, j));
-      });
+    for (int m = 0; m < 2 && !single(cand); ++m)
+      cand = keep_min(cand, [&](int, u32 pi) { return key_nm(t, pi, m != 0); });
     return perm_of(__builtin_ctz(cand));   // any remaining tie: identical permuted states
   }
   RMC_HD static u64 fingerprint_tlc(const Work& t, u64 seed, const MembRuntime& rt) {
