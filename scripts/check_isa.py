@@ -1,6 +1,6 @@
 """Static checks of the gfx950 code object inside libraftmc.so (no GPU needed).
 
-    python scripts/check_isa.py [path/to/libraftmc.so]
+    python scripts/check_isa.py [path/to/libraftmc.so | path/to/x.hsaco ...]
 
 For every kernel: instruction count, long-branch sequences (s_getpc_b64 +
 s_setpc_b64, emitted when a kernel outgrows the 16-bit branch range) and the
@@ -28,14 +28,20 @@ MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 
 def code_objects(lib):
-    """The .hip_fatbin section holds one offload bundle per translation unit; unbundle each."""
+    """The .hip_fatbin section holds one offload bundle per translation unit; unbundle each.
+    A generated path's code object (`_build/tlagen_co/*.hsaco`, hiprtc output) is one bundle."""
     d = tempfile.mkdtemp()
     fat = os.path.join(d, "fat.bin")
-    # objcopy without an output operand rewrites its input in place: dump from a copy, never
-    # from the library a running process may have mapped
-    copy = os.path.join(d, "lib.so")
-    shutil.copyfile(lib, copy)
-    subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=" + fat, copy, os.path.join(d, "discard.so")], check=True)
+    with open(lib, "rb") as f:
+        raw = f.read(len(MAGIC)) == MAGIC
+    if raw:
+        shutil.copyfile(lib, fat)
+    else:
+        # objcopy without an output operand rewrites its input in place: dump from a copy, never
+        # from the library a running process may have mapped
+        copy = os.path.join(d, "lib.so")
+        shutil.copyfile(lib, copy)
+        subprocess.run(["objcopy", "--dump-section", ".hip_fatbin=" + fat, copy, os.path.join(d, "discard.so")], check=True)
     blob = open(fat, "rb").read()
     starts = [m.start() for m in re.finditer(re.escape(MAGIC), blob)]
     out = []
@@ -49,21 +55,27 @@ def code_objects(lib):
     return out
 
 
-def kernels(co):
+def kernels(co, functions=False):
     dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", co], capture_output=True,
                          text=True, check=True).stdout
     out, cur = {}, None
     smem_pending = False
+    getpc_at = -99
     for line in dis.splitlines():
         m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
         if m:
             cur = m.group(1)
             out[cur] = {"instructions": 0, "long_branches": 0, "smem_store_hazards": 0}
             smem_pending = False
+            getpc_at = -99
             continue
         if cur and line.startswith("\t"):
             out[cur]["instructions"] += 1
-            if "s_setpc_b64" in line:
+            # a long branch is s_getpc_b64 + offset arithmetic + s_setpc_b64; a function's return
+            # is a bare s_setpc_b64 of the return address (not counted)
+            if "s_getpc_b64" in line:
+                getpc_at = out[cur]["instructions"]
+            if "s_setpc_b64" in line and out[cur]["instructions"] - getpc_at <= 4:
                 out[cur]["long_branches"] += 1
             # a scalar load from memory other than the kernel arguments (s[0:1]) still in flight
             # while a vector store / atomic is issued: the two paths are not ordered, so a store
@@ -88,17 +100,29 @@ def kernels(co):
             if k < len(lds): out[s]["lds_bytes"] = int(lds[k])
             if k < len(vgpr): out[s]["vgprs"] = int(vgpr[k])
             if k < len(agpr): out[s]["agprs"] = int(agpr[k])
-    return {k: v for k, v in out.items() if "scratch_bytes" in v}
+    # functions=True: device functions too (the generated path's kernels call the functions its
+    # front end outlines; a long branch or store hazard inside one is as bad as in a kernel)
+    return {k if "scratch_bytes" in v else "fn:" + k: v for k, v in out.items() if functions or "scratch_bytes" in v}
+
+
+def violations(ks, allow_scratch=False):
+    """Kernels/functions breaking the rules: long branches, store-after-scalar-load hazards, and
+    (unless allowed) scratch.  The generated path's code objects are allowed scratch: their
+    kernels call outlined functions (a call stack) and keep a state's variable handles in a
+    private array; the hand-compiled library is not."""
+    return {k: v for k, v in ks.items()
+            if v["long_branches"] or v["smem_store_hazards"] or (not allow_scratch and v.get("scratch_bytes"))}
 
 
 def main():
-    lib = sys.argv[1] if len(sys.argv) > 1 else DEFAULT
+    libs = sys.argv[1:] or [DEFAULT]
+    gen = all(l.endswith(".hsaco") for l in libs)
     ks = {}
-    for co in code_objects(lib):
-        ks.update(kernels(co))
+    for lib in libs:
+        for co in code_objects(lib):
+            ks.update({(k if len(libs) == 1 else os.path.basename(lib) + ":" + k): v for k, v in kernels(co, gen).items()})
     print(json.dumps(ks, indent=1, sort_keys=True))
-    bad = {k: v for k, v in ks.items() if v["long_branches"] or v["scratch_bytes"] or v["smem_store_hazards"]}
-    return 1 if bad else 0
+    return 1 if violations(ks, allow_scratch=gen) else 0
 
 
 if __name__ == "__main__":

@@ -109,6 +109,24 @@ def test_kernels_short_branch_and_no_scratch():
     assert not bad, bad
 
 
+def test_generated_code_objects_short_branch_and_ordered_stores():
+    """The same check over the generated path's prebuilt code objects (`_build/tlagen_co/*.hsaco`,
+    hiprtc output for every spec `prebuild.py` compiles), kernels and the device functions the
+    front end outlines: no long branches, no store issued under an outstanding scalar load.  They
+    may use scratch (a call stack and each lane's variable-handle array)."""
+    import glob
+    import json
+    import subprocess
+    import sys
+    cos = sorted(glob.glob(os.path.join(ROOT, "raft-tla_amd", "_build", "tlagen_co", "*.hsaco")))
+    assert len(cos) >= 10, "build() prebuilds the generated specs' code objects"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_isa.py"), *cos], capture_output=True, text=True)
+    ks = json.loads(r.stdout)
+    assert sum(k.endswith(":tlg_expand_k") for k in ks) == len(cos)
+    bad = {k: v for k, v in ks.items() if v["long_branches"] or v["smem_store_hazards"]}
+    assert not bad and r.returncode == 0, bad
+
+
 PUNCT_CWCL = os.path.join(CONFIGS, "scen_CommitWhenConcurrentLeaders_punct.cfg")
 
 
