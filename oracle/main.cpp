@@ -13,6 +13,7 @@
 // ============================================================================
 #include <iostream>
 
+#include "raft_dricketts.h"
 #include "raft_membership.h"
 #include "raft_original.h"
 #include "tla_parse.h"
@@ -35,6 +36,7 @@ static std::string json_str(const std::string& s) {
 static std::string detect_spec(const std::string& text) {
   if (text.find("raftmc-base: thirdparty/raft_original.tla") != std::string::npos) return "original";
   if (text.find("raftmc-base: tlc_membership/raft.tla") != std::string::npos) return "membership";
+  if (text.find("raftmc-base: thirdparty/raft_dricketts.tla") != std::string::npos) return "ricketts";
   if (text.find("VARIABLE elections") != std::string::npos && text.find("VARIABLE allLogs") != std::string::npos) return "original";
   if (text.find("NextAsyncCrash") != std::string::npos) return "membership";
   throw EvalError("unrecognised spec module");
@@ -76,6 +78,7 @@ int main(int argc, char** argv) {
     Cfg cfg = parse_cfg(read_file(cfgp));
     std::unique_ptr<Spec> sp;
     if (family == "original") sp.reset(new RaftOriginal(cfg));
+    else if (family == "ricketts") sp.reset(new RaftRicketts(cfg));
     else {
       auto* m = new RaftMembership(cfg);
       if (!gc.empty()) m->golden_cwcl = load_golden_global(gc);

@@ -194,7 +194,9 @@ struct Gen {
     auto id = std::make_shared<Node>(fc);
     id->k = K::Ident; id->s = fc.binds[0].names[0]; id->a.clear(); id->binds.clear();
     in->a = {id, fc.binds[0].set};
-    return "if (!truth(A, " + ex(in, inner) + ")) { A.err |= E_DOMAIN; return 0u; }\n return " + ex(fc.a[0], inner) + ";\n";
+    return "if (!truth(A, " + ex(in, inner) + ")) { A.err |= E_DOMAIN; return 0u; }\n"
+           " if (A.rdepth >= kMaxRecDepth) { A.err |= E_UNSUP; return 0u; }\n"
+           " ++A.rdepth; const u32 r_ = " + ex(fc.a[0], inner) + ";\n --A.rdepth; return r_;\n";
   }
   std::string rec_call(const Sym& s, const std::string& arg) {
     return s.cxx + "(" + s.cxx + ", " + arg + ")";   // a generic lambda that receives itself

@@ -80,6 +80,9 @@ std::string lib_dir() {
 }
 
 const char* kOpts[] = {"--offload-arch=gfx950", "-O2", "-std=c++17"};
+// per-lane stack of a kernel that evaluates recursive function definitions (tlv::kMaxRecDepth
+// nested calls of a few hundred bytes each, over the kernel's own frame)
+constexpr size_t kRecStackBytes = 16384;
 
 #define HIPOK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { err = std::string(#x) + ": " + hipGetErrorString(e_); return MC_E_NO_DEVICE; } } while (0)
 
@@ -293,6 +296,11 @@ struct TlagenBackend : Backend {
       }
     } sc;
     size_t sort_bytes = 0;
+    // A spec with a recursive function definition compiles to kernels whose stack size the
+    // compiler cannot bound (dynamic stack): give each lane room for tlv::kMaxRecDepth nested
+    // calls (the generated code refuses deeper recursion with an evaluation error), instead of the
+    // runtime's default, which the static part of such a kernel's frame already exceeds.
+    if (src.find("kMaxRecDepth) {") != std::string::npos) HIPOK(hipDeviceSetLimit(hipLimitStackSize, kRecStackBytes));
     HIPOK(hipModuleLoadData(&sc.mod, image.data()));
     hipFunction_t f_init, f_expand, f_keys, f_mat, f_stop;
     HIPOK(hipModuleGetFunction(&f_init, sc.mod, "tlg_init_k"));

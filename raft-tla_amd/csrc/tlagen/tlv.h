@@ -63,14 +63,18 @@ struct Ar {
   u32 err;
   const u32* akey;   // per atom id: AK_MV bit for model values, then its rank in TLC's order (generated)
   u32 nakey;
+  u32 rdepth;        // calls of recursive function definitions in progress (bounded: kMaxRecDepth)
 };
+// deepest recursion of a recursive function definition a lane evaluates (deeper: E_UNSUP).  The
+// kernels' stack is sized for it (tlagen_backend.cpp kRecStackBytes).
+constexpr u32 kMaxRecDepth = 48;
 enum : u32 { AK_MV = 1u << 30 };
 
 TLV_HD u32 hdr(u32 tag, u32 n) { return tag | (n << 3); }
 TLV_HD u32 tg(const Ar& a, u32 v) { return a.w[v] & 7u; }
 TLV_HD u32 sz(const Ar& a, u32 v) { return a.w[v] >> 3; }
 TLV_HD void init(Ar& a, u32* w, u32 cap, u32* hs, u32 hcap) {
-  a.w = w; a.cap = cap; a.hs = hs; a.hcap = hcap; a.htop = 0; a.err = 0; a.akey = nullptr; a.nakey = 0;
+  a.w = w; a.cap = cap; a.hs = hs; a.hcap = hcap; a.htop = 0; a.err = 0; a.akey = nullptr; a.nakey = 0; a.rdepth = 0;
   w[0] = hdr(T_BOOL, 2); w[1] = 0; w[2] = hdr(T_BOOL, 2); w[3] = 1; a.top = 4;
 }
 TLV_HD u32 alloc(Ar& a, u32 n) {
@@ -430,23 +434,46 @@ TLV_NI u32 permutations(Ar& a, u32 s) {
   return set_end(a, outer);
 }
 // v with every atom in DOMAIN pi renamed to pi[atom] (sets and function domains re-sorted); a
-// value that contains no renamed atom comes back as the same handle (nothing is rebuilt)
+// value that contains no renamed atom comes back as the same handle (nothing is rebuilt).
+// Iterative over an explicit stack of collections being rebuilt: a recursive device function
+// makes the kernel's stack size dynamic, and the GPU's default per-lane stack does not hold a
+// state's nesting (messages -> record -> log -> entry ...).
 TLV_NI u32 perm_value(Ar& a, u32 v, u32 pi) {
-  const u32 t = tg(a, v);
-  if (t == T_BOOL || t == T_INT) return v;
-  if (t == T_ATOM) { const u32 r = lookup(a, pi, v); return r ? r : v; }
-  const u32 n = count(a, v), mark = a.htop;
-  bool changed = false;
-  u32 e = first(v);
-  for (u32 i = 0; i < n * (t == T_FUN ? 2u : 1u); ++i, e = nextv(a, e)) {
-    const u32 r = perm_value(a, e, pi);
-    changed |= r != e;
-    hpush(a, r);
+  struct Fr { u32 v, left, e, mark, changed; };   // left: element handles still to visit
+  constexpr int D = 24;
+  Fr st[D];
+  int sp = 0;
+  u32 x = v;   // the value to rename next
+  for (;;) {
+    const u32 t = tg(a, x);
+    u32 r = x;   // x renamed, once known
+    bool done = true;
+    if (t == T_ATOM) {
+      const u32 q = lookup(a, pi, x);
+      r = q ? q : x;
+    } else if (t == T_SEQ || t == T_FUN || t == T_SET) {
+      const u32 n = count(a, x) * (t == T_FUN ? 2u : 1u);
+      if (n > 0) {
+        if (sp == D) { a.err |= E_UNSUP; return v; }   // (nesting deeper than any spec value)
+        st[sp++] = Fr{x, n, first(x), a.htop, 0u};
+        x = first(x);
+        done = false;
+      }
+    }
+    if (!done) continue;
+    // r is the renamed x: hand it to the enclosing collections, closing each that is complete
+    for (;;) {
+      if (sp == 0) return r;
+      Fr& f = st[sp - 1];
+      f.changed |= r != f.e ? 1u : 0u;
+      hpush(a, r);
+      if (--f.left > 0) { f.e = nextv(a, f.e); x = f.e; break; }
+      const u32 tf = tg(a, f.v);
+      if (!f.changed) { a.htop = f.mark; r = f.v; }
+      else r = tf == T_SET ? set_end(a, f.mark) : tf == T_FUN ? fun_end(a, f.mark) : seq_end(a, f.mark);
+      --sp;
+    }
   }
-  if (!changed) { a.htop = mark; return v; }
-  if (t == T_SET) return set_end(a, mark);
-  if (t == T_FUN) return fun_end(a, mark);
-  return seq_end(a, mark);
 }
 
 // ---- the standard Bags module (a bag: a function from elements to positive counts)
