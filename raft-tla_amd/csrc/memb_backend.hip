@@ -206,6 +206,9 @@ __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
   S::unpack(w, s);
   u32 err = 0;
   S::template apply<TLC>(s, k, sub, t, err, a.rt);
+#ifdef RMC_FP_DUP_APPLY   // timing experiment: the re-derivation twice
+  { W t2; u32 e2 = 0; int k2 = k; asm volatile("" : "+v"(k2)); S::template apply<TLC>(s, k2, sub, t2, e2, a.rt); asm volatile("" :: "v"((u32)t2.hr0), "v"(t2.term), "v"(e2)); }
+#endif
   a.cand[cell] = TLC ? S::fingerprint_tlc(t, a.seed, a.rt) : S::fingerprint_orbit(t, a.seed, a.rt);
   }
 }

@@ -1727,6 +1727,12 @@ struct Memb {
     for (int q = 0; q < MK; ++q) { base[q * stride] = t.bag.v[q]; len += t.bag.v[q] != EMPTY; }
     const u32 pi = tlc_min_perm(t, BagRef{base, stride}, len, ce, rt.cfg_type);
     const u64 best = ce ? view_hash1<true>(t, pi, seed, rt.cfg_type) : view_hash1<false>(t, pi, seed, rt.cfg_type);
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RMC_FP_DUP_MINPERM)   // timing experiment: the search twice
+    { int l2 = len; asm volatile("" : "+v"(l2)); const u32 p2 = tlc_min_perm(t, BagRef{base, stride}, l2, ce, rt.cfg_type); asm volatile("" :: "v"(p2)); }
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && defined(RMC_FP_DUP_VIEW)      // timing experiment: the view hash twice
+    { u32 p2 = pi; asm volatile("" : "+v"(p2)); const u64 b2 = ce ? view_hash1<true>(t, p2, seed, rt.cfg_type) : view_hash1<false>(t, p2, seed, rt.cfg_type); asm volatile("" :: "v"((u32)b2), "v"((u32)(b2 >> 32))); }
+#endif
     const u64 fp = fmix(best ^ seed);
     return fp ? fp : 1ull;
   }

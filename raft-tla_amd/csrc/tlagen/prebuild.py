@@ -25,6 +25,8 @@ SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing
           ("countdown_evalerr", "configs/tlagen/Countdown.tla", "configs/tlagen/Countdown_evalerr.cfg"),
           ("ricketts_c1", "configs/ricketts_mc.tla", "configs/ricketts_c1.cfg"),
           ("ricketts_noleader", "configs/ricketts_mc.tla", "configs/ricketts_noleader.cfg"),
+          ("ricketts_election_safety", "configs/ricketts_mc.tla", "configs/ricketts_election_safety.cfg"),
+          ("ricketts_safety", "configs/ricketts_mc.tla", "configs/ricketts_safety.cfg"),
           ("toy_ring_view", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing_view.cfg"),
           ("rec_fun", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun.cfg"),
           ("rec_fun_fact", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_fact.cfg"),
@@ -34,6 +36,9 @@ SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing
           ("memb_nosym_gen", "configs/raft_membership_mc.tla", "configs/memb_nosym.cfg"),
           ("memb_shipped_gen", "configs/raft_membership_mc.tla", "configs/membership_shipped.cfg"),
           ("memb_two_gen", "configs/raft_membership_mc.tla", "configs/memb_two.cfg"),
+          # the punctuated searches: golden-trace prefix constraints, an ACTION_CONSTRAINT
+          ("memb_morc_gen", "configs/raft_membership_mc.tla", "configs/scen_MajorityOfClusterRestarts_punct.cfg"),
+          ("memb_cwcl_gen", "configs/raft_membership_mc.tla", "configs/scen_CommitWhenConcurrentLeaders_punct.cfg"),
           # the reference's Apalache spec with its own shipped cfg (TLC syntax): recursive Sum
           ("apalache_nm", REF + "/apalache_no_membership/raft.tla", REF + "/apalache_no_membership/raft.cfg")]
 

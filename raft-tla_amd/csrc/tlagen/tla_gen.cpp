@@ -287,6 +287,56 @@ struct Gen {
     return set_loop(setx, el, body, restore);
   }
 
+  // ---- outlining of large constructors: a sequence / set / record literal of many nodes (the
+  // golden TLC traces pasted into tlc_membership/raft.tla:1201,1231 are ~2K nodes) built inline
+  // would make one function larger than the short-branch range; each element then becomes a
+  // function of its own, taking the bound values it reads as arguments
+  static size_t node_count(const NP& e) {
+    if (!e) return 0;
+    size_t k = 1;
+    for (auto& c : e->a) k += node_count(c);
+    for (auto& b : e->binds) k += node_count(b.set);
+    for (auto& u : e->ups) { k += node_count(u.rhs); for (auto& st : u.path) k += node_count(st.idx); }
+    for (auto& d : e->defs) k += node_count(d->body);
+    return k;
+  }
+  static bool has_at(const NP& e) {
+    if (!e) return false;
+    if (e->k == K::At) return true;
+    for (auto& c : e->a) if (has_at(c)) return true;
+    for (auto& b : e->binds) if (has_at(b.set)) return true;
+    for (auto& u : e->ups) { if (has_at(u.rhs)) return true; for (auto& st : u.path) if (has_at(st.idx)) return true; }
+    for (auto& d : e->defs) if (has_at(d->body)) return true;
+    return false;
+  }
+  static constexpr size_t kOutlineCtor = 160, kOutlineElem = 8;   // constructor / element node counts
+  std::string element(const NP& e, Scope& sc, bool big) {
+    if (!big || node_count(e) < kOutlineElem || has_at(e)) return ex(e, sc);
+    std::vector<std::pair<std::string, const Sym*>> used;   // innermost binding of each name e reads
+    std::set<std::string> seen;
+    for (auto it = sc.rbegin(); it != sc.rend(); ++it) {
+      if (!seen.insert(it->first).second || !mentions(e, it->first)) continue;
+      if (it->second.kind != Sym::Val) return ex(e, sc);   // a LET operator / recursive function: inline
+      used.push_back({it->first, &it->second});
+    }
+    const std::string fn = "lit_" + std::to_string(fn_protos.size());
+    std::string sig = "TLV_NI u32 " + fn + "(Cx& c", call = fn + "(c";
+    Scope inner;
+    for (size_t i = 0; i < used.size(); ++i) {
+      Sym v = *used[i].second;
+      const std::string q = "q" + std::to_string(i);
+      sig += ", u32 " + q;
+      call += ", " + v.cxx;
+      v.cxx = q;
+      inner.push_back({used[i].first, v});
+    }
+    sig += ")";
+    const std::string body = ex(e, inner);
+    fn_protos.push_back(sig + ";");
+    fn_bodies.push_back(sig + " {\n  Ar& A = *c.A; (void)A;\n  return " + body + ";\n}\n");
+    return call + ")";
+  }
+
   // ---- expressions: a C++ expression yielding a value handle
   std::string ex(const NP& e, Scope& sc) {
     const Node& n = *e;
@@ -363,14 +413,16 @@ struct Gen {
       case K::SetEnum: {
         if (n.a.empty()) return "set_end(A, A.htop)";
         const std::string m = fresh("m");
+        const bool big = node_count(e) >= kOutlineCtor;
         std::string o = "[&]() -> u32 { const u32 " + m + " = A.htop;\n";
-        for (auto& a : n.a) o += " hpush(A, " + ex(a, sc) + ");\n";
+        for (auto& a : n.a) o += " hpush(A, " + element(a, sc, big) + ");\n";
         return o + " return set_end(A, " + m + ");\n}()";
       }
       case K::Tuple: {
         const std::string m = fresh("m");
+        const bool big = node_count(e) >= kOutlineCtor;
         std::string o = "[&]() -> u32 { const u32 " + m + " = A.htop;\n";
-        for (auto& a : n.a) o += " hpush(A, " + ex(a, sc) + ");\n";
+        for (auto& a : n.a) o += " hpush(A, " + element(a, sc, big) + ");\n";
         return o + " return seq_end(A, " + m + ");\n}()";
       }
       case K::SetFilter: case K::SetMap: {
@@ -412,11 +464,12 @@ struct Gen {
       case K::Dot: return "apply(A, " + ex(n.a[0], sc) + ", mk_atom(A, " + std::to_string(str_atom(n.s)) + "u))";
       case K::Record: {
         const std::string m = fresh("m");
+        const bool big = node_count(e) >= kOutlineCtor;
         std::string o = "[&]() -> u32 { const u32 " + m + " = A.htop;\n";
         for (size_t i = 0; i < n.fields.size(); ++i) {
           const std::string kv = fresh("k");
           o += " { const u32 " + kv + " = mk_atom(A, " + std::to_string(str_atom(n.fields[i])) + "u); const u32 v_ = " +
-               ex(n.a[i], sc) + "; hpush(A, " + kv + "); hpush(A, v_); }\n";
+               element(n.a[i], sc, big) + "; hpush(A, " + kv + "); hpush(A, v_); }\n";
         }
         return o + " return fun_end(A, " + m + ");\n}()";
       }
@@ -757,7 +810,6 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
   Generated out;
   out.variables = prog.variables;
   if (prog.variables.size() > 64) throw CfgError(MC_E_UNSUPPORTED, "more than 64 state variables");
-  if (!cfg.action_constraints.empty()) throw CfgError(MC_E_UNSUPPORTED, "ACTION_CONSTRAINTS on the generated path");
   // a model with temporal properties must not report "No error has been found" without checking them
   if (!cfg.properties.empty()) throw CfgError(MC_E_UNSUPPORTED, "temporal PROPERTIES are not supported");
   std::ostringstream consts;
@@ -787,11 +839,24 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
     out.constraints.push_back(n);
   }
   cons += "  return true;\n}\n";
+  // ACTION_CONSTRAINTS: predicates of a transition (c.cur the parent, c.nxt the successor, every
+  // variable assigned); a successor is in the model when the state constraints and these hold
+  // (the oracle's in_model && in_actions, oracle/engine.h)
+  cons += "TLV_NI bool action_constraints(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
+  for (auto& n : cfg.action_constraints) {
+    auto d = g.cfg_def(n, "ACTION_CONSTRAINT");
+    Scope s0;
+    cons += "  if (!truth(A, " + g.ex(d->body, s0) + ")) return false;\n";
+    out.constraints.push_back(n);
+  }
+  cons += "  return true;\n}\n";
   std::string invs = "TLV_NI int invariants(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
   for (size_t i = 0; i < cfg.invariants.size(); ++i) {
     auto d = g.cfg_def(cfg.invariants[i], "INVARIANT");
     Scope s0;
-    invs += "  if (!truth(A, " + g.ex(d->body, s0) + ")) return " + std::to_string(i) + ";\n";
+    // an invariant whose evaluation fails (TLC: "Evaluating invariant X failed") is the one
+    // returned, with the error bits set: the caller reports EVAL_ERROR naming it
+    invs += "  if (!truth(A, " + g.ex(d->body, s0) + ") || A.err) return " + std::to_string(i) + ";\n";
     out.invariants.push_back(cfg.invariants[i]);
   }
   invs += "  return -1;\n}\n";
@@ -829,7 +894,7 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
   s << "struct Cx { Ar* A; u32 k[" << std::max<size_t>(1, prog.constants.size() + g.cache_slot.size()) << "]; u32 cur[" << std::max<size_t>(1, prog.variables.size())
     << "]; u32 nxt[" << std::max<size_t>(1, prog.variables.size()) << "]; unsigned long long asg; int act; };\n";
   for (auto& p : g.fn_protos) s << p << "\n";
-  s << "TLV_NI bool constraints(Cx& c);\nTLV_NI int invariants(Cx& c);\nTLV_NI u32 view(Cx& c);\nTLV_NI u32 symmetry(Cx& c);\n";
+  s << "TLV_NI bool constraints(Cx& c);\nTLV_NI bool action_constraints(Cx& c);\nTLV_NI int invariants(Cx& c);\nTLV_NI u32 view(Cx& c);\nTLV_NI u32 symmetry(Cx& c);\n";
   for (auto& b : g.fn_bodies) s << b;
   // atoms in TLC's order (tlv ocmp): strings by text, model values by name (s1 < s2 < ..., the
   // declaration order of the cfg's model values), model values after strings

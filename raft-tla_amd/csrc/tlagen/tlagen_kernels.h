@@ -162,7 +162,9 @@ struct Em {
     const bool keyed = a->fifo && parent != ~0ull;   // FIFO pass 1 (initial states: stored at once)
     ++gen;
     ++act_gen[c.act];
-    const bool im = tlg::constraints(d);
+    // in the model: the state constraints, then (a transition, not an initial state) the action
+    // constraints over (parent, successor)
+    const bool im = tlg::constraints(d) && (parent == ~0ull || tlg::action_constraints(c));
     if (A.err) {   // a constraint could not be evaluated on this successor: TLC's evaluation error
       error_event(A, key, keyed);
       A.top = t0;

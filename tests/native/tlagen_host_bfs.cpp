@@ -27,6 +27,7 @@ struct Succ { std::vector<u32> w, key; int act; bool im, cerr; };   // key: the 
 
 struct Emit {
   std::vector<Succ>* out;
+  bool init;   // initial states: no transition, no action constraints
   void operator()(tlg::Cx& c) {
     tlv::Ar& A = *c.A;
     const u32 t0 = A.top;
@@ -34,7 +35,7 @@ struct Emit {
     for (int i = 0; i < tlg::NV; ++i) d.cur[i] = c.nxt[i];
     Succ s;
     const u32 e0 = A.err;
-    s.im = tlg::constraints(d);
+    s.im = tlg::constraints(d) && (init || tlg::action_constraints(c));
     s.cerr = A.err != e0;   // a constraint could not be evaluated: TLC's evaluation error
     A.err = e0;
     for (int i = 0; i < tlg::NV; ++i) { const u32 h = c.nxt[i]; s.w.insert(s.w.end(), A.w + h, A.w + h + tlv::sz(A, h)); }
@@ -148,7 +149,7 @@ int main(int argc, char** argv) {
   };
   {
     std::vector<Succ> init;
-    Emit em{&init};
+    Emit em{&init, true};
     A.top = floor;
     tlg::init_states(c, em);
     err |= A.err;
@@ -168,7 +169,7 @@ int main(int argc, char** argv) {
     next.clear();
     for (size_t fi = 0; fi < frontier.size() && verdict == "OK"; ++fi) {
       std::vector<Succ> succ;
-      Emit em{&succ};
+      Emit em{&succ, false};
       A.top = floor;
       A.err = 0;
       load(c, all[frontier[fi]]);

@@ -103,18 +103,53 @@ def test_generated_deadlock_and_eval_error(raftmc, cfg, verdict, depth, code):
 
 def test_ricketts_on_gpu(raftmc):
     """thirdparty/raft_dricketts.tla (Bags module, TLAPS-only in the reference) through the generated
-    path to depth 12: the host build's counts (tests/test_tlagen.py, parity unpinned), and NoLeader's
-    depth."""
-    from test_tlagen import RICKETTS_D12
+    path, pinned by the oracle's restatement (tests/golden/ricketts_oracle.json): to depth 12 with
+    per-action counts; NoLeader's counterexample and ElectionSafety's evaluation error (Max({}))
+    with TLC's counters at the stop point and the oracle's trace; the whole space of ricketts_safety
+    (1,943,913 states, depth 53) with its three election/log invariants holding."""
+    from test_gpu import trace_states
+    from test_tlagen import RICKETTS, generated_actions
+    g = RICKETTS["c1_d12"]
     with raftmc.ModelChecker(gen_source("ricketts_c1"), os.path.join(CONFIGS, "ricketts_c1.cfg"), frontend="generated",
-                             workers=0, max_depth=12, **SMALL) as mc:
+                             workers=1, max_depth=12, **SMALL) as mc:
         r = mc.run()
     assert r.verdict == "DEPTH_LIMIT", r.error
-    assert (r.generated, r.distinct, [lv[0] for lv in r.levels]) == (RICKETTS_D12["generated"], RICKETTS_D12["distinct"], RICKETTS_D12["levels"])
-    with raftmc.ModelChecker(gen_source("ricketts_noleader"), os.path.join(CONFIGS, "ricketts_noleader.cfg"), frontend="generated",
-                             workers=0, **SMALL) as mc:
+    assert (r.generated, r.distinct, [lv[0] for lv in r.levels]) == (g["generated"], g["distinct"], g["levels"])
+    assert generated_actions({k: list(v) for k, v in r.actions.items()}) == g["actions"]
+    for case, verdict, violated in (("noleader", "INVARIANT_VIOLATION", "NoLeader"), ("election_safety", "EVAL_ERROR", "ElectionSafety")):
+        g = RICKETTS[case]
+        for workers in (1, 0):   # -workers N: the event is searched again in FIFO order
+            with raftmc.ModelChecker(gen_source("ricketts_" + case), os.path.join(CONFIGS, g["cfg"] + ".cfg"), frontend="generated",
+                                     workers=workers, **SMALL) as mc:
+                r = mc.run()
+            assert (r.verdict, r.violated, r.depth) == (verdict, violated, g["depth"]), r.error
+            assert (r.generated, r.distinct, r.left_on_queue) == (g["generated"], g["distinct"], g["left_on_queue"])
+            assert [x for _, x in trace_states(r)] == [t["state"] for t in g["trace"]]
+    g = RICKETTS["safety"]
+    with raftmc.ModelChecker(gen_source("ricketts_safety"), os.path.join(CONFIGS, "ricketts_safety.cfg"), frontend="generated",
+                             workers=1, fp_table_bytes=1 << 28, state_store_bytes=8 << 30) as mc:
         r = mc.run()
-    assert (r.verdict, r.violated, r.depth) == ("INVARIANT_VIOLATION", "NoLeader", 10)
+    assert r.verdict == "OK", r.error
+    assert (r.generated, r.distinct, r.depth, [lv[0] for lv in r.levels]) == (g["generated"], g["distinct"], g["depth"], g["levels"])
+    assert generated_actions({k: list(v) for k, v in r.actions.items()}) == g["actions"]
+
+
+@pytest.mark.parametrize("case,gen", [("punct_MajorityOfClusterRestarts", "memb_morc_gen"),
+                                      ("punct_CommitWhenConcurrentLeaders", "memb_cwcl_gen")])
+def test_generated_punctuated_search_on_gpu(raftmc, case, gen):
+    """The reference's punctuated searches on the unmodified tlc_membership/raft.tla through the
+    generated path: the golden-trace prefix constraints of raft.tla:1198-1234 and (CWCL) the
+    ACTION_CONSTRAINT CommitWhenConcurrentLeaders_action_constraint, in TLC's FIFO order: TLC's
+    counters at the stop point and the counterexample state by state equal the oracle's."""
+    from test_gpu import trace_states
+    from test_tlagen import strip_history_global
+    g = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))[case]
+    with raftmc.ModelChecker(gen_source(gen), os.path.join(CONFIGS, g["cfg"] + ".cfg"), frontend="generated", workers=1,
+                             deadlock=False, **SMALL) as mc:
+        r = mc.run()
+    assert (r.verdict, r.violated, r.depth, r.distinct) == (g["verdict"], g["violated"], g["depth"], g["distinct"]), r.error
+    assert 0 <= r.generated - g["generated"] <= g["actions"]["HandleCheckOldConfig"][0]
+    assert [strip_history_global(x) for _, x in trace_states(r)] == [t["state"] for t in g["trace"]]
 
 
 def test_generated_fifo_trace_equals_oracle(raftmc):

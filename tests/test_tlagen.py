@@ -245,29 +245,72 @@ def test_countdown_verdicts(cfg, verdict, depth):
     assert (r["verdict"], r["depth"], r["distinct"]) == (verdict, depth, depth)
 
 
+def strip_history_global(state_line):
+    """The oracle's membership state text leaves out history["global"] (its dump_line; the record
+    it keeps per state is the rank summary, oracle/raft_membership.h): drop the field to compare."""
+    a = state_line.index("global |-> ")
+    b = state_line.index(", hadNumClientRequests", a)
+    return state_line[:a] + state_line[b + 2:]
+
+
+@needs_tool
+@needs_ref
+def test_generated_punctuated_search():
+    """The reference's punctuated search (tlc_membership/raft.tla:1212-1234): the state constraint
+    MajorityOfClusterRestarts_constraint holds history["global"] to a prefix of the golden TLC trace
+    pasted into raft.tla itself, evaluated by the generated code from the spec's own text (IsPrefix,
+    SubSeq, \\E over three servers).  TLC's counters at the stop point and the counterexample, state by
+    state, equal the oracle's (tests/golden/memb_parity.json); the GPU test adds the
+    CommitWhenConcurrentLeaders search, whose cfg also has an ACTION_CONSTRAINT."""
+    g = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))["punct_MajorityOfClusterRestarts"]
+    r = host_bfs(generate(os.path.join(CONFIGS, "raft_membership_mc.tla"), os.path.join(CONFIGS, g["cfg"] + ".cfg")),
+                 "--no-deadlock", "--trace")
+    assert (r["verdict"], r["violated"], r["generated"], r["distinct"], r["depth"]) == \
+        (g["verdict"], g["violated"], g["generated"], g["distinct"], g["depth"])
+    assert [strip_history_global(x) for x in r["trace"]] == [t["state"] for t in g["trace"]]
+
+
 # Ricketts' spec (thirdparty/raft_dricketts.tla, TLAPS-proved, no TLC cfg in the reference) on the
-# generated path through configs/ricketts_mc.tla: the oracle has no restatement of it, so these
-# counts are the host build's of the generated code ("parity unpinned"); the GPU test holds the
-# GPU kernels to the same numbers.
-RICKETTS_D12 = dict(generated=538450, distinct=68004, levels=[1, 3, 15, 61, 195, 483, 985, 2181, 5019, 9747, 16557, 32757])
+# generated path through configs/ricketts_mc.tla, pinned by the oracle's hand restatement of it
+# (oracle/raft_dricketts.h; tests/golden/ricketts_oracle.json, tests/golden/make_ricketts_oracle.py).
+RICKETTS = json.load(open(os.path.join(GOLDEN, "ricketts_oracle.json")))
+RICKETTS_D12 = {k: RICKETTS["c1_d12"][k] for k in ("generated", "distinct", "levels")}
+
+
+def generated_actions(acts):
+    """The generated path's per-action counts without the never-taken entry "Next" (the action name
+    TLC gives a Next with no split point; Ricketts' Next is a disjunction, so it never fires)."""
+    return {k: v for k, v in acts.items() if not (k == "Next" and v == [0, 0])}
 
 
 @needs_tool
 @needs_ref
 def test_ricketts_depth_limited():
+    """To depth 12: generated, distinct, level sizes and per-action (generated, distinct) counts.
+    Ricketts' Next is a disjunction: TLC splits it into its actions; inside Receive, UpdateTerm(i, j, m)
+    is a disjunct of its own, `m.mtype = .. /\\ Handle..(i, j, m)` is a conjunction (named Receive) --
+    the oracle counts its handlers under the same names."""
+    g = RICKETTS["c1_d12"]
     r = host_bfs(generate(os.path.join(CONFIGS, "ricketts_mc.tla"), os.path.join(CONFIGS, "ricketts_c1.cfg")), "--max-depth", "12")
     assert (r["verdict"], r["err"]) == ("DEPTH_LIMIT", 0)
     assert {k: r[k] for k in RICKETTS_D12} == RICKETTS_D12
-    # Ricketts' Next is a disjunction: TLC splits it into its actions; inside Receive, UpdateTerm(i, j, m)
-    # is a disjunct of its own, `m.mtype = .. /\ Handle..(i, j, m)` is a conjunction (named Receive)
-    assert {"Restart", "Timeout", "RequestVote", "BecomeLeader", "Receive", "UpdateTerm", "DropMessage"} <= set(r["actions"])
+    assert generated_actions(r["actions"]) == g["actions"]
 
 
 @needs_tool
 @needs_ref
-def test_ricketts_noleader():
-    r = host_bfs(generate(os.path.join(CONFIGS, "ricketts_mc.tla"), os.path.join(CONFIGS, "ricketts_noleader.cfg")))
-    assert (r["verdict"], r["violated"], r["depth"]) == ("INVARIANT_VIOLATION", "NoLeader", 10)
+@pytest.mark.parametrize("case,verdict,violated", [("noleader", "INVARIANT_VIOLATION", "NoLeader"),
+                                                   ("election_safety", "EVAL_ERROR", "ElectionSafety")])
+def test_ricketts_stop_points(case, verdict, violated):
+    """NoLeader's counterexample, and ElectionSafety's evaluation error (Max({}) = CHOOSE over the
+    empty set, raft_dricketts.tla:106-108, once a leader has no entry of its own term,
+    :1123-1128): both at the first leader, depth 10, with the oracle's trace state by state and
+    distinct count at the stop point."""
+    g = RICKETTS[case]
+    r = host_bfs(generate(os.path.join(CONFIGS, "ricketts_mc.tla"), os.path.join(CONFIGS, g["cfg"] + ".cfg")), "--trace")
+    assert (r["verdict"], r["violated"], r["depth"]) == (verdict, violated, g["depth"])
+    assert (g["verdict"], g["distinct"]) == (verdict, r["distinct"])
+    assert r["trace"] == [t["state"] for t in g["trace"]]
 
 
 @needs_tool
