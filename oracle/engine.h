@@ -14,6 +14,7 @@
 //   FIFO order         (v)   single worker, level order, TLC action order
 // ============================================================================
 #pragma once
+#include <cstdlib>
 #include <atomic>
 #include <cstring>
 #include <chrono>
@@ -407,6 +408,10 @@ inline Result bfs(const Spec& sp, const Cfg& cfg, const Options& o) {
               nextf.push_back((int64_t)store.size() - 1);
               r.act_distinct[su.action]++;
               if (dump) std::fprintf(dump, "%s\n", sp.dump_line(su.s).c_str());
+              // debugging aid: ORACLE_FIND=<state text> prints that state's parent and action
+              static const char* find_text = std::getenv("ORACLE_FIND");
+              if (find_text && sp.dump_line(su.s) == find_text)
+                std::fprintf(stderr, "FOUND via %s from\n%s\n", sp.action_names()[su.action].c_str(), sp.dump_line(cur).c_str());
             }
           }
           if (isnew || (!im && o.inv_out_of_model)) {

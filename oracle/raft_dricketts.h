@@ -11,7 +11,10 @@
 // Differences from raft_original.h that matter for the counts: `messages` is a Bags-module bag
 // (WithoutMessage drops an element whose count reaches 0, raft_dricketts.tla:92), no history
 // variables (elections, allLogs, voterLog), AppendEntries guards prevLogTerm and carries no mlog
-// (:171-192), and the invariants are the spec's own (:1032-1135).
+// (:171-192), AppendEntriesAlreadyDone's UNCHANGED covers commitIndex (below), and the invariants
+// are the spec's own (:1032-1135).  The AlreadyDone rule was first restated as in raft_original.h;
+// the whole-space comparison with the generated path (which follows TLC's reading of UNCHANGED)
+// found 6 states apart at depth 18, and TLC's semantics decide for the generated path.
 // ============================================================================
 #pragma once
 #include "engine.h"
@@ -207,7 +210,12 @@ struct RaftRicketts : Spec {
     if (mterm == ct && eq(st, Follower) && logOk) {                                                  // Accept (:333-341)
       int64_t index = pli + 1;
       V ents = ap(m, "mentries");
-      if (len(ents) == 0 || (len(li) >= index && eq(ap(ap(li, index), "term"), ap(ap(ents, 1), "term")))) {   // AlreadyDone (:301-317)
+      // AlreadyDone (:301-317).  It assigns commitIndex' and then asserts UNCHANGED <<serverVars,
+      // logVars>> with logVars == <<log, commitIndex>> (:51): under TLC that conjunct is a test of
+      // commitIndex' = commitIndex, so the step exists only when m.mcommitIndex equals the
+      // follower's commitIndex (Ongaro's raft_original.tla leaves commitIndex out of the UNCHANGED)
+      if ((len(ents) == 0 || (len(li) >= index && eq(ap(ap(li, index), "term"), ap(ap(ents, 1), "term")))) &&
+          eq(ap(m, "mcommitIndex"), ap(s[commitIndex], i))) {
         State t = s;
         t[commitIndex] = except(s[commitIndex], i, ap(m, "mcommitIndex"));
         V resp = rec({{"mtype", AEResp}, {"mterm", Int(ct)}, {"msuccess", Bool(true)},

@@ -1284,7 +1284,7 @@ struct RouteArgs {
 };
 
 // Sharded route over the compacted records: workgroup b takes generate-workgroup b's records,
-// drops the successors its 256 parents produce more than once (an exact LDS set, LDS CAS), and
+// drops the successors its 256 parents produce more than once (the first-come LDS filter), and
 // buckets the rest by owner, 16 records per thread at a time: LDS histogram, one global atomic
 // per (workgroup, round, owner).  Records are (fp, state in chunk << 8 | instance).
 __global__ void __launch_bounds__(BS) orig_route_blk(RouteArgs a) {
@@ -1311,16 +1311,9 @@ __global__ void __launch_bounds__(BS) orig_route_blk(RouteArgs a) {
       fp[j] = i < n ? fps[at] : 0ull;
       const u32 lk = i < n ? keys[at] : 0u;
       slot[j] = (((u64)blockIdx.x * BS + (lk >> 8)) << 8) | (u64)(lk & 255u);
-      if (fp[j]) {   // produced before by this workgroup's parents?
-        u32 h = (u32)(fp[j] >> 20) & (LDS_FP_SLOTS - 1);
-#pragma unroll 1
-        for (int p = 0; p < 8; ++p) {
-          const unsigned long long cur = atomicCAS(&lds_fp[h], 0ull, (unsigned long long)fp[j]);
-          if (cur == 0ull) break;                    // first here
-          if (cur == fp[j]) { fp[j] = 0; break; }    // duplicate
-          h = (h + 1) & (LDS_FP_SLOTS - 1);
-        }
-      }
+      // produced before by this workgroup's parents?  The first-come filter of orig_dedup_plain
+      // (plain LDS loads and stores: a race only lets a duplicate through to its owner's seen-set)
+      if (fp[j] && !lds_first(lds_fp, fp[j])) fp[j] = 0;
       own[j] = fp[j] ? (int)fp_owner(fp[j], a.world) : -1;
       off[j] = own[j] >= 0 ? atomicAdd(&hist[own[j]], 1u) : 0u;
     }

@@ -62,6 +62,8 @@ CASES = {
     "tlc:memb_two@16": ("memb_two", 16),
     "tlc:memb_dynamic3@14": ("memb_dynamic3", 14),
     "tlc:memb_four@13": ("memb_four", 13),
+    # bench.py's membership scale workload (C3's model without LeaderVotesQuorum), depth-bounded
+    "tlc:memb_four_scale@15": ("memb_four_scale", 15),
     "tlc:scen_FirstCommit": ("scen_FirstCommit", 0),
     "tlc:punct_MajorityOfClusterRestarts@30": ("scen_MajorityOfClusterRestarts_punct", 30, "MajorityOfClusterRestarts_constraint"),
     # the NEXT relations on their own (raft.tla:909-916, :924-932) and the other verdict classes

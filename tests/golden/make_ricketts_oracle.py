@@ -11,7 +11,7 @@ must reproduce them on the host build of its generated code (tests/test_tlagen.p
     python tests/golden/make_ricketts_oracle.py [name ...]
 
 ricketts_safety (the whole space of 3 servers, term <= 2, log <= 1, one message in flight:
-1,943,913 states, depth 53) takes about 4 minutes on 6 threads.
+1,542,177 states, depth 49) takes about 4 minutes on 6 threads.
 """
 import json
 import os

@@ -3,10 +3,10 @@
 // (tests/test_tlagen.py).  It is the same code the GPU path compiles for gfx950; the GPU engine
 // is raft-tla_amd/csrc/tlagen/tlagen_kernels.h.
 //
-//   tlagen_host_bfs [--max-depth D] [--no-deadlock] [--trace]
+//   tlagen_host_bfs [--max-depth D] [--no-deadlock] [--trace] [--dump FILE]
 // prints {"verdict", "generated", "distinct", "depth", "levels", "actions", "violated", "err"}
 // (--trace: and "trace", the counterexample to a violating new state, one line per state, in the
-// format of the library's trace printer)
+// format of the library's trace printer; --dump: every kept state's text, one per line)
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -105,10 +105,12 @@ static void load(tlg::Cx& c, const std::vector<u32>& w) {
 int main(int argc, char** argv) {
   long long max_depth = 0;
   bool deadlock = true, want_trace = false;
+  const char* dump_path = nullptr;
   for (int i = 1; i < argc; ++i) {
     if (!std::strcmp(argv[i], "--max-depth") && i + 1 < argc) max_depth = std::atoll(argv[++i]);
     else if (!std::strcmp(argv[i], "--no-deadlock")) deadlock = false;
     else if (!std::strcmp(argv[i], "--trace")) want_trace = true;
+    else if (!std::strcmp(argv[i], "--dump") && i + 1 < argc) dump_path = argv[++i];
   }
   static u32 words[1 << 22], hs[1 << 16];
   tlv::Ar A;
@@ -200,6 +202,12 @@ int main(int argc, char** argv) {
     }
     if (!next.empty()) { ++depth; levels.push_back((long long)next.size()); }
     frontier.swap(next);
+  }
+  if (dump_path) {
+    if (std::FILE* f = std::fopen(dump_path, "w")) {
+      for (auto& w : all) std::fprintf(f, "%s\n", state_text(w).c_str());
+      std::fclose(f);
+    }
   }
   size_t nwords = 0;
   for (auto& w : seen) nwords += w.size();

@@ -266,7 +266,7 @@ def _memb_prefixes(g):
     return {con: tla_text(json.load(open(os.path.join(GOLDEN, fixture)))["value"])}
 
 
-@pytest.mark.parametrize("case,world", [("membership_shipped@14", 2), ("memb_dynamic3@14", 3), ("tlc:memb_four@13", 2),
+@pytest.mark.parametrize("case,world", [("membership_shipped@14", 2), ("memb_dynamic3@14", 3), ("tlc:memb_four@13", 2), ("tlc:memb_four_scale@15", 2),
                                         ("punct_MajorityOfClusterRestarts@30", 3)])
 def test_membership_native_loop_loopback(case, world, tmp_path):
     """The FIFO-ranked sharded level loop in C++ (csrc/fifo_shard_loop.h, what mc_shard_run_rccl runs

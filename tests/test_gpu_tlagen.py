@@ -106,7 +106,7 @@ def test_ricketts_on_gpu(raftmc):
     path, pinned by the oracle's restatement (tests/golden/ricketts_oracle.json): to depth 12 with
     per-action counts; NoLeader's counterexample and ElectionSafety's evaluation error (Max({}))
     with TLC's counters at the stop point and the oracle's trace; the whole space of ricketts_safety
-    (1,943,913 states, depth 53) with its three election/log invariants holding."""
+    (1,542,177 states, depth 49) with its three election/log invariants holding."""
     from test_gpu import trace_states
     from test_tlagen import RICKETTS, generated_actions
     g = RICKETTS["c1_d12"]
