@@ -1,8 +1,8 @@
 #!/bin/bash
 # full GPU suite; C3 (TLC's SYMMETRY mode) with the fingerprint's parts duplicated one at a time;
 # the sharded loop at world 1; the bench
-O=gpurun_out/r4i; mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+O=${OUT:-gpurun_out/r4i}; mkdir -p $O
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 $O/pytest.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 200 python -u scripts/memb_probe.py memb_four > $O/c3_base.jsonl 2>&1 || exit 1

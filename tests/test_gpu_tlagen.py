@@ -144,8 +144,9 @@ def test_generated_punctuated_search_on_gpu(raftmc, case, gen):
     from test_gpu import trace_states
     from test_tlagen import strip_history_global
     g = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))[case]
+    # states carry history["global"] (up to 28 records): ~6 KB of words each
     with raftmc.ModelChecker(gen_source(gen), os.path.join(CONFIGS, g["cfg"] + ".cfg"), frontend="generated", workers=1,
-                             deadlock=False, **SMALL) as mc:
+                             deadlock=False, fp_table_bytes=1 << 26, state_store_bytes=8 << 30) as mc:
         r = mc.run()
     assert (r.verdict, r.violated, r.depth, r.distinct) == (g["verdict"], g["violated"], g["depth"], g["distinct"]), r.error
     assert 0 <= r.generated - g["generated"] <= g["actions"]["HandleCheckOldConfig"][0]
