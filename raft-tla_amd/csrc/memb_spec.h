@@ -1674,29 +1674,49 @@ struct Memb {
       cand = cm; last = best; have_last = true; j0 = 1;
     }
 #endif
+    // Automorphic candidates (symmetric states: servers in the same role): when every remaining
+    // permutation maps the bag to the same function -- its permuted codes with their counts,
+    // compared by a sum of 64-bit mixes (the fingerprint's own collision class) -- the domain and
+    // count stages below tie for all of them: skipped (their cost is |cand| * len^2 code renamings)
+    bool bag_tie = false;
+    if (!single(cand)) {
+      u64 h0 = 0;
+      bag_tie = true;
 #pragma unroll 1
-    for (int j = j0; j == 0 || (j < len && !single(cand)); ++j) {   // (one pass even for an empty bag)
-      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); });
-      last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
-      have_last = true;
-#ifdef RMC_TLC_DEDUP
-      if (j == 0 && !single(cand) && popc32(cand) <= 8) cand = dedup_auto(t, cand, cfgt);
-#endif
+      for (u32 m = cand; m; m &= m - 1u) {
+        const u32 pi = perm_of(__builtin_ctz(m));
+        u64 h = 0;
+#pragma unroll 1
+        for (int q = 0; q < len; ++q) { const u64 e = bag[q]; h += fmix(((perm_code(mcode(e), pi, ce, cfgt) + 1ull) * P1) ^ (u64)mcount(e)); }
+        if (m == cand) h0 = h;
+        else if (h != h0) { bag_tie = false; break; }
+      }
     }
-    have_last = false;
+    if (!bag_tie) {
 #pragma unroll 1
-    for (int j = 0; j < len && !single(cand); ++j) {   // same permuted domain: the counts in domain order
-      const u64 code = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
-      cand = keep_min(cand, [&](int, u32 pi) {
-        u64 cnt = 0;
+      for (int j = j0; j == 0 || (j < len && !single(cand)); ++j) {   // (one pass even for an empty bag)
+        cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); });
+        last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+        have_last = true;
+#ifdef RMC_TLC_DEDUP
+        if (j == 0 && !single(cand) && popc32(cand) <= 8) cand = dedup_auto(t, cand, cfgt);
+#endif
+      }
+      have_last = false;
 #pragma unroll 1
-        for (int q = 0; q < len; ++q) {
-          const u64 e = bag[q];
-          if (perm_code(mcode(e), pi, ce, cfgt) == code) cnt = (u64)mcount(e);
-        }
-        return cnt;
-      });
-      last = code; have_last = true;
+      for (int j = 0; j < len && !single(cand); ++j) {   // same permuted domain: the counts in domain order
+        const u64 code = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+        cand = keep_min(cand, [&](int, u32 pi) {
+          u64 cnt = 0;
+#pragma unroll 1
+          for (int q = 0; q < len; ++q) {
+            const u64 e = bag[q];
+            if (perm_code(mcode(e), pi, ce, cfgt) == code) cnt = (u64)mcount(e);
+          }
+          return cnt;
+        });
+        last = code; have_last = true;
+      }
     }
     // history: [global, hadNum* (invariant), server], currentTerm, state, votedFor, log, commitIndex,
     // votesResponded, votesGranted, nextIndex, matchIndex — each a function over the servers, in

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cstdio>
 #include <functional>
 #include <map>
 #include <set>
@@ -137,6 +138,54 @@ struct Gen {
     visiting.erase(d->name);
     free_memo[d->name] = r;
     return r;
+  }
+
+  // the state variables an expression reads, a bit per variable, transitively through the
+  // definitions it uses; all bits for anything the analysis does not follow (primes, temporal
+  // operators, a definition without a body).  Names are matched without scopes, so a bound name
+  // that shadows a variable or definition only adds bits (conservative).  The kernels skip a
+  // constraint or invariant whose variables a successor left unchanged: its parent, which is in
+  // the model and satisfies every invariant, gives the same value.
+  std::map<std::string, unsigned long long> mask_memo;
+  bool mask_cycle = false;
+  unsigned long long var_mask(const NP& e, std::set<std::string>& visiting) {
+    if (!e) return 0;
+    if (e->k == K::Prime || e->k == K::Unchanged || e->k == K::Enabled || e->k == K::Temporal) return ~0ull;
+    unsigned long long m = 0;
+    if (e->k == K::Ident || e->k == K::OpApp || e->k == K::Binary) {
+      auto v = var_idx.find(e->s);
+      if (v != var_idx.end()) m |= 1ull << v->second;
+      else if (auto d = global(e->s)) {
+        if (!d->body) return ~0ull;
+        m |= def_mask(d, visiting);
+      }
+    }
+    for (auto& c : e->a) m |= var_mask(c, visiting);
+    for (auto& b : e->binds) m |= var_mask(b.set, visiting);
+    for (auto& u : e->ups) { m |= var_mask(u.rhs, visiting); for (auto& st : u.path) m |= var_mask(st.idx, visiting); }
+    for (auto& d : e->defs) m |= var_mask(d->body, visiting);
+    return m;
+  }
+  unsigned long long def_mask(const std::shared_ptr<Def>& d, std::set<std::string>& visiting) {
+    auto it = mask_memo.find(d->name);
+    if (it != mask_memo.end()) return it->second;
+    if (visiting.count(d->name)) { mask_cycle = true; return 0; }   // the enclosing visit covers the rest
+    const bool outer = visiting.empty();
+    if (outer) mask_cycle = false;
+    visiting.insert(d->name);
+    const unsigned long long m = var_mask(d->body, visiting);
+    visiting.erase(d->name);
+    if (!mask_cycle || outer) mask_memo[d->name] = m;   // a partial mask inside a cycle is not kept
+    return m;
+  }
+  std::string mask_of(const std::shared_ptr<Def>& d) {
+    std::set<std::string> visiting;
+    mask_cycle = false;
+    visiting.insert(d->name);
+    const unsigned long long m = var_mask(d->body, visiting);
+    char b[32];
+    std::snprintf(b, sizeof b, "0x%llxull", m);
+    return b;
   }
 
   // ---- a global operator as a C++ function (emitted once)
@@ -831,11 +880,14 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
   g.init_mode = false;
   const int next_label = g.action_id(out.next_name);
   const std::string next_body = g.act(nextd->body, sc, "if (c.asg == " + full + ") em(c); else A.err |= E_ASSIGN;\n", true, next_label);
-  std::string cons = "TLV_NI bool constraints(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
+  // chg: the variables the successor changed (a bit each; all for an initial state): a constraint
+  // or invariant reading none of them holds as it held for the parent (Gen::var_mask)
+  std::string cons = "TLV_NI bool constraints(Cx& c, unsigned long long chg) {\n  Ar& A = *c.A; (void)A; (void)chg;\n";
   for (auto& n : cfg.constraints) {
     auto d = g.cfg_def(n, "CONSTRAINT");
     Scope s0;
-    cons += "  if (!truth(A, " + g.ex(d->body, s0) + ")) return false;\n";
+    const std::string mk = d->params.empty() ? g.mask_of(d) : "~0ull";
+    cons += "  if ((chg & " + mk + ") && !truth(A, " + g.ex(d->body, s0) + ")) return false;\n";
     out.constraints.push_back(n);
   }
   cons += "  return true;\n}\n";
@@ -850,13 +902,14 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
     out.constraints.push_back(n);
   }
   cons += "  return true;\n}\n";
-  std::string invs = "TLV_NI int invariants(Cx& c) {\n  Ar& A = *c.A; (void)A;\n";
+  std::string invs = "TLV_NI int invariants(Cx& c, unsigned long long chg) {\n  Ar& A = *c.A; (void)A; (void)chg;\n";
   for (size_t i = 0; i < cfg.invariants.size(); ++i) {
     auto d = g.cfg_def(cfg.invariants[i], "INVARIANT");
     Scope s0;
     // an invariant whose evaluation fails (TLC: "Evaluating invariant X failed") is the one
     // returned, with the error bits set: the caller reports EVAL_ERROR naming it
-    invs += "  if (!truth(A, " + g.ex(d->body, s0) + ") || A.err) return " + std::to_string(i) + ";\n";
+    const std::string mk = d->params.empty() ? g.mask_of(d) : "~0ull";
+    invs += "  if ((chg & " + mk + ") && (!truth(A, " + g.ex(d->body, s0) + ") || A.err)) return " + std::to_string(i) + ";\n";
     out.invariants.push_back(cfg.invariants[i]);
   }
   invs += "  return -1;\n}\n";
@@ -894,7 +947,7 @@ Generated generate(const Program& prog, const CfgFile& cfg) {
   s << "struct Cx { Ar* A; u32 k[" << std::max<size_t>(1, prog.constants.size() + g.cache_slot.size()) << "]; u32 cur[" << std::max<size_t>(1, prog.variables.size())
     << "]; u32 nxt[" << std::max<size_t>(1, prog.variables.size()) << "]; unsigned long long asg; int act; };\n";
   for (auto& p : g.fn_protos) s << p << "\n";
-  s << "TLV_NI bool constraints(Cx& c);\nTLV_NI bool action_constraints(Cx& c);\nTLV_NI int invariants(Cx& c);\nTLV_NI u32 view(Cx& c);\nTLV_NI u32 symmetry(Cx& c);\n";
+  s << "TLV_NI bool constraints(Cx& c, unsigned long long chg = ~0ull);\nTLV_NI bool action_constraints(Cx& c);\nTLV_NI int invariants(Cx& c, unsigned long long chg = ~0ull);\nTLV_NI u32 view(Cx& c);\nTLV_NI u32 symmetry(Cx& c);\n";
   for (auto& b : g.fn_bodies) s << b;
   // atoms in TLC's order (tlv ocmp): strings by text, model values by name (s1 < s2 < ..., the
   // declaration order of the cfg's model values), model values after strings

@@ -139,32 +139,48 @@ struct Em {
   unsigned long long j;             // M_MAT: the next winner key of this parent
   unsigned long long act_gen[tlg::NACT > 0 ? tlg::NACT : 1], act_dist[tlg::NACT > 0 ? tlg::NACT : 1];
 
-  __device__ __attribute__((noinline)) void operator()(tlg::Cx& c) {
-    Ar& A = *c.A;
-    if (A.err) return;   // computed after an evaluation error: not a successor (the parent reports the error)
-    const unsigned long long o = ord++;   // this successor's ordinal in the parent's list
-    const u32 t0 = A.top;
-    u32 n = 0;
+  // the parent's per-variable fingerprint terms (expand_state), reused for the variables a
+  // successor leaves unchanged
+  unsigned long long ph[tlg::NV > 0 ? tlg::NV : 1];
+
+  // the successor's canonical words laid out contiguously at the arena top (only for a state that
+  // is stored or reported: the fingerprint and the checks work on the variables' own values)
+  __device__ bool layout(Ar& A, tlg::Cx& c, u32& w0, u32& n) {
+    n = 0;
     for (int i = 0; i < tlg::NV; ++i) n += sz(A, c.nxt[i]);
-    const u32 w0 = alloc(A, n);
-    if (A.err & E_OVF) return;
+    w0 = alloc(A, n);
+    if (A.err & E_OVF) return false;
     u32 q0 = w0;
     for (int i = 0; i < tlg::NV; ++i) {
       const u32 h = c.nxt[i], m = sz(A, h);
       for (u32 q = 0; q < m; ++q) A.w[q0 + q] = A.w[h + q];
       q0 += m;
     }
+    return true;
+  }
+
+  __device__ __attribute__((noinline)) void operator()(tlg::Cx& c) {
+    Ar& A = *c.A;
+    if (A.err) return;   // computed after an evaluation error: not a successor (the parent reports the error)
+    const unsigned long long o = ord++;   // this successor's ordinal in the parent's list
+    const u32 t0 = A.top;
+    // the variables this successor changed (a handle differs from the parent's; all for Init)
+    unsigned long long chg = ~0ull;
+    if (parent != ~0ull) {
+      chg = 0;
+      for (int i = 0; i < tlg::NV; ++i) chg |= (c.nxt[i] != c.cur[i] ? 1ull : 0ull) << i;
+    }
     tlg::Cx d = c;
     for (int i = 0; i < tlg::NV; ++i) d.cur[i] = c.nxt[i];
     const unsigned long long key = (rank << ORD_BITS) | o;
-    if (mode == M_MAT) { materialize(A, d, c, w0, n, key); A.top = t0; return; }
-    if (mode == M_STOP) { stop_count(A, c, w0, n, o); A.top = t0; return; }
+    if (mode == M_MAT) { materialize(A, d, c, key, chg); A.top = t0; return; }
+    if (mode == M_STOP) { stop_count(A, c, o, chg); A.top = t0; return; }
     const bool keyed = a->fifo && parent != ~0ull;   // FIFO pass 1 (initial states: stored at once)
     ++gen;
     ++act_gen[c.act];
     // in the model: the state constraints, then (a transition, not an initial state) the action
     // constraints over (parent, successor)
-    const bool im = tlg::constraints(d) && (parent == ~0ull || tlg::action_constraints(c));
+    const bool im = tlg::constraints(d, chg) && (parent == ~0ull || tlg::action_constraints(c));
     if (A.err) {   // a constraint could not be evaluated on this successor: TLC's evaluation error
       error_event(A, key, keyed);
       A.top = t0;
@@ -178,7 +194,7 @@ struct Em {
         if (A.err) { error_event(A, key, keyed); A.top = t0; return; }
         fp = fp_words(A.w + vh, sz(A, vh), a->seed);
       } else {
-        fp = fp_words(A.w + w0, n, a->seed);
+        fp = state_fp(A, c, chg);
       }
       if (keyed) {
         unsigned long long pos = 0;
@@ -189,10 +205,10 @@ struct Em {
       } else {
         unsigned long long pos = 0;
         const bool fresh = a->fifo ? insert_keyed(*a, fp, key, pos) : insert_plain(*a, fp);
-        if (fresh) store_now(A, d, c, w0, n);
+        if (fresh) store_now(A, d, c, chg);
       }
     } else if (a->inv_oom) {
-      const int bad = tlg::invariants(d);
+      const int bad = tlg::invariants(d, chg);
       if (A.err) {   // evaluation error of an invariant on an out-of-model successor
         error_event(A, key, keyed);
       } else if (bad >= 0) {
@@ -200,13 +216,30 @@ struct Em {
         else if (claim(*a)) {
           a->ctr[C_KIND] = 2; a->ctr[C_SID] = parent; a->ctr[C_INV] = (unsigned long long)bad;
           a->ctr[C_EACT] = (unsigned long long)c.act;
-          const u32 m = n < a->evcap ? n : a->evcap;
+          u32 w0 = 0, n = 0;
+          const u32 m = layout(A, c, w0, n) ? (n < a->evcap ? n : a->evcap) : 0u;
           for (u32 q = 0; q < m; ++q) a->evbuf[q] = A.w[w0 + q];
           a->ctr[C_EWORDS] = m;
         }
       }
     }
     A.top = t0;
+  }
+
+  // a state's fingerprint: the sum of per-variable terms (fp_words of the variable's canonical
+  // words under a per-variable seed), mixed; a variable the successor left unchanged reuses the
+  // parent's term, so only changed variables are read and hashed
+  __device__ static unsigned long long var_term(const Ar& A, u32 h, int v, unsigned long long seed) {
+    return fp_words(A.w + h, sz(A, h), seed ^ (0x9E3779B97F4A7C15ull * (unsigned long long)(v + 1)));
+  }
+  __device__ unsigned long long state_fp(const Ar& A, tlg::Cx& c, unsigned long long chg) const {
+    unsigned long long s = 0;
+    for (int i = 0; i < tlg::NV; ++i) s += ((chg >> i) & 1ull) ? var_term(A, c.nxt[i], i, a->seed) : ph[i];
+    s = fmix(s ^ a->seed);
+    return s ? s : 1ull;
+  }
+  __device__ void parent_terms(const Ar& A, tlg::Cx& c) {
+    for (int i = 0; i < tlg::NV; ++i) ph[i] = var_term(A, c.cur[i], i, a->seed);
   }
 
   // a constraint / VIEW / out-of-model invariant could not be evaluated on a successor
@@ -221,8 +254,10 @@ struct Em {
   }
 
   // -workers N (and the initial states): the inserting lane stores the new state at once
-  __device__ void store_now(Ar& A, tlg::Cx& d, tlg::Cx& c, u32 w0, u32 n) {
+  __device__ void store_now(Ar& A, tlg::Cx& d, tlg::Cx& c, unsigned long long chg) {
     ++act_dist[c.act];
+    u32 w0 = 0, n = 0;
+    if (!layout(A, c, w0, n)) { atomicOr(&a->ctr[C_CAP], 4ull); return; }   // arena overflow: searched again, larger
     const unsigned long long sid = atomicAdd(a->n_states, 1ull);
     const unsigned long long wp = atomicAdd(a->words_used, (unsigned long long)n);
     if (sid >= a->states_cap || wp + n > a->words_cap) { atomicOr(&a->ctr[C_CAP], 1ull); return; }
@@ -231,7 +266,7 @@ struct Em {
     a->parent[sid] = parent;
     a->act[sid] = (u32)c.act;
     atomicAdd(a->n_committed, 1ull);
-    const int bad = tlg::invariants(d);
+    const int bad = tlg::invariants(d, chg);
     if (A.err) {   // an invariant could not be evaluated on the new state: TLC's evaluation error
       if (!(A.err & E_OVF) && claim(*a)) { a->ctr[C_KIND] = 5; a->ctr[C_SID] = sid; a->ctr[C_INV] = (unsigned long long)bad; }
       A.err = 0;
@@ -241,11 +276,13 @@ struct Em {
   }
 
   // FIFO pass 2: the successor is stored iff its key is this parent's next winner key
-  __device__ void materialize(Ar& A, tlg::Cx& d, tlg::Cx& c, u32 w0, u32 n, unsigned long long key) {
+  __device__ void materialize(Ar& A, tlg::Cx& d, tlg::Cx& c, unsigned long long key, unsigned long long chg) {
     if (j >= a->n_w || a->wkeys[j] != key) return;
     const unsigned long long sid = a->level_end + j;
     ++j;
     ++act_dist[c.act];
+    u32 w0 = 0, n = 0;
+    if (!layout(A, c, w0, n)) { atomicOr(&a->ctr[C_CAP], 4ull); return; }
     const unsigned long long wp = atomicAdd(a->words_used, (unsigned long long)n);
     if (sid >= a->states_cap || wp + n > a->words_cap) { atomicOr(&a->ctr[C_CAP], 1ull); return; }
     for (u32 q = 0; q < n; ++q) a->words[wp + q] = A.w[w0 + q];
@@ -253,7 +290,7 @@ struct Em {
     a->parent[sid] = parent;
     a->act[sid] = (u32)c.act;
     atomicAdd(a->n_committed, 1ull);
-    const int bad = tlg::invariants(d);
+    const int bad = tlg::invariants(d, chg);
     if (A.err) {
       if (!(A.err & E_OVF)) event(*a, key, EV_INV_ERROR_NEW);
       A.err = 0;
@@ -266,19 +303,20 @@ struct Em {
   // to the event's one; per action, the event parent's only up to the event's successor; none of
   // it when the event is an error computing those successors or a deadlock), and the words of the
   // event's successor
-  __device__ void stop_count(Ar& A, tlg::Cx& c, u32 w0, u32 n, unsigned long long o) {
+  __device__ void stop_count(Ar& A, tlg::Cx& c, unsigned long long o, unsigned long long chg) {
     const bool at_event = rank == a->stop_rank;
     if (at_event && (a->stop_kind == (int)EV_NEXT_ERROR || a->stop_kind == (int)EV_DEADLOCK)) return;
     ++gen;
     if (!at_event || o <= a->stop_ord) ++act_gen[c.act];
     if (at_event && o == a->stop_ord) {
       a->ctr[C_EACT] = (unsigned long long)c.act;
-      const u32 m = n < a->evcap ? n : a->evcap;
+      u32 w0 = 0, n = 0;
+      const u32 m = layout(A, c, w0, n) ? (n < a->evcap ? n : a->evcap) : 0u;
       for (u32 q = 0; q < m; ++q) a->evbuf[q] = A.w[w0 + q];
       a->ctr[C_EWORDS] = m;
       tlg::Cx d = c;
       for (int i = 0; i < tlg::NV; ++i) d.cur[i] = c.nxt[i];
-      const int bad = tlg::invariants(d);
+      const int bad = tlg::invariants(d, chg);
       a->ctr[C_EVINV] = (unsigned long long)(bad < 0 ? 0 : bad);
       A.err = 0;
     }
@@ -307,6 +345,7 @@ __device__ inline u32 expand_state(Args& a, Ar& A, tlg::Cx& c, Em& em, u32 floor
   A.top = floor; A.htop = 0; A.err = 0;
   const tlv::u32* p = a.words + a.offs[sid];
   for (int v = 0; v < tlg::NV; ++v) { c.cur[v] = tlv::copy_in(A, p); p += p[0] >> 3; }
+  if (!(tlg::HAS_VIEW || tlg::HAS_SYMMETRY)) em.parent_terms(A, c);
   em.parent = sid;
   em.ord = 0;
   tlg::next_states(c, em);

@@ -16,7 +16,7 @@ import pytest
 from oracle_util import CONFIGS, GOLDEN, ROOT, golden_file
 
 SHAPES = {"membership_shipped": (3, 2), "memb_dynamic3": (3, 2), "memb_nosym": (3, 2), "memb_two": (2, 1),
-          "memb_four": (4, 2), "memb_async": (3, 2), "scen_CommitWhenConcurrentLeaders_punct": (3, 2),
+          "memb_four": (4, 2), "memb_four_scale": (4, 2), "memb_async": (3, 2), "scen_CommitWhenConcurrentLeaders_punct": (3, 2),
           "scen_MajorityOfClusterRestarts_punct": (3, 2)}
 FIX = json.load(open(os.path.join(GOLDEN, "memb_parity.json")))
 
