@@ -78,6 +78,7 @@ struct MGenArgs {
   u32 inv_oom, deadlock;
   unsigned long long* ctr;
   u32* defer;                              // TLC mode: cells whose state holds a ConfigEntry (ctr[C_DEFER] of them)
+  unsigned long long* prof;                // RMC_FP_PROF builds: wave cycles per fingerprint stage (else null)
 };
 
 // Phase 1 for the instances [K0, K1) with NS successors each.  The bounds are compile-time so
@@ -205,9 +206,11 @@ __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
 #pragma unroll
   for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
   W s, t;
+  unsigned long long pt = RMC_PROF_T();
   S::unpack(w, s);
   u32 err = 0;
   S::template apply<TLC>(s, k, sub, t, err, a.rt);
+  RMC_PROF_ADD(a.prof, 0, pt);
 #ifdef RMC_FP_DUP_APPLY   // timing experiment: the re-derivation twice
   { W t2; u32 e2 = 0; int k2 = k; asm volatile("" : "+v"(k2)); S::template apply<TLC>(s, k2, sub, t2, e2, a.rt); asm volatile("" :: "v"((u32)t2.hr0), "v"(t2.term), "v"(e2)); }
 #endif
@@ -227,7 +230,7 @@ __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
     }
     if (ce) continue;
   }
-  a.cand[cell] = TLC ? S::fingerprint_tlc(t, a.seed, a.rt) : S::fingerprint_orbit(t, a.seed, a.rt);
+  a.cand[cell] = TLC ? S::fingerprint_tlc(t, a.seed, a.rt, a.prof) : S::fingerprint_orbit(t, a.seed, a.rt);
   }
 }
 
@@ -250,8 +253,10 @@ __global__ void __launch_bounds__(BS) memb_fingerprint_ce(MGenArgs a) {
     W s, t;
     S::unpack(w, s);
     u32 err = 0;
+    unsigned long long pt = RMC_PROF_T();
     S::template apply<true>(s, k, sub, t, err, a.rt);
-    a.cand[cell] = S::fingerprint_tlc(t, a.seed, a.rt);
+    RMC_PROF_ADD(a.prof, 7, pt);
+    a.cand[cell] = S::fingerprint_tlc(t, a.seed, a.rt, a.prof);
   }
 }
 
@@ -1769,6 +1774,11 @@ class MembGpu : public Backend {
   // phase 2 on the stream: the symmetric fingerprints of the chunk's in-model cells (TLC mode: the
   // states with a ConfigEntry queued to memb_fingerprint_ce, full waves of their own)
   int launch_fingerprint(MGenArgs g, u32 nblk, std::string& err) {
+    g.prof = nullptr;
+#ifdef RMC_FP_PROF
+    if (!d_prof_) { HIPCHK(hipMalloc(&d_prof_, 8 * 8)); HIPCHK(hipMemset(d_prof_, 0, 8 * 8)); }
+    g.prof = d_prof_;
+#endif
     if (rt_dev_.sym_tlc) {
       g.defer = d_defer_;
       HIPCHK(hipMemsetAsync(d_ctr_ + C_DEFER, 0, 8, stream_));
@@ -1783,10 +1793,19 @@ class MembGpu : public Backend {
     return 0;
   }
   u32* d_defer_ = nullptr;
+  unsigned long long* d_prof_ = nullptr;   // RMC_FP_PROF builds (printed to stderr by release)
 
   void release() {
     if (d_defer_) (void)hipFree(d_defer_);
     d_defer_ = nullptr;
+    if (d_prof_) {
+      unsigned long long h[8] = {0};
+      if (hipMemcpy(h, d_prof_, sizeof h, hipMemcpyDeviceToHost) == hipSuccess)
+        std::fprintf(stderr, "FP_PROF apply %llu prologue %llu first %llu tie %llu bagloops %llu tail %llu view %llu apply_ce %llu\n",
+                     h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+      (void)hipFree(d_prof_);
+      d_prof_ = nullptr;
+    }
     for (auto& p : d_ptab_) { if (p) (void)hipFree(p); p = nullptr; }
     for (void* q : {(void*)d_lvl_, (void*)d_sorted_, (void*)d_newrec_lvl_, (void*)d_sort_tmp_, (void*)d_nsucc_lvl_}) if (q) (void)hipFree(q);
     d_lvl_ = nullptr; d_sorted_ = nullptr; d_newrec_lvl_ = nullptr; d_sort_tmp_ = nullptr; d_nsucc_lvl_ = nullptr; lvl_cap_ = 0;

@@ -29,6 +29,20 @@
 //    permutation.  Equal fingerprints <=> same orbit of the view (up to
 //    64-bit hash collisions, reported as TLC does).
 #pragma once
+// Cost attribution (RMC_FP_PROF builds only): wave cycles per stage of the TLC-mode fingerprint,
+// summed into prof[stage] by one lane of each wave (memb_backend.hip RAFTMC fp profile)
+#if defined(RMC_FP_PROF) && defined(__HIP_DEVICE_COMPILE__)
+#define RMC_PROF_T() __builtin_readcyclecounter()
+#define RMC_PROF_ADD(prof, i, t0)                                                                  \
+  do {                                                                                             \
+    const unsigned long long t1_ = __builtin_readcyclecounter();                                   \
+    if ((prof) && __lane_id() == __ffsll((unsigned long long)__ballot(1)) - 1) atomicAdd(&(prof)[i], t1_ - (t0)); \
+    (t0) = t1_;                                                                                    \
+  } while (0)
+#else
+#define RMC_PROF_T() 0ull
+#define RMC_PROF_ADD(prof, i, t0) do { (void)(prof); (void)(t0); } while (0)
+#endif
 #include "common.h"
 
 namespace rmc {
@@ -1653,7 +1667,8 @@ struct Memb {
     return m;
   }
   // the permutation TLC picks: least permuted variable tuple, variable by variable
-  RMC_HD static u32 tlc_min_perm(const Work& t, const BagRef& bag, int len, bool ce, u32 cfgt) {
+  RMC_HD static u32 tlc_min_perm(const Work& t, const BagRef& bag, int len, bool ce, u32 cfgt, unsigned long long* prof = nullptr) {
+    unsigned long long pt = RMC_PROF_T();
     u32 cand = (u32)lomask(NPERM);
     // messages: a function from message records to counts (oracle Fcn order: DOMAIN size — equal
     // for all — then the domain elements ascending, then the counts in domain order)
@@ -1678,6 +1693,7 @@ struct Memb {
     // permutation maps the bag to the same function -- its permuted codes with their counts,
     // compared by a sum of 64-bit mixes (the fingerprint's own collision class) -- the domain and
     // count stages below tie for all of them: skipped (their cost is |cand| * len^2 code renamings)
+    RMC_PROF_ADD(prof, 2, pt);
     bool bag_tie = false;
     if (!single(cand)) {
       u64 h0 = 0;
@@ -1692,6 +1708,7 @@ struct Memb {
         else if (h != h0) { bag_tie = false; break; }
       }
     }
+    RMC_PROF_ADD(prof, 3, pt);
     if (!bag_tie) {
 #pragma unroll 1
       for (int j = j0; j == 0 || (j < len && !single(cand)); ++j) {   // (one pass even for an empty bag)
@@ -1718,6 +1735,7 @@ struct Memb {
         last = code; have_last = true;
       }
     }
+    RMC_PROF_ADD(prof, 4, pt);
     // history: [global, hadNum* (invariant), server], currentTerm, state, votedFor, log, commitIndex,
     // votesResponded, votesGranted, nextIndex, matchIndex — each a function over the servers, in
     // the fused runs of key_scalars / key_log / key_cv / key_nm
@@ -1729,9 +1747,11 @@ struct Memb {
 #pragma unroll 1
     for (int m = 0; m < 2 && !single(cand); ++m)
       cand = keep_min(cand, [&](int, u32 pi) { return key_nm(t, pi, m != 0); });
+    RMC_PROF_ADD(prof, 5, pt);
     return perm_of(__builtin_ctz(cand));   // any remaining tie: identical permuted states
   }
-  RMC_HD static u64 fingerprint_tlc(const Work& t, u64 seed, const MembRuntime& rt) {
+  RMC_HD static u64 fingerprint_tlc(const Work& t, u64 seed, const MembRuntime& rt, unsigned long long* prof = nullptr) {
+    unsigned long long pt = RMC_PROF_T();
     const bool ce = has_config_entries(t, rt.cfg_type);
 #if defined(__HIP_DEVICE_COMPILE__)
     __shared__ u64 sbag[MK * 256];   // every kernel runs 256-lane workgroups; one slice per lane
@@ -1745,8 +1765,11 @@ struct Memb {
     int len = 0;
 #pragma unroll
     for (int q = 0; q < MK; ++q) { base[q * stride] = t.bag.v[q]; len += t.bag.v[q] != EMPTY; }
-    const u32 pi = tlc_min_perm(t, BagRef{base, stride}, len, ce, rt.cfg_type);
+    RMC_PROF_ADD(prof, 1, pt);
+    const u32 pi = tlc_min_perm(t, BagRef{base, stride}, len, ce, rt.cfg_type, prof);
+    pt = RMC_PROF_T();
     const u64 best = ce ? view_hash1<true>(t, pi, seed, rt.cfg_type) : view_hash1<false>(t, pi, seed, rt.cfg_type);
+    RMC_PROF_ADD(prof, 6, pt);
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RMC_FP_DUP_MINPERM)   // timing experiment: the search twice
     { int l2 = len; asm volatile("" : "+v"(l2)); const u32 p2 = tlc_min_perm(t, BagRef{base, stride}, l2, ce, rt.cfg_type); asm volatile("" :: "v"(p2)); }
 #endif
