@@ -1694,46 +1694,80 @@ struct Memb {
     // compared by a sum of 64-bit mixes (the fingerprint's own collision class) -- the domain and
     // count stages below tie for all of them: skipped (their cost is |cand| * len^2 code renamings)
     RMC_PROF_ADD(prof, 2, pt);
-    bool bag_tie = false;
-    if (!single(cand)) {
-      u64 h0 = 0;
-      bag_tie = true;
+    // the bag under permutation pi as one 64-bit value: its permuted codes with their counts, a sum
+    // of mixes (a function from codes to counts; equal values <=> equal permuted bags, up to the
+    // fingerprint's own collision class)
+    auto bag_hash = [&](u32 pi) -> u64 {
+      u64 h = 0;
 #pragma unroll 1
-      for (u32 m = cand; m; m &= m - 1u) {
-        const u32 pi = perm_of(__builtin_ctz(m));
-        u64 h = 0;
+      for (int q = 0; q < len; ++q) { const u64 e = bag[q]; h += fmix(((perm_code(mcode(e), pi, ce, cfgt) + 1ull) * P1) ^ (u64)mcount(e)); }
+      return h;
+    };
+    // The next messages in domain order, a few at most: each usually halves the candidates.
+    int j = j0;
 #pragma unroll 1
-        for (int q = 0; q < len; ++q) { const u64 e = bag[q]; h += fmix(((perm_code(mcode(e), pi, ce, cfgt) + 1ull) * P1) ^ (u64)mcount(e)); }
-        if (m == cand) h0 = h;
-        else if (h != h0) { bag_tie = false; break; }
-      }
+    for (; (j == 0 || (j < len && !single(cand))) && j < j0 + 2; ++j) {   // (one pass even for an empty bag)
+      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); });
+      last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+      have_last = true;
     }
     RMC_PROF_ADD(prof, 3, pt);
-    if (!bag_tie) {
+    // Candidates that map the bag to the same function tie through the rest of the domain and all
+    // the counts: a symmetric state (servers in the same role) keeps such groups to the last
+    // message.  The stages below run on one representative per group and stop once one group is
+    // left; its members all go on to the history.
+    const u32 group_of_all = cand;
+    bool grouped = false, bag_done = false;
+    if (!single(cand) && j < len) {
+      u32 reps = 0, first_grp = 0;
 #pragma unroll 1
-      for (int j = j0; j == 0 || (j < len && !single(cand)); ++j) {   // (one pass even for an empty bag)
-        cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); });
-        last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
-        have_last = true;
-#ifdef RMC_TLC_DEDUP
-        if (j == 0 && !single(cand) && popc32(cand) <= 8) cand = dedup_auto(t, cand, cfgt);
-#endif
+      for (u32 left = cand; left;) {
+        const int p = __builtin_ctz(left);
+        const u64 h = bag_hash(perm_of(p));
+        u32 grp = 1u << p;
+#pragma unroll 1
+        for (u32 m = left & (left - 1u); m; m &= m - 1u) {
+          const int q = __builtin_ctz(m);
+          if (bag_hash(perm_of(q)) == h) grp |= 1u << q;
+        }
+        if (!reps) first_grp = grp;
+        reps |= 1u << p;
+        left &= ~grp;
       }
-      have_last = false;
+      if (single(reps)) { cand = first_grp; bag_done = true; }   // one group: the bag stages tie for all of it
+      else { cand = reps; grouped = true; }
+    }
 #pragma unroll 1
-      for (int j = 0; j < len && !single(cand); ++j) {   // same permuted domain: the counts in domain order
-        const u64 code = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
-        cand = keep_min(cand, [&](int, u32 pi) {
-          u64 cnt = 0;
+    for (; !bag_done && j < len && !single(cand); ++j) {
+      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); });
+      last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+      have_last = true;
+    }
+    have_last = false;
 #pragma unroll 1
-          for (int q = 0; q < len; ++q) {
-            const u64 e = bag[q];
-            if (perm_code(mcode(e), pi, ce, cfgt) == code) cnt = (u64)mcount(e);
-          }
-          return cnt;
-        });
-        last = code; have_last = true;
+    for (int jc = 0; !bag_done && jc < len && !single(cand); ++jc) {   // same permuted domain: the counts in domain order
+      const u64 code = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+      cand = keep_min(cand, [&](int, u32 pi) {
+        u64 cnt = 0;
+#pragma unroll 1
+        for (int q = 0; q < len; ++q) {
+          const u64 e = bag[q];
+          if (perm_code(mcode(e), pi, ce, cfgt) == code) cnt = (u64)mcount(e);
+        }
+        return cnt;
+      });
+      last = code; have_last = true;
+    }
+    if (grouped) {
+      // the winning representative's whole group (members of other groups lost on the bag)
+      const u64 h = bag_hash(perm_of(__builtin_ctz(cand)));
+      u32 grp = cand;
+#pragma unroll 1
+      for (u32 m = group_of_all & ~cand; m; m &= m - 1u) {
+        const int q = __builtin_ctz(m);
+        if (bag_hash(perm_of(q)) == h) grp |= 1u << q;
       }
+      cand = grp;
     }
     RMC_PROF_ADD(prof, 4, pt);
     // history: [global, hadNum* (invariant), server], currentTerm, state, votedFor, log, commitIndex,
