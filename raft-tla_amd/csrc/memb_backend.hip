@@ -1779,6 +1779,12 @@ class MembGpu : public Backend {
     if (!d_prof_) { HIPCHK(hipMalloc(&d_prof_, 8 * 8)); HIPCHK(hipMemset(d_prof_, 0, 8 * 8)); }
     g.prof = d_prof_;
 #endif
+#ifdef RMC_NO_CE_DEFER   // experiment: every TLC-mode fingerprint in memb_fingerprint
+    if (rt_dev_.sym_tlc) {
+      g.defer = nullptr;
+      hipLaunchKernelGGL((memb_fingerprint<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
+    } else
+#endif
     if (rt_dev_.sym_tlc) {
       g.defer = d_defer_;
       HIPCHK(hipMemsetAsync(d_ctr_ + C_DEFER, 0, 8, stream_));

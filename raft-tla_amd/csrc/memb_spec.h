@@ -1154,6 +1154,21 @@ struct Memb {
   RMC_HD static u64 fmix(u64 h) { h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32; return h; }
   // any ConfigEntry (server-valued) inside a log or a log-carrying message?  Without one,
   // permuting the view only renames the server-valued fields (the cheap path).
+  // a message code carrying a ConfigEntry (in its log / entries field): its permuted code renames
+  // config values too (perm_entries), not only its server fields
+  RMC_HD static bool msg_has_config(u64 c, u32 cfgt) {
+    const u64 dp = mdesc_packed(mcls(c));
+    const int ol = (int)((dp >> 28) & 127), kind = (int)((dp >> 35) & 3);
+    bool any = false;
+    if (kind == 1) {
+      const int cnt = (int)fld(c, ol, IB);
+#pragma unroll
+      for (int p = 0; p < MAXLOG; ++p) if (p < cnt && etype((u32)fld(c, ol + IB + p * EW, EW)) == cfgt) any = true;
+    } else if (kind == 2) {
+      if (fld(c, ol, 1) && etype((u32)fld(c, ol + 1, EW)) == cfgt) any = true;
+    }
+    return any;
+  }
   RMC_HD static bool has_config_entries(const Work& t, u32 cfgt) {
     bool any = false;
 #pragma unroll
@@ -1676,16 +1691,34 @@ struct Memb {
     bool have_last = false;
     int j0 = 0;
 #ifndef RMC_TLC_NO_CANON
-    if (!ce && len > 0) {
+    if (len > 0) {
       // the first (least) permuted message in closed form: the least canonical code over the
       // messages, and the permutations that give some message of that code its canonical labels
-      // (instead of the least permuted code under each of the N! permutations)
+      // (instead of the least permuted code under each of the N! permutations).  A message that
+      // carries a ConfigEntry (only when ce) renames config values too: its least code and the
+      // permutations reaching it are found by trying the N! permutations on it alone.
       u64 best = ~0ull;
 #pragma unroll 1
-      for (int q = 0; q < len; ++q) { u32 lab; const u64 cc = canon_code(mcode(bag[q]), lab); best = cc < best ? cc : best; }
+      for (int q = 0; q < len; ++q) {
+        const u64 c = mcode(bag[q]);
+        if (ce && msg_has_config(c, cfgt)) {
+#pragma unroll 1
+          for (int p = 0; p < NPERM; ++p) { const u64 v = perm_code(c, perm_of(p), true, cfgt); best = v < best ? v : best; }
+        } else {
+          u32 lab; const u64 cc = canon_code(c, lab); best = cc < best ? cc : best;
+        }
+      }
       u32 cm = 0;
 #pragma unroll 1
-      for (int q = 0; q < len; ++q) { u32 lab; if (canon_code(mcode(bag[q]), lab) == best) cm |= cand_of(lab); }
+      for (int q = 0; q < len; ++q) {
+        const u64 c = mcode(bag[q]);
+        if (ce && msg_has_config(c, cfgt)) {
+#pragma unroll 1
+          for (int p = 0; p < NPERM; ++p) cm |= perm_code(c, perm_of(p), true, cfgt) == best ? 1u << p : 0u;
+        } else {
+          u32 lab; if (canon_code(c, lab) == best) cm |= cand_of(lab);
+        }
+      }
       cand = cm; last = best; have_last = true; j0 = 1;
     }
 #endif
