@@ -54,7 +54,6 @@ namespace rmc {
 namespace {
 enum {
   C_CELLS = 0, C_ERR = 1, C_EVENT = 2, C_NEW = 3, C_ERRGID = 4, C_GEN_IN = 5, C_CELLS_OOM = 6,
-  C_DEFER = 7,   // TLC-mode fingerprints deferred to memb_fingerprint_ce
   C_ACT = 8, C_SHARD = C_ACT + 2 * MA_NACT, C_NCTR = C_SHARD + 8   // C_SHARD: per-rank bucket counters
 };
 enum { EV_NEXT_ERROR = 0, EV_DEADLOCK = 1, EV_INV_ERROR = 2, EV_VIOLATION = 3 };
@@ -77,7 +76,6 @@ struct MGenArgs {
   MembRuntime rt;
   u32 inv_oom, deadlock;
   unsigned long long* ctr;
-  u32* defer;                              // TLC mode: cells whose state holds a ConfigEntry (ctr[C_DEFER] of them)
   unsigned long long* prof;                // RMC_FP_PROF builds: wave cycles per fingerprint stage (else null)
 };
 
@@ -214,49 +212,7 @@ __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
 #ifdef RMC_FP_DUP_APPLY   // timing experiment: the re-derivation twice
   { W t2; u32 e2 = 0; int k2 = k; asm volatile("" : "+v"(k2)); S::template apply<TLC>(s, k2, sub, t2, e2, a.rt); asm volatile("" :: "v"((u32)t2.hr0), "v"(t2.term), "v"(e2)); }
 #endif
-  if constexpr (TLC) {
-    // A state with a ConfigEntry in a log or message renames config values inside the codes, so
-    // its least permutation takes the general search over all 24 permutations (no closed-form
-    // first stage): ~7% of C3's states, but spread over nearly every wave, each of which then
-    // waited for its slowest lane.  They are queued and searched on full waves of their own.
-    const bool ce = a.defer && S::has_config_entries(t, a.rt.cfg_type);
-    const unsigned long long m = __ballot(ce);
-    if (m) {
-      const int first = __ffsll(m) - 1;
-      unsigned long long base = 0;
-      if (__lane_id() == first) base = atomicAdd(&a.ctr[C_DEFER], (unsigned long long)__popcll(m));
-      base = __shfl(base, first);
-      if (ce) a.defer[base + (u64)__popcll(m & ((1ull << __lane_id()) - 1ull))] = cell;
-    }
-    if (ce) continue;
-  }
   a.cand[cell] = TLC ? S::fingerprint_tlc(t, a.seed, a.rt, a.prof) : S::fingerprint_orbit(t, a.seed, a.rt);
-  }
-}
-
-// TLC mode, the queued cells (memb_fingerprint): re-derive, least permutation, fingerprint; a
-// grid-stride loop over ctr[C_DEFER] entries (the count stays on the device)
-template <class S>
-__global__ void __launch_bounds__(BS) memb_fingerprint_ce(MGenArgs a) {
-  using W = typename S::Work;
-  constexpr int NWP = S::NWP;
-  const u64 n = a.ctr[C_DEFER];
-  for (u64 i = (u64)blockIdx.x * BS + threadIdx.x; i < n; i += (u64)gridDim.x * BS) {
-    const u32 cell = a.defer[i];
-    const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
-    int k, sub;
-    S::inst_of_slot((int)slot, k, sub);
-    u32 w[NWP];
-    const uint4* src = reinterpret_cast<const uint4*>(a.states + (a.chunk_begin + st) * NWP);
-#pragma unroll
-    for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
-    W s, t;
-    S::unpack(w, s);
-    u32 err = 0;
-    unsigned long long pt = RMC_PROF_T();
-    S::template apply<true>(s, k, sub, t, err, a.rt);
-    RMC_PROF_ADD(a.prof, 7, pt);
-    a.cand[cell] = S::fingerprint_tlc(t, a.seed, a.rt, a.prof);
   }
 }
 
@@ -868,7 +824,6 @@ class MembGpu : public Backend {
     HIPCHK(hipMalloc(&d_nsucc_, chunk_ * 2));
     HIPCHK(hipMalloc(&d_cells_, chunk_ * S::NSLOT * 4));
     HIPCHK(hipMalloc(&d_cells_oom_, chunk_ * S::NSLOT * 4));
-    HIPCHK(hipMalloc(&d_defer_, chunk_ * S::NSLOT * 4));
     HIPCHK(hipMalloc(&d_cell_count_, 2 * ((chunk_ + BS - 1) / BS) * 4));
     HIPCHK(hipMalloc(&d_woff_, chunk_ * 4));
     HIPCHK(hipMalloc(&d_bsum_, SCAN_MAX_BLOCKS * 8));
@@ -1771,44 +1726,29 @@ class MembGpu : public Backend {
   bool have_prefix_[2] = {false, false};
   u64* d_ptab_[2] = {nullptr, nullptr};
 
-  // phase 2 on the stream: the symmetric fingerprints of the chunk's in-model cells (TLC mode: the
-  // states with a ConfigEntry queued to memb_fingerprint_ce, full waves of their own)
+  // phase 2 on the stream: the symmetric fingerprints of the chunk's in-model cells.  (Round 4 tried
+  // queueing the states with a ConfigEntry to a second kernel on full waves of their own: 1531 vs
+  // 1267 ms of C3 fingerprint time, the re-derivation of the queued cells costing more than their
+  // lanes' divergence had.)
   int launch_fingerprint(MGenArgs g, u32 nblk, std::string& err) {
     g.prof = nullptr;
 #ifdef RMC_FP_PROF
     if (!d_prof_) { HIPCHK(hipMalloc(&d_prof_, 8 * 8)); HIPCHK(hipMemset(d_prof_, 0, 8 * 8)); }
     g.prof = d_prof_;
 #endif
-#ifdef RMC_NO_CE_DEFER   // experiment: every TLC-mode fingerprint in memb_fingerprint
-    if (rt_dev_.sym_tlc) {
-      g.defer = nullptr;
-      hipLaunchKernelGGL((memb_fingerprint<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
-    } else
-#endif
-    if (rt_dev_.sym_tlc) {
-      g.defer = d_defer_;
-      HIPCHK(hipMemsetAsync(d_ctr_ + C_DEFER, 0, 8, stream_));
-      hipLaunchKernelGGL((memb_fingerprint<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
-      HIPCHK(hipGetLastError());
-      hipLaunchKernelGGL((memb_fingerprint_ce<S>), dim3(std::min<u32>(nblk, 2048u)), dim3(BS), 0, stream_, g);
-    } else {
-      g.defer = nullptr;
-      hipLaunchKernelGGL((memb_fingerprint<S, false>), dim3(nblk), dim3(BS), 0, stream_, g);
-    }
+    if (rt_dev_.sym_tlc) hipLaunchKernelGGL((memb_fingerprint<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
+    else hipLaunchKernelGGL((memb_fingerprint<S, false>), dim3(nblk), dim3(BS), 0, stream_, g);
     HIPCHK(hipGetLastError());
     return 0;
   }
-  u32* d_defer_ = nullptr;
   unsigned long long* d_prof_ = nullptr;   // RMC_FP_PROF builds (printed to stderr by release)
 
   void release() {
-    if (d_defer_) (void)hipFree(d_defer_);
-    d_defer_ = nullptr;
     if (d_prof_) {
       unsigned long long h[8] = {0};
       if (hipMemcpy(h, d_prof_, sizeof h, hipMemcpyDeviceToHost) == hipSuccess)
-        std::fprintf(stderr, "FP_PROF apply %llu prologue %llu first %llu tie %llu bagloops %llu tail %llu view %llu apply_ce %llu\n",
-                     h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7]);
+        std::fprintf(stderr, "FP_PROF apply %llu prologue %llu first %llu narrow %llu bagloops %llu tail %llu view %llu\n",
+                     h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
       (void)hipFree(d_prof_);
       d_prof_ = nullptr;
     }
