@@ -1630,12 +1630,11 @@ struct Memb {
     int stride;
     RMC_HD u64 operator[](int q) const { return p[q * stride]; }
   };
-  // cfgm: bit q set when message q carries a ConfigEntry (only those rename config values)
-  RMC_HD static u64 next_perm_code(const BagRef& bag, int len, u32 pi, u32 cfgm, u32 cfgt, bool have_last, u64 last) {
+  RMC_HD static u64 next_perm_code(const BagRef& bag, int len, u32 pi, bool ce, u32 cfgt, bool have_last, u64 last) {
     u64 best = ~0ull;   // the least permuted message code above `last`
 #pragma unroll 1
     for (int q = 0; q < len; ++q) {
-      const u64 c = perm_code(mcode(bag[q]), pi, (cfgm >> q) & 1u, cfgt);
+      const u64 c = perm_code(mcode(bag[q]), pi, ce, cfgt);
       if ((!have_last || c > last) && c < best) best = c;
     }
     return best;
@@ -1683,7 +1682,7 @@ struct Memb {
     return m;
   }
   // the permutation TLC picks: least permuted variable tuple, variable by variable
-  RMC_HD static u32 tlc_min_perm(const Work& t, const BagRef& bag, int len, u32 cfgm, u32 cfgt, unsigned long long* prof = nullptr) {
+  RMC_HD static u32 tlc_min_perm(const Work& t, const BagRef& bag, int len, bool ce, u32 cfgt, unsigned long long* prof = nullptr) {
     unsigned long long pt = RMC_PROF_T();
     u32 cand = (u32)lomask(NPERM);
     // messages: a function from message records to counts (oracle Fcn order: DOMAIN size — equal
@@ -1696,13 +1695,13 @@ struct Memb {
       // the first (least) permuted message in closed form: the least canonical code over the
       // messages, and the permutations that give some message of that code its canonical labels
       // (instead of the least permuted code under each of the N! permutations).  A message that
-      // carries a ConfigEntry (a bit of cfgm) renames config values too: its least code and the
+      // carries a ConfigEntry (only when ce) renames config values too: its least code and the
       // permutations reaching it are found by trying the N! permutations on it alone.
       u64 best = ~0ull;
 #pragma unroll 1
       for (int q = 0; q < len; ++q) {
         const u64 c = mcode(bag[q]);
-        if ((cfgm >> q) & 1u) {
+        if (ce && msg_has_config(c, cfgt)) {
 #pragma unroll 1
           for (int p = 0; p < NPERM; ++p) { const u64 v = perm_code(c, perm_of(p), true, cfgt); best = v < best ? v : best; }
         } else {
@@ -1713,7 +1712,7 @@ struct Memb {
 #pragma unroll 1
       for (int q = 0; q < len; ++q) {
         const u64 c = mcode(bag[q]);
-        if ((cfgm >> q) & 1u) {
+        if (ce && msg_has_config(c, cfgt)) {
 #pragma unroll 1
           for (int p = 0; p < NPERM; ++p) cm |= perm_code(c, perm_of(p), true, cfgt) == best ? 1u << p : 0u;
         } else {
@@ -1734,15 +1733,15 @@ struct Memb {
     auto bag_hash = [&](u32 pi) -> u64 {
       u64 h = 0;
 #pragma unroll 1
-      for (int q = 0; q < len; ++q) { const u64 e = bag[q]; h += fmix(((perm_code(mcode(e), pi, (cfgm >> q) & 1u, cfgt) + 1ull) * P1) ^ (u64)mcount(e)); }
+      for (int q = 0; q < len; ++q) { const u64 e = bag[q]; h += fmix(((perm_code(mcode(e), pi, ce, cfgt) + 1ull) * P1) ^ (u64)mcount(e)); }
       return h;
     };
     // The next messages in domain order, a few at most: each usually halves the candidates.
     int j = j0;
 #pragma unroll 1
     for (; (j == 0 || (j < len && !single(cand))) && j < j0 + 2; ++j) {   // (one pass even for an empty bag)
-      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, cfgm, cfgt, have_last, last); });
-      last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), cfgm, cfgt, have_last, last);
+      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); });
+      last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
       have_last = true;
     }
     RMC_PROF_ADD(prof, 3, pt);
@@ -1773,20 +1772,20 @@ struct Memb {
     }
 #pragma unroll 1
     for (; !bag_done && j < len && !single(cand); ++j) {
-      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, cfgm, cfgt, have_last, last); });
-      last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), cfgm, cfgt, have_last, last);
+      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); });
+      last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
       have_last = true;
     }
     have_last = false;
 #pragma unroll 1
     for (int jc = 0; !bag_done && jc < len && !single(cand); ++jc) {   // same permuted domain: the counts in domain order
-      const u64 code = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), cfgm, cfgt, have_last, last);
+      const u64 code = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
       cand = keep_min(cand, [&](int, u32 pi) {
         u64 cnt = 0;
 #pragma unroll 1
         for (int q = 0; q < len; ++q) {
           const u64 e = bag[q];
-          if (perm_code(mcode(e), pi, (cfgm >> q) & 1u, cfgt) == code) cnt = (u64)mcount(e);
+          if (perm_code(mcode(e), pi, ce, cfgt) == code) cnt = (u64)mcount(e);
         }
         return cnt;
       });
@@ -1831,21 +1830,15 @@ struct Memb {
     constexpr int stride = 1;
 #endif
     int len = 0;
-    u32 cfgm = 0;   // the messages that carry a ConfigEntry (the bag is kept packed: EMPTY entries last)
 #pragma unroll
-    for (int q = 0; q < MK; ++q) {
-      const u64 e = t.bag.v[q];
-      base[q * stride] = e;
-      len += e != EMPTY;
-      if (ce && e != EMPTY && msg_has_config(mcode(e), rt.cfg_type)) cfgm |= 1u << q;
-    }
+    for (int q = 0; q < MK; ++q) { base[q * stride] = t.bag.v[q]; len += t.bag.v[q] != EMPTY; }
     RMC_PROF_ADD(prof, 1, pt);
-    const u32 pi = tlc_min_perm(t, BagRef{base, stride}, len, cfgm, rt.cfg_type, prof);
+    const u32 pi = tlc_min_perm(t, BagRef{base, stride}, len, ce, rt.cfg_type, prof);
     pt = RMC_PROF_T();
     const u64 best = ce ? view_hash1<true>(t, pi, seed, rt.cfg_type) : view_hash1<false>(t, pi, seed, rt.cfg_type);
     RMC_PROF_ADD(prof, 6, pt);
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RMC_FP_DUP_MINPERM)   // timing experiment: the search twice
-    { int l2 = len; asm volatile("" : "+v"(l2)); const u32 p2 = tlc_min_perm(t, BagRef{base, stride}, l2, cfgm, rt.cfg_type); asm volatile("" :: "v"(p2)); }
+    { int l2 = len; asm volatile("" : "+v"(l2)); const u32 p2 = tlc_min_perm(t, BagRef{base, stride}, l2, ce, rt.cfg_type); asm volatile("" :: "v"(p2)); }
 #endif
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RMC_FP_DUP_VIEW)      // timing experiment: the view hash twice
     { u32 p2 = pi; asm volatile("" : "+v"(p2)); const u64 b2 = ce ? view_hash1<true>(t, p2, seed, rt.cfg_type) : view_hash1<false>(t, p2, seed, rt.cfg_type); asm volatile("" :: "v"((u32)b2), "v"((u32)(b2 >> 32))); }
