@@ -269,13 +269,14 @@ TLV_NI u32 set_union(Ar& a, u32 x, u32 y) {   // linear merge of two sorted sets
   if (count(a, y) == 0) return x;
   if (count(a, x) == 0) return y;
   const u32 mark = a.htop;
-  u32 e = first(x), f = first(y), i = 0, j = 0;
+  u32 e = first(x), f = first(y), i = 0, j = 0, added = 0;
   const u32 n = count(a, x), m = count(a, y);
   while (i < n || j < m) {
     int c = i == n ? 1 : j == m ? -1 : ocmp(a, e, f);
     if (c <= 0) { hpush(a, e); e = nextv(a, e); ++i; if (c == 0) { f = nextv(a, f); ++j; } }
-    else { hpush(a, f); f = nextv(a, f); ++j; }
+    else { hpush(a, f); f = nextv(a, f); ++j; ++added; }
   }
+  if (!added) { a.htop = mark; return x; }   // y adds nothing: x itself
   return write_coll(a, T_SET, mark, 1, 0, false);
 }
 TLV_HD u32 coll_card(Ar& a, u32 f) {   // Cardinality(DOMAIN f) without building the domain
@@ -289,6 +290,7 @@ TLV_NI u32 set_filter_in(Ar& a, u32 x, u32 y, bool keep_in) {   // x \cap y (kee
   u32 e = first(x);
   for (u32 i = 0, n = count(a, x); i < n; ++i, e = nextv(a, e))
     if (set_in(a, e, y) == keep_in) hpush(a, e);
+  if (a.htop - mark == count(a, x)) { a.htop = mark; return x; }   // every element kept: x itself
   return write_coll(a, T_SET, mark, 1, 0, false);   // a subsequence of a sorted set
 }
 TLV_HD u32 set_cap(Ar& a, u32 x, u32 y) { return set_filter_in(a, x, y, true); }
@@ -376,6 +378,7 @@ TLV_NI u32 except(Ar& a, u32 f, u32 x, u32 v) {
   if (t != T_SEQ && t != T_FUN) { a.err |= E_TYPE; return f; }
   const u32 at = lookup(a, f, x);
   if (!at) return f;
+  if (eqv(a, at, v)) return f;   // the same value: f itself (no copy; the successor shows the variable unchanged)
   const u32 old = sz(a, at), nw = sz(a, v), total = sz(a, f) - old + nw;
   const u32 r = alloc(a, total);
   if (a.err & E_OVF) return 0;
