@@ -4,6 +4,9 @@
 //
 //   hipcc -O3 --offload-arch=gfx950 -o seen_set_bench scripts/seen_set_bench.hip
 //   ./seen_set_bench                -> one JSON line per (table MiB, mode)
+//   ./seen_set_bench calib          -> the 4 GiB table, probe mode only (2^28 probes per launch):
+//                                      the known probe count that calibrates rocprofv3's
+//                                      FETCH_SIZE for 8-B random loads (scripts/fetch_calib.sh)
 //
 // Keys: splitmix64 from seed 0x9E3779B97F4A7C15.  Modes: "probe" = a load of
 // the home slot per key (the seen-set lookup of a duplicate successor); "insert" = the
@@ -12,6 +15,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 typedef unsigned long long u64;
@@ -45,8 +49,9 @@ __global__ void __launch_bounds__(BS) probe(u64* table, u64 mask, u64 n, u64 sal
   if (acc == salt + 1) out[0] = acc;   // keep the loads live (never true: salt + 1 is even, acc's keys are odd)
 }
 
-int main() {
-  const u64 mib[] = {4, 16, 64, 256, 1024, 4096};
+int main(int argc, char** argv) {
+  const bool calib = argc > 1 && !std::strcmp(argv[1], "calib");
+  const std::vector<u64> mib = calib ? std::vector<u64>{4096} : std::vector<u64>{4, 16, 64, 256, 1024, 4096};
   const u64 n = 1ull << 28;   // 268M probes per launch
   for (u64 m : mib) {
     const u64 slots = m << 17;   // MiB -> 8-B slots
@@ -57,7 +62,7 @@ int main() {
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     const unsigned grid = (unsigned)((n + BS * PER - 1) / (BS * PER));
-    for (int mode = 0; mode < 2; ++mode) {
+    for (int mode = 0; mode < (calib ? 1 : 2); ++mode) {
       // warm-up launch, then 3 timed launches with fresh keys
       if (mode) hipLaunchKernelGGL(probe<true>, dim3(grid), dim3(BS), 0, 0, t, slots - 1, n, 0ull, out);
       else hipLaunchKernelGGL(probe<false>, dim3(grid), dim3(BS), 0, 0, t, slots - 1, n, 0ull, out);
