@@ -2,7 +2,7 @@
 
     python scripts/rocpd_summary.py stats  RUN_DB OUT.csv          # per-kernel calls / total / avg (us)
     python scripts/rocpd_summary.py pmc    RUN_DB COUNTER OUT.csv  # per-kernel mean counter value per dispatch
-    python scripts/rocpd_summary.py traffic FETCH_DB WRITE_DB KERNEL_SUBSTR OUT.json [WORKLOAD]
+    python scripts/rocpd_summary.py traffic FETCH_DB WRITE_DB KERNEL_SUBSTR OUT.json [WORKLOAD] [--random]
     python scripts/rocpd_summary.py valu   PMC_DB KERNEL_SUBSTR OUT.json [WORKLOAD]   # VALU/SALU wave-instructions per dispatch
 
 WORKLOAD (default "c2.cfg") names the model the profiled command checked, as bench.py's workload key
@@ -55,17 +55,26 @@ def main():
         for r in rows:
             print(r)
     elif mode == "traffic":
-        fetch = {r[0]: r for r in pmc(sys.argv[2], "FETCH_SIZE")}
-        write = {r[0]: r for r in pmc(sys.argv[3], "WRITE_SIZE")}
-        name = next(k for k in fetch if sys.argv[4] in k)
+        args = [a for a in sys.argv if a != "--random"]
+        random_probes = "--random" in sys.argv
+        fetch = {r[0]: r for r in pmc(args[2], "FETCH_SIZE")}
+        write = {r[0]: r for r in pmc(args[3], "WRITE_SIZE")}
+        name = next(k for k in fetch if args[4] in k)
         f_kib, w_kib = fetch[name][2], write[name][2]
-        doc = {"kernel_name": sys.argv[4], "kernel_symbol": name, "dispatches": fetch[name][1],
-               "workload": sys.argv[6] if len(sys.argv) > 6 else "c2.cfg",
+        # streaming reads: FETCH_SIZE is half the bytes (MI355X_MICROARCH.md); random 8-B probes: one
+        # 64-B request per probe is charged 64 B (profiles/r04_fetch_size_calibration.json), so the
+        # counter is taken as is (--random: the seen-set kernels)
+        factor = 1 if random_probes else 2
+        doc = {"kernel_name": args[4], "kernel_symbol": name, "dispatches": fetch[name][1],
+               "workload": args[6] if len(args) > 6 else "c2.cfg",
                "fetch_bytes_per_launch_raw": f_kib * 1024, "write_bytes_per_launch": w_kib * 1024,
-               "hbm_bytes_per_launch": 2 * f_kib * 1024 + w_kib * 1024,
+               "hbm_bytes_per_launch": factor * f_kib * 1024 + w_kib * 1024,
                "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over `bench.py --steps 1 "
-                         "--warmup 0`; KiB*1024 averaged over the kernel's dispatches; FETCH_SIZE doubled per "
-                         "MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B), WRITE_SIZE as is"}
+                         "--warmup 0 --no-extra`; KiB*1024 averaged over the kernel's dispatches; " +
+                         ("FETCH_SIZE as is: random 8-B probes are charged 64 B per request, calibrated on "
+                          "scripts/seen_set_bench.hip (profiles/r04_fetch_size_calibration.json)" if random_probes else
+                          "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B)") +
+                         ", WRITE_SIZE as is"}
         json.dump(doc, open(sys.argv[5], "w"), indent=1)
         print(json.dumps(doc, indent=1))
     elif mode == "valu":
