@@ -1509,7 +1509,7 @@ struct Memb {
   // keep, among the candidate permutations, those whose key (p, pi) is least
   // (one pass: each candidate's key is evaluated once)
   template <class F>
-  RMC_HD static u32 keep_min(u32 cand, F key) {
+  RMC_HD static u32 keep_min(u32 cand, F key, u64* least = nullptr) {
     u64 best = ~0ull;
     u32 out = 0;
 #pragma unroll 1
@@ -1519,6 +1519,7 @@ struct Memb {
       out = k < best ? (1u << p) : k == best ? (out | 1u << p) : out;
       best = k < best ? k : best;
     }
+    if (least) *least = best;   // the kept candidates' key
     return out;
   }
   // pi^-1 packed like pi (2 bits per server): pinv(pi, s) == pi_of(inv_of(pi), s)
@@ -1698,25 +1699,21 @@ struct Memb {
       // carries a ConfigEntry (only when ce) renames config values too: its least code and the
       // permutations reaching it are found by trying the N! permutations on it alone.
       u64 best = ~0ull;
+      u32 cm = 0;   // one pass: the least code so far and the permutations reaching it
 #pragma unroll 1
       for (int q = 0; q < len; ++q) {
         const u64 c = mcode(bag[q]);
         if (ce && msg_has_config(c, cfgt)) {
 #pragma unroll 1
-          for (int p = 0; p < NPERM; ++p) { const u64 v = perm_code(c, perm_of(p), true, cfgt); best = v < best ? v : best; }
+          for (int p = 0; p < NPERM; ++p) {
+            const u64 v = perm_code(c, perm_of(p), true, cfgt);
+            cm = v < best ? 1u << p : v == best ? cm | 1u << p : cm;
+            best = v < best ? v : best;
+          }
         } else {
-          u32 lab; const u64 cc = canon_code(c, lab); best = cc < best ? cc : best;
-        }
-      }
-      u32 cm = 0;
-#pragma unroll 1
-      for (int q = 0; q < len; ++q) {
-        const u64 c = mcode(bag[q]);
-        if (ce && msg_has_config(c, cfgt)) {
-#pragma unroll 1
-          for (int p = 0; p < NPERM; ++p) cm |= perm_code(c, perm_of(p), true, cfgt) == best ? 1u << p : 0u;
-        } else {
-          u32 lab; if (canon_code(c, lab) == best) cm |= cand_of(lab);
+          u32 lab;
+          const u64 cc = canon_code(c, lab);
+          if (cc <= best) { const u32 m = cand_of(lab); cm = cc < best ? m : cm | m; best = cc; }
         }
       }
       cand = cm; last = best; have_last = true; j0 = 1;
@@ -1740,8 +1737,9 @@ struct Memb {
     int j = j0;
 #pragma unroll 1
     for (; (j == 0 || (j < len && !single(cand))) && j < j0 + 2; ++j) {   // (one pass even for an empty bag)
-      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); });
-      last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+      u64 next = 0;
+      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); }, &next);
+      last = next;
       have_last = true;
     }
     RMC_PROF_ADD(prof, 3, pt);
@@ -1772,8 +1770,9 @@ struct Memb {
     }
 #pragma unroll 1
     for (; !bag_done && j < len && !single(cand); ++j) {
-      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); });
-      last = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+      u64 next = 0;
+      cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); }, &next);
+      last = next;
       have_last = true;
     }
     have_last = false;
