@@ -351,7 +351,7 @@ struct Memb {
   // positions of the fields every handler needs: (dst, src, term) offsets per class; plus the
   // permutation descriptor (server-valued fields and config-carrying logs)
   struct MDesc { int dst, src, term, srv, log, kind; };   // kind: 0 none, 1 message log, 2 AE entry
-  RMC_HD static MDesc mdesc(int cls) {
+  RMC_HD static constexpr MDesc mdesc(int cls) {
     switch (cls) {
       case K_COC: return {O_COC_DST, O_COC_SRC, O_COC_TERM, O_COC_SRV, 0, 0};
       case K_RVQ: return {O_RVQ_DST, O_RVQ_SRC, O_RVQ_TERM, 0, 0, 0};
@@ -363,6 +363,19 @@ struct Memb {
       default: return {O_AEQ_DST, O_AEQ_SRC, O_AEQ_TERM, 0, O_AEQ_ENT, 2};
     }
   }
+  // one descriptor field of every class, a byte per class (class k in byte k): a field is one
+  // 64-bit shift and mask on the lane's class, for the per-message hot loops of TLC's symmetry
+  // rule (perm_code, canon_code), instead of the 8-way select chain below
+  RMC_HD static constexpr u64 md_lut(int f) {
+    u64 r = 0;
+    for (int k = 0; k < 8; ++k) {
+      const MDesc d = mdesc(k);
+      const int v = f == 0 ? d.dst : f == 1 ? d.src : d.srv;
+      r |= (u64)(v & 255) << (8 * k);
+    }
+    return r;
+  }
+  RMC_HD static int md_field(u64 lut, int cls) { return (int)((lut >> (8 * cls)) & 255u); }
   // a select-chain lookup of the descriptor (no divergence across lanes holding different classes)
   RMC_HD static u64 mdesc_packed(int cls) {
     u64 r = 0;
@@ -1443,8 +1456,9 @@ struct Memb {
   // a message code with every server-valued field renamed by pi (and config values inside its
   // log / entry when ce); order preserving like the code itself
   RMC_HD static u64 perm_code(u64 c, u32 pi, bool ce, u32 cfgt) {
-    const u64 dp = mdesc_packed(mcls(c));
-    const int od = (int)(dp & 127), os = (int)((dp >> 7) & 127), ov = (int)((dp >> 21) & 127);
+    constexpr u64 MD_DST = md_lut(0), MD_SRC = md_lut(1), MD_SRV = md_lut(2);
+    const int cl = mcls(c);
+    const int od = md_field(MD_DST, cl), os = md_field(MD_SRC, cl), ov = md_field(MD_SRV, cl);
     const int sd = CODEB - od - SB, ss = CODEB - os - SB, sv = CODEB - ov - SB;
     u64 x = c & ~(lomask(SB) << sd) & ~(lomask(SB) << ss);
     if (ov) x &= ~(lomask(SB) << sv);
@@ -1646,8 +1660,9 @@ struct Memb {
   // the next to 2.  *lab: the servers of those fields and their labels (server | label << 4, per
   // field, most significant first), for cand_of.
   RMC_HD static u64 canon_code(u64 c, u32& lab) {
-    const u64 dp = mdesc_packed(mcls(c));
-    const int od = (int)(dp & 127), os = (int)((dp >> 7) & 127), ov = (int)((dp >> 21) & 127);
+    constexpr u64 MD_DST = md_lut(0), MD_SRC = md_lut(1), MD_SRV = md_lut(2);
+    const int cl = mcls(c);
+    const int od = md_field(MD_DST, cl), os = md_field(MD_SRC, cl), ov = md_field(MD_SRV, cl);
     const int sd = CODEB - od - SB, ss = CODEB - os - SB, sv = CODEB - ov - SB;
     const bool has_v = ov != 0;
     // the fields (shift, server), most significant (largest shift) first: a 3-element sorting
