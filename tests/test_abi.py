@@ -109,6 +109,21 @@ def test_kernels_short_branch_and_no_scratch():
     assert not bad, bad
 
 
+def test_fingerprint_kernels_keep_two_waves_per_simd():
+    """The symmetric-fingerprint kernels hold their bag in 64 KB of LDS per workgroup, so a CU runs
+    two workgroups = two waves per SIMD, which needs <= 256 VGPRs + AGPRs per lane: one more
+    register and the kernel drops to one wave per SIMD (round 4: a per-message ConfigEntry mask
+    took TLC-mode C3 from 1.27 to 1.90 s of fingerprint time)."""
+    import json
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_isa.py")], capture_output=True, text=True)
+    ks = {k: v for k, v in json.loads(r.stdout).items() if "memb_fingerprint" in k}
+    assert ks
+    over = {k: (v.get("vgprs"), v.get("agprs")) for k, v in ks.items() if (v.get("vgprs") or 0) + (v.get("agprs") or 0) > 256}
+    assert not over, over
+
+
 def test_generated_code_objects_short_branch_and_ordered_stores():
     """The same check over the generated path's prebuilt code objects (`_build/tlagen_co/*.hsaco`,
     hiprtc output for every spec `prebuild.py` compiles), kernels and the device functions the
