@@ -1749,9 +1749,12 @@ struct Memb {
       return h;
     };
     // The next messages in domain order, a few at most: each usually halves the candidates.
+#ifndef RMC_TLC_NARROW
+#define RMC_TLC_NARROW 2
+#endif
     int j = j0;
 #pragma unroll 1
-    for (; (j == 0 || (j < len && !single(cand))) && j < j0 + 2; ++j) {   // (one pass even for an empty bag)
+    for (; (j == 0 || (j < len && !single(cand))) && j < j0 + RMC_TLC_NARROW; ++j) {   // (one pass even for an empty bag)
       u64 next = 0;
       cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); }, &next);
       last = next;
