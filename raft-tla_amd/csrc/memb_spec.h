@@ -1509,10 +1509,10 @@ struct Memb {
 #pragma unroll 1
         for (int q = 0; q < NPERM; ++q) {
           const u32 rq = hrank(t, q);
-          if (rq > rp) continue;
-          const u64 kq = entry_key(xe, ye, perm_of(q), cfgt);
-          r += (rq < rp || kq < kp) ? 1u : 0u;
-          distinct &= q == p || rq != rp || kq != kp;
+          if (rq != rp) { r += rq < rp ? 1u : 0u; continue; }   // another rank class: the old rank decides
+          const u64 kq = entry_key(xe, ye, perm_of(q), cfgt);    // same class: the new entry's key
+          r += kq < kp ? 1u : 0u;
+          distinct &= q == p || kq != kp;
         }
         if (p < RPW) w0 |= (u64)r << (RKB * p); else w1 |= (u64)r << (RKB * (p - RPW));
       }
