@@ -1504,15 +1504,21 @@ struct Memb {
 #pragma unroll 1
       for (int p = 0; p < NPERM; ++p) {
         const u32 rp = hrank(t, p);
-        const u64 kp = entry_key(xe, ye, perm_of(p), cfgt);
-        u32 r = 0;
+        u32 r = 0, same = 0;   // permutations of a lower old rank; the others of p's rank class
 #pragma unroll 1
         for (int q = 0; q < NPERM; ++q) {
           const u32 rq = hrank(t, q);
-          if (rq != rp) { r += rq < rp ? 1u : 0u; continue; }   // another rank class: the old rank decides
-          const u64 kq = entry_key(xe, ye, perm_of(q), cfgt);    // same class: the new entry's key
-          r += kq < kp ? 1u : 0u;
-          distinct &= q == p || kq != kp;
+          r += rq < rp ? 1u : 0u;
+          same |= (rq == rp && q != p) ? 1u << q : 0u;
+        }
+        if (same) {   // the new entry's keys order p's rank class (a singleton class needs none)
+          const u64 kp = entry_key(xe, ye, perm_of(p), cfgt);
+#pragma unroll 1
+          for (u32 m = same; m; m &= m - 1u) {
+            const u64 kq = entry_key(xe, ye, perm_of(__builtin_ctz(m)), cfgt);
+            r += kq < kp ? 1u : 0u;
+            distinct &= kq != kp;
+          }
         }
         if (p < RPW) w0 |= (u64)r << (RKB * p); else w1 |= (u64)r << (RKB * (p - RPW));
       }
