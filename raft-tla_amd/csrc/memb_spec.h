@@ -151,6 +151,35 @@ constexpr u64 rank_to_mask_lut(int n) {
 }
 constexpr int factorial(int n) { return n <= 1 ? 1 : n * factorial(n - 1); }
 
+// Permutation tables in constant memory (a load each instead of a Lehmer decode or a 24-step
+// scan per use in the symmetry code): perm[p] = the p-th permutation of N servers in Lehmer order,
+// 2 bits per server; pos[s * 4 + l] = the permutations that send server s to l.
+constexpr u32 lehmer_perm(int n, int p) {
+  u32 avail = 0x3210u, pi = 0;
+  int rem = p;
+  for (int i = 0; i < n; ++i) {
+    const int f = factorial(n - 1 - i), d = rem / f;
+    rem -= d * f;
+    pi |= ((avail >> (4 * d)) & 15u) << (2 * i);
+    avail = (avail & (u32)lomask(4 * d)) | ((avail >> (4 * (d + 1))) << (4 * d));
+  }
+  return pi;
+}
+struct PermTables { u32 perm[24]; u32 pos[16]; };
+constexpr PermTables make_perm_tables(int n) {
+  PermTables t{};
+  for (int p = 0; p < factorial(n) && p < 24; ++p) {
+    t.perm[p] = lehmer_perm(n, p);
+    for (int s = 0; s < n; ++s) t.pos[s * 4 + (int)((t.perm[p] >> (2 * s)) & 3u)] |= 1u << p;
+  }
+  return t;
+}
+#if defined(__HIPCC__)
+__device__ constexpr PermTables kPermTables[5] = {make_perm_tables(0), make_perm_tables(1), make_perm_tables(2), make_perm_tables(3), make_perm_tables(4)};
+#else
+constexpr PermTables kPermTables[5] = {make_perm_tables(0), make_perm_tables(1), make_perm_tables(2), make_perm_tables(3), make_perm_tables(4)};
+#endif
+
 template <int N_, int NV_, int MK_>
 struct Memb {
   static constexpr int N = N_, NV = NV_, MK = MK_;
@@ -1207,17 +1236,9 @@ struct Memb {
     return any;
   }
   // permutation number p (0 <= p < N!) -> pi packed 2 bits per server (Lehmer code)
-  RMC_HD static u32 perm_of(int p) {
-    u32 avail = 0x3210u, pi = 0;
-    int rem = p;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const int f = factorial(N - 1 - i), d = rem / f;
-      rem -= d * f;
-      pi |= ((avail >> (4 * d)) & 15u) << (2 * i);
-      avail = (avail & (u32)lomask(4 * d)) | ((avail >> (4 * (d + 1))) << (4 * d));
-    }
-    return pi;
+  RMC_HD static u32 perm_of(int p) {   // the p-th permutation (Lehmer order), 2 bits per server
+    static_assert(N <= 4, "permutation tables hold N <= 4");
+    return kPermTables[N].perm[p];
   }
   // Permutation-aware hashing of the view (SYMMETRY perms): for every permutation p, the hash of
   // the permuted view is a sum of element hashes (servers, bag entries), so each element is
@@ -1693,14 +1714,9 @@ struct Memb {
   }
   // the permutations that rename the fields as canon_code's labels say
   RMC_HD static u32 cand_of(u32 lab) {
-    u32 m = 0;
-#pragma unroll 1
-    for (int p = 0; p < NPERM; ++p) {
-      const u32 pi = perm_of(p);
-      bool ok = pi_of(pi, (int)(lab & 15u)) == (int)((lab >> 4) & 15u) && pi_of(pi, (int)((lab >> 8) & 15u)) == (int)((lab >> 12) & 15u);
-      if ((lab >> 23) & 1u) ok = ok && pi_of(pi, (int)((lab >> 16) & 15u)) == (int)((lab >> 20) & 7u);
-      m |= ok ? 1u << p : 0u;
-    }
+    const u32* pos = kPermTables[N].pos;
+    u32 m = pos[(lab & 15u) * 4 + ((lab >> 4) & 15u)] & pos[((lab >> 8) & 15u) * 4 + ((lab >> 12) & 15u)];
+    if ((lab >> 23) & 1u) m &= pos[((lab >> 16) & 15u) * 4 + ((lab >> 20) & 7u)];
     return m;
   }
   // the permutation TLC picks: least permuted variable tuple, variable by variable
