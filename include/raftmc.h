@@ -93,15 +93,21 @@ typedef struct mc_opts {
                                  an in-process loopback of device copies): the multi-GPU level loop on
                                  a one-GPU machine (tests); 0 = one device per rank (default)        */
   int32_t frontend;           /* MC_FRONTEND_*: which compiled form of the module mc_open uses          */
-  int32_t reserved[5];
+  int32_t count_final_level;  /* with max_depth, raft_original, workers != 1, single GPU: the states of the
+                                 last level (depth == max_depth, never expanded) are fingerprinted,
+                                 counted and invariant-checked but not written to the state store, so a
+                                 depth-bounded search holds one more level than the store (an event
+                                 still re-runs in FIFO order, storing every level).  Counts, levels and
+                                 verdicts are unchanged; mc_dump_states refuses (MC_E_STATE).  0 = off */
+  int32_t reserved[4];
 } mc_opts;
 
 /* mc_opts.frontend.  AUTO: the hand-compiled kernels for thirdparty/raft_original.tla and
  * tlc_membership/raft.tla (and their configs/ wrappers), the generated path for any other module.
  * GENERATED: the SANY-subset front end for any module (csrc/tlagen: parse, generate C++ over
  * tlv.h, hiprtc to a gfx950 code object cached by source hash; a path ending in .gen.hip is taken
- * as an already generated source); single GPU, TLC -workers N semantics (every count exact, the
- * kept parents first-come), no SYMMETRY / VIEW / ACTION_CONSTRAINTS.  HAND: the hand-compiled
+ * as an already generated source); single GPU; SYMMETRY (TLC's rule), VIEW, ACTION_CONSTRAINTS and
+ * TLC's single-worker FIFO order (workers = 1) as on the hand path.  HAND: the hand-compiled
  * families only (MC_E_UNSUPPORTED otherwise). */
 #define MC_FRONTEND_AUTO 0
 #define MC_FRONTEND_GENERATED 1

@@ -31,6 +31,9 @@ struct RunOpts {
   // checkpoint_every levels to checkpoint_path; resume the next run from recover_path
   std::string checkpoint_path, recover_path;
   int checkpoint_every = 0;
+  // mc_opts.count_final_level: the last level of a depth-bounded -workers N search is counted and
+  // checked, not stored (raft_original; ignored elsewhere)
+  bool count_final_level = false;
 };
 
 struct LevelStat { int64_t states = 0, generated = 0; double kernel_ms = 0; };

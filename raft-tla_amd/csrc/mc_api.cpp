@@ -119,6 +119,7 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
   c->ro.check_deadlock = o->check_deadlock != 0;
   c->ro.block_size = o->block_size ? o->block_size : 256;
   c->ro.workers = o->workers;
+  c->ro.count_final_level = o->count_final_level != 0;
   try {
     if (o->frontend < MC_FRONTEND_AUTO || o->frontend > MC_FRONTEND_HAND) throw rmc::CfgError(MC_E_INVALID, "bad mc_opts.frontend");
     std::string fam;

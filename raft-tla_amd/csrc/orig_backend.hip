@@ -990,6 +990,8 @@ struct MatPlainArgs {
   u64 dst_base, cap;           // new state i of the chunk goes to dst_base + ctr[K_LEVEL_NEW] + i (device index)
   OrigRuntime rt;
   unsigned long long* ctr;
+  u32 store;                   // 0: the last level of a depth-bounded search (count_final_level):
+                               // counted and invariant-checked, not written
 };
 
 // grid-stride over the chunk's new states (their count stays on the device: no host wait)
@@ -1022,12 +1024,14 @@ __global__ void __launch_bounds__(BS) orig_materialize_plain(MatPlainArgs a) {
     u32 pw[NW];
     S::pack(t, pw);
     const u64 dst = base + i;
-    if (act >= 0 && dst < a.cap) {
-      uint4* o = reinterpret_cast<uint4*>(a.states + dst * NWP);
+    if (act >= 0 && (!a.store || dst < a.cap)) {
+      if (a.store) {
+        uint4* o = reinterpret_cast<uint4*>(a.states + dst * NWP);
 #pragma unroll
-      for (int q = 0; q < NWP / 4; ++q)
-        o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
-      a.meta[dst] = (pgid << 24) | ((u64)act << 16) | (u64)k;
+        for (int q = 0; q < NWP / 4; ++q)
+          o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
+        a.meta[dst] = (pgid << 24) | ((u64)act << 16) | (u64)k;
+      }
       atomicAdd(&lds_cnt[act], 1u);
       if (S::violated(t, a.rt.invariants & S::inv_frame(act))) { const u64 e = ev_word(pgid, (u32)k, EV_VIOLATION); ev = e < ev ? e : ev; }
     } else {
@@ -1663,12 +1667,17 @@ class OrigGpu : public Backend {
     }
     }
 
+    // count_final_level: the level at depth max_depth is never expanded, so the -workers N search
+    // counts and checks its states without storing them (an event re-runs FIFO, which stores all)
+    const bool count_last = o.count_final_level && !fifo && o.max_depth > 0 && o.checkpoint_path.empty();
+    unstored_ = 0;
     while (level_count > 0) {
       if (o.max_depth && r.depth >= o.max_depth) { r.left_on_queue = (int64_t)level_count; r.verdict = MC_VERDICT_DEPTH_LIMIT; break; }
+      const bool last = count_last && r.depth + 1 >= o.max_depth;
       // the device keeps what the search still reads (the frontier) and writes (the next
       // level); when the next level, predicted from the last growth ratio with a 1.5x margin,
       // might not fit behind what is stored, the completed levels move to host memory
-      if (level_begin > base_) {
+      if (level_begin > base_ && !last) {
         const double prev = r.levels.size() >= 2 ? (double)r.levels[r.levels.size() - 2].states : 1.0;
         const double pred = (double)level_count * std::max(1.0, (double)level_count / std::max(prev, 1.0)) * 1.5;
         if ((double)(total_ - base_) + pred > (double)cap_) {
@@ -1743,7 +1752,7 @@ class OrigGpu : public Backend {
         } else {
           MatPlainArgs m;
           m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.base = base_; m.dst_base = level_end - base_;
-          m.cap = cap_; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_;
+          m.cap = cap_; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.store = last ? 0u : 1u;
           hipLaunchKernelGGL((orig_materialize_plain<S>), dim3((unsigned)std::min<u64>(4096, (cnt * 2 + BS - 1) / BS)), dim3(BS), 0, stream_, m);
         }
         HIPCHK(hipGetLastError());
@@ -1775,12 +1784,13 @@ class OrigGpu : public Backend {
       const u64 next_write = level_end + nnew;
       if (progress_)   // TLC's progress line, per BFS level (RAFTMC_PROGRESS=1), on stderr
         std::fprintf(stderr, "Progress(%lld) at %.3f s: %lld states generated, %llu distinct states found, %llu states left on queue "
-                             "(level kernels %.1f ms, %d chunk(s), store %llu/%llu, %llu on the host)\n",
+                             "(level kernels %.1f ms, %d chunk(s), store %llu/%llu, %llu on the host%s)\n",
                      (long long)r.depth + 1,
                      std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(),
                      (long long)(r.generated + (int64_t)[&] { u64 g = 0; for (int k = 0; k < OA_NACT; ++k) g += c[K_ACT + k]; return g; }()),
                      (unsigned long long)(level_end + nnew), (unsigned long long)nnew, level_ms, nch,
-                     (unsigned long long)(next_write - base_), (unsigned long long)cap_, (unsigned long long)base_);
+                     (unsigned long long)((last ? level_end : next_write) - base_), (unsigned long long)cap_, (unsigned long long)base_,
+                     last ? "; the last level counted, not stored" : "");
       if (progress_ && (c[K_EVENT] != ~0ull || c[K_ERR]))
         std::fprintf(stderr, "level %lld: event word 0x%llx, error flags 0x%llx\n", (long long)r.depth + 1,
                      (unsigned long long)c[K_EVENT], (unsigned long long)c[K_ERR]);
@@ -1799,7 +1809,7 @@ class OrigGpu : public Backend {
       r.kernels[3].algo_bytes += (double)level_count * WW * 8 + (double)nnew * (S_B + S_B + 8);
       r.seconds_kernels += level_ms / 1000.0;
       r.n_launches += 1;
-      if (next_write - base_ > cap_) c[K_ERR] |= OE_CAP_STORE;
+      if (!last && next_write - base_ > cap_) c[K_ERR] |= OE_CAP_STORE;
       if (c[K_EVENT] != ~0ull && !fifo && (c[K_ERR] & ~(u64)OE_CAP_STORE) == 0) {
         // TLC -workers N found an event: TLC's counterexample and stop point are the single-worker
         // search's, so the model is searched again in FIFO order (it stops at this level)
@@ -1842,8 +1852,9 @@ class OrigGpu : public Backend {
       r.generated_in_model += (int64_t)G_in;
       r.seen_set_probes += (int64_t)c[K_PROBES];
       r.algo_bytes += (double)level_count * S_B + (double)G_in * 8 + (double)nnew * (16 + S_B);
-      total_ += nnew;
-      r.distinct = (int64_t)total_;
+      if (last) unstored_ = nnew;   // counted, not in the store (total_ counts stored states)
+      else total_ += nnew;
+      r.distinct = (int64_t)(total_ + unstored_);
       r.levels.back().generated = gen;
       r.levels.back().kernel_ms = level_ms;
       if (nnew > 0) { r.levels.push_back({(int64_t)nnew, 0, 0.0}); r.depth += 1; }
@@ -2089,6 +2100,7 @@ class OrigGpu : public Backend {
 
   int dump_states(const std::string& path, std::string& err) override {
     if (!d_states_) { err = "mc_dump_states before mc_run"; return MC_E_STATE; }
+    if (unstored_) { err = "mc_dump_states: the last level was counted, not stored (count_final_level)"; return MC_E_STATE; }
     std::vector<u32> h(total_ * NWP);
     host_.for_each_segment([&](u64 g0, u64 n, const u32* st, const u64*) { std::memcpy(h.data() + g0 * NWP, st, n * NWP * 4); });
     HIPCHK(hipMemcpy(h.data() + base_ * NWP, d_states_, (total_ - base_) * NWP * 4, hipMemcpyDeviceToHost));
@@ -2589,6 +2601,7 @@ class OrigGpu : public Backend {
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_[9] = {};
   u64 table_mask_ = 0, cap_ = 0, total_ = 0, chunk_states_ = 0;
+  u64 unstored_ = 0;   // states of the last level counted but not stored (count_final_level)
   int dev_ = -1, alloc_world_ = 0; uint64_t req_table_ = 0, req_store_ = 0;
   // sharded-mode state
   int rank_ = 0, world_ = 1;

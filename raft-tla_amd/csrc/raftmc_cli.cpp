@@ -2,7 +2,9 @@
 //   raftmc [-config F.cfg] [-workers N] [-deadlock] [-depth D] [-device K]
 //          [-fptable BYTES] [-store BYTES] [-seed S] [-no-inv-oom] [-dump FILE] [-json]
 //          [-checkpoint LEVELS] [-checkpoint-file FILE] [-recover FILE] [-symmetry tlc|orbit]
-//          [-gpus N] F.tla
+//          [-gpus N] [-countfinal] F.tla
+// (-countfinal, with -depth D and -workers N: the states at depth D are counted and checked, not
+// stored; mc_opts.count_final_level)
 // (-gpus N: the node's GPUs -device .. -device+N-1 share one search, owner-partitioned fingerprints,
 // one host thread per GPU over an in-process RCCL communicator; TLC's -workers keeps its meaning)
 // (-checkpoint counts BFS levels where TLC counts minutes; the file defaults to states/raftmc.ckpt)
@@ -33,6 +35,7 @@ int main(int argc, char** argv) {
     else if (k == "-workers") o.workers = std::atoi(val());
     else if (k == "-deadlock") o.check_deadlock = 0;   // TLC: -deadlock turns deadlock checking OFF
     else if (k == "-depth") o.max_depth = std::atoll(val());
+    else if (k == "-countfinal") o.count_final_level = 1;
     else if (k == "-device") o.device = std::atoi(val());
     else if (k == "-gpus") o.n_gpus = std::atoi(val());
     else if (k == "-frontend") {   // "auto" (default), "generated" (the SANY-subset front end for any module), "hand"

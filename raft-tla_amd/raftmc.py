@@ -39,7 +39,7 @@ class McOpts(ctypes.Structure):
                 ("state_store_bytes", ctypes.c_uint64), ("max_depth", ctypes.c_int64), ("seed", ctypes.c_uint64),
                 ("tlc_compat_flags", ctypes.c_uint32), ("check_deadlock", ctypes.c_int32),
                 ("block_size", ctypes.c_int32), ("same_device", ctypes.c_int32), ("frontend", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 5)]
+                ("count_final_level", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
 
 
 class McSummary(ctypes.Structure):
@@ -144,12 +144,14 @@ class ModelChecker:
     # sym_tlc: SYMMETRY as TLC applies it (the default, MC_COMPAT_SYM_TLC); False = the orbit mode
     def __init__(self, spec, config=None, workers=1, deadlock=True, device=0, max_depth=0,
                  fp_table_bytes=0, state_store_bytes=0, seed=0, inv_out_of_model=True, sym_tlc=True, n_gpus=1,
-                 same_device=False, frontend="auto"):
+                 same_device=False, frontend="auto", count_final_level=False):
         """n_gpus > 1: one search over the GPUs device .. device + n_gpus - 1 (owner-partitioned
         fingerprints, one host thread per GPU inside the library, in-process RCCL); same_device: all
         those ranks on `device` (the multi-GPU level loop on a one-GPU machine).  frontend: "auto"
         (hand-compiled kernels for the two Raft families, the generated path otherwise),
-        "generated" (the SANY-subset front end for any module, or a .gen.hip source), "hand"."""
+        "generated" (the SANY-subset front end for any module, or a .gen.hip source), "hand".
+        count_final_level (raft_original, workers != 1, with max_depth): the last level's states are
+        counted and checked but not stored, so the store needs room for the levels before it only."""
         self.lib = load_library()
         if config is None:
             config = spec[:-4] + ".cfg" if spec.endswith(".tla") else spec + ".cfg"
@@ -158,6 +160,7 @@ class ModelChecker:
         o.device, o.workers, o.max_depth = device, workers, max_depth
         o.n_gpus, o.same_device = n_gpus, 1 if same_device else 0
         o.frontend = {"auto": 0, "generated": 1, "hand": 2}[frontend]
+        o.count_final_level = 1 if count_final_level else 0
         o.fp_table_bytes, o.state_store_bytes, o.seed = fp_table_bytes, state_store_bytes, seed
         o.check_deadlock = 1 if deadlock else 0
         o.tlc_compat_flags = (MC_COMPAT_INV_OUT_OF_MODEL if inv_out_of_model else 0) | (MC_COMPAT_SYM_TLC if sym_tlc else 0)
@@ -299,6 +302,8 @@ def tlc_main(argv):
             kw["deadlock"] = False
         elif a == "-depth":
             kw["max_depth"] = int(next(it))
+        elif a == "-countfinal":                 # raftmc: with -depth, the last level counted, not stored
+            kw["count_final_level"] = True
         elif a == "-gpus":
             kw["n_gpus"] = int(next(it))
         elif a == "-frontend":                   # raftmc: auto (default) | generated | hand

@@ -257,6 +257,58 @@ def test_c5v2_deep_properties(raftmc):
     assert sum(v[1] for v in a.actions.values()) + 1 == a.distinct
 
 
+def test_count_final_level(raftmc, tmp_path):
+    """mc_opts.count_final_level: the level at depth max_depth is never expanded, so the -workers N
+    search fingerprints, counts and invariant-checks its states without writing them to the store.
+    Every count equals the storing run's; mc_dump_states refuses; an event in that level re-runs
+    TLC's FIFO order (which stores every level) and gives the same counterexample (NoLeader at depth
+    10, tests/golden/orig_events.json)."""
+    cfg = os.path.join(CONFIGS, "c5v2.cfg")
+    a = raftmc.check(ORIG_MC, cfg, max_depth=10, workers=0)
+    with raftmc.ModelChecker(ORIG_MC, cfg, max_depth=10, workers=0, count_final_level=True) as mc:
+        b = mc.run()
+        with pytest.raises(raftmc.RaftMCError):
+            mc.dump_states(str(tmp_path / "states.txt"))
+    assert a.verdict == b.verdict == "DEPTH_LIMIT", (a.error, b.error)
+    assert (a.generated, a.distinct, a.left_on_queue, a.depth) == (b.generated, b.distinct, b.left_on_queue, b.depth)
+    assert [lv[0] for lv in a.levels] == [lv[0] for lv in b.levels]
+    # per-action distinct counts are first-come under -workers N (order-dependent): their sum is not
+    assert {k: v[0] for k, v in a.actions.items()} == {k: v[0] for k, v in b.actions.items()}
+    assert sum(v[1] for v in b.actions.values()) + 1 == b.distinct
+    ev = os.path.join(CONFIGS, "c2_noleader.cfg")
+    c = raftmc.check(ORIG_MC, ev, max_depth=10, workers=0)
+    d = raftmc.check(ORIG_MC, ev, max_depth=10, workers=0, count_final_level=True)
+    assert c.verdict == d.verdict == "INVARIANT_VIOLATION" and d.violated == "NoLeader" and d.depth == 10
+    assert (c.generated, c.distinct, c.left_on_queue, c.trace_text) == (d.generated, d.distinct, d.left_on_queue, d.trace_text)
+
+
+def test_c5v2_depth13_count_final_level(raftmc):
+    """C5v2 to depth 13 on one MI355X: 2.44e9 distinct states, whose level 13 (1.96e9 states, ~329 GB
+    at 168 B stored) fits neither HBM nor the host, so it is counted, not stored (count_final_level).
+    The levels through 12 are the storing pipeline's (bench.py's scale_workload), the counts do not
+    depend on the fingerprint seed, the levels sum to the distinct count and the per-action counts to
+    TLC's generated/distinct bookkeeping."""
+    cfg = os.path.join(CONFIGS, "c5v2.cfg")
+    runs = []
+    for seed in (1, 0xC5C5C5):
+        with raftmc.ModelChecker(ORIG_MC, cfg, max_depth=13, workers=0, count_final_level=True, seed=seed,
+                                 fp_table_bytes=64 << 30, state_store_bytes=120 << 30) as mc:
+            runs.append(mc.run())
+    a, b = runs
+    assert a.verdict == b.verdict == "DEPTH_LIMIT", (a.error, b.error)
+    assert (a.generated, a.distinct, a.left_on_queue, a.depth) == (b.generated, b.distinct, b.left_on_queue, b.depth)
+    assert [lv[0] for lv in a.levels] == [lv[0] for lv in b.levels]
+    assert [lv[0] for lv in a.levels][:12] == [1, 6, 45, 330, 2190, 13761, 82510, 475485, 2648995, 14330920,
+                                               75545752, 389107090]
+    # both seeds: 2,442,107,060.  Seed 0x5EED (scripts/c5_probe.py, profiles/r04_c5v2_d13.jsonl) finds
+    # one fewer in level 13: a 64-bit fingerprint collision, which at 2.44e9 states TLC's optimistic
+    # estimate n^2 / 2^65 puts at 0.16 expected
+    assert (a.depth, a.distinct, a.generated) == (13, 2442107060, 18179584961)
+    assert sum(lv[0] for lv in a.levels) == a.distinct and a.left_on_queue == a.levels[-1][0]
+    assert sum(v[0] for v in a.actions.values()) + 1 == a.generated
+    assert sum(v[1] for v in a.actions.values()) + 1 == a.distinct
+
+
 def test_c5_compact_election_records(raftmc, tmp_path):
     """A reachable 5-server election on the GPU: election records of 5 servers with a 341-log universe
     do not fit 64 bits, so the shape stores them compactly (orig_spec.h ECOMPACT: the voterLog row's
