@@ -16,4 +16,6 @@ for waves in sys.argv[1:] or ["8"]:
         r = mc.run()
     print(json.dumps({"workload": "C2 via the generated path", "waves_per_cu": int(waves), "verdict": r.verdict,
                       "distinct": r.distinct, "generated": r.generated, "depth": r.depth, "run_s": round(r.seconds, 3),
-                      "kernel_s": round(r.kernel_seconds, 3), "distinct_per_s": r.distinct / r.seconds}), flush=True)
+                      "kernel_s": round(r.kernel_seconds, 3), "distinct_per_s": r.distinct / r.seconds,
+                      "kernels_ms": {k: round(v["ms"], 1) for k, v in r.kernels.items()},
+                      "levels": [[lv[0], lv[1], round(lv[2], 1)] for lv in r.levels]}), flush=True)
