@@ -22,7 +22,8 @@ region; each with its own barrier-bracketed max-over-ranks timing):
   variants        C2 with MaxMsgDomain = 6 (configs/c2_md6.cfg): AppendEntries responses and
                   commits fire, which C2 as frozen (5 messages) never reaches; at N=1 also C2
                   through the generated path (the front end's code for the
-                  unmodified raft_original.tla, one run)
+                  unmodified raft_original.tla, one run) and C5v2 to depth 13 (2.44e9 distinct,
+                  its last level counted, not stored: mc_opts.count_final_level)
 
 The JSON line adds:
   roofline      dominant kernel (the one with the most HIP-event time): SURVEY.md
@@ -136,13 +137,13 @@ def main():
     mod = importlib.import_module("raft-tla_amd")
     shard = importlib.import_module("raft-tla_amd.shard") if world > 1 else None
 
-    def checker(cfg, max_depth, store, table, workers, tla=TLA):
+    def checker(cfg, max_depth, store, table, workers, tla=TLA, count_final=False):
         if world > 1:
             # owner-partitioned fingerprints, 3 RCCL all-to-alls per level chunk (raft-tla_amd/shard.py)
             return shard.ShardedChecker(tla, cfg, rank, world, device_index=local, seed=0x5EED, fp_table_bytes=table,
                                         state_store_bytes=store, max_depth=max_depth)
         return mod.ModelChecker(tla, cfg, device=local, seed=0x5EED, fp_table_bytes=table, state_store_bytes=store,
-                                workers=workers, max_depth=max_depth)
+                                workers=workers, max_depth=max_depth, count_final_level=count_final)
 
     def barrier_sync():
         if dist is not None:
@@ -158,9 +159,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t[0])
 
-    def measure(cfg, max_depth, steps, warmup, store, table, workers, tla=TLA):
+    def measure(cfg, max_depth, steps, warmup, store, table, workers, tla=TLA, count_final=False):
         """W untimed runs, then K timed runs bracketed by barrier + device sync; max over ranks"""
-        mc = checker(cfg, max_depth, store, table, workers, tla)
+        mc = checker(cfg, max_depth, store, table, workers, tla, count_final)
         try:
             for _ in range(warmup):
                 mc.run()
@@ -196,13 +197,16 @@ def main():
                 "generated_per_run": r1.generated, "kernels_ms": {k: v["ms"] for k, v in r1.kernels.items() if v["launches"]}}
         assert (r1.distinct, r1.generated, r1.depth) == (res.distinct, res.generated, res.depth)
 
-    def side(cfg, max_depth, store_gib, table_gib, steps, tla=TLA, workers=None):
+    def side(cfg, max_depth, store_gib, table_gib, steps, tla=TLA, workers=None, count_final=False):
         """a second workload at the same N through the same path; its failure is reported, not fatal"""
         name = workload_name(cfg, max_depth) if tla == TLA else "tlc_membership/raft.tla + configs/%s%s" % (
             os.path.basename(cfg), " to depth %d" % max_depth if max_depth else "")
+        if count_final:
+            name += ", its last level counted, not stored (count_final_level)"
         try:
             store = int(store_gib * (1 << 30) / world * (1.3 if world > 1 else 1.0))
-            r, t = measure(cfg, max_depth, steps, 1, store, int(table_gib * (1 << 30)), args.workers if workers is None else workers, tla)
+            r, t = measure(cfg, max_depth, steps, 1, store, int(table_gib * (1 << 30)), args.workers if workers is None else workers, tla,
+                           count_final)
             out = {"workload": name, "value": r.distinct / t, "unit": "distinct states/s",
                    "ms_per_step": t * 1e3, "steps": steps, "distinct_per_run": r.distinct, "generated_per_run": r.generated,
                    "depth": r.depth, "verdict": r.verdict,
@@ -248,6 +252,10 @@ def main():
         extra["variants"] = {"c2_md6": side(os.path.join(ROOT, "configs", "c2_md6.cfg"), 0, 64, 8, 2)}
         if world == 1:
             extra["variants"]["c2_generated"] = generated_c2()
+            # C5v2 to depth 13 (2.44e9 distinct): level 13 counted, not stored (mc_opts.count_final_level),
+            # the store holding levels 0-12 (81 GB); one GPU only (the sharded loop has no such mode)
+            extra["variants"]["c5v2_d13_count_final"] = side(os.path.join(ROOT, "configs", "c5v2.cfg"), 13, 120, 64, 1,
+                                                             count_final=True)
 
     if rank == 0:
         total_distinct = float(res.distinct)    # the sharded result is global (every rank reports the model's counts)
