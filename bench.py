@@ -19,11 +19,14 @@ Beside the headline, every invocation measures (same N, same path, outside the h
 region; each with its own barrier-bracketed max-over-ranks timing):
   scale_workload  C5v2 to depth 12 (configs/c5v2.cfg: BASELINE configs[4]'s 5-server model,
                   482M distinct states), the workload large enough for a 1/2/4/8-GPU curve
+  scale_workload_configs4  C5v2 to depth 13 (2.44e9 distinct, its last level counted, not stored:
+                  mc_opts.count_final_level, single GPU and the sharded native loop alike), at every
+                  N; at N=8 also scale_workload_configs4_d14, depth 14 (~1e10 distinct: the config's
+                  scale, its levels 0-13 stored over the 8 ranks)
   variants        C2 with MaxMsgDomain = 6 (configs/c2_md6.cfg): AppendEntries responses and
                   commits fire, which C2 as frozen (5 messages) never reaches; at N=1 also C2
                   through the generated path (the front end's code for the
-                  unmodified raft_original.tla, one run) and C5v2 to depth 13 (2.44e9 distinct,
-                  its last level counted, not stored: mc_opts.count_final_level)
+                  unmodified raft_original.tla, one run)
 
 The JSON line adds:
   roofline      dominant kernel (the one with the most HIP-event time): SURVEY.md
@@ -137,12 +140,15 @@ def main():
     mod = importlib.import_module("raft-tla_amd")
     shard = importlib.import_module("raft-tla_amd.shard") if world > 1 else None
 
-    def checker(cfg, max_depth, store, table, workers, tla=TLA, count_final=False):
+    def checker(cfg, max_depth, store, table, workers, tla=TLA, count_final=False, seed=0x5EED):
         if world > 1:
-            # owner-partitioned fingerprints, 3 RCCL all-to-alls per level chunk (raft-tla_amd/shard.py)
-            return shard.ShardedChecker(tla, cfg, rank, world, device_index=local, seed=0x5EED, fp_table_bytes=table,
-                                        state_store_bytes=store, max_depth=max_depth)
-        return mod.ModelChecker(tla, cfg, device=local, seed=0x5EED, fp_table_bytes=table, state_store_bytes=store,
+            # owner-partitioned fingerprints, 3 RCCL all-to-alls per level chunk (the library's native
+            # level loop, raft-tla_amd/shard.py ShardedChecker); raft_original's sharded search has
+            # -workers N semantics (count_final_level needs it said: workers != 1)
+            return shard.ShardedChecker(tla, cfg, rank, world, device_index=local, seed=seed, fp_table_bytes=table,
+                                        state_store_bytes=store, max_depth=max_depth, workers=workers,
+                                        count_final_level=count_final)
+        return mod.ModelChecker(tla, cfg, device=local, seed=seed, fp_table_bytes=table, state_store_bytes=store,
                                 workers=workers, max_depth=max_depth, count_final_level=count_final)
 
     def barrier_sync():
@@ -159,9 +165,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t[0])
 
-    def measure(cfg, max_depth, steps, warmup, store, table, workers, tla=TLA, count_final=False):
+    def measure(cfg, max_depth, steps, warmup, store, table, workers, tla=TLA, count_final=False, seed=0x5EED):
         """W untimed runs, then K timed runs bracketed by barrier + device sync; max over ranks"""
-        mc = checker(cfg, max_depth, store, table, workers, tla, count_final)
+        mc = checker(cfg, max_depth, store, table, workers, tla, count_final, seed)
         try:
             for _ in range(warmup):
                 mc.run()
@@ -197,19 +203,27 @@ def main():
                 "generated_per_run": r1.generated, "kernels_ms": {k: v["ms"] for k, v in r1.kernels.items() if v["launches"]}}
         assert (r1.distinct, r1.generated, r1.depth) == (res.distinct, res.generated, res.depth)
 
-    def side(cfg, max_depth, store_gib, table_gib, steps, tla=TLA, workers=None, count_final=False):
-        """a second workload at the same N through the same path; its failure is reported, not fatal"""
+    def side(cfg, max_depth, store_gib, table_gib, steps, tla=TLA, workers=None, count_final=False, seed=0x5EED,
+             split_table=False):
+        """a second workload at the same N through the same path; its failure is reported, not fatal.
+        store_gib: the whole job's (split over the ranks with a 1.3x margin); table_gib: per rank, or the
+        whole job's with split_table (a power of two per rank)"""
         name = workload_name(cfg, max_depth) if tla == TLA else "tlc_membership/raft.tla + configs/%s%s" % (
             os.path.basename(cfg), " to depth %d" % max_depth if max_depth else "")
         if count_final:
             name += ", its last level counted, not stored (count_final_level)"
         try:
             store = int(store_gib * (1 << 30) / world * (1.3 if world > 1 else 1.0))
-            r, t = measure(cfg, max_depth, steps, 1, store, int(table_gib * (1 << 30)), args.workers if workers is None else workers, tla,
-                           count_final)
+            table = int(table_gib * (1 << 30))
+            if split_table:
+                table = 1 << max(24, (table // world - 1).bit_length())
+            r, t = measure(cfg, max_depth, steps, 1, store, table, args.workers if workers is None else workers, tla,
+                           count_final, seed)
             out = {"workload": name, "value": r.distinct / t, "unit": "distinct states/s",
                    "ms_per_step": t * 1e3, "steps": steps, "distinct_per_run": r.distinct, "generated_per_run": r.generated,
-                   "depth": r.depth, "verdict": r.verdict,
+                   "depth": r.depth, "verdict": r.verdict, "seed": seed,
+                   "collision_prob_optimistic": r.collision_prob_optimistic,
+                   "store_bytes_per_rank": store, "table_bytes_per_rank": table,
                    "kernels_ms": {k: v["ms"] for k, v in r.kernels.items() if v["launches"]}}
             ks = {k: v for k, v in r.kernels.items() if v["launches"]}
             if ks and r.algo_bytes:   # the dominant kernel against the HBM roofline, SURVEY.md 8(d) bytes
@@ -234,7 +248,8 @@ def main():
                 t = time.perf_counter() - t0
             return {"workload": "C2 via the generated path (front end + generic kernels)", "value": r.distinct / t,
                     "unit": "distinct states/s", "ms_per_step": t * 1e3, "steps": 1, "distinct_per_run": r.distinct,
-                    "generated_per_run": r.generated, "depth": r.depth, "verdict": r.verdict}
+                    "generated_per_run": r.generated, "depth": r.depth, "verdict": r.verdict,
+                    "collision_prob_optimistic": r.collision_prob_optimistic}
         except Exception as e:   # noqa: BLE001
             return {"workload": "C2 via the generated path", "error": str(e)[:300]}
 
@@ -250,12 +265,20 @@ def main():
         extra["scale_workload_membership"] = side(os.path.join(ROOT, "configs", "memb_four_scale.cfg"), 20, 64, 8, 2,
                                                   tla=TLA_MEMB, workers=1)
         extra["variants"] = {"c2_md6": side(os.path.join(ROOT, "configs", "c2_md6.cfg"), 0, 64, 8, 2)}
+        # BASELINE configs[4] (raft_original, 5 servers, term <= 3, log <= 3): C5v2 to depth 13, 2.44e9
+        # distinct states, at every N (the same workload along the 1/2/4/8 curve), its level 13 counted, not
+        # stored (mc_opts.count_final_level: single GPU and the sharded native loop), the stores holding
+        # levels 0-12 (81 GB over the ranks); seed 1 (0x5EED loses one state of this model to a 64-bit
+        # fingerprint collision, tests/test_gpu.py test_c5v2_depth13_count_final_level)
+        c5v2 = os.path.join(ROOT, "configs", "c5v2.cfg")
+        extra["scale_workload_configs4"] = side(c5v2, 13, 96 if world > 1 else 120, 64, 1, workers=0, count_final=True, seed=1,
+                                                split_table=True)
+        if world == 8:
+            # depth 14 (~1e10 distinct, the config's scale): levels 0-13 stored over the 8 ranks (410 GB)
+            extra["scale_workload_configs4_d14"] = side(c5v2, 14, 420, 256, 1, workers=0, count_final=True, seed=1,
+                                                        split_table=True)
         if world == 1:
             extra["variants"]["c2_generated"] = generated_c2()
-            # C5v2 to depth 13 (2.44e9 distinct): level 13 counted, not stored (mc_opts.count_final_level),
-            # the store holding levels 0-12 (81 GB); one GPU only (the sharded loop has no such mode)
-            extra["variants"]["c5v2_d13_count_final"] = side(os.path.join(ROOT, "configs", "c5v2.cfg"), 13, 120, 64, 1,
-                                                             count_final=True)
 
     if rank == 0:
         total_distinct = float(res.distinct)    # the sharded result is global (every rank reports the model's counts)
@@ -298,7 +321,8 @@ def main():
                        "distinct_per_run": res.distinct, "generated_per_run": res.generated, "depth": res.depth,
                        "generated_in_model_per_run": res.generated_in_model,
                        "kernel_ms_per_run": res.kernel_seconds * 1000.0, "launches_per_run": res.n_launches,
-                       "state_bytes": res.state_bytes,
+                       "state_bytes": res.state_bytes, "seed": 0x5EED,
+                       "collision_prob_optimistic": res.collision_prob_optimistic,
                        "parallelism": "single" if world == 1 else "fp-owner-sharded x%d (RCCL all-to-all)" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": tj.get("hbm_bytes_per_launch") if tj else None,

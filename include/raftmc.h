@@ -37,7 +37,9 @@
 extern "C" {
 #endif
 
-#define RAFTMC_ABI_VERSION 1
+/* 2: mc_summary_t gained seen_set_probes and a reserved tail (a caller built against version 1
+ * passes a smaller struct, so mc_open refuses version-1 opts rather than let mc_summary write past it) */
+#define RAFTMC_ABI_VERSION 2
 
 /* error codes */
 #define MC_OK 0
@@ -93,12 +95,17 @@ typedef struct mc_opts {
                                  an in-process loopback of device copies): the multi-GPU level loop on
                                  a one-GPU machine (tests); 0 = one device per rank (default)        */
   int32_t frontend;           /* MC_FRONTEND_*: which compiled form of the module mc_open uses          */
-  int32_t count_final_level;  /* with max_depth, raft_original, workers != 1, single GPU: the states of the
-                                 last level (depth == max_depth, never expanded) are fingerprinted,
-                                 counted and invariant-checked but not written to the state store, so a
-                                 depth-bounded search holds one more level than the store (an event
-                                 still re-runs in FIFO order, storing every level).  Counts, levels and
-                                 verdicts are unchanged; mc_dump_states refuses (MC_E_STATE).  0 = off */
+  int32_t count_final_level;  /* with max_depth, raft_original, workers != 1 (single GPU, n_gpus > 1 or
+                                 mc_shard_run_rccl): the states of the last level (depth == max_depth,
+                                 never expanded) are fingerprinted, counted and invariant-checked but not
+                                 written to the state store (sharded: not shipped to their owners either),
+                                 so a depth-bounded search holds one more level than the store.  Counts,
+                                 levels and verdicts are unchanged; mc_dump_states refuses (MC_E_STATE).
+                                 An event on one GPU still re-runs in TLC's FIFO order, which stores every
+                                 level: when that does not fit, the verdict is CAPACITY_OVERFLOW and the
+                                 error names the event found.  mc_open refuses it (MC_E_UNSUPPORTED) for
+                                 any other spec family, workers = 1 or max_depth = 0, and
+                                 mc_set_checkpoint refuses a checkpoint path.  0 = off */
   int32_t reserved[4];
 } mc_opts;
 
@@ -133,6 +140,7 @@ typedef struct mc_summary_t {
   char spec[32];              /* "raft_original" | "tlc_membership"                        */
   int64_t seen_set_probes;    /* fingerprints that probed the seen-set (device counter; the
                                  successors a workgroup's parents produce twice probe once)   */
+  int64_t reserved[8];        /* zero; later fields come out of this tail (the size stays)  */
 } mc_summary_t;
 
 /* Fill opts with defaults. */

@@ -13,6 +13,7 @@
 // ============================================================================
 #include <iostream>
 
+#include "raft_apalache.h"
 #include "raft_dricketts.h"
 #include "raft_membership.h"
 #include "raft_original.h"
@@ -37,6 +38,8 @@ static std::string detect_spec(const std::string& text) {
   if (text.find("raftmc-base: thirdparty/raft_original.tla") != std::string::npos) return "original";
   if (text.find("raftmc-base: tlc_membership/raft.tla") != std::string::npos) return "membership";
   if (text.find("raftmc-base: thirdparty/raft_dricketts.tla") != std::string::npos) return "ricketts";
+  if (text.find("raftmc-base: apalache_no_membership/raft.tla") != std::string::npos) return "apalache";
+  if (text.find("WrapMsg(m) ==") != std::string::npos && text.find("hadAtLeastOneLeader") != std::string::npos) return "apalache";
   if (text.find("VARIABLE elections") != std::string::npos && text.find("VARIABLE allLogs") != std::string::npos) return "original";
   if (text.find("NextAsyncCrash") != std::string::npos) return "membership";
   throw EvalError("unrecognised spec module");
@@ -79,6 +82,7 @@ int main(int argc, char** argv) {
     std::unique_ptr<Spec> sp;
     if (family == "original") sp.reset(new RaftOriginal(cfg));
     else if (family == "ricketts") sp.reset(new RaftRicketts(cfg));
+    else if (family == "apalache") sp.reset(new RaftApalache(cfg));
     else {
       auto* m = new RaftMembership(cfg);
       if (!gc.empty()) m->golden_cwcl = load_golden_global(gc);

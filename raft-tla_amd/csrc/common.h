@@ -110,6 +110,25 @@ struct FpBase {
     const u64 h = fmix64(acc ^ seed ^ ((u64)NW32 * P4));
     return h ? h : 1ull;
   }
+  // fp64 of the parent's words `base` plus d * 2^P (P a compile-time bit offset into the packed
+  // state, d = +-1): the successor that changes one small field by one, where the field does not
+  // carry out of its own bits (so at most the two 64-bit words holding bits P.. change)
+  template <int P>
+  RMC_HD u64 fp_add_bit(const u32 (&base)[NW32], int d, u64 seed) const {
+    constexpr int K = P >> 6, B = P & 63;
+    const u64 lo = word(base, K);
+    const u64 nlo = d > 0 ? lo + (1ull << B) : lo - (1ull << B);
+    u64 acc = sum - term[K] + fmix64(nlo ^ key(seed, K));
+    if constexpr (K + 1 < NW64) {   // a carry / borrow into the next word (the field straddles it)
+      const bool c = d > 0 ? nlo < lo : nlo > lo;
+      if (c) {
+        const u64 hi = word(base, K + 1), nhi = d > 0 ? hi + 1 : hi - 1;
+        acc += fmix64(nhi ^ key(seed, K + 1)) - term[K + 1];
+      }
+    }
+    const u64 h = fmix64(acc ^ seed ^ ((u64)NW32 * P4));
+    return h ? h : 1ull;
+  }
 };
 
 // Compile-time bit-stream writer/reader over a u32 word array (offsets are

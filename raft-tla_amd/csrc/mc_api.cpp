@@ -130,6 +130,11 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
       catch (const rmc::CfgError&) { if (o->frontend == MC_FRONTEND_HAND) throw; fam = "tlagen"; }
     }
     rmc::CfgFile cfg = rmc::parse_cfg_text(rmc::read_text_file(cfg_path));
+    // count_final_level exists for raft_original's -workers N search with a depth bound (single GPU
+    // or sharded): anywhere else it would be silently ignored, so it is refused
+    if (o->count_final_level && (fam != "raft_original" || o->workers == 1 || o->max_depth <= 0))
+      throw rmc::CfgError(MC_E_UNSUPPORTED, "count_final_level needs thirdparty/raft_original.tla (hand-compiled), workers != 1 "
+                                            "and max_depth > 0");
     if (fam == "tlagen" && c->n_gpus > 1) throw rmc::CfgError(MC_E_UNSUPPORTED, "the generated path runs on one GPU (n_gpus = 1)");
     auto make = [&]() -> rmc::Backend* {
       if (fam == "raft_original") return rmc::make_orig_backend(cfg);
@@ -181,6 +186,10 @@ int mc_set_history_prefix(mc_ctx* c, const char* constraint, const char* trace_t
 int mc_set_checkpoint(mc_ctx* c, const char* path, int32_t every_levels) {
   if (!c || every_levels < 0) return MC_E_INVALID;
   if (!c->be) return MC_E_STATE;
+  if (path && c->ro.count_final_level) {   // a checkpoint must hold every level it names
+    c->last_error = "checkpoints store every level: not with count_final_level";
+    return MC_E_UNSUPPORTED;
+  }
   c->ro.checkpoint_path = path ? path : "";
   c->ro.checkpoint_every = path ? every_levels : 0;
   return MC_OK;
@@ -233,18 +242,10 @@ int run_multi(mc_ctx* c) {
   std::vector<std::string> errs(W);
   // A rank that leaves the loop early (shard_open failed, a rank-local capacity error, a transfer
   // error) must not leave its peers blocked in the next collective: the loopback world releases
-  // every rendezvous, and on RCCL every local communicator is aborted (ncclCommAbort stops the
-  // peers' pending send/recv/all-reduce kernels; an aborted communicator is never reused).
-  std::mutex abort_mu;
-  bool comms_aborted = false;
-  auto abort_all = [&]() {
-    world.abort();
-    if (!use_rccl) return;
-    std::lock_guard<std::mutex> lk(abort_mu);
-    if (comms_aborted) return;
-    comms_aborted = true;
-    for (ncclComm_t x : c->local_comms) if (x) (void)rmc::rccl().CommAbort(x);
-  };
+  // every rendezvous, and on RCCL the communicators are aborted through RcclAbort (which waits for
+  // every rank to be outside its RCCL calls first, so no rank uses a freed communicator; ncclCommAbort
+  // stops the peers' pending send/recv/all-reduce kernels; an aborted communicator is never reused).
+  rmc::RcclAbort ab(W);
   auto rank_main = [&](int r) {
     rmc::Backend* be = c->rank_backend(r);
     rmc::RunOpts o = c->ro;
@@ -252,22 +253,28 @@ int run_multi(mc_ctx* c) {
     std::string e;
     int rc = be->shard_open(o, r, W, e);   // selects the device on this thread
     if (!rc) {
-      if (use_rccl) { rmc::RcclTransport t(c->local_comms[r]); rc = be->shard_run_native(t, e); }
+      if (use_rccl) { rmc::RcclTransport t(c->local_comms[r], &ab, r); rc = be->shard_run_native(t, e); }
       else { rmc::LoopbackTransport t(world, r); rc = be->shard_run_native(t, e); }
     }
-    if (rc) abort_all();
+    if (rc) {
+      int expect = -1;
+      ab.first.compare_exchange_strong(expect, r);   // the first rank to fail reports the cause
+      world.abort();
+      if (use_rccl) ab.abort_all(r, c->local_comms);
+    }
     rcs[r] = rc; errs[r] = e;
   };
   std::vector<std::thread> th;
   for (int r = 1; r < W; ++r) th.emplace_back(rank_main, r);
   rank_main(0);
   for (auto& x : th) x.join();
-  if (comms_aborted) c->local_comms.clear();   // aborted: the next run builds fresh communicators
+  if (ab.done) c->local_comms.clear();   // aborted (and freed by the abort): the next run builds fresh communicators
   // report the rank that failed first in its own right (not a peer released by the abort)
-  for (int pass = 0; pass < 2; ++pass)
-    for (int r = 0; r < W; ++r)
-      if (rcs[r] && (pass == 1 || errs[r].find("another rank left") == std::string::npos))
-        { c->last_error = "rank " + std::to_string(r) + ": " + errs[r]; return rcs[r]; }
+  if (ab.first.load() >= 0) {
+    const int r = ab.first.load();
+    c->last_error = "rank " + std::to_string(r) + ": " + errs[r];
+    return rcs[r];
+  }
   c->res = *c->be->shard_result();                 // every rank holds the global counts
   for (int r = 0; r < W && c->res.violated.empty(); ++r) c->res.violated = c->rank_backend(r)->shard_result()->violated;
   // the counterexample: the lowest rank holding the stop's head, then the parent chain by owner

@@ -46,6 +46,7 @@
 #include <functional>
 #include <map>
 #include <sstream>
+#include <type_traits>
 
 #include "../../include/raftmc.h"
 #include "backend.h"
@@ -78,6 +79,15 @@ constexpr int BS = 256;                       // workgroup size of every kernel 
 constexpr int LDS_FP_SLOTS = RMC_LDS_SLOTS;   // workgroup-local fingerprint set (8 B fp + 4 B key per slot)
 constexpr int MAT_CAP = 2048;      // winners staged in LDS per materialize round
 constexpr int SCAN_BS = 1024;      // orig_scan workgroup
+
+// f(std::integral_constant<int, Q>) for Q = B .. E-1: a loop whose index is a compile-time constant
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
 
 // 64-bit event word: key << 2 | kind, key = parent gid << 8 | instance (gid < 2^40)
 RMC_HD u64 ev_word(u64 gid, u32 inst, u32 kind) { return (((gid << 8) | (u64)inst) << 2) | (u64)kind; }
@@ -128,6 +138,9 @@ template <class S>
 #endif
 #ifndef RMC_GEN_INC
 #define RMC_GEN_INC 1
+#endif
+#ifndef RMC_GEN_DD_LOOP
+#define RMC_GEN_DD_LOOP 0   // 1: DuplicateMessage / DropMessage through the generic loop (apply + pack), A/B only
 #endif
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 15 ? RMC_GEN_WAVES : 1))) orig_generate(GenArgs a) {
   using W = typename S::Work;
@@ -187,8 +200,11 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
   // instead -- SURVEY.md §7 hard part 8 -- and measured 19.5 vs 14.5 ms of orig_generate per C2 run
   // on MI355X, round 4: the per-lane instance index turns the decode and selects into vector work
   // and the saved iterations do not pay for it.)
+  // DuplicateMessage / DropMessage [I_DUP, NI) change one message count and nothing else: with the
+  // incremental fingerprint they are the unrolled section after this loop (no apply, no pack)
+  constexpr int KEND = (INC && !RMC_GEN_DD_LOOP) ? S::I_DUP : S::NI;
 #pragma unroll 1
-  for (int kk = 0; kk < S::NI; ++kk) {
+  for (int kk = 0; kk < KEND; ++kk) {
 #ifndef RMC_DBG_NO_SKIP
     if (kk == S::LEAD_LO) kk = S::LEAD_HI;      // wave-uniform
 #endif
@@ -322,6 +338,57 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
     }
     wcount += (u32)__popcll(mask);
   }
+#ifndef RMC_GEN_BINNED
+  if constexpr (KEND < S::NI) {
+    // DuplicateMessage(m) / DropMessage(m) (raft_original.tla:442-449) for bag slot q, in instance
+    // order, unrolled (q is a compile-time constant): the successor is the parent (allLogs' applied)
+    // with one message count +-1 — the count field is the low CNTB bits of bag entry q, at the
+    // compile-time bit offset BAG_OFF + q * ENTB of the packed state.  Every other constraint reads
+    // what the parent already satisfies, so the successor is in the model iff BoundedMessages keeps
+    // the new count in [MinMsgCount, MaxMsgCount]; no invariant reads the bag (S::inv_frame), so an
+    // out-of-model one is only counted.  Its fingerprint re-mixes the one or two 64-bit words that
+    // hold the field (FpBase::fp_add_bit): no apply, no pack.  (C2: 532M of the 1,348M generated
+    // successors, 266M of the 590M in the model; orig_materialize_plain still re-derives the new
+    // ones through S::apply.)  The per-action count is uniform over the wave: one ballot and one LDS
+    // atomic per slot.
+    const bool bounded = (a.rt.constraints & OC_BoundedMessages) != 0;
+    static_for<0, 2 * S::MK>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      constexpr bool dup = q < S::MK;
+      constexpr int slot = dup ? q : q - S::MK;
+      constexpr int k = S::I_DUP + q;
+      const typename S::BE ent = s.bag.v[slot];
+      const bool on = active && ent != S::BEMPTY;
+      const int c = S::ecount(ent) + (dup ? 1 : -1);
+      bool have = false;
+      u64 fp = 0;
+      if (on) {
+        ++nsucc;
+        if (bounded && (c < a.rt.min_count || c > a.rt.max_count)) {
+          // out of the model (S::quick_out_of_model): counted only
+        } else if (c < -8 || c > 7) {
+          err |= OE_CAP_COUNT;                              // the packed count field holds -8..7 (bag_add_at)
+        } else {
+          have = true;
+          ++nin;
+          fp = fb.template fp_add_bit<S::BAG_OFF + slot * S::ENTB>(bw, dup ? 1 : -1, a.seed);
+        }
+      }
+      {
+        const u64 om = __ballot(on);
+        if (om && lane == __ffsll((unsigned long long)om) - 1)
+          atomicAdd(&lds_cnt[dup ? OA_DuplicateMessage : OA_DropMessage], (unsigned)__popcll(om));
+      }
+      const u64 mask = __ballot(have);
+      if (have) {
+        const u32 idx = wcount + __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
+        rfp[idx] = fp;
+        rkey[idx] = (unsigned short)((threadIdx.x << 8) | (unsigned)k);
+      }
+      wcount += (u32)__popcll(mask);
+    });
+  }
+#endif
   if (active) {
     if (err & OE_EVAL_LOG_INDEX) { const u64 e = ev_word(gid, 0, EV_NEXT_ERROR); ev = e < ev ? e : ev; }
     if (nsucc == 0 && a.deadlock && !lead) { const u64 e = ev_word(gid, 0, EV_DEADLOCK); ev = e < ev ? e : ev; }
@@ -459,16 +526,32 @@ struct WaveRegions {
   }
 };
 
-// Workgroup-local first-come fingerprint filter: answers only "certainly produced here before".
-// Plain LDS loads and stores: a race can make the set forget an entry (a duplicate reaches the
-// seen-set, which decides), never report a first occurrence as a duplicate.
-RMC_HD bool lds_first(unsigned long long* set, u64 fp) {
+// Workgroup-local first-come fingerprint filter: answers only "certainly produced here before"
+// (a full probe window lets the record through: the seen-set decides).  An empty slot is claimed
+// by LDS CAS, so the set is exact up to the window: with plain stores (RMC_LDS_PLAIN, the round-4
+// form) two lanes inserting different fingerprints into one slot at once left one of them out of
+// the set, and two lanes with the same fingerprint both passed.  Measured on C2 (round 5,
+// profiles/r05_dedup_ab.txt): 339.5M seen-set probes per run instead of 367.0M, orig_dedup_plain
+// 11.30 vs 11.51 ms; a 16-slot window changed nothing (366.5M: overflow is not the leak) and an
+// 8192-slot set (64 KB) cost occupancy (14.96 ms).
+#ifndef RMC_LDS_WIN
+#define RMC_LDS_WIN 8
+#endif
+__device__ __forceinline__ bool lds_first(unsigned long long* set, u64 fp) {
   u32 h = (u32)(fp >> 20) & (LDS_FP_SLOTS - 1);
 #pragma unroll 1
-  for (int p = 0; p < 8; ++p) {
-    const unsigned long long cur = set[h];
+  for (int p = 0; p < RMC_LDS_WIN; ++p) {
+    unsigned long long cur = set[h];
     if (cur == fp) return false;            // produced here before
+#ifndef RMC_LDS_PLAIN
+    if (cur == 0ull) {                      // claim the slot; a lane that loses the race looks at the winner's fp
+      cur = atomicCAS(&set[h], 0ull, (unsigned long long)fp);
+      if (cur == 0ull) return true;
+      if (cur == fp) return false;
+    }
+#else
     if (cur == 0ull) { set[h] = fp; return true; }
+#endif
     h = (h + 1) & (LDS_FP_SLOTS - 1);
   }
   return true;                              // window full: let the seen-set decide
@@ -643,7 +726,9 @@ __global__ void __launch_bounds__(BS) orig_merge(DedupArgs a) {
 // Seen-set insertion, part 2 (HBM random access): workgroup b probes the seen-set once per
 // distinct fingerprint of region b, DEDUP_PER probes in flight per thread (insert-if-absent by CAS
 // of the fp, then atomicMax of ~key: the entry keeps the minimum key), and appends the inserted
-// entries' positions (one global atomic per workgroup and round).
+// entries' positions (one global atomic per workgroup and round).  COUNT: also count the probes
+// (ctr[K_PROBES]; RAFTMC_COUNT_PROBES, a run of its own: timed runs leave the atomic out)
+template <bool COUNT>
 __global__ void __launch_bounds__(BS) orig_probe(DedupArgs a) {
   __shared__ u32 wave_tot[BS / 64];
   __shared__ unsigned long long base_sh;
@@ -651,7 +736,7 @@ __global__ void __launch_bounds__(BS) orig_probe(DedupArgs a) {
   const ulonglong2* in = a.urec + (u64)blockIdx.x * a.region;
   u32 err = 0;
   const u64 t0 = a.prof ? wall_clock64() : 0;
-  if (threadIdx.x == 0 && n) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)n);
+  if (COUNT && threadIdx.x == 0 && n) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)n);
 #pragma unroll 1
   for (u32 i0 = 0; i0 < n; i0 += DEDUP_PER * BS) {
     u64 fp[DEDUP_PER], nk[DEDUP_PER], pos[DEDUP_PER];
@@ -748,7 +833,7 @@ __global__ void __launch_bounds__(BS) orig_merge_plain(DedupArgs a) {
 // thread); the new states' producers are marked in an LDS (parent, instance) mask and written in
 // parent-major, instance order (one global atomic per workgroup): the next level keeps siblings
 // adjacent, so its diamonds land in one workgroup again and its waves hold similar states
-template <int WW>
+template <int WW, bool COUNT>
 __global__ void __launch_bounds__(BS) orig_probe_plain(DedupArgs a) {
   __shared__ u32 wave_tot[BS / 64];
   __shared__ unsigned long long base_sh;
@@ -759,7 +844,7 @@ __global__ void __launch_bounds__(BS) orig_probe_plain(DedupArgs a) {
   const ulonglong2* in = a.urec + (u64)blockIdx.x * a.region;
   const u64 pgid0 = a.gid0 + (u64)blockIdx.x * BS;   // global id of this workgroup's first parent
   u32 err = 0;
-  if (threadIdx.x == 0 && n) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)n);
+  if (COUNT && threadIdx.x == 0 && n) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)n);
 #pragma unroll 1
   for (u32 i0 = 0; i0 < n; i0 += DEDUP_PER * BS) {
     u64 fp[DEDUP_PER], key[DEDUP_PER], pos[DEDUP_PER];
@@ -801,7 +886,7 @@ __global__ void __launch_bounds__(BS) orig_probe_plain(DedupArgs a) {
 }
 
 // Fused variant for TLC -workers N (what the pipeline runs): records through a first-come LDS
-// filter (plain LDS loads and stores, 32 KB: a race can only let a duplicate through to the
+// filter (lds_first: an LDS CAS claims each empty slot, 32 KB; a full window lets a record through to the
 // seen-set, never drop a state), the survivors probe the 8-B seen-set DEDUP_PER at a time, and
 // the new states' producers go out parent-major as in orig_probe_plain.  COUNT: also count the
 // fingerprints that reach the seen-set (ctr[K_PROBES], one atomic per workgroup) -- a separate
@@ -1316,7 +1401,7 @@ __global__ void __launch_bounds__(BS) orig_route_blk(RouteArgs a) {
       const u32 lk = i < n ? keys[at] : 0u;
       slot[j] = (((u64)blockIdx.x * BS + (lk >> 8)) << 8) | (u64)(lk & 255u);
       // produced before by this workgroup's parents?  The first-come filter of orig_dedup_plain
-      // (plain LDS loads and stores: a race only lets a duplicate through to its owner's seen-set)
+      // (lds_first: a full probe window only lets a duplicate through to its owner's seen-set)
       if (fp[j] && !lds_first(lds_fp, fp[j])) fp[j] = 0;
       own[j] = fp[j] ? (int)fp_owner(fp[j], a.world) : -1;
       off[j] = own[j] >= 0 ? atomicAdd(&hist[own[j]], 1u) : 0u;
@@ -1387,6 +1472,8 @@ struct MatShArgs {
   u32* st_states;
   u64* st_meta;
   u64 st_dst, st_cap;
+  u32 store;                   // 0: the last level of a depth-bounded search (count_final_level):
+                               // counted and invariant-checked, neither stored nor shipped
 };
 
 template <class S>
@@ -1418,7 +1505,9 @@ __global__ void __launch_bounds__(BS) orig_materialize_sh(MatShArgs a) {
     S::pack(t, pw);
     const u64 fp = fp64(pw, a.seed);
     const u64 meta = ((a.rank_bits | gid) << 24) | ((u64)(act < 0 ? 0 : act) << 16) | k;
-    if (a.st_states) {
+    if (!a.store) {
+      // counted only (count_final_level)
+    } else if (a.st_states) {
       const u64 dst = a.st_dst + i;
       if (dst < a.st_cap) {
         uint4* o = reinterpret_cast<uint4*>(a.st_states + dst * NWP);
@@ -1619,6 +1708,7 @@ class OrigGpu : public Backend {
   }
 
   int run(const RunOpts& o, RunResult& r, std::string& err) override {
+    unstored_ = 0;   // a previous run's unstored level must not outlive it (mc_dump_states)
     if (int rc = ensure_alloc(o, 0, err)) return rc;   // world 0 = single-GPU pipeline
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
@@ -1715,12 +1805,14 @@ class OrigGpu : public Backend {
         if (fifo) {
           hipLaunchKernelGGL(orig_merge, dim3(nblk), dim3(BS), 0, stream_, d);
           HIPCHK(hipGetLastError());
-          hipLaunchKernelGGL(orig_probe, dim3(nblk), dim3(BS), 0, stream_, d);
+          if (count_probes) hipLaunchKernelGGL((orig_probe<true>), dim3(nblk), dim3(BS), 0, stream_, d);
+          else hipLaunchKernelGGL((orig_probe<false>), dim3(nblk), dim3(BS), 0, stream_, d);
         } else {
           if (split_plain_) {
             hipLaunchKernelGGL(orig_merge_plain, dim3(nblk), dim3(BS), 0, stream_, d);
             HIPCHK(hipGetLastError());
-            hipLaunchKernelGGL((orig_probe_plain<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
+            if (count_probes) hipLaunchKernelGGL((orig_probe_plain<WW, true>), dim3(nblk), dim3(BS), 0, stream_, d);
+            else hipLaunchKernelGGL((orig_probe_plain<WW, false>), dim3(nblk), dim3(BS), 0, stream_, d);
           } else if (dedup_queue_) {
             hipLaunchKernelGGL((orig_dedup_queue<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
           } else if (count_probes) {
@@ -1817,7 +1909,17 @@ class OrigGpu : public Backend {
         o1.workers = 1;
         o1.recover_path.clear();        // a checkpoint of this search is in its order, not TLC's: start over
         o1.checkpoint_path.clear();
-        return run(o1, r, err);
+        const u64 evw = c[K_EVENT];
+        const int64_t ev_depth = r.depth + 1;
+        const int rc = run(o1, r, err);
+        if (rc == 0 && r.verdict == MC_VERDICT_CAPACITY_OVERFLOW) {
+          // the FIFO re-search stores every level (count_final_level included): when it does not
+          // fit, the event the -workers N pass found is still reported, not lost
+          static const char* const kind[4] = {"an evaluation error", "a deadlock", "an invariant evaluation error", "an invariant violation"};
+          r.error = std::string("the -workers N search found ") + kind[evw & 3] + " at depth " + std::to_string(ev_depth) +
+                    "; TLC's single-worker re-search of it (for TLC's counterexample and stop point) ran out of capacity: " + r.error;
+        }
+        return rc;
       }
       if (c[K_EVENT] != ~0ull && (c[K_ERR] & ~(u64)OE_CAP_STORE) == 0) {
         // the level's first event in TLC's order stops the search; a full state store only
@@ -2121,6 +2223,7 @@ class OrigGpu : public Backend {
     if (world < 1 || world > 8 || rank < 0 || rank >= world) { err = "sharded mode supports 1..8 ranks"; return MC_E_INVALID; }
     if (int rc = ensure_alloc(o, world, err)) return rc;
     rank_ = rank; world_ = world; sopts_ = o;
+    unstored_ = 0;
     last_fifo_ = false;   // 8-B entries (observed_collision)
     HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
     HIPCHK(hipMemsetAsync(d_ctr_, 0, K_NCTR * 8, stream_));
@@ -2255,7 +2358,7 @@ class OrigGpu : public Backend {
       m.states = d_states_; m.acks = (const u64*)acks + seg_off_ack_[r]; m.n = n; m.chunk_begin = sh_chunk_begin_;
       m.chunk_count = sh_chunk_count_; m.out = d_stout_ + seg_off_ack_[r] * (NWP + 4); m.rank_bits = (u64)rank_ << 37;
       m.seed = sres_.seed; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_;
-      m.st_states = nullptr; m.st_meta = nullptr; m.st_dst = 0; m.st_cap = 0;
+      m.st_states = nullptr; m.st_meta = nullptr; m.st_dst = 0; m.st_cap = 0; m.store = 1;
       hipLaunchKernelGGL((orig_materialize_sh<S>), dim3((unsigned)((n + BS - 1) / BS)), dim3(BS), 0, stream_, m);
       HIPCHK(hipGetLastError());
     }
@@ -2308,8 +2411,14 @@ class OrigGpu : public Backend {
       std::ostringstream os; os << "error flags 0x" << std::hex << g[3] << " raised on some rank"; sres_.error = os.str();
       *done = 1;
     }
-    sres_.distinct += g[0];
-    if (g[0] > 0) { sres_.levels.push_back({g[0], 0, 0.0}); sres_.depth += 1; }
+    if (*done && sres_.verdict == MC_VERDICT_CAPACITY_OVERFLOW) {
+      // as on one GPU: the summary counts the completed levels; the interrupted one is not a level
+      sres_.error += "; the summary counts the " + std::to_string(sres_.distinct) + " states of the " +
+                     std::to_string(sres_.depth) + " completed levels";
+    } else {
+      sres_.distinct += g[0];
+      if (g[0] > 0) { sres_.levels.push_back({g[0], 0, 0.0}); sres_.depth += 1; }
+    }
     if (!*done && g[4]) { sres_.verdict = MC_VERDICT_INVARIANT_VIOLATION; *done = 1; sres_.left_on_queue = g[0]; }
     if (!*done && sopts_.check_deadlock && g[5]) { sres_.verdict = MC_VERDICT_DEADLOCK; *done = 1; sres_.left_on_queue = g[0]; }
     if (!*done && g[0] == 0) *done = 1;
@@ -2471,8 +2580,22 @@ class OrigGpu : public Backend {
       if (int rc = allreduce_level(z, rounds(sh_level_count_), nchunks)) return rc;
     }
     const u64 route_cap = chunk_states_ * S::NI;
+    // count_final_level: the level at depth max_depth is never expanded, so its new states are
+    // deduplicated by their owners, counted and invariant-checked by the generating rank, but
+    // neither shipped to the owners nor stored (no STATES exchange, no store kernel): the ranks'
+    // stores hold the levels before it (BASELINE configs[4], C5v2 to depth 14 on 8 GPUs)
+    const bool count_last = sopts_.count_final_level && sopts_.max_depth > 0;
+    unstored_ = 0;
     for (;;) {
       const u64 front = sh_level_count_;
+      const bool last = count_last && sres_.depth + 1 >= sopts_.max_depth;
+      if (const char* inj = std::getenv("RAFTMC_TEST_SHARD_FAIL")) {   // test hook: "rank:depth" leaves the loop there
+        int fr = -1, fd = -1;
+        if (std::sscanf(inj, "%d:%d", &fr, &fd) == 2 && fr == me && (int64_t)fd == sres_.depth) {
+          err = "injected failure (RAFTMC_TEST_SHARD_FAIL) at depth " + std::to_string(fd);
+          return MC_E_STATE;
+        }
+      }
       for (int64_t c = 0; c < nchunks; ++c) {
         const u64 begin = std::min<u64>((u64)c * chunk, front);
         const u64 count = std::min<u64>(chunk, front - begin);
@@ -2531,25 +2654,31 @@ class OrigGpu : public Backend {
         {
           u64 off = 0;
           for (int r = 0; r < W; ++r) { seg_off_ack_[r] = off; off += ack[r]; }
-          void* so = d_stout_;
-          u64 socap = stout_cap_ * SBW;
-          if (int rc = grow(so, socap, atot * SBW)) return rc;
-          d_stout_ = (u32*)so; stout_cap_ = socap / SBW;
+          if (!last) {
+            void* so = d_stout_;
+            u64 socap = stout_cap_ * SBW;
+            if (int rc = grow(so, socap, atot * SBW)) return rc;
+            d_stout_ = (u32*)so; stout_cap_ = socap / SBW;
+          }
           for (int r = 0; r < W; ++r) {
             if (!ack[r]) continue;
             MatShArgs m;
             m.states = d_states_; m.acks = r == me ? d_newrec_ + seg_off_[me] : (const u64*)nat_acks_ + seg_off_ack_[r];
             m.n = ack[r]; m.chunk_begin = sh_chunk_begin_;
-            m.chunk_count = sh_chunk_count_; m.out = d_stout_ + seg_off_ack_[r] * (NWP + 4); m.rank_bits = (u64)me << 37;
+            m.chunk_count = sh_chunk_count_; m.out = last ? nullptr : d_stout_ + seg_off_ack_[r] * (NWP + 4); m.rank_bits = (u64)me << 37;
             m.seed = sres_.seed; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_;
-            m.st_states = nullptr; m.st_meta = nullptr; m.st_dst = 0; m.st_cap = 0;
-            if (r == me) {   // my own new states: into my store after the ones of lower ranks
+            m.st_states = nullptr; m.st_meta = nullptr; m.st_dst = 0; m.st_cap = 0; m.store = last ? 0u : 1u;
+            if (r == me && !last) {   // my own new states: into my store after the ones of lower ranks
               u64 before = 0; for (int q = 0; q < me; ++q) before += rep[q];
               m.st_states = d_states_; m.st_meta = d_meta_; m.st_dst = sh_next_write_ + before; m.st_cap = cap_;
             }
             NAT_TIMED(3, hipLaunchKernelGGL((orig_materialize_sh<S>), dim3((unsigned)((ack[r] + BS - 1) / BS)), dim3(BS), 0, stream_, m));
           }
-          sres_.kernels[3].algo_bytes += (double)atot * (8 + NWP * 4 + SBW);
+          sres_.kernels[3].algo_bytes += (double)atot * (8 + NWP * 4 + (last ? 0 : SBW));
+        }
+        if (last) {   // the owners count their new states of the final level; nothing is shipped
+          for (int r = 0; r < W; ++r) sh_new_ += rep[r];
+          continue;
         }
         // ---- STATES: packed states + parent pointers to their owners (sizes known: no sync)
         for (int r = 0; r < W; ++r) { sb[r] = ack[r] * SBW; rb[r] = rep[r] * SBW; src[r] = (const char*)(d_stout_ + seg_off_ack_[r] * (NWP + 4)); }
@@ -2579,6 +2708,7 @@ class OrigGpu : public Backend {
       if (int rc = shard_level_stats(g, err)) return rc;
       int64_t next_chunks = 0;
       if (int rc = allreduce_level(g, rounds(sh_new_), next_chunks)) return rc;
+      if (last) unstored_ = sh_new_;   // this rank's share of the final level: counted, not in the store
       int done = 0;
       if (int rc = shard_level_commit(g, &done, err)) return rc;
       if (done) break;

@@ -104,6 +104,7 @@ struct Orig {
   static constexpr int PBITS = N * TB + N * 2 + N * VB + N * CIB + N * N + N * N + N * N * NIB + N * N * CIB +
                                N * (SLLB + ML * EB) + N * N * VLB + (int)U + EMAX * ELB + MK * ENTB;
   static constexpr int NW = (PBITS + 31) / 32;      // u32 words per stored state
+  static constexpr int BAG_OFF = PBITS - MK * ENTB; // bit offset of bag entry 0 (its count: the low CNTB bits)
   static constexpr int NI = 3 * N + 2 * N * N + N * NV + N + 3 * MK;   // action instances per state
   // the instances that need a Leader (ClientRequest, AdvanceCommitIndex, AppendEntries) or a
   // Candidate holding a quorum (BecomeLeader): one contiguous range [LEAD_LO, LEAD_HI) of apply's

@@ -12,11 +12,13 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <climits>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rccl_api.h"
@@ -30,14 +32,56 @@ struct ShardTransport {
   virtual int allreduce(int64_t* d_sum, int n_sum, int64_t* d_max, int n_max, hipStream_t s, std::string& err) = 0;
 };
 
+// Abort coordination of the in-process multi-GPU run (mc_api.cpp run_multi): the ranks' RcclTransports
+// share one RcclAbort.  Every RCCL call of a rank is bracketed by its `busy` flag, raised BEFORE the
+// `aborted` flag is read (both sequentially consistent), so the aborting thread either sees the rank
+// inside a call and waits for it to leave, or the rank sees `aborted` and returns an error without
+// touching its communicator.  Only then is the communicator aborted (ncclCommAbort frees it and stops
+// its pending kernels, which releases a peer blocked in a stream synchronisation on them): no rank
+// uses a freed communicator.  A rank blocked inside an RCCL call for longer than the grace period
+// (a connection setup waiting for the failed peer) is aborted anyway: that call cannot return otherwise.
+struct RcclAbort {
+  explicit RcclAbort(int w) : busy(w) { for (auto& b : busy) b.store(false); }
+  std::vector<std::atomic<bool>> busy;   // [rank] inside an RCCL call
+  std::atomic<bool> aborted{false};
+  std::atomic<int> first{-1};            // the rank that failed first in its own right
+  std::mutex mu;
+  bool done = false;                     // communicators aborted (under mu)
+  // called by a failing rank; returns after every communicator is aborted
+  void abort_all(int rank, std::vector<ncclComm_t>& comms) {
+    int expect = -1;
+    first.compare_exchange_strong(expect, rank);
+    aborted.store(true);
+    std::lock_guard<std::mutex> lk(mu);
+    if (done) return;
+    done = true;
+    for (size_t r = 0; r < comms.size(); ++r) {
+      for (int spin = 0; busy[r].load() && spin < 5000; ++spin) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      if (comms[r]) (void)rccl().CommAbort(comms[r]);
+      comms[r] = nullptr;                // freed by the abort: never destroyed again
+    }
+  }
+};
+
 // RCCL over xGMI: grouped ncclSend/ncclRecv straight between the kernels' buffers
 struct RcclTransport : ShardTransport {
   ncclComm_t comm;
-  explicit RcclTransport(ncclComm_t c) : comm(c) {}
+  RcclAbort* ab;   // the in-process run's abort coordination (nullptr: one rank per process)
+  int rank;
+  explicit RcclTransport(ncclComm_t c, RcclAbort* a = nullptr, int r = 0) : comm(c), ab(a), rank(r) {}
+  // raise busy, then check aborted (see RcclAbort); false = aborted, the call must not run
+  bool enter(std::string& err) {
+    if (!ab) return true;
+    ab->busy[rank].store(true);
+    if (ab->aborted.load()) { ab->busy[rank].store(false); err = "RCCL: another rank left the loop (communicators aborted)"; return false; }
+    return true;
+  }
+  void leave() { if (ab) ab->busy[rank].store(false); }
   int exchange(int me, int W, const char* const* src, const uint64_t* sbytes, char* const* dst, const uint64_t* rbytes,
                hipStream_t s, std::string& err) override {
     RcclApi& R = rccl();
     if (W <= 1) return 0;
+    if (!enter(err)) return -5;
     ncclResult_t r = R.GroupStart();
     for (int p = 0; p < W && r == ncclSuccess; ++p) {
       if (p == me) continue;
@@ -45,15 +89,18 @@ struct RcclTransport : ShardTransport {
       if (r == ncclSuccess && rbytes[p]) r = R.Recv(dst[p], rbytes[p], ncclUint8, p, comm, s);
     }
     const ncclResult_t r2 = R.GroupEnd();
+    leave();
     if (r != ncclSuccess || r2 != ncclSuccess) { err = std::string("RCCL exchange: ") + R.GetErrorString(r != ncclSuccess ? r : r2); return -5; }
     return 0;
   }
   int allreduce(int64_t* d_sum, int n_sum, int64_t* d_max, int n_max, hipStream_t s, std::string& err) override {
     RcclApi& R = rccl();
+    if (!enter(err)) return -5;
     ncclResult_t r = R.GroupStart();
     if (r == ncclSuccess) r = R.AllReduce(d_sum, d_sum, n_sum, ncclInt64, ncclSum, comm, s);
     if (r == ncclSuccess) r = R.AllReduce(d_max, d_max, n_max, ncclInt64, ncclMax, comm, s);
     const ncclResult_t r2 = R.GroupEnd();
+    leave();
     if (r != ncclSuccess || r2 != ncclSuccess) { err = std::string("RCCL all-reduce: ") + R.GetErrorString(r != ncclSuccess ? r : r2); return -5; }
     return 0;
   }

@@ -40,7 +40,10 @@ SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing
           ("memb_morc_gen", "configs/raft_membership_mc.tla", "configs/scen_MajorityOfClusterRestarts_punct.cfg"),
           ("memb_cwcl_gen", "configs/raft_membership_mc.tla", "configs/scen_CommitWhenConcurrentLeaders_punct.cfg"),
           # the reference's Apalache spec with its own shipped cfg (TLC syntax): recursive Sum
-          ("apalache_nm", REF + "/apalache_no_membership/raft.tla", REF + "/apalache_no_membership/raft.cfg")]
+          ("apalache_nm", REF + "/apalache_no_membership/raft.tla", REF + "/apalache_no_membership/raft.cfg"),
+          # ... and with its commented-out test-case invariants (pinned by oracle/raft_apalache.h)
+          ("apalache_nm_boundedtrace", REF + "/apalache_no_membership/raft.tla", "configs/apalache_nm_boundedtrace.cfg"),
+          ("apalache_nm_firstbecomeleader", REF + "/apalache_no_membership/raft.tla", "configs/apalache_nm_firstbecomeleader.cfg")]
 
 
 def key_of(src):

@@ -83,6 +83,9 @@ const char* kOpts[] = {"--offload-arch=gfx950", "-O2", "-std=c++17"};
 // per-lane stack of a kernel that evaluates recursive function definitions (tlv::kMaxRecDepth
 // nested calls of a few hundred bytes each, over the kernel's own frame)
 constexpr size_t kRecStackBytes = 16384;
+// the text the generator emits into a recursive function definition's depth guard: a source holding
+// it gets kRecStackBytes per lane (scripts/check_isa.py reads the same marker)
+constexpr const char* kRecMarker = "kMaxRecDepth) {";
 
 #define HIPOK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { err = std::string(#x) + ": " + hipGetErrorString(e_); return MC_E_NO_DEVICE; } } while (0)
 
@@ -255,16 +258,23 @@ struct TlagenBackend : Backend {
       int rc = run_once(o, r, err, again);
       if (rc == 0 && again) {
         // TLC -workers N found an event: TLC's counterexample and stop point are the single-worker
-        // search's, so the model is searched again in FIFO order (as the hand-compiled paths do)
+        // search's, so the model is searched again in FIFO order (as the hand-compiled paths do).
+        // That search needs more HBM per state (44 B of bookkeeping instead of 20, 16-B seen-set
+        // entries): when it does not fit, the event the first search found is still reported
         RunOpts o1 = o;
         o1.workers = 1;
+        const std::string found = workers_event_;
         rc = run_once(o1, r, err, again);
+        if (rc == 0 && r.verdict == MC_VERDICT_CAPACITY_OVERFLOW && !arena_overflow)
+          r.error = "the -workers N search found " + found + "; TLC's single-worker re-search of it (for TLC's "
+                    "counterexample and stop point) ran out of capacity: " + r.error;
       }
       if (rc != 0 || !arena_overflow || arena_scale >= 64) return rc;
     }
   }
   u32 arena_scale = 1;
   bool arena_overflow = false;
+  std::string workers_event_;   // what a -workers N search stopped on (named if its FIFO re-search overflows)
 
   int run_once(const RunOpts& o, RunResult& r, std::string& err, bool& again) {
     again = false;
@@ -287,7 +297,11 @@ struct TlagenBackend : Backend {
       std::vector<void*> bufs;
       void* sort_tmp = nullptr;
       hipEvent_t e0 = nullptr, e1 = nullptr;
+      size_t prev_stack = 0;       // the device's stack limit before a recursive module raised it
+      bool stack_raised = false;
       ~Scratch() {
+        // hipLimitStackSize is process-wide: later kernels (the hand-compiled paths) get their limit back
+        if (stack_raised) (void)hipDeviceSetLimit(hipLimitStackSize, prev_stack);
         for (void* p : bufs) if (p) (void)hipFree(p);
         if (sort_tmp) (void)hipFree(sort_tmp);
         if (e0) (void)hipEventDestroy(e0);
@@ -300,7 +314,13 @@ struct TlagenBackend : Backend {
     // compiler cannot bound (dynamic stack): give each lane room for tlv::kMaxRecDepth nested
     // calls (the generated code refuses deeper recursion with an evaluation error), instead of the
     // runtime's default, which the static part of such a kernel's frame already exceeds.
-    if (src.find("kMaxRecDepth) {") != std::string::npos) HIPOK(hipDeviceSetLimit(hipLimitStackSize, kRecStackBytes));
+    // (scripts/check_isa.py fails the build for a code object with a dynamic stack whose source lacks
+    // this marker, or with a static frame above kRecStackBytes)
+    if (src.find(kRecMarker) != std::string::npos) {
+      HIPOK(hipDeviceGetLimit(&sc.prev_stack, hipLimitStackSize));
+      HIPOK(hipDeviceSetLimit(hipLimitStackSize, kRecStackBytes));
+      sc.stack_raised = true;
+    }
     HIPOK(hipModuleLoadData(&sc.mod, image.data()));
     hipFunction_t f_init, f_expand, f_keys, f_mat, f_stop;
     HIPOK(hipModuleGetFunction(&f_init, sc.mod, "tlg_init_k"));
@@ -427,7 +447,15 @@ struct TlagenBackend : Backend {
       first += count; count = fresh;
       if (fresh) ++r.depth; else r.levels.pop_back();
     }
-    if (!fifo && h[C_FLAG] && !h[C_CAP]) { again = true; return 0; }   // (searched again in FIFO order by run())
+    if (!fifo && h[C_FLAG] && !h[C_CAP]) {   // (searched again in FIFO order by run())
+      // tlagen_kernels.h C_KIND: 1/2 violation, 3 evaluation error, 4 deadlock, 5 invariant evaluation error
+      static const char* const kinds[] = {"an event", "an invariant violation", "an invariant violation",
+                                          "an evaluation error", "a deadlock", "an invariant evaluation error"};
+      const u64 kd = h[C_KIND];
+      workers_event_ = std::string(kd < 6 ? kinds[kd] : "an event") + " at depth " + std::to_string(r.depth + 1);
+      again = true;
+      return 0;
+    }
     // on a store overflow some ids were handed out without their words: only the committed states
     // are stored (and ids are no longer dense, so traces and dumps are refused below)
     store_complete = h[nctr - 3] == h[nctr - 2];

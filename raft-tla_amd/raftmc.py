@@ -16,7 +16,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RAFTMC_LIB") or os.path.join(_HERE, "_build", "libraftmc.so")   # RAFTMC_LIB: experiment builds only
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 VERDICTS = {0: "OK", 1: "INVARIANT_VIOLATION", 2: "EVAL_ERROR", 3: "CAPACITY_OVERFLOW", 4: "DEADLOCK", 5: "DEPTH_LIMIT"}
 MC_COMPAT_INV_OUT_OF_MODEL = 0x1
@@ -49,7 +49,8 @@ class McSummary(ctypes.Structure):
                 ("seconds_total", ctypes.c_double), ("seconds_kernels", ctypes.c_double),
                 ("fp_seed", ctypes.c_uint64), ("algo_bytes", ctypes.c_double),
                 ("generated_in_model", ctypes.c_int64), ("state_bytes", ctypes.c_int32), ("n_launches", ctypes.c_int32),
-                ("violated", ctypes.c_char * 64), ("spec", ctypes.c_char * 32), ("seen_set_probes", ctypes.c_int64)]
+                ("violated", ctypes.c_char * 64), ("spec", ctypes.c_char * 32), ("seen_set_probes", ctypes.c_int64),
+                ("reserved", ctypes.c_int64 * 8)]
 
 
 class RaftMCError(RuntimeError):

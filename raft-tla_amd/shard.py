@@ -458,6 +458,8 @@ class ShardedChecker:
         (RCCL), else torch."""
         self.rank, self.world = rank, world
         self.device = torch.device("cuda", device_index)
+        if kw.get("count_final_level") and transport == "torch":
+            raise ValueError("count_final_level runs in the library's native level loop (transport rccl), not shard.py's")
         self.mc = _rm.ModelChecker(spec, config, device=device_index, **kw)
         for con, text in (history_prefixes or {}).items():   # punctuated-search golden traces
             self.mc.set_history_prefix(con, text)

@@ -11,6 +11,12 @@ suite runs this check (tests/test_abi.py).  Round 3 adds a memory-ordering check
 no vector store or atomic may issue while a scalar load (other than of the kernel
 arguments) is outstanding — the compiler reordered a counter store ahead of the
 scalar load of the same counter, and the GPU intermittently lost new states.
+Round 5 adds the stack check (round 4's fault: gpurun_out/r4f, an illegal address in
+tlg_expand_k of the generated membership code, whose recursive perm_value ran a lane's stack
+past the runtime's default per-lane stack): a generated code object may use a dynamic stack
+only when its source carries the recursion marker, for which the backend raises the per-lane
+stack to REC_STACK_BYTES (tlagen_backend.cpp kRecStackBytes), and no kernel's static frame may
+exceed that.
 """
 import json
 import os
@@ -22,6 +28,9 @@ import tempfile
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 DEFAULT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raft-tla_amd", "_build", "libraftmc.so")
+# tlagen_backend.cpp: kRecMarker (a source holding it runs with kRecStackBytes per lane)
+REC_MARKER = "kMaxRecDepth) {"
+REC_STACK_BYTES = 16384
 
 
 MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
@@ -92,6 +101,7 @@ def kernels(co, functions=False):
     priv = re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)
     syms = re.findall(r"\.symbol:\s+(\S+)\.kd", notes)
     lds = re.findall(r"\.group_segment_fixed_size:\s+(\d+)", notes)
+    dyn = re.findall(r"\.uses_dynamic_stack:\s+(\S+)", notes)
     vgpr = re.findall(r"\.vgpr_count:\s+(\d+)", notes)
     agpr = re.findall(r"\.agpr_count:\s+(\d+)", notes)
     for k, (s, p) in enumerate(zip(syms, priv)):
@@ -100,18 +110,43 @@ def kernels(co, functions=False):
             if k < len(lds): out[s]["lds_bytes"] = int(lds[k])
             if k < len(vgpr): out[s]["vgprs"] = int(vgpr[k])
             if k < len(agpr): out[s]["agprs"] = int(agpr[k])
+            if k < len(dyn): out[s]["dynamic_stack"] = dyn[k] == "true"
     # functions=True: device functions too (the generated path's kernels call the functions its
     # front end outlines; a long branch or store hazard inside one is as bad as in a kernel)
     return {k if "scratch_bytes" in v else "fn:" + k: v for k, v in out.items() if functions or "scratch_bytes" in v}
 
 
+def stack_ok(v):
+    """a kernel's stack fits what the backend gives it: a dynamic stack only in a code object whose
+    source carries the recursion marker (v["raised_stack"]), and a static frame within the raised
+    per-lane stack"""
+    if v.get("dynamic_stack") and not v.get("raised_stack"):
+        return False
+    return v.get("scratch_bytes", 0) <= REC_STACK_BYTES
+
+
 def violations(ks, allow_scratch=False):
-    """Kernels/functions breaking the rules: long branches, store-after-scalar-load hazards, and
-    (unless allowed) scratch.  The generated path's code objects are allowed scratch: their
-    kernels call outlined functions (a call stack) and keep a state's variable handles in a
-    private array; the hand-compiled library is not."""
+    """Kernels/functions breaking the rules: long branches, store-after-scalar-load hazards, stacks the
+    backend does not provide (stack_ok), and (unless allowed) scratch.  The generated path's code
+    objects are allowed scratch: their kernels call outlined functions (a call stack) and keep a
+    state's variable handles in a private array; the hand-compiled library is not."""
     return {k: v for k, v in ks.items()
-            if v["long_branches"] or v["smem_store_hazards"] or (not allow_scratch and v.get("scratch_bytes"))}
+            if v["long_branches"] or v["smem_store_hazards"] or (not allow_scratch and v.get("scratch_bytes")) or not stack_ok(v)}
+
+
+def raised_stack(hsaco):
+    """True when the generated source of this code object (a *.gen.hip next to it whose cache key is
+    the file name, prebuild.py key_of) carries the recursion marker"""
+    d = os.path.dirname(os.path.abspath(hsaco))
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raft-tla_amd", "csrc", "tlagen"))
+    from prebuild import key_of
+    want = os.path.basename(hsaco)[:-len(".hsaco")]
+    for f in os.listdir(d):
+        if f.endswith(".gen.hip"):
+            src = open(os.path.join(d, f)).read()
+            if key_of(src) == want:
+                return REC_MARKER in src
+    return False
 
 
 def main():
@@ -119,8 +154,11 @@ def main():
     gen = all(l.endswith(".hsaco") for l in libs)
     ks = {}
     for lib in libs:
+        raised = lib.endswith(".hsaco") and raised_stack(lib)
         for co in code_objects(lib):
-            ks.update({(k if len(libs) == 1 else os.path.basename(lib) + ":" + k): v for k, v in kernels(co, gen).items()})
+            for k, v in kernels(co, gen).items():
+                v["raised_stack"] = raised
+                ks[k if len(libs) == 1 else os.path.basename(lib) + ":" + k] = v
     print(json.dumps(ks, indent=1, sort_keys=True))
     return 1 if violations(ks, allow_scratch=gen) else 0
 

@@ -1,0 +1,60 @@
+#!/bin/bash
+# One GPU session as a list of named steps (run through gpurun from the repo root):
+#   bash scripts/steps.sh OUT STEP [STEP ...]
+# Every step has its own time limit and writes under OUT; the first failing step ends the session
+# (after a GPU fault, abort, timeout or hang nothing else touches the GPU in that call).
+#   tests[=EXPR]        pytest -m gpu (optionally -k EXPR)
+#   smoke               __graft_entry__.smoke()
+#   bench               bench.py with its defaults (the driver's line)
+#   c2[=NAME[=LIB]]     bench.py C2 only (no extras, no CPU baseline) with library LIB (default: the
+#                       in-tree build), 8 timed steps; prints ms/step, kernels, seen-set probes
+#   prof                rocprofv3 --kernel-trace --stats of a short C2 bench
+#   pmc                 FETCH_SIZE / WRITE_SIZE / SQ passes over one C2 run (scripts/pmc_passes.sh)
+#   memb_prof           rocprofv3 stats + PMC passes of C3 (scripts/memb_prof.sh)
+#   py=SCRIPT ARGS..    python3 SCRIPT with its arguments (':' separates them: py=scripts/x.py:a:b)
+set -o pipefail
+O=${1:?OUT}; shift
+mkdir -p "$O"
+export TMPDIR=/tmp
+R=$(pwd)
+for step in "$@"; do
+  name=${step%%=*}; arg=${step#*=}; [ "$arg" = "$step" ] && arg=""
+  echo "== $step ($(date +%T))"
+  case $name in
+    tests)
+      k=(); [ -n "$arg" ] && k=(-k "$arg")
+      timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" > "$O/pytest.log" 2>&1
+      rc=$?; tail -3 "$O/pytest.log" ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
+      rc=$?; tail -1 "$O/smoke.log" ;;
+    bench)
+      timeout -k 10 600 python -u bench.py > "$O/bench.json" 2> "$O/bench.err"
+      rc=$?; cut -c1-600 "$O/bench.json" ;;
+    c2)
+      n=${arg%%=*}; lib=${arg#*=}; [ "$lib" = "$arg" ] && lib=""; n=${n:-base}
+      timeout -k 10 200 env ${lib:+RAFTMC_LIB=$lib} python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-extra --fifo-steps 0 \
+        > "$O/c2_$n.json" 2> "$O/c2_$n.err"
+      rc=$?
+      [ $rc -eq 0 ] && python3 -c "
+import json
+d = json.loads(open('$O/c2_$n.json').read().strip().splitlines()[-1])
+print('$n', round(d['ms_per_step'], 2), {k: round(v['ms'], 2) for k, v in d['kernels'].items()}, d['config']['distinct_per_run'],
+      'probes', d.get('dedup_set', {}).get('probes_per_run'))" ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_stats" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra --fifo-steps 0 > "$O/prof_stats.log" 2>&1
+      rc=$? ;;
+    pmc)
+      bash scripts/pmc_passes.sh "${O#$R/}/pmc"; rc=$? ;;
+    memb_prof)
+      bash scripts/memb_prof.sh "${O#$R/}/memb_prof" "${arg:-r05}"; rc=$? ;;
+    py)
+      IFS=':' read -r -a a <<< "$arg"
+      timeout -k 10 900 python3 -u "${a[@]}" > "$O/py_$(basename "${a[0]}" .py).log" 2>&1
+      rc=$?; tail -3 "$O/py_$(basename "${a[0]}" .py).log" ;;
+    *) echo "unknown step $name"; rc=2 ;;
+  esac
+  echo "== $step rc=$rc"
+  [ $rc -ne 0 ] && exit $rc
+done
+exit 0

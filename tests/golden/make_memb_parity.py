@@ -15,7 +15,11 @@ Punctuated-search cases take the golden history trace of their prefix
 constraint from the committed trace fixtures (tests/golden/*_trace.json, the
 TLC traces of tlc_membership/raft.tla:1201 and :1231).
 
-    python tests/golden/make_memb_parity.py [case ...]
+    python tests/golden/make_memb_parity.py [--workers T] [--out FILE] [case ...]
+
+--workers T expands each batch of parents on T threads with the frontier-order merge (results
+identical to one worker, oracle/engine.h); --out writes the cases into FILE instead of
+memb_parity.json (to run several cases in parallel and merge them afterwards).
 """
 import hashlib
 import json
@@ -65,6 +69,23 @@ CASES = {
     # bench.py's membership scale workload (C3's model without LeaderVotesQuorum), depth-bounded
     "tlc:memb_four_scale@15": ("memb_four_scale", 15),
     "tlc:scen_FirstCommit": ("scen_FirstCommit", 0),
+    # C4 in TLC's SYMMETRY rule (the drop-in default): every scenario property of raft.tla:1143-1278
+    # the oracle's exact search reaches (NewlyJoinedBecomeLeader: tests/golden/gpu_traces, lean mode)
+    "tlc:scen_FirstBecomeLeader": ("scen_FirstBecomeLeader", 0),
+    "tlc:scen_EntryCommitted": ("scen_EntryCommitted", 0),
+    "tlc:scen_ConcurrentLeaders": ("scen_ConcurrentLeaders", 0),
+    "tlc:scen_LeadershipChange": ("scen_LeadershipChange", 0),
+    "tlc:scen_BoundedTrace": ("scen_BoundedTrace", 0),
+    "tlc:scen_FirstRestart": ("scen_FirstRestart", 0),
+    "tlc:scen_MembershipChange": ("scen_MembershipChange", 0),
+    "tlc:scen_MultipleMembershipChanges": ("scen_MultipleMembershipChanges", 0),
+    "tlc:scen_AddSucessful": ("scen_AddSucessful", 0),
+    "tlc:scen_MembershipChangeCommits": ("scen_MembershipChangeCommits", 0),
+    "tlc:scen_AddCommits": ("scen_AddCommits", 0),
+    "tlc:scen_MultipleMembershipChangesCommit": ("scen_MultipleMembershipChangesCommit", 0),
+    "tlc:scen_LeaderChangesDuringConfChange": ("scen_LeaderChangesDuringConfChange", 0),
+    "tlc:punct_CommitWhenConcurrentLeaders": ("scen_CommitWhenConcurrentLeaders_punct", 0, "CommitWhenConcurrentLeaders_unique"),
+    "tlc:punct_MajorityOfClusterRestarts": ("scen_MajorityOfClusterRestarts_punct", 0, "MajorityOfClusterRestarts_constraint"),
     "tlc:punct_MajorityOfClusterRestarts@30": ("scen_MajorityOfClusterRestarts_punct", 30, "MajorityOfClusterRestarts_constraint"),
     # the NEXT relations on their own (raft.tla:909-916, :924-932) and the other verdict classes
     "memb_async@16": ("memb_async", 16),
@@ -82,7 +103,7 @@ def digest_lines(path):
     return hashlib.sha256("\n".join(lines).encode()).hexdigest(), len(lines)
 
 
-def main(names, out=OUT):
+def main(names, out=OUT, workers=1):
     doc = json.load(open(out)) if os.path.exists(out) else {}
     for n in names:
         cfg, depth = CASES[n][:2]
@@ -90,7 +111,7 @@ def main(names, out=OUT):
         fd, dump = tempfile.mkstemp(suffix=".txt")
         os.close(fd)
         sym = "tlc" if n.startswith("tlc:") else "view"
-        args = ["--sym", sym, "--dump", dump, "--trace"] + (["--deadlock"] if n in DEADLOCK else [])
+        args = ["--sym", sym, "--dump", dump, "--trace", "--workers", workers] + (["--deadlock"] if n in DEADLOCK else [])
         if prefix:
             flag, fixture = PREFIXES[prefix]
             args += [flag, golden_file(fixture)[0]]
@@ -112,4 +133,11 @@ def main(names, out=OUT):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or list(CASES))
+    argv = sys.argv[1:]
+    kw = {}
+    for flag, key in (("--workers", "workers"), ("--out", "out")):
+        if flag in argv:
+            i = argv.index(flag)
+            kw[key] = argv[i + 1]
+            del argv[i:i + 2]
+    main(argv or list(CASES), **kw)

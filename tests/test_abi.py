@@ -25,6 +25,66 @@ def test_library_exports_every_declared_symbol(raftmc):
         assert hasattr(lib, name), name
 
 
+def _c_layout(struct, fields, tmp):
+    """sizeof / offsetof of a struct of include/raftmc.h as the C compiler lays it out (gcc)"""
+    import subprocess
+    src = tmp / "layout.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "raftmc.h"\nint main(void) {\n'
+                   '  printf("%%zu", sizeof(%s));\n' % struct +
+                   "".join('  printf(" %%zu", offsetof(%s, %s));\n' % (struct, f) for f in fields) +
+                   '  printf("\\n");\n  return 0;\n}\n')
+    exe = tmp / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)], check=True)
+    return [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+
+
+@pytest.mark.parametrize("struct,mirror", [("mc_summary_t", "McSummary"), ("mc_opts", "McOpts")])
+def test_struct_layout_matches_ctypes_mirror(raftmc, struct, mirror, tmp_path):
+    """The ctypes mirrors of mc_summary_t / mc_opts (raftmc.py) have the C header's size and field
+    offsets: mc_summary writes sizeof(mc_summary_t) bytes into the caller's struct."""
+    import importlib
+    rm = importlib.import_module("raft-tla_amd.raftmc")
+    cls = getattr(rm, mirror)
+    names = [f[0] for f in cls._fields_]
+    got = _c_layout(struct, names, tmp_path)
+    assert got[0] == __import__("ctypes").sizeof(cls)
+    assert got[1:] == [getattr(cls, n).offset for n in names]
+
+
+def test_abi_version_mismatch_refused(raftmc):
+    """an mc_opts of another ABI version (e.g. a caller built against version 1, whose mc_summary_t
+    is smaller) is refused by mc_open"""
+    import ctypes
+    lib = raftmc.load_library()
+    rm = __import__("importlib").import_module("raft-tla_amd.raftmc")
+    o = rm.McOpts()
+    lib.mc_default_opts(ctypes.byref(o))
+    assert o.abi_version == raftmc.ABI_VERSION == 2
+    o.abi_version = 1
+    h = ctypes.c_void_p()
+    rc = lib.mc_open(ORIG_MC.encode(), os.path.join(CONFIGS, "c2.cfg").encode(), ctypes.byref(o), ctypes.byref(h))
+    assert rc == -1 and not h
+
+
+@pytest.mark.parametrize("spec,cfg,kw", [
+    (ORIG_MC, "c2.cfg", dict(workers=1, max_depth=5)),          # TLC's FIFO order stores every level
+    (ORIG_MC, "c2.cfg", dict(workers=0, max_depth=0)),          # no final level without a depth bound
+    (MEMB_MC, "membership_shipped.cfg", dict(workers=0, max_depth=5)),   # raft_original only
+])
+def test_count_final_level_refused_where_unsupported(raftmc, spec, cfg, kw):
+    """count_final_level is refused (MC_E_UNSUPPORTED) wherever it would be ignored"""
+    with pytest.raises(raftmc.RaftMCError) as e:
+        raftmc.ModelChecker(spec, os.path.join(CONFIGS, cfg), count_final_level=True, **kw)
+    assert e.value.code == -4
+
+
+def test_count_final_level_refuses_checkpoint(raftmc, tmp_path):
+    with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c2.cfg"), workers=0, max_depth=5, count_final_level=True) as mc:
+        with pytest.raises(raftmc.RaftMCError) as e:
+            mc.set_checkpoint(str(tmp_path / "x.ckpt"), 1)
+    assert e.value.code == -4
+
+
 def test_describe_c2(raftmc):
     with raftmc.ModelChecker(ORIG_MC, os.path.join(CONFIGS, "c2.cfg")) as mc:
         d = mc.describe()
@@ -140,6 +200,35 @@ def test_generated_code_objects_short_branch_and_ordered_stores():
     assert sum(k.endswith(":tlg_expand_k") for k in ks) == len(cos)
     bad = {k: v for k, v in ks.items() if v["long_branches"] or v["smem_store_hazards"]}
     assert not bad and r.returncode == 0, bad
+
+
+def test_isa_check_refuses_an_unprovided_dynamic_stack(tmp_path):
+    """The stack rule of scripts/check_isa.py (round 4's illegal-address fault): a code
+    object whose kernel recurses (dynamic stack) but whose generated source lacks the recursion marker
+    runs with the runtime's default per-lane stack, so the check fails it; the same code with the
+    marker (the backend then raises the stack to 16 KB per lane) passes."""
+    import json
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "raft-tla_amd", "csrc", "tlagen"))
+    from prebuild import OPTS, key_of
+    body = ("#include <hip/hip_runtime.h>\n"
+            "__device__ __attribute__((noinline)) int walk(int n, int* p) { if (n <= 0) return p[0]; int a[8]; "
+            "for (int k = 0; k < 8; ++k) a[k] = p[k] + n; return walk(n - 1, a) + a[n & 7]; }\n"
+            "extern \"C\" __global__ void tlg_expand_k(int* p, int n) { p[threadIdx.x] = walk(n, p); }\n")
+    rcs = {}
+    for marked in (False, True):
+        d = tmp_path / ("m" if marked else "u")
+        d.mkdir()
+        src = body + ("// guard: if (depth > tlv::kMaxRecDepth) { ... }\n" if marked else "")
+        (d / "x.gen.hip").write_text(src)
+        co = d / (key_of(src) + ".hsaco")
+        subprocess.run(["/opt/rocm/bin/hipcc", "--genco", *OPTS, "-o", str(co), "-x", "hip", str(d / "x.gen.hip")], check=True)
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "check_isa.py"), str(co)], capture_output=True, text=True)
+        k = json.loads(r.stdout)["tlg_expand_k"]
+        assert k["dynamic_stack"] and k["raised_stack"] == marked
+        rcs[marked] = r.returncode
+    assert rcs == {False: 1, True: 0}
 
 
 PUNCT_CWCL = os.path.join(CONFIGS, "scen_CommitWhenConcurrentLeaders_punct.cfg")

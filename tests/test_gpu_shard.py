@@ -7,6 +7,7 @@ identical generated / distinct / depth and per-action generated counts, and
 on a violation a shortest counterexample reassembled across ranks."""
 import importlib
 import json
+import time
 import os
 import socket
 
@@ -374,3 +375,65 @@ def test_n_gpus_membership(raftmc, case, world):
     else:
         assert r.violated == g["violated"]
         _trace_blocks_match(r.trace_text, g)
+
+
+# ---------------------------------------------------------------- count_final_level and rank failures in the native loop
+def test_native_loop_count_final_level(raftmc, tmp_path):
+    """count_final_level in the sharded native loop (BASELINE configs[4]: C5v2 to depth 14 on 8 GPUs):
+    the final level's new states are deduplicated by their owners and counted by the generating ranks,
+    never shipped or stored.  Two loopback ranks on C5v2 to depth 10 give the single-GPU storing run's
+    counts and levels; so does mc_opts.n_gpus = 2, whose dump refuses (the last level is not stored)."""
+    shard = importlib.import_module("raft-tla_amd.shard")
+    cfg = os.path.join(CONFIGS, "c5v2.cfg")
+    a = raftmc.check(ORIG_MC, cfg, max_depth=10, workers=0)
+    assert a.verdict == "DEPTH_LIMIT" and a.distinct == sum([1, 6, 45, 330, 2190, 13761, 82510, 475485, 2648995, 14330920])
+    want = (a.generated, a.distinct, a.depth, a.left_on_queue, {k: v[0] for k, v in a.actions.items()})
+    kw = dict(max_depth=10, workers=0, count_final_level=True, fp_table_bytes=1 << 30, state_store_bytes=1 << 30)
+    out = shard.check_loopback(ORIG_MC, cfg, 2, **kw)
+    for r in out:
+        assert r.verdict == "DEPTH_LIMIT", r.error
+        assert (r.generated, r.distinct, r.depth, r.left_on_queue, {k: v[0] for k, v in r.actions.items()}) == want
+        assert [lv[0] for lv in r.levels] == [lv[0] for lv in a.levels]
+        assert sum(v[1] for v in r.actions.values()) + 1 == r.distinct
+    with raftmc.ModelChecker(ORIG_MC, cfg, n_gpus=2, same_device=torch.cuda.device_count() < 2, **kw) as mc:
+        r = mc.run()
+        with pytest.raises(raftmc.RaftMCError):
+            mc.dump_states(str(tmp_path / "s.txt"))
+    assert (r.generated, r.distinct, r.depth, r.left_on_queue, {k: v[0] for k, v in r.actions.items()}) == want
+
+
+def test_native_loop_store_overflow(raftmc):
+    """The ranks' stores fill (each holds 12M of C2's 54.4M states; whichever rank overflows first
+    raises the flag): the capacity error travels in the level all-reduce, every rank stops at the same
+    level with CAPACITY_OVERFLOW naming the full store, the summary counts the completed levels, and
+    nothing hangs."""
+    shard = importlib.import_module("raft-tla_amd.shard")
+    cfg = os.path.join(CONFIGS, "c2.cfg")
+    t0 = time.time()
+    out = shard.check_loopback(ORIG_MC, cfg, 2, workers=0, fp_table_bytes=1 << 30,
+                               state_store_bytes=12_000_000 * _slot_bytes(raftmc, cfg))
+    assert time.time() - t0 < 120
+    for r in out:
+        assert r.verdict == "CAPACITY_OVERFLOW" and "error flags" in r.error, (r.verdict, r.error)
+        assert [lv[0] for lv in r.levels] == [lv[0] for lv in out[0].levels]
+    assert out[0].distinct == sum(lv[0] for lv in out[0].levels) < 54426066
+
+
+def test_n_gpus_rank_failure_releases_peers(raftmc, monkeypatch):
+    """A rank that leaves the native loop early (here an injected failure of rank 1 at depth 5,
+    RAFTMC_TEST_SHARD_FAIL) releases its peers instead of leaving them in the next collective: mc_run
+    returns the failing rank's error, naming it, within seconds; the same handle then runs the model to
+    completion (fresh communicators on a node: the aborted ones are never reused)."""
+    cfg = os.path.join(CONFIGS, "c2.cfg")
+    kw = dict(workers=0, fp_table_bytes=2 << 30, state_store_bytes=2 << 30)
+    with raftmc.ModelChecker(ORIG_MC, cfg, n_gpus=2, same_device=torch.cuda.device_count() < 2, **kw) as mc:
+        monkeypatch.setenv("RAFTMC_TEST_SHARD_FAIL", "1:5")
+        t0 = time.time()
+        with pytest.raises(raftmc.RaftMCError) as e:
+            mc.run()
+        assert time.time() - t0 < 60
+        assert "rank 1" in str(e.value) and "injected failure" in str(e.value), str(e.value)
+        monkeypatch.delenv("RAFTMC_TEST_SHARD_FAIL")
+        r = mc.run()
+    g = json.load(open(os.path.join(GOLDEN, "c2_exact.json")))
+    assert (r.verdict, r.generated, r.distinct, r.depth) == ("OK", g["generated"], g["distinct"], g["depth"]), r.error

@@ -221,15 +221,47 @@ def test_recursive_functions_on_gpu(raftmc, workers):
 
 
 def test_apalache_no_membership_on_gpu(raftmc):
-    """apalache_no_membership/raft.tla with its shipped raft.cfg (recursive Sum in the constraints):
-    the host build's counts to depth 9 (tests/test_tlagen.py; parity unpinned), both search orders."""
-    from test_tlagen import APALACHE_D9
+    """apalache_no_membership/raft.tla with its shipped raft.cfg (recursive Sum in the constraints),
+    pinned by the oracle's restatement (oracle/raft_apalache.h, tests/golden/apalache_oracle.json): the
+    shipped model to depth 11 (1.3M states of ~800 words, history["global"] included) -- counts, level
+    sizes, per-action generated counts in both search orders, per-action distinct counts and the SHA-256
+    of the whole kept state set in TLC's FIFO order."""
+    import hashlib
+    import tempfile
+    from test_tlagen import APALACHE
+    g = APALACHE["shipped_d11"]
     for workers in (1, 0):
         with raftmc.ModelChecker(gen_source("apalache_nm"), os.path.join(ROOT, "configs", "apalache_nm.cfg"), frontend="generated",
-                                 workers=workers, max_depth=9, **SMALL) as mc:
+                                 workers=workers, max_depth=11, fp_table_bytes=1 << 28, state_store_bytes=24 << 30) as mc:
             r = mc.run()
+            if workers == 1:
+                fd, path = tempfile.mkstemp(suffix=".txt")
+                os.close(fd)
+                mc.dump_states(path)
+                lines = sorted(l.rstrip("\n") for l in open(path))
+                os.unlink(path)
+                assert hashlib.sha256("\n".join(lines).encode()).hexdigest() == g["states_sha256"]
+                assert {k: v for k, v in r.actions.items()} == g["actions"]
         assert r.verdict == "DEPTH_LIMIT", r.error
-        assert {"generated": r.generated, "distinct": r.distinct, "levels": [lv[0] for lv in r.levels]} == APALACHE_D9
+        assert (r.generated, r.distinct, r.left_on_queue, [lv[0] for lv in r.levels]) == (g["generated"], g["distinct"], g["left_on_queue"], g["levels"])
+        assert {k: v[0] for k, v in r.actions.items()} == {k: v[0] for k, v in g["actions"].items()}
+
+
+@pytest.mark.parametrize("case,gen", [("BoundedTrace", "apalache_nm_boundedtrace"), ("FirstBecomeLeader", "apalache_nm_firstbecomeleader")])
+def test_apalache_counterexamples_on_gpu(raftmc, case, gen):
+    """The shipped cfg's commented-out test-case invariants (raft.cfg:22-24, raft.tla:776-785) on the GPU:
+    TLC's FIFO counterexample state by state and TLC's counters at the stop point, as the oracle's
+    restatement finds them; -workers N searches the event's level again in FIFO order."""
+    from test_gpu import trace_states
+    from test_tlagen import APALACHE
+    g = APALACHE[case]
+    for workers in (1, 0):
+        with raftmc.ModelChecker(gen_source(gen), os.path.join(CONFIGS, g["cfg"] + ".cfg"), frontend="generated",
+                                 workers=workers, fp_table_bytes=1 << 26, state_store_bytes=4 << 30) as mc:
+            r = mc.run()
+        assert (r.verdict, r.violated, r.depth, r.exit_code) == (g["verdict"], g["violated"], g["depth"], 12), r.error
+        assert (r.generated, r.distinct, r.left_on_queue) == (g["generated"], g["distinct"], g["left_on_queue"])
+        assert [s for _, s in trace_states(r)] == [t["state"] for t in g["trace"]]
 
 
 @pytest.mark.parametrize("case,gen", [("memb_nosym@13", "memb_nosym_gen"), ("tlc:membership_shipped@16", "memb_shipped_gen"),

@@ -12,7 +12,7 @@ import tempfile
 
 import pytest
 
-from oracle_util import CONFIGS, GOLDEN, ORIG_MC
+from oracle_util import CONFIGS, GOLDEN, ORIG_MC, run_oracle
 from tlagen_models import rec_fun, token_ring
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -211,19 +211,47 @@ def test_invariant_evaluation_error():
 
 # apalache_no_membership/raft.tla with its shipped raft.cfg (TLC syntax): the first spec of SURVEY.md
 # 8(f) rank 3 that needs recursive function definitions (TypedBags' Sum via BagCardinality in
-# BoundedInFlightMessages).  No oracle restates this spec: the counts are the host build's of the
-# generated code ("parity unpinned"); the GPU test holds the kernels to the same numbers.
+# BoundedInFlightMessages).  Pinned by the oracle's hand restatement of the spec
+# (oracle/raft_apalache.h; tests/golden/apalache_oracle.json, tests/golden/make_apalache_oracle.py):
+# the shipped model to depth 11 and the cfg's two commented-out test-case invariants.
+APALACHE = json.load(open(os.path.join(GOLDEN, "apalache_oracle.json")))
 APALACHE_D9 = dict(generated=141083, distinct=60955, levels=[1, 2, 6, 28, 120, 520, 2310, 10388, 47580])
 
 
 @needs_tool
 @needs_ref
 def test_apalache_no_membership_shipped_cfg():
+    """The host build of the generated code to depth 9: the oracle's level sizes (the first 9 levels of
+    its depth-11 fixture; levels are order independent), counts, and every kept state (the state set
+    of the oracle's own depth-9 run)."""
     spec = os.path.join(REF, "apalache_no_membership", "raft.tla")
-    r = host_bfs(generate(spec, os.path.join(REF, "apalache_no_membership", "raft.cfg")), "--max-depth", "9")
+    cfg = os.path.join(REF, "apalache_no_membership", "raft.cfg")
+    dump = tempfile.mktemp(suffix=".txt")
+    r = host_bfs(generate(spec, cfg), "--max-depth", "9", "--dump", dump)
     assert (r["verdict"], r["err"]) == ("DEPTH_LIMIT", 0)
     assert {k: r[k] for k in APALACHE_D9} == APALACHE_D9
-    assert sum(r["levels"]) == r["distinct"]
+    assert r["levels"] == APALACHE["shipped_d11"]["levels"][:9]
+    got = sorted(l.rstrip("\n") for l in open(dump))
+    os.unlink(dump)
+    o = run_oracle("bfs", spec, os.path.join(CONFIGS, "apalache_nm.cfg"), "--max-depth", "9", "--dump", dump)
+    want = sorted(l.rstrip("\n") for l in open(dump))
+    os.unlink(dump)
+    assert (o["generated"], o["distinct"], o["levels"]) == (APALACHE_D9["generated"], APALACHE_D9["distinct"], APALACHE_D9["levels"])
+    assert got == want
+
+
+@needs_tool
+@needs_ref
+@pytest.mark.parametrize("case", ["BoundedTrace", "FirstBecomeLeader"])
+def test_apalache_counterexamples(case):
+    """The shipped cfg's test-case invariants (raft.cfg:22-24) on the host build of the generated code:
+    TLC's FIFO counterexample and its stop-point counters, as the oracle's restatement finds them."""
+    g = APALACHE[case]
+    spec = os.path.join(REF, "apalache_no_membership", "raft.tla")
+    r = host_bfs(generate(spec, os.path.join(CONFIGS, g["cfg"] + ".cfg")), "--trace")
+    assert (r["verdict"], r["violated"], r["depth"], r["distinct"]) == (g["verdict"], g["violated"], g["depth"], g["distinct"])
+    assert r["generated"] == g["generated"]
+    assert r["trace"] == [t["state"] for t in g["trace"]]
 
 
 @needs_tool
