@@ -711,6 +711,81 @@ struct Orig {
 #pragma unroll
     for (int k = 0; k < NW; ++k) w[k] = o.w[k];
   }
+  // ---------------------------------------------------------------- field groups of the packed layout
+  // (pack's order and widths): a successor differs from its parent in a few groups only, so its packed
+  // words can be the parent's with those groups re-inserted (pack_patch) instead of a whole pack
+  enum { PG_TERM, PG_ST, PG_VOTED, PG_COMMIT, PG_VRESP, PG_VGRANT, PG_NEXTI, PG_MATCHI, PG_LOG, PG_VL, PG_EL, PG_BAG, NPG };
+  static constexpr int LOGW = SLLB + ML * EB;   // a stored log: length + ML entries
+  static constexpr int OFF_TERM = 0, OFF_ST = OFF_TERM + N * TB, OFF_VOTED = OFF_ST + N * 2, OFF_COMMIT = OFF_VOTED + N * VB,
+                       OFF_VRESP = OFF_COMMIT + N * CIB, OFF_VGRANT = OFF_VRESP + N * N, OFF_NEXTI = OFF_VGRANT + N * N,
+                       OFF_MATCHI = OFF_NEXTI + N * N * NIB, OFF_LOG = OFF_MATCHI + N * N * CIB, OFF_VL = OFF_LOG + N * LOGW,
+                       OFF_ALL = OFF_VL + N * N * VLB, OFF_EL = OFF_ALL + (int)U, OFF_BAG = OFF_EL + EMAX * ELB;
+  static_assert(OFF_BAG == BAG_OFF && OFF_BAG + MK * ENTB == PBITS, "pack_patch offsets follow pack");
+  // the groups instance k can change when its action is the same for every state (a superset; ~0u for
+  // Receive, whose handler depends on the message: dirty_of decides per successor)
+  RMC_HD static u32 dirty_static(int k) {
+    if (k < N) return 1u << PG_ST | 1u << PG_VRESP | 1u << PG_VGRANT | 1u << PG_VL | 1u << PG_NEXTI | 1u << PG_MATCHI | 1u << PG_COMMIT;   // Restart
+    if (k < 2 * N) return 1u << PG_ST | 1u << PG_TERM | 1u << PG_VOTED | 1u << PG_VRESP | 1u << PG_VGRANT | 1u << PG_VL;      // Timeout
+    if (k < 2 * N + N * N) return 1u << PG_BAG;                                                                              // RequestVote
+    if (k < 3 * N + N * N) return 1u << PG_ST | 1u << PG_NEXTI | 1u << PG_MATCHI | 1u << PG_EL;                              // BecomeLeader
+    if (k < 3 * N + N * N + N * NV) return 1u << PG_LOG;                                                                     // ClientRequest
+    if (k < 4 * N + N * N + N * NV) return 1u << PG_COMMIT;                                                                  // AdvanceCommitIndex
+    if (k < I_RECV) return 1u << PG_BAG;                                                                                     // AppendEntries
+    if (k < I_DUP) return ~0u;                                                                                               // Receive
+    return 1u << PG_BAG;                                                                                                     // Duplicate / Drop
+  }
+  // the groups in which t differs from s (field compares)
+  RMC_HD static u32 dirty_of(const Work& s, const Work& t) {
+    u32 d = (t.term != s.term ? 1u << PG_TERM : 0u) | (t.st != s.st ? 1u << PG_ST : 0u) | (t.voted != s.voted ? 1u << PG_VOTED : 0u) |
+            (t.commit != s.commit ? 1u << PG_COMMIT : 0u) | (t.vresp != s.vresp ? 1u << PG_VRESP : 0u) |
+            (t.vgrant != s.vgrant ? 1u << PG_VGRANT : 0u);
+    bool ni = false, mi = false, lg = false, vl = false, el = false, bg = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i) { ni |= t.nexti.v[i] != s.nexti.v[i]; mi |= t.matchi.v[i] != s.matchi.v[i]; lg |= t.log.v[i] != s.log.v[i]; vl |= t.vl.v[i] != s.vl.v[i]; }
+#pragma unroll
+    for (int q = 0; q < EMAX; ++q) el |= t.el[q] != s.el[q];
+#pragma unroll
+    for (int q = 0; q < MK; ++q) bg |= t.bag.v[q] != s.bag.v[q];
+    return d | (ni ? 1u << PG_NEXTI : 0u) | (mi ? 1u << PG_MATCHI : 0u) | (lg ? 1u << PG_LOG : 0u) | (vl ? 1u << PG_VL : 0u) |
+           (el ? 1u << PG_EL : 0u) | (bg ? 1u << PG_BAG : 0u);
+  }
+  // v (< 2^NB) into bits [P, P + NB) of w, the other bits kept (P, NB compile-time: shifts and masks only)
+  template <int P, int NB>
+  RMC_HD static void put_at(u32 (&w)[NW], u64 v) {
+    constexpr int q = P >> 5, r = P & 31;
+    constexpr u64 m = lomask(NB);
+    w[q] = (w[q] & ~(u32)(m << r)) | (u32)(v << r);
+    if constexpr (r + NB > 32) w[q + 1] = (w[q + 1] & ~(u32)(m >> (32 - r))) | (u32)(v >> (32 - r));
+    if constexpr (r + NB > 64) w[q + 2] = (w[q + 2] & ~(u32)(m >> (64 - r))) | (u32)(v >> (64 - r));
+  }
+  template <int B, int E, class F>
+  RMC_HD static void for_c(F&& f) { if constexpr (B < E) { f(std::integral_constant<int, B>{}); for_c<B + 1, E>(f); } }
+  // pack(t) given base = pack of a state that equals t outside the groups of `dirty` (dirty is
+  // wave-uniform on the device: each group is one scalar branch)
+  RMC_HD static void pack_patch(const Work& t, u32 dirty, const u32 (&base)[NW], u32 (&w)[NW]) {
+#pragma unroll
+    for (int k = 0; k < NW; ++k) w[k] = base[k];
+    if (dirty & 1u << PG_TERM) put_at<OFF_TERM, N * TB>(w, t.term);
+    if (dirty & 1u << PG_ST) put_at<OFF_ST, N * 2>(w, t.st);
+    if (dirty & 1u << PG_VOTED) put_at<OFF_VOTED, N * VB>(w, t.voted);
+    if (dirty & 1u << PG_COMMIT) put_at<OFF_COMMIT, N * CIB>(w, t.commit);
+    if (dirty & 1u << PG_VRESP) put_at<OFF_VRESP, N * N>(w, t.vresp);
+    if (dirty & 1u << PG_VGRANT) put_at<OFF_VGRANT, N * N>(w, t.vgrant);
+    if (dirty & 1u << PG_NEXTI) for_c<0, N>([&](auto ic) { constexpr int i = decltype(ic)::value; put_at<OFF_NEXTI + i * N * NIB, N * NIB>(w, t.nexti.v[i]); });
+    if (dirty & 1u << PG_MATCHI) for_c<0, N>([&](auto ic) { constexpr int i = decltype(ic)::value; put_at<OFF_MATCHI + i * N * CIB, N * CIB>(w, t.matchi.v[i]); });
+    if (dirty & 1u << PG_LOG)
+      for_c<0, N>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        const u32 lw = t.log.v[i];
+        put_at<OFF_LOG + i * LOGW, SLLB>(w, (u64)(lw & lomask(LLB)));
+        put_at<OFF_LOG + i * LOGW + SLLB, ML * EB>(w, (u64)(lw >> LLB) & lomask(ML * EB));
+      });
+    if (dirty & 1u << PG_VL) for_c<0, N>([&](auto ic) { constexpr int i = decltype(ic)::value; put_at<OFF_VL + i * N * VLB, N * VLB>(w, (u64)t.vl.v[i]); });
+    if (dirty & 1u << PG_EL) for_c<0, EMAX>([&](auto qc) { constexpr int q = decltype(qc)::value; put_at<OFF_EL + q * ELB, ELB>(w, t.el[q] == EMPTY ? 0ull : t.el[q]); });
+    if (dirty & 1u << PG_BAG)
+      for_c<0, MK>([&](auto qc) { constexpr int q = decltype(qc)::value; put_at<OFF_BAG + q * ENTB, ENTB>(w, t.bag.v[q] == BEMPTY ? 0ull : (u64)t.bag.v[q]); });
+  }
+
   template <int M>
   RMC_HD static void unpack(const u32 (&w)[M], Work& t) {
     static_assert(M >= NW, "packed array too small");
