@@ -71,6 +71,9 @@ enum { OE_CAP_STORE = 0x100, OE_TABLE_FULL = 0x200 };
 #ifndef RMC_DEDUP_PER
 #define RMC_DEDUP_PER 8
 #endif
+#ifndef RMC_DEDUP_PIPE
+#define RMC_DEDUP_PIPE 0    // 1: orig_dedup_pipe (software-pipelined probes) instead of orig_dedup_plain
+#endif
 #ifndef RMC_LDS_SLOTS
 #define RMC_LDS_SLOTS 4096
 #endif
@@ -138,6 +141,13 @@ template <class S>
 #endif
 #ifndef RMC_GEN_INC
 #define RMC_GEN_INC 1
+#endif
+#ifndef RMC_GEN_PATCH
+// in-model successors packed by patching the parent's words (S::pack_patch) instead of a whole pack:
+// 1 = every instance (Receive: the wave's union of changed groups, one ballot per group), 2 = only the
+// instances whose changed groups are static (Receive packs whole), 0 = whole packs (the default:
+// round 5 measured mode 1 at 14.45 vs 13.37 ms of orig_generate per C2 run, profiles/r05_generate_ab.txt)
+#define RMC_GEN_PATCH 0
 #endif
 #ifndef RMC_GEN_DD_LOOP
 #define RMC_GEN_DD_LOOP 0   // 1: DuplicateMessage / DropMessage through the generic loop (apply + pack), A/B only
@@ -296,7 +306,25 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
           ++nin;
           have = true;
           u32 pw[NW];
-          S::pack(t, pw);
+          if constexpr (INC && RMC_GEN_PATCH) {
+            // the parent's words with the groups the action changed re-inserted (S::pack_patch): the
+            // groups are known from the wave-uniform instance, except for Receive, whose handler depends
+            // on the message: there the union over the wave's in-model successors (one ballot per group)
+            u32 du = S::dirty_static(k);
+            if (du != ~0u) {
+              S::pack_patch(t, du, bw, pw);
+            } else if (RMC_GEN_PATCH == 1) {
+              const u32 d = S::dirty_of(s, t);
+              du = 0;
+#pragma unroll
+              for (int g = 0; g < S::NPG; ++g) du |= __ballot((d >> g) & 1u) ? 1u << g : 0u;
+              S::pack_patch(t, __builtin_amdgcn_readfirstlane(du), bw, pw);
+            } else {
+              S::pack(t, pw);
+            }
+          } else {
+            S::pack(t, pw);
+          }
           if constexpr (INC) fp = fb.fp(pw, bw, a.seed);
           else fp = fp64(pw, a.seed);
 #ifdef RMC_EXP_DOUBLE_PACKFP
@@ -483,7 +511,8 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
       if (S::in_model(t, a.rt)) {
         ++nin;
         u32 pw[NW];
-        S::pack(t, pw);
+        if constexpr (INC && RMC_GEN_PATCH) S::pack_patch(t, S::dirty_static(k), bw, pw);   // k uniform: static groups
+        else S::pack(t, pw);
         u64 fp;
         if constexpr (INC) fp = fb.fp(pw, bw, a.seed);
         else fp = fp64(pw, a.seed);
@@ -935,6 +964,145 @@ __global__ void __launch_bounds__(BS) orig_dedup_plain(DedupArgs a) {
 #pragma unroll
     for (int j = 0; j < DEDUP_PER; ++j)
       if ((ins >> j) & 1u) atomicOr(&win[(key[j] >> 8) * WW + ((key[j] & 255) >> 6)], 1ull << (key[j] & 63));
+  }
+  __shared__ u32 wave_probes[BS / 64];
+  if constexpr (COUNT) {
+    u32 wp = probes;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) wp += __shfl_xor(wp, d);
+    if (__lane_id() == 0) wave_probes[threadIdx.x >> 6] = wp;
+  }
+  __syncthreads();
+  if constexpr (COUNT) {
+    if (threadIdx.x == 0) {
+      u32 t = 0;
+#pragma unroll
+      for (int w = 0; w < BS / 64; ++w) t += wave_probes[w];
+      if (t) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)t);
+    }
+  }
+  u64 wm[WW];
+  u32 mine = 0;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) { wm[q] = win[threadIdx.x * WW + q]; mine += (u32)__popcll(wm[q]); }
+  u32 total = 0;
+  const u32 off = block_excl_scan(mine, wave_tot, &total);
+  if (threadIdx.x == 0) base_sh = total ? atomicAdd(&a.ctr[K_CHUNK_NEW], (unsigned long long)total) : 0ull;
+  __syncthreads();
+  u64 o = base_sh + off;
+  const u64 pg = a.gid0 + (u64)blockIdx.x * BS + threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) {
+    u64 m = wm[q];
+    while (m) {
+      const int k = q * 64 + __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      a.newpos[o++] = (pg << 8) | (u64)k;
+    }
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+}
+
+// The same kernel software-pipelined (RMC_DEDUP_PIPE): a wave's seen-set probes of batch t are in
+// flight while it loads and LDS-filters batch t + 1.  Vector-memory loads complete in issue order
+// (one vmcnt counter), so the order of issue is what lets them overlap: per iteration the record
+// loads of batch t + 2 are issued BEFORE the probes of batch t + 1, and waiting for those records
+// (older) does not wait for the probes (newer).
+//   prologue: records 0; filter 0; records 1; probes 0
+//   iteration t: filter t + 1 (its records arrived) | finish probes t (compare, CAS the empty slots,
+//                walk the rare collisions, mark winners) | records t + 2; probes t + 1
+template <int WW, bool COUNT>
+__global__ void __launch_bounds__(BS) orig_dedup_pipe(DedupArgs a) {
+  constexpr int P = DEDUP_PER;
+  __shared__ unsigned long long lfp[LDS_FP_SLOTS];
+  __shared__ u32 wave_tot[BS / 64];
+  __shared__ unsigned long long base_sh;
+  __shared__ unsigned long long win[BS * WW];
+  for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lfp[t] = 0ull;
+  for (int t = threadIdx.x; t < BS * WW; t += BS) win[t] = 0ull;
+  __syncthreads();
+  const WaveRegions wr(a.rcnt + 4 * blockIdx.x, a.region / 4);
+  const u32 n = wr.n;
+  const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
+  const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
+  const u64* table = a.table;
+  const u64 mask = a.table_mask;
+  u32 err = 0;
+  u32 probes = 0;
+  auto load_records = [&](u32 i0, u64 (&fp)[P], u64 (&key)[P]) {
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      const u64 at = wr.at(i);
+      fp[j] = i < n ? fps[at] : 0ull;
+      key[j] = i < n ? (u64)keys[at] : 0ull;
+    }
+  };
+  auto filter = [&](u64 (&fp)[P]) {
+#pragma unroll
+    for (int j = 0; j < P; ++j)
+      if (fp[j] && !lds_first(lfp, fp[j])) fp[j] = 0ull;
+    if constexpr (COUNT) {
+#pragma unroll
+      for (int j = 0; j < P; ++j) probes += fp[j] ? 1u : 0u;
+    }
+  };
+  auto issue = [&](const u64 (&fp)[P], u64 (&cur)[P]) {
+#pragma unroll
+    for (int j = 0; j < P; ++j) cur[j] = fp[j] ? table[fp[j] & mask] : ~0ull;
+  };
+  // probe_batch's second half over pre-loaded first slots (8-B entries, no keys)
+  auto finish = [&](const u64 (&fp)[P], const u64 (&key)[P], u64 (&cur)[P]) {
+    u32 ins = 0, done = 0;
+    u64 pos[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      pos[j] = fp[j] & mask;
+      if (fp[j] && cur[j] == 0ull) {
+        cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[pos[j]], 0ull, (unsigned long long)fp[j]);
+        if (cur[j] == 0ull) { ins |= 1u << j; done |= 1u << j; }
+      }
+      if (!fp[j] || cur[j] == fp[j]) done |= 1u << j;
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      if ((done >> j) & 1u) continue;
+      u64 slot = (pos[j] + 1) & mask;
+      for (u64 probe = 0;; ++probe) {
+        if (probe > mask || probe >= (1u << 20)) { err |= OE_TABLE_FULL; break; }
+        const u64 c = a.table[slot];
+        if (c == fp[j]) break;
+        if (c == 0ull) {
+          const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[slot], 0ull, (unsigned long long)fp[j]);
+          if (old == 0ull) { ins |= 1u << j; break; }
+          if (old == fp[j]) break;
+        }
+        slot = (slot + 1) & mask;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j)
+      if ((ins >> j) & 1u) atomicOr(&win[(key[j] >> 8) * WW + ((key[j] & 255) >> 6)], 1ull << (key[j] & 63));
+  };
+  constexpr u32 STEP = (u32)P * BS;
+  u64 fpA[P], keyA[P], curA[P], fpB[P], keyB[P];
+  if (n) {
+    load_records(0, fpA, keyA);
+    filter(fpA);
+    load_records(STEP, fpB, keyB);   // (zeros past the end)
+    issue(fpA, curA);
+  }
+#pragma unroll 1
+  for (u32 i0 = 0; i0 < n; i0 += STEP) {
+    const bool more = i0 + STEP < n;   // workgroup-uniform
+    if (more) filter(fpB);             // its records arrived; the probes of batch A are in flight
+    finish(fpA, keyA, curA);
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < P; ++j) { fpA[j] = fpB[j]; keyA[j] = keyB[j]; }
+      load_records(i0 + 2 * STEP, fpB, keyB);
+      issue(fpA, curA);
+    }
   }
   __shared__ u32 wave_probes[BS / 64];
   if constexpr (COUNT) {
@@ -1815,6 +1983,9 @@ class OrigGpu : public Backend {
             else hipLaunchKernelGGL((orig_probe_plain<WW, false>), dim3(nblk), dim3(BS), 0, stream_, d);
           } else if (dedup_queue_) {
             hipLaunchKernelGGL((orig_dedup_queue<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
+          } else if (RMC_DEDUP_PIPE) {
+            if (count_probes) hipLaunchKernelGGL((orig_dedup_pipe<WW, true>), dim3(nblk), dim3(BS), 0, stream_, d);
+            else hipLaunchKernelGGL((orig_dedup_pipe<WW, false>), dim3(nblk), dim3(BS), 0, stream_, d);
           } else if (count_probes) {
             hipLaunchKernelGGL((orig_dedup_plain<WW, true>), dim3(nblk), dim3(BS), 0, stream_, d);
           } else {

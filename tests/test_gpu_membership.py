@@ -67,6 +67,11 @@ def test_membership_parity(raftmc, case):
 
 @pytest.mark.parametrize("case", VIOLATIONS)
 def test_scenario_shortest_counterexample(raftmc, case):
+    """Every scenario property of tlc_membership/raft.tla:1143-1278 (C4, BASELINE configs[3]) as an
+    invariant: TLC's shortest counterexample state by state and TLC's counters at the stop point, in
+    the orbit mode and (the "tlc:" fixtures, oracle --sym tlc) in TLC's SYMMETRY rule, the drop-in
+    default -- NewlyJoinedBecomeLeader, beyond the exact oracle's reach, in
+    test_counterexamples_beyond_oracle_reach."""
     g = FIX[case]
     with open_case(raftmc, g, **SMALL) as mc:
         r = mc.run()
@@ -163,17 +168,26 @@ def test_c3_counterexample_matches_committed_trace(raftmc, mode):
 GPU_TRACES = json.load(open(os.path.join(GOLDEN, "gpu_traces", "index.json")))["cases"]
 
 
-@pytest.mark.parametrize("cfg", sorted(GPU_TRACES))
-def test_counterexamples_beyond_oracle_reach(raftmc, cfg):
-    """Counterexamples at 14.6M-468M distinct states (tests/golden/gpu_traces/, each validated
+@pytest.mark.parametrize("cfg,mode", [(c, m) for c in sorted(GPU_TRACES)
+                                      for m in ["fixture"] + (["tlc"] if "oracle_pin_tlc" in GPU_TRACES[c] else [])])
+def test_counterexamples_beyond_oracle_reach(raftmc, cfg, mode):
+    """Counterexamples at 3.4M-468M distinct states (tests/golden/gpu_traces/, each validated
     state by state by the oracle's check-trace, tests/test_oracle.py): TLC's single-worker FIFO
     order makes them reproducible — the same trace, depth and stop-point counters on every run.
     Among them the positive controls of the invariant kernels (VotesGrantedInv_false,
-    LeaderCompleteness_false) and a LogMatching violation of the dynamic-membership model."""
+    LeaderCompleteness_false), a LogMatching violation of the dynamic-membership model and
+    NewlyJoinedBecomeLeader, whose stop point the oracle's lean BFS reaches in both SYMMETRY modes
+    ("oracle_pin", "oracle_pin_tlc"; its growing cluster has no SYMMETRY, so the two coincide):
+    mode "tlc" runs it in TLC's rule, the drop-in default, against that pin."""
     g = GPU_TRACES[cfg]
-    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, cfg + ".cfg"), deadlock=False, sym_tlc=g.get("sym") == "tlc")
+    sym_tlc = g.get("sym") == "tlc" if mode == "fixture" else True
+    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, cfg + ".cfg"), deadlock=False, sym_tlc=sym_tlc)
     assert (r.verdict, r.violated) == (g["verdict"], g["violated"]), r.error
     assert (r.depth, r.distinct, r.generated, r.left_on_queue) == (g["depth"], g["distinct"], g["generated"], g["left_on_queue"])
+    if mode == "tlc":
+        pin = g["oracle_pin_tlc"]
+        assert (r.verdict, r.violated, r.depth, r.distinct, r.generated, r.left_on_queue) == (
+            pin["verdict"], pin["violated"], pin["depth"], pin["distinct"], pin["generated"], pin["left_on_queue"])
     got = [" ".join(b.split("\n")[1:]) for b in r.trace_text.strip().split("\n\n")]
     assert got == open(os.path.join(GOLDEN, "gpu_traces", cfg + ".txt")).read().strip().split("\n")
 
