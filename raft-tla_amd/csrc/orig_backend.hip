@@ -149,6 +149,9 @@ template <class S>
 // round 5 measured mode 1 at 14.45 vs 13.37 ms of orig_generate per C2 run, profiles/r05_generate_ab.txt)
 #define RMC_GEN_PATCH 0
 #endif
+#ifndef RMC_GEN_UCOUNT
+#define RMC_GEN_UCOUNT 0    // 1: per-action counts of the uniform-action instances aggregated per wave
+#endif
 #ifndef RMC_GEN_DD_LOOP
 #define RMC_GEN_DD_LOOP 0   // 1: DuplicateMessage / DropMessage through the generic loop (apply + pack), A/B only
 #endif
@@ -300,7 +303,10 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
 #ifdef RMC_GEN_WAVE_COUNTS
         cnt_act = act;
 #else
-        atomicAdd(&lds_cnt[act], 1u);
+        // instances before Receive have one action for every state (Restart, Timeout, RequestVote):
+        // counted per wave below, one LDS atomic instead of 64 conflicting ones
+        if (RMC_GEN_UCOUNT && k < S::I_RECV) cnt_act = act;
+        else atomicAdd(&lds_cnt[act], 1u);
 #endif
         if (S::in_model(t, a.rt)) {
           ++nin;
@@ -356,7 +362,14 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
       }
     }
 #else
-    (void)cnt_act;
+    if (RMC_GEN_UCOUNT && k < S::I_RECV) {   // wave-uniform branch: one action for every lane
+      const u64 am = __ballot(cnt_act >= 0);
+      if (am) {
+        const int first = __ffsll((unsigned long long)am) - 1;
+        const int a0 = __shfl(cnt_act, first);
+        if (lane == first) atomicAdd(&lds_cnt[a0], (unsigned)__popcll(am));
+      }
+    }
 #endif
     const u64 mask = __ballot(have);
     if (have) {

@@ -23,3 +23,6 @@ python3 scripts/rocpd_summary.py traffic $(db $O/fetch) $(db $O/write) memb_dedu
 python3 scripts/rocpd_summary.py valu $(db $O/sq) memb_fingerprint $O/valu_${TAG}_c3_fingerprint.json memb_four.cfg &&
 python3 scripts/rocpd_summary.py valu $(db $O/sq) memb_expand $O/valu_${TAG}_c3_expand.json memb_four.cfg &&
 python3 scripts/pmc_table.py $(db $O/sq) > $O/${TAG}_c3_sq_table.txt
+rc=$?
+rm -rf $O/stats $O/fetch $O/write $O/sq   # (gpurun copies back at most 64 MiB)
+exit $rc

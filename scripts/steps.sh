@@ -9,7 +9,7 @@
 #   c2[=NAME[=LIB]]     bench.py C2 only (no extras, no CPU baseline) with library LIB (default: the
 #                       in-tree build), 8 timed steps; prints ms/step, kernels, seen-set probes
 #   prof                rocprofv3 --kernel-trace --stats of a short C2 bench
-#   pmc                 FETCH_SIZE / WRITE_SIZE / SQ passes over one C2 run (scripts/pmc_passes.sh)
+#   c2_prof[=TAG]       rocprofv3 stats + FETCH/WRITE/SQ passes of C2, summarised (scripts/c2_prof.sh)
 #   memb_prof           rocprofv3 stats + PMC passes of C3 (scripts/memb_prof.sh)
 #   py=SCRIPT ARGS..    python3 SCRIPT with its arguments (':' separates them: py=scripts/x.py:a:b)
 set -o pipefail
@@ -44,8 +44,8 @@ print('$n', round(d['ms_per_step'], 2), {k: round(v['ms'], 2) for k, v in d['ker
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_stats" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra --fifo-steps 0 > "$O/prof_stats.log" 2>&1
       rc=$? ;;
-    pmc)
-      bash scripts/pmc_passes.sh "${O#$R/}/pmc"; rc=$? ;;
+    c2_prof)
+      bash scripts/c2_prof.sh "${O#$R/}/c2_prof" "${arg:-r05}"; rc=$? ;;
     memb_prof)
       bash scripts/memb_prof.sh "${O#$R/}/memb_prof" "${arg:-r05}"; rc=$? ;;
     py)
