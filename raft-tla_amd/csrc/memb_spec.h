@@ -43,6 +43,14 @@
 #define RMC_PROF_T() 0ull
 #define RMC_PROF_ADD(prof, i, t0) do { (void)(prof); (void)(t0); } while (0)
 #endif
+// Host harness statistics (tests/native/memb_host_bfs.cpp built with -DRMC_FP_STATS): work counts of
+// the TLC-mode canonical-permutation search
+#if defined(RMC_FP_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+extern long long rmc_fp_stats[32];
+#define RMC_FPS(i, v) (rmc_fp_stats[i] += (long long)(v))
+#else
+#define RMC_FPS(i, v) ((void)0)
+#endif
 #include "common.h"
 
 namespace rmc {
@@ -1478,6 +1486,10 @@ struct Memb {
   // log / entry when ce); order preserving like the code itself
   RMC_HD static u64 perm_code(u64 c, u32 pi, bool ce, u32 cfgt) {
     constexpr u64 MD_DST = md_lut(0), MD_SRC = md_lut(1), MD_SRV = md_lut(2);
+    RMC_FPS(13, 1); RMC_FPS(19, ce);
+#if defined(RMC_FP_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+    RMC_FPS(26, ce && msg_has_config(c, cfgt));
+#endif
     const int cl = mcls(c);
     const int od = md_field(MD_DST, cl), os = md_field(MD_SRC, cl), ov = md_field(MD_SRV, cl);
     const int sd = CODEB - od - SB, ss = CODEB - os - SB, sv = CODEB - ov - SB;
@@ -1667,16 +1679,23 @@ struct Memb {
   // The bag as an array indexed at run time (tlc_min_perm reads entries by runtime index inside its
   // permutation loops; from the register array every read is a select chain over MK+1 entries): on
   // the device a per-lane slice of LDS (lane-interleaved, conflict-free), on the host a local array.
+#ifndef RMC_TLC_CFG_MASK
+#define RMC_TLC_CFG_MASK 1
+#endif
+  // cfgm: the entries whose message carries a ConfigEntry (the only ones perm_entries changes;
+  // with RMC_TLC_CFG_MASK 0 every entry of a state with config entries anywhere, as in round 4)
   struct BagRef {
     const u64* p;
     int stride;
+    u32 cfgm;
     RMC_HD u64 operator[](int q) const { return p[q * stride]; }
+    RMC_HD bool cfg(int q) const { return (cfgm >> q) & 1u; }
   };
   RMC_HD static u64 next_perm_code(const BagRef& bag, int len, u32 pi, bool ce, u32 cfgt, bool have_last, u64 last) {
     u64 best = ~0ull;   // the least permuted message code above `last`
 #pragma unroll 1
     for (int q = 0; q < len; ++q) {
-      const u64 c = perm_code(mcode(bag[q]), pi, ce, cfgt);
+      const u64 c = perm_code(mcode(bag[q]), pi, ce && bag.cfg(q), cfgt);
       if ((!have_last || c > last) && c < best) best = c;
     }
     return best;
@@ -1723,6 +1742,7 @@ struct Memb {
   RMC_HD static u32 tlc_min_perm(const Work& t, const BagRef& bag, int len, bool ce, u32 cfgt, unsigned long long* prof = nullptr) {
     unsigned long long pt = RMC_PROF_T();
     u32 cand = (u32)lomask(NPERM);
+    RMC_FPS(0, 1); RMC_FPS(1, len);
     // messages: a function from message records to counts (oracle Fcn order: DOMAIN size — equal
     // for all — then the domain elements ascending, then the counts in domain order)
     u64 last = 0;
@@ -1740,7 +1760,8 @@ struct Memb {
 #pragma unroll 1
       for (int q = 0; q < len; ++q) {
         const u64 c = mcode(bag[q]);
-        if (ce && msg_has_config(c, cfgt)) {
+        if (ce && (RMC_TLC_CFG_MASK ? bag.cfg(q) : msg_has_config(c, cfgt))) {
+          RMC_FPS(25, 1);
 #pragma unroll 1
           for (int p = 0; p < NPERM; ++p) {
             const u64 v = perm_code(c, perm_of(p), true, cfgt);
@@ -1756,6 +1777,7 @@ struct Memb {
       cand = cm; last = best; have_last = true; j0 = 1;
     }
 #endif
+    RMC_FPS(2, __builtin_popcount(cand));
     // Automorphic candidates (symmetric states: servers in the same role): when every remaining
     // permutation maps the bag to the same function -- its permuted codes with their counts,
     // compared by a sum of 64-bit mixes (the fingerprint's own collision class) -- the domain and
@@ -1767,21 +1789,24 @@ struct Memb {
     auto bag_hash = [&](u32 pi) -> u64 {
       u64 h = 0;
 #pragma unroll 1
-      for (int q = 0; q < len; ++q) { const u64 e = bag[q]; h += fmix(((perm_code(mcode(e), pi, ce, cfgt) + 1ull) * P1) ^ (u64)mcount(e)); }
+      for (int q = 0; q < len; ++q) { const u64 e = bag[q]; h += fmix(((perm_code(mcode(e), pi, ce && bag.cfg(q), cfgt) + 1ull) * P1) ^ (u64)mcount(e)); }
       return h;
     };
-    // The next messages in domain order, a few at most: each usually halves the candidates.
+    // The next messages in domain order, a few at most: each usually halves the candidates (3:
+    // memb_fingerprint 531 vs 546 ms per C3 run at 2, round 5; more saves nothing on the host counts)
 #ifndef RMC_TLC_NARROW
-#define RMC_TLC_NARROW 2
+#define RMC_TLC_NARROW 3
 #endif
     int j = j0;
 #pragma unroll 1
     for (; (j == 0 || (j < len && !single(cand))) && j < j0 + RMC_TLC_NARROW; ++j) {   // (one pass even for an empty bag)
       u64 next = 0;
+      RMC_FPS(15, 1); RMC_FPS(16, __builtin_popcount(cand));
       cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); }, &next);
       last = next;
       have_last = true;
     }
+    RMC_FPS(3, __builtin_popcount(cand)); RMC_FPS(22, single(cand));
     RMC_PROF_ADD(prof, 3, pt);
     // Candidates that map the bag to the same function tie through the rest of the domain and all
     // the counts: a symmetric state (servers in the same role) keeps such groups to the last
@@ -1789,12 +1814,19 @@ struct Memb {
     // left; its members all go on to the history.
     const u32 group_of_all = cand;
     bool grouped = false, bag_done = false;
-    if (!single(cand) && j < len) {
+    // (also when the narrowing already compared the whole domain: the counts loop below would
+    // otherwise run over every message for candidates that map the bag to the same function)
+#ifndef RMC_TLC_GROUP_ALL
+#define RMC_TLC_GROUP_ALL 1
+#endif
+    if (!single(cand) && (RMC_TLC_GROUP_ALL ? len > 0 : j < len)) {
+      RMC_FPS(4, 1); RMC_FPS(14, len); RMC_FPS(20, __builtin_popcount(cand));
       u32 reps = 0, first_grp = 0;
 #pragma unroll 1
       for (u32 left = cand; left;) {
         const int p = __builtin_ctz(left);
         const u64 h = bag_hash(perm_of(p));
+        RMC_FPS(5, 1 + __builtin_popcount(left & (left - 1u)));
         u32 grp = 1u << p;
 #pragma unroll 1
         for (u32 m = left & (left - 1u); m; m &= m - 1u) {
@@ -1805,26 +1837,30 @@ struct Memb {
         reps |= 1u << p;
         left &= ~grp;
       }
-      if (single(reps)) { cand = first_grp; bag_done = true; }   // one group: the bag stages tie for all of it
-      else { cand = reps; grouped = true; }
+      if (single(reps)) { cand = first_grp; bag_done = true; RMC_FPS(6, 1); }   // one group: the bag stages tie for all of it
+      else { cand = reps; grouped = true; RMC_FPS(7, 1); RMC_FPS(21, __builtin_popcount(reps)); }
     }
 #pragma unroll 1
     for (; !bag_done && j < len && !single(cand); ++j) {
+      RMC_FPS(8, 1); RMC_FPS(9, __builtin_popcount(cand));
       u64 next = 0;
       cand = keep_min(cand, [&](int, u32 pi) { return next_perm_code(bag, len, pi, ce, cfgt, have_last, last); }, &next);
       last = next;
       have_last = true;
     }
     have_last = false;
+    RMC_FPS(23, !bag_done && !grouped && len > 0 && !single(cand));
 #pragma unroll 1
-    for (int jc = 0; !bag_done && jc < len && !single(cand); ++jc) {   // same permuted domain: the counts in domain order
+    for (int jc = 0; !bag_done && jc < len && !single(cand); ++jc) {
+      RMC_FPS(24, !grouped);   // same permuted domain: the counts in domain order
       const u64 code = next_perm_code(bag, len, perm_of(__builtin_ctz(cand)), ce, cfgt, have_last, last);
+      RMC_FPS(10, 1); RMC_FPS(11, __builtin_popcount(cand));
       cand = keep_min(cand, [&](int, u32 pi) {
         u64 cnt = 0;
 #pragma unroll 1
         for (int q = 0; q < len; ++q) {
           const u64 e = bag[q];
-          if (perm_code(mcode(e), pi, ce, cfgt) == code) cnt = (u64)mcount(e);
+          if (perm_code(mcode(e), pi, ce && bag.cfg(q), cfgt) == code) cnt = (u64)mcount(e);
         }
         return cnt;
       });
@@ -1834,6 +1870,7 @@ struct Memb {
       // the winning representative's whole group (members of other groups lost on the bag)
       const u64 h = bag_hash(perm_of(__builtin_ctz(cand)));
       u32 grp = cand;
+      RMC_FPS(12, 1 + __builtin_popcount(group_of_all & ~cand));
 #pragma unroll 1
       for (u32 m = group_of_all & ~cand; m; m &= m - 1u) {
         const int q = __builtin_ctz(m);
@@ -1845,6 +1882,7 @@ struct Memb {
     // history: [global, hadNum* (invariant), server], currentTerm, state, votedFor, log, commitIndex,
     // votesResponded, votesGranted, nextIndex, matchIndex — each a function over the servers, in
     // the fused runs of key_scalars / key_log / key_cv / key_nm
+    RMC_FPS(17, !single(cand)); RMC_FPS(18, single(cand) ? 0 : __builtin_popcount(cand));
     if (!single(cand)) cand = keep_min(cand, [&](int p, u32 pi) { return key_scalars(t, p, pi); });
 #pragma unroll 1
     for (int x = 0; x < N && !single(cand); ++x)
@@ -1869,15 +1907,20 @@ struct Memb {
     constexpr int stride = 1;
 #endif
     int len = 0;
+    u32 cfgm = 0;
 #pragma unroll
-    for (int q = 0; q < MK; ++q) { base[q * stride] = t.bag.v[q]; len += t.bag.v[q] != EMPTY; }
+    for (int q = 0; q < MK; ++q) {
+      base[q * stride] = t.bag.v[q];
+      len += t.bag.v[q] != EMPTY;
+      if (ce && t.bag.v[q] != EMPTY && (!RMC_TLC_CFG_MASK || msg_has_config(mcode(t.bag.v[q]), rt.cfg_type))) cfgm |= 1u << q;
+    }
     RMC_PROF_ADD(prof, 1, pt);
-    const u32 pi = tlc_min_perm(t, BagRef{base, stride}, len, ce, rt.cfg_type, prof);
+    const u32 pi = tlc_min_perm(t, BagRef{base, stride, cfgm}, len, ce, rt.cfg_type, prof);
     pt = RMC_PROF_T();
     const u64 best = ce ? view_hash1<true>(t, pi, seed, rt.cfg_type) : view_hash1<false>(t, pi, seed, rt.cfg_type);
     RMC_PROF_ADD(prof, 6, pt);
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RMC_FP_DUP_MINPERM)   // timing experiment: the search twice
-    { int l2 = len; asm volatile("" : "+v"(l2)); const u32 p2 = tlc_min_perm(t, BagRef{base, stride}, l2, ce, rt.cfg_type); asm volatile("" :: "v"(p2)); }
+    { int l2 = len; asm volatile("" : "+v"(l2)); const u32 p2 = tlc_min_perm(t, BagRef{base, stride, cfgm}, l2, ce, rt.cfg_type); asm volatile("" :: "v"(p2)); }
 #endif
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RMC_FP_DUP_VIEW)      // timing experiment: the view hash twice
     { u32 p2 = pi; asm volatile("" : "+v"(p2)); const u64 b2 = ce ? view_hash1<true>(t, p2, seed, rt.cfg_type) : view_hash1<false>(t, p2, seed, rt.cfg_type); asm volatile("" :: "v"((u32)b2), "v"((u32)(b2 >> 32))); }

@@ -133,11 +133,11 @@ __device__ __forceinline__ void exp_launder(typename S::Work& s) {
 // instance a wave ballot, one LDS atomic per wave for the base, and consecutive stores
 // (only ~21% of C2's instance slots carry an in-model successor).
 template <class S>
-// 3 waves per SIMD (<= 168 VGPRs) measured fastest for C2's expand (19.9 vs 22.3 ms without the
-// hint, 26.6 ms at the 2 waves the incremental fingerprint would otherwise get); larger states
-// (C5: 24 words) would spill at 3 and get no hint.
+// 4 waves per SIMD (<= 128 VGPRs, no spill since the Dup/Drop section stopped going through apply):
+// 11.7 vs 13.4 ms of orig_generate per C2 run at 3 (round 5, profiles/r05_generate_ab.txt; round 2
+// measured 3 at 19.9 vs 22.3 ms without the hint); 5 spills.  Larger states (C5: 24 words) get no hint.
 #ifndef RMC_GEN_WAVES
-#define RMC_GEN_WAVES 3
+#define RMC_GEN_WAVES 4
 #endif
 #ifndef RMC_GEN_INC
 #define RMC_GEN_INC 1

@@ -291,7 +291,11 @@ struct TlagenBackend : Backend {
     dev = o.device;
     HIPOK(hipSetDevice(dev));
     std::string image;
+    // RAFTMC_TLAGEN_TIMING=1: where mc_run's wall time goes outside the kernels (stderr)
+    const bool timing = std::getenv("RAFTMC_TLAGEN_TIMING") != nullptr;
+    auto since = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
     if (int rc = code_object(image, err)) return rc;
+    const double t_co = since();
     struct Scratch {   // everything but the store (kept for traces / dump_states) is freed on every return
       hipModule_t mod = nullptr;
       std::vector<void*> bufs;
@@ -362,6 +366,8 @@ struct TlagenBackend : Backend {
     }
     HIPOK(hipMemset(d_table, 0, slots * entry));
     HIPOK(hipMemset(d_ctr, 0, nctr * 8));
+    if (timing) HIPOK(hipDeviceSynchronize());
+    const double t_setup = since();
     KArgs a{};
     a.words = d_words; a.words_used = d_ctr + nctr - 1; a.words_cap = words_cap;
     a.offs = d_offs; a.parent = d_parent; a.act = d_act; a.states_cap = states_cap;
@@ -447,6 +453,11 @@ struct TlagenBackend : Backend {
       first += count; count = fresh;
       if (fresh) ++r.depth; else r.levels.pop_back();
     }
+    const double t_loop = since();
+    if (timing)
+      std::fprintf(stderr, "tlagen timing: code object %.3f s, module load + allocation + clears %.3f s, level loop %.3f s "
+                           "(kernels %.3f s), store %.1f GiB, arena %.1f GiB\n", t_co, t_setup - t_co, t_loop - t_setup,
+                   r.seconds_kernels, store / 1073741824.0, (double)lanes * (acap + hcap) * 4 / 1073741824.0);
     if (!fifo && h[C_FLAG] && !h[C_CAP]) {   // (searched again in FIFO order by run())
       // tlagen_kernels.h C_KIND: 1/2 violation, 3 evaluation error, 4 deadlock, 5 invariant evaluation error
       static const char* const kinds[] = {"an event", "an invariant violation", "an invariant violation",

@@ -8,6 +8,7 @@
 #   bench               bench.py with its defaults (the driver's line)
 #   c2[=NAME[=LIB]]     bench.py C2 only (no extras, no CPU baseline) with library LIB (default: the
 #                       in-tree build), 8 timed steps; prints ms/step, kernels, seen-set probes
+#   memb[=NAME[=LIB]]   scripts/memb_probe.py memb_four (C3, TLC's symmetry rule) with library LIB, twice
 #   prof                rocprofv3 --kernel-trace --stats of a short C2 bench
 #   c2_prof[=TAG]       rocprofv3 stats + FETCH/WRITE/SQ passes of C2, summarised (scripts/c2_prof.sh)
 #   memb_prof           rocprofv3 stats + PMC passes of C3 (scripts/memb_prof.sh)
@@ -41,6 +42,15 @@ import json
 d = json.loads(open('$O/c2_$n.json').read().strip().splitlines()[-1])
 print('$n', round(d['ms_per_step'], 2), {k: round(v['ms'], 2) for k, v in d['kernels'].items()}, d['config']['distinct_per_run'],
       'probes', d.get('dedup_set', {}).get('probes_per_run'))" ;;
+    memb)
+      n=${arg%%=*}; lib=${arg#*=}; [ "$lib" = "$arg" ] && lib=""; n=${n:-base}
+      timeout -k 10 200 env ${lib:+RAFTMC_LIB=$lib} python3 scripts/memb_probe.py memb_four 0 0 > "$O/memb_$n.json" 2> "$O/memb_$n.err"
+      rc=$?
+      [ $rc -eq 0 ] && python3 -c "
+import json
+for l in open('$O/memb_$n.json').read().strip().splitlines():
+    d = json.loads(l)
+    print('$n', d['verdict'], d['distinct'], d['depth'], d['run_s'], d['kernels_ms'])" ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_stats" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra --fifo-steps 0 > "$O/prof_stats.log" 2>&1
       rc=$? ;;

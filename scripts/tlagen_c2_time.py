@@ -16,6 +16,7 @@ src = os.path.join(ROOT, "raft-tla_amd", "_build", "tlagen_co", "c2.gen.hip")
 for spec in sys.argv[1:] or ["8@200"]:
     waves, _, gib = spec.partition("@")
     os.environ["RAFTMC_TLAGEN_WAVES"] = waves
+    os.environ["RAFTMC_TLAGEN_TIMING"] = "1"
     with rm.ModelChecker(src, os.path.join(ROOT, "configs", "c2.cfg"), frontend="generated", workers=0,
                          fp_table_bytes=1 << 30, state_store_bytes=int(gib or 200) << 30) as mc:
         r = mc.run()

@@ -22,6 +22,9 @@
 #include "../../raft-tla_amd/csrc/memb_prefix.h"
 #include "../../raft-tla_amd/csrc/memb_text.h"
 
+#ifdef RMC_FP_STATS   // work counts of the TLC-mode canonical-permutation search (memb_spec.h RMC_FPS), on stderr
+long long rmc_fp_stats[32];
+#endif
 using namespace rmc;
 using S = Memb<SHAPE_N, SHAPE_NV, 2 * SHAPE_N * SHAPE_N>;
 using W = S::Work;
@@ -132,5 +135,10 @@ int main(int argc, char** argv) {
               generated, seen.size(), depth, left, err, verdict.c_str(), violated.c_str());
   for (int k = 0; k < MA_NACT; ++k) std::printf("%s\"%s\": [%lld, %lld]", k ? ", " : "", kMembActNames[k], gen_act[k], dist_act[k]);
   std::printf("}}\n");
+#ifdef RMC_FP_STATS
+  std::fprintf(stderr, "fp_stats");
+  for (int i = 0; i < 32; ++i) std::fprintf(stderr, " %d:%lld", i, rmc_fp_stats[i]);
+  std::fprintf(stderr, "\n");
+#endif
   return 0;
 }
