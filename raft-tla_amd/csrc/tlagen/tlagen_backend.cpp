@@ -172,6 +172,29 @@ struct TlagenBackend : Backend {
   u32* d_words = nullptr; u64* d_offs = nullptr; u64 n_stored = 0, words_stored = 0;
   bool store_complete = true;   // false after a store overflow (ids handed out without words)
   int dev = 0;
+  // The run's device buffers (store, seen-set, lane arenas, FIFO key arrays), kept from one run to the
+  // next when the sizes and the device are unchanged: allocating a 200 GiB store costs ~2.5 s on
+  // MI355X and freeing the buffers ~2.5 s more (scripts/hipmalloc_time.py), i.e. a quarter of C2's
+  // run, so only a changed size (or a larger arena after an overflow) allocates again.
+  struct Pool {
+    int dev = -1;
+    std::vector<u64> bytes;
+    std::vector<void*> ptr;
+    void free_all() {
+      for (void* q : ptr) if (q) (void)hipFree(q);
+      ptr.clear(); bytes.clear(); dev = -1;
+    }
+    // buffers of these sizes on device d (0 bytes: none); false = allocation failed (nothing kept)
+    bool get(int d, const std::vector<u64>& want) {
+      if (d == dev && want == bytes) return true;
+      free_all();
+      ptr.assign(want.size(), nullptr);
+      for (size_t i = 0; i < want.size(); ++i)
+        if (want[i] && hipMalloc(&ptr[i], want[i]) != hipSuccess) { ptr[i] = nullptr; free_all(); return false; }
+      bytes = want; dev = d;
+      return true;
+    }
+  } pool;
 
   TlagenBackend(const std::string& tla_path, const CfgFile& cfg) {
     if (tla_path.size() > 8 && tla_path.compare(tla_path.size() - 8, 8, ".gen.hip") == 0) {
@@ -200,8 +223,7 @@ struct TlagenBackend : Backend {
   }
   ~TlagenBackend() override { release(); }
   void release() {
-    if (d_words) (void)hipFree(d_words);
-    if (d_offs) (void)hipFree(d_offs);
+    pool.free_all();
     d_words = nullptr; d_offs = nullptr;
   }
 
@@ -296,9 +318,8 @@ struct TlagenBackend : Backend {
     auto since = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(); };
     if (int rc = code_object(image, err)) return rc;
     const double t_co = since();
-    struct Scratch {   // everything but the store (kept for traces / dump_states) is freed on every return
+    struct Scratch {   // freed on every return (the device buffers stay in the pool)
       hipModule_t mod = nullptr;
-      std::vector<void*> bufs;
       void* sort_tmp = nullptr;
       hipEvent_t e0 = nullptr, e1 = nullptr;
       size_t prev_stack = 0;       // the device's stack limit before a recursive module raised it
@@ -306,7 +327,6 @@ struct TlagenBackend : Backend {
       ~Scratch() {
         // hipLimitStackSize is process-wide: later kernels (the hand-compiled paths) get their limit back
         if (stack_raised) (void)hipDeviceSetLimit(hipLimitStackSize, prev_stack);
-        for (void* p : bufs) if (p) (void)hipFree(p);
         if (sort_tmp) (void)hipFree(sort_tmp);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
@@ -332,7 +352,6 @@ struct TlagenBackend : Backend {
     HIPOK(hipModuleGetFunction(&f_keys, sc.mod, "tlg_keys_k"));
     HIPOK(hipModuleGetFunction(&f_mat, sc.mod, "tlg_mat_k"));
     HIPOK(hipModuleGetFunction(&f_stop, sc.mod, "tlg_stop_k"));
-    release();
     // HBM layout: store words + per-state offsets/parents/actions, seen-set, lanes' arenas (+ FIFO:
     // the level's inserted entries and their keys, unsorted and sorted)
     const u64 store = o.state_store_bytes ? o.state_store_bytes : (16ull << 30);
@@ -354,16 +373,17 @@ struct TlagenBackend : Backend {
     const int nact = (int)meta.actions.size();
     const size_t nctr = C_ACT + 2 * (size_t)nact + 4;   // + n_committed, n_states, words_used
     const u64 kcap = fifo ? std::min<u64>(states_cap, slots) : 1;
-    bool oom = hipMalloc(&d_words, words_cap * 4) || hipMalloc(&d_offs, states_cap * 8) || hipMalloc(&d_parent, states_cap * 8) ||
-               hipMalloc(&d_act, states_cap * 4) || hipMalloc(&d_table, slots * entry) || hipMalloc(&d_ctr, nctr * 8) ||
-               hipMalloc(&d_arena, lanes * acap * 4) || hipMalloc(&d_hs, lanes * hcap * 4) || hipMalloc(&d_ev, evcap * 4);
-    if (!oom && fifo) oom = hipMalloc(&d_newpos, kcap * 8) || hipMalloc(&d_keys, kcap * 8) || hipMalloc(&d_sorted, kcap * 8);
-    sc.bufs = {d_parent, d_table, d_ctr, d_act, d_arena, d_hs, d_ev, d_newpos, d_keys, d_sorted};
-    if (oom) {
-      release();
+    const u64 kb = fifo ? kcap * 8 : 0;
+    d_words = nullptr; d_offs = nullptr;
+    if (!pool.get(dev, {words_cap * 4, states_cap * 8, states_cap * 8, states_cap * 4, slots * entry, nctr * 8,
+                        lanes * acap * 4, lanes * hcap * 4, evcap * 4, kb, kb, kb})) {
       err = "device allocation failed";
       return MC_E_OOM;
     }
+    d_words = (u32*)pool.ptr[0]; d_offs = (u64*)pool.ptr[1]; d_parent = (u64*)pool.ptr[2]; d_act = (u32*)pool.ptr[3];
+    d_table = (u64*)pool.ptr[4]; d_ctr = (u64*)pool.ptr[5]; d_arena = (u32*)pool.ptr[6]; d_hs = (u32*)pool.ptr[7];
+    d_ev = (u32*)pool.ptr[8]; d_newpos = (u64*)pool.ptr[9]; d_keys = (u64*)pool.ptr[10]; d_sorted = (u64*)pool.ptr[11];
+    n_stored = 0; words_stored = 0; store_complete = false;
     HIPOK(hipMemset(d_table, 0, slots * entry));
     HIPOK(hipMemset(d_ctr, 0, nctr * 8));
     if (timing) HIPOK(hipDeviceSynchronize());

@@ -8,6 +8,7 @@
 #   bench               bench.py with its defaults (the driver's line)
 #   c2[=NAME[=LIB]]     bench.py C2 only (no extras, no CPU baseline) with library LIB (default: the
 #                       in-tree build), 8 timed steps; prints ms/step, kernels, seen-set probes
+#   c2t=GIB             the C2 line with a GIB-GiB seen-set (--fp-table-bytes), 8 timed steps
 #   memb[=NAME[=LIB]]   scripts/memb_probe.py memb_four (C3, TLC's symmetry rule) with library LIB, twice
 #   prof                rocprofv3 --kernel-trace --stats of a short C2 bench
 #   c2_prof[=TAG]       rocprofv3 stats + FETCH/WRITE/SQ passes of C2, summarised (scripts/c2_prof.sh)
@@ -41,6 +42,15 @@ for step in "$@"; do
 import json
 d = json.loads(open('$O/c2_$n.json').read().strip().splitlines()[-1])
 print('$n', round(d['ms_per_step'], 2), {k: round(v['ms'], 2) for k, v in d['kernels'].items()}, d['config']['distinct_per_run'],
+      'probes', d.get('dedup_set', {}).get('probes_per_run'))" ;;
+    c2t)
+      timeout -k 10 200 python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-extra --fifo-steps 0 \
+        --fp-table-bytes $((arg << 30)) > "$O/c2t_$arg.json" 2> "$O/c2t_$arg.err"
+      rc=$?
+      [ $rc -eq 0 ] && python3 -c "
+import json
+d = json.loads(open('$O/c2t_$arg.json').read().strip().splitlines()[-1])
+print('table $arg GiB', round(d['ms_per_step'], 2), {k: round(v['ms'], 2) for k, v in d['kernels'].items()}, d['config']['distinct_per_run'],
       'probes', d.get('dedup_set', {}).get('probes_per_run'))" ;;
     memb)
       n=${arg%%=*}; lib=${arg#*=}; [ "$lib" = "$arg" ] && lib=""; n=${n:-base}
