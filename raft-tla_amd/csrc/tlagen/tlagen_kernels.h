@@ -333,9 +333,7 @@ struct Em {
 };
 
 __device__ inline void lane_init(Args& a, Ar& A, tlg::Cx& c, Em& em, unsigned long long lane, u32 mode) {
-  // lane-interleaved (tlv::Wp): the wave's region holds TLV_LANES lanes' words side by side
-  const unsigned long long grp = lane / TLV_LANES, sub = lane % TLV_LANES;
-  init(A, a.arena + grp * TLV_LANES * a.acap + sub, a.acap, a.hstack + grp * TLV_LANES * a.hcap + sub, a.hcap);
+  init(A, a.arena + lane * a.acap, a.acap, a.hstack + lane * a.hcap, a.hcap);
   c.A = &A;
   tlg::init_consts(c);
   em.a = &a; em.mode = mode; em.gen = em.gin = em.ord = 0; em.j = 0; em.rank = 0;

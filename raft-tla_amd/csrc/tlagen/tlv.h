@@ -55,26 +55,10 @@ enum : u32 {
   E_UNSUP = 128u     // construct outside the compiled subset reached at run time
 };
 
-// A lane's arena and handle stack on the device are lane-interleaved: word i of lane l of a wave sits
-// at base + i * 64 + l, so when the lanes of a wave touch the same offset (the parent copy, the
-// fixed part of every state's layout, the constants) one wave instruction reads 256 contiguous
-// bytes instead of 64 lines.  On the host (tests, CPU harnesses) the stride is 1.
-#ifndef TLV_LANES
-#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC_RTC__)
-#define TLV_LANES 64
-#else
-#define TLV_LANES 1
-#endif
-#endif
-struct Wp {
-  u32* p;
-  TLV_HD u32& operator[](u32 i) const { return p[i * (u32)TLV_LANES]; }
-  TLV_HD Wp operator+(u32 i) const { return Wp{p + i * (u32)TLV_LANES}; }
-};
 struct Ar {
-  Wp w;         // values grow up from 4 (0: FALSE, 2: TRUE)
+  u32* w;       // values grow up from 4 (0: FALSE, 2: TRUE)
   u32 top, cap;
-  Wp hs;        // handle stack (builders)
+  u32* hs;      // handle stack (builders)
   u32 htop, hcap;
   u32 err;
   const u32* akey;   // per atom id: AK_MV bit for model values, then its rank in TLC's order (generated)
@@ -90,8 +74,8 @@ TLV_HD u32 hdr(u32 tag, u32 n) { return tag | (n << 3); }
 TLV_HD u32 tg(const Ar& a, u32 v) { return a.w[v] & 7u; }
 TLV_HD u32 sz(const Ar& a, u32 v) { return a.w[v] >> 3; }
 TLV_HD void init(Ar& a, u32* w, u32 cap, u32* hs, u32 hcap) {
-  a.w = Wp{w}; a.cap = cap; a.hs = Wp{hs}; a.hcap = hcap; a.htop = 0; a.err = 0; a.akey = nullptr; a.nakey = 0; a.rdepth = 0;
-  a.w[0] = hdr(T_BOOL, 2); a.w[1] = 0; a.w[2] = hdr(T_BOOL, 2); a.w[3] = 1; a.top = 4;
+  a.w = w; a.cap = cap; a.hs = hs; a.hcap = hcap; a.htop = 0; a.err = 0; a.akey = nullptr; a.nakey = 0; a.rdepth = 0;
+  w[0] = hdr(T_BOOL, 2); w[1] = 0; w[2] = hdr(T_BOOL, 2); w[3] = 1; a.top = 4;
 }
 TLV_HD u32 alloc(Ar& a, u32 n) {
   if (a.err & E_OVF) return 0;
@@ -579,8 +563,7 @@ TLV_HD u32 tail(Ar& a, u32 s) {
 
 // ---- state words and fingerprint
 TLV_HD u64 fmix(u64 h) { h ^= h >> 33; h *= 0xff51afd7ed558ccdULL; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ULL; h ^= h >> 33; return h; }
-template <class P>   // P: const u32* (the store) or Wp (an arena)
-TLV_NI u64 fp_words(P w, u32 n, u64 seed) {
+TLV_NI u64 fp_words(const u32* w, u32 n, u64 seed) {
   u64 h = seed ^ ((u64)n * 0x9e3779b97f4a7c15ULL);
   u32 q = 0;
   for (; q + 1 < n; q += 2) h = fmix(h ^ (((u64)w[q + 1] << 32) | w[q])) + 0x9e3779b97f4a7c15ULL;

@@ -38,10 +38,10 @@ struct Emit {
     s.im = tlg::constraints(d) && (init || tlg::action_constraints(c));
     s.cerr = A.err != e0;   // a constraint could not be evaluated: TLC's evaluation error
     A.err = e0;
-    for (int i = 0; i < tlg::NV; ++i) { const u32 h = c.nxt[i]; s.w.insert(s.w.end(), A.w.p + h, A.w.p + h + tlv::sz(A, h)); }
+    for (int i = 0; i < tlg::NV; ++i) { const u32 h = c.nxt[i]; s.w.insert(s.w.end(), A.w + h, A.w + h + tlv::sz(A, h)); }
     if ((tlg::HAS_VIEW || tlg::HAS_SYMMETRY) && s.im && !s.cerr) {   // TLC's VIEW / SYMMETRY: states told apart by canon_view
       const u32 vh = tlg::canon_view(d);
-      s.key.assign(A.w.p + vh, A.w.p + vh + tlv::sz(A, vh));   // (host: stride 1)
+      s.key.assign(A.w + vh, A.w + vh + tlv::sz(A, vh));
       if (A.err != e0) { s.cerr = true; A.err = e0; }
     } else {
       s.key = s.w;
