@@ -77,8 +77,6 @@ struct MGenArgs {
   u32 inv_oom, deadlock;
   unsigned long long* ctr;
   unsigned long long* prof;                // RMC_FP_PROF builds: wave cycles per fingerprint stage (else null)
-  u32* hard;                               // TLC mode: cells memb_fingerprint deferred to memb_fingerprint_hard
-  u32* hard_n;                             // ... and their count (zeroed before each chunk's memb_fingerprint)
 };
 
 // Phase 1 for the instances [K0, K1) with NS successors each.  The bounds are compile-time so
@@ -191,9 +189,13 @@ __global__ void __launch_bounds__(BS) memb_expand(MGenArgs a) {
 // symmetric FP64 into its cell (cand[slot][state]).
 // TLC = MC_COMPAT_SYM_TLC (a kernel of its own, so the orbit mode keeps its registers).
 template <class S, bool TLC>
-__device__ __forceinline__ void rederive(const MGenArgs& a, u32 cell, typename S::Work& t) {
+__global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
   using W = typename S::Work;
   constexpr int NWP = S::NWP;
+  const u32 n = a.cell_count[2 * blockIdx.x];
+  const u32* cells = a.cells + (u64)blockIdx.x * (BS * S::NSLOT);
+  for (u32 i = threadIdx.x; i < n; i += BS) {
+  const u32 cell = cells[i];
   const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
   int k, sub;
   S::inst_of_slot((int)slot, k, sub);
@@ -201,58 +203,16 @@ __device__ __forceinline__ void rederive(const MGenArgs& a, u32 cell, typename S
   const uint4* src = reinterpret_cast<const uint4*>(a.states + (a.chunk_begin + st) * NWP);
 #pragma unroll
   for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
-  W s;
+  W s, t;
+  unsigned long long pt = RMC_PROF_T();
   S::unpack(w, s);
   u32 err = 0;
   S::template apply<TLC>(s, k, sub, t, err, a.rt);
+  RMC_PROF_ADD(a.prof, 0, pt);
 #ifdef RMC_FP_DUP_APPLY   // timing experiment: the re-derivation twice
   { W t2; u32 e2 = 0; int k2 = k; asm volatile("" : "+v"(k2)); S::template apply<TLC>(s, k2, sub, t2, e2, a.rt); asm volatile("" :: "v"((u32)t2.hr0), "v"(t2.term), "v"(e2)); }
 #endif
-}
-
-template <class S, bool TLC>
-__global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
-  using W = typename S::Work;
-  const u32 n = a.cell_count[2 * blockIdx.x];
-  const u32* cells = a.cells + (u64)blockIdx.x * (BS * S::NSLOT);
-  const int lane = __lane_id();
-  for (u32 i = threadIdx.x; i < n; i += BS) {
-    const u32 cell = cells[i];
-    W t;
-    unsigned long long pt = RMC_PROF_T();
-    rederive<S, TLC>(a, cell, t);
-    RMC_PROF_ADD(a.prof, 0, pt);
-    if constexpr (TLC) {
-      // a cell whose candidates map the bag to different functions goes to memb_fingerprint_hard (one
-      // counter atomic per wave and loop trip; the order in the list is immaterial: cand is by cell)
-      const u64 fp = S::fingerprint_tlc(t, a.seed, a.rt, a.prof, a.hard != nullptr);
-      const bool defer = fp == 0ull;
-      const u64 dm = __ballot(defer);
-      if (dm) {
-        const int leader = __ffsll((unsigned long long)dm) - 1;
-        u32 base = 0;
-        if (lane == leader) base = atomicAdd(a.hard_n, (u32)__popcll(dm));
-        base = __shfl(base, leader);
-        if (defer) a.hard[base + (u32)__popcll(dm & ((1ull << lane) - 1ull))] = cell;
-      }
-      if (!defer) a.cand[cell] = fp;
-    } else {
-      a.cand[cell] = S::fingerprint_orbit(t, a.seed, a.rt);
-    }
-  }
-}
-
-// The deferred cells of the chunk (TLC mode): the whole canonical-permutation search, on waves whose
-// lanes all need the bag stages (grid-stride over *hard_n, which the device wrote)
-template <class S>
-__global__ void __launch_bounds__(BS) memb_fingerprint_hard(MGenArgs a) {
-  using W = typename S::Work;
-  const u32 n = *a.hard_n;
-  for (u32 i = blockIdx.x * BS + threadIdx.x; i < n; i += gridDim.x * BS) {
-    const u32 cell = a.hard[i];
-    W t;
-    rederive<S, true>(a, cell, t);
-    a.cand[cell] = S::fingerprint_tlc(t, a.seed, a.rt);
+  a.cand[cell] = TLC ? S::fingerprint_tlc(t, a.seed, a.rt, a.prof) : S::fingerprint_orbit(t, a.seed, a.rt);
   }
 }
 
@@ -864,7 +824,6 @@ class MembGpu : public Backend {
     HIPCHK(hipMalloc(&d_nsucc_, chunk_ * 2));
     HIPCHK(hipMalloc(&d_cells_, chunk_ * S::NSLOT * 4));
     HIPCHK(hipMalloc(&d_cells_oom_, chunk_ * S::NSLOT * 4));
-    HIPCHK(hipMalloc(&d_hard_, chunk_ * S::NSLOT * 4 + 64));   // the deferred cells, then their count
     HIPCHK(hipMalloc(&d_cell_count_, 2 * ((chunk_ + BS - 1) / BS) * 4));
     HIPCHK(hipMalloc(&d_woff_, chunk_ * 4));
     HIPCHK(hipMalloc(&d_bsum_, SCAN_MAX_BLOCKS * 8));
@@ -1734,7 +1693,7 @@ class MembGpu : public Backend {
   MembText<S> text_;
   u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr;
   u64* d_cand_ = nullptr; u64* d_newrec_ = nullptr; unsigned short* d_nsucc_ = nullptr; unsigned int* d_woff_ = nullptr;
-  u32* d_cells_ = nullptr; u32* d_cells_oom_ = nullptr; u32* d_cell_count_ = nullptr; u32* d_hard_ = nullptr;
+  u32* d_cells_ = nullptr; u32* d_cells_oom_ = nullptr; u32* d_cell_count_ = nullptr;
   u64* d_bsum_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_[9] = {};
@@ -1777,21 +1736,8 @@ class MembGpu : public Backend {
     if (!d_prof_) { HIPCHK(hipMalloc(&d_prof_, 8 * 8)); HIPCHK(hipMemset(d_prof_, 0, 8 * 8)); }
     g.prof = d_prof_;
 #endif
-#ifndef RMC_FP_DEFER
-#define RMC_FP_DEFER 1
-#endif
-    g.hard = nullptr; g.hard_n = nullptr;
-    if (rt_dev_.sym_tlc) {
-      if (RMC_FP_DEFER) {
-        g.hard = d_hard_;
-        g.hard_n = d_hard_ + chunk_ * S::NSLOT;   // (a cell list never exceeds chunk * NSLOT entries)
-        HIPCHK(hipMemsetAsync(g.hard_n, 0, 4, stream_));
-      }
-      hipLaunchKernelGGL((memb_fingerprint<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
-      if (RMC_FP_DEFER) hipLaunchKernelGGL((memb_fingerprint_hard<S>), dim3((nblk + 3) / 4), dim3(BS), 0, stream_, g);
-    } else {
-      hipLaunchKernelGGL((memb_fingerprint<S, false>), dim3(nblk), dim3(BS), 0, stream_, g);
-    }
+    if (rt_dev_.sym_tlc) hipLaunchKernelGGL((memb_fingerprint<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
+    else hipLaunchKernelGGL((memb_fingerprint<S, false>), dim3(nblk), dim3(BS), 0, stream_, g);
     HIPCHK(hipGetLastError());
     return 0;
   }
@@ -1810,14 +1756,12 @@ class MembGpu : public Backend {
     for (void* q : {(void*)d_lvl_, (void*)d_sorted_, (void*)d_newrec_lvl_, (void*)d_sort_tmp_, (void*)d_nsucc_lvl_}) if (q) (void)hipFree(q);
     d_lvl_ = nullptr; d_sorted_ = nullptr; d_newrec_lvl_ = nullptr; d_sort_tmp_ = nullptr; d_nsucc_lvl_ = nullptr; lvl_cap_ = 0;
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_cand_, (void*)d_newrec_,
-                    (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_, (void*)d_cells_oom_, (void*)d_cell_count_,
-                    (void*)d_hard_})
+                    (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_, (void*)d_cells_oom_, (void*)d_cell_count_})
       if (p) (void)hipFree(p);
     for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
     if (stream_) (void)hipStreamDestroy(stream_);
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_cand_ = nullptr; d_newrec_ = nullptr;
     d_nsucc_ = nullptr; d_woff_ = nullptr; d_bsum_ = nullptr; d_cells_ = nullptr; d_cells_oom_ = nullptr; d_cell_count_ = nullptr; stream_ = nullptr;
-    d_hard_ = nullptr;
   }
   // stored state `gid` (global id) and its parent pointer, from the host part or the device
   void read_state(u64 gid, W& s, u64* meta = nullptr) const {

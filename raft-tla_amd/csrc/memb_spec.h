@@ -1739,14 +1739,7 @@ struct Memb {
     return m;
   }
   // the permutation TLC picks: least permuted variable tuple, variable by variable
-  // defer (device kernels only): instead of running the bag stages for candidates that map the bag to
-  // different functions (~2% of C3's fingerprints, but enough that most waves waited for one such lane),
-  // return DEFERRED: memb_fingerprint hands the cell to memb_fingerprint_hard, which runs the whole
-  // search on waves of such cells only.  (A value, not a flag through a pointer: that put the flag in
-  // scratch memory.)
-  static constexpr u32 DEFERRED = ~0u;
-  RMC_HD static u32 tlc_min_perm(const Work& t, const BagRef& bag, int len, bool ce, u32 cfgt, unsigned long long* prof = nullptr,
-                                 bool defer = false) {
+  RMC_HD static u32 tlc_min_perm(const Work& t, const BagRef& bag, int len, bool ce, u32 cfgt, unsigned long long* prof = nullptr) {
     unsigned long long pt = RMC_PROF_T();
     u32 cand = (u32)lomask(NPERM);
     RMC_FPS(0, 1); RMC_FPS(1, len);
@@ -1870,9 +1863,6 @@ struct Memb {
 #if RMC_TLC_ONEPASS
     if (one_group && !single(cand)) bag_done = true;   // (the narrowing's hashes: one group)
 #endif
-    // one message: every candidate gives it the least code the first stage found, with its one count
-    if (len == 1 && !single(cand)) bag_done = true;
-    if (defer && !bag_done && !single(cand) && len > 1) return DEFERRED;
     // (also when the narrowing already compared the whole domain: the counts loop below would
     // otherwise run over every message for candidates that map the bag to the same function)
 #ifndef RMC_TLC_GROUP_ALL
@@ -1953,9 +1943,7 @@ struct Memb {
     RMC_PROF_ADD(prof, 5, pt);
     return perm_of(__builtin_ctz(cand));   // any remaining tie: identical permuted states
   }
-  // 0 (never a fingerprint) when defer and the search was deferred (tlc_min_perm)
-  RMC_HD static u64 fingerprint_tlc(const Work& t, u64 seed, const MembRuntime& rt, unsigned long long* prof = nullptr,
-                                    bool defer = false) {
+  RMC_HD static u64 fingerprint_tlc(const Work& t, u64 seed, const MembRuntime& rt, unsigned long long* prof = nullptr) {
     unsigned long long pt = RMC_PROF_T();
     const bool ce = has_config_entries(t, rt.cfg_type);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1976,8 +1964,7 @@ struct Memb {
       if (ce && t.bag.v[q] != EMPTY && (!RMC_TLC_CFG_MASK || msg_has_config(mcode(t.bag.v[q]), rt.cfg_type))) cfgm |= 1u << q;
     }
     RMC_PROF_ADD(prof, 1, pt);
-    const u32 pi = tlc_min_perm(t, BagRef{base, stride, cfgm}, len, ce, rt.cfg_type, prof, defer);
-    if (pi == DEFERRED) return 0;
+    const u32 pi = tlc_min_perm(t, BagRef{base, stride, cfgm}, len, ce, rt.cfg_type, prof);
     pt = RMC_PROF_T();
     const u64 best = ce ? view_hash1<true>(t, pi, seed, rt.cfg_type) : view_hash1<false>(t, pi, seed, rt.cfg_type);
     RMC_PROF_ADD(prof, 6, pt);
