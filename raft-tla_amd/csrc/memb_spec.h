@@ -1863,6 +1863,8 @@ struct Memb {
 #if RMC_TLC_ONEPASS
     if (one_group && !single(cand)) bag_done = true;   // (the narrowing's hashes: one group)
 #endif
+    // one message: every candidate gives it the least code the first stage found, with its one count
+    if (len == 1 && !single(cand)) bag_done = true;
     // (also when the narrowing already compared the whole domain: the counts loop below would
     // otherwise run over every message for candidates that map the bag to the same function)
 #ifndef RMC_TLC_GROUP_ALL
