@@ -122,8 +122,8 @@ def main():
     ap.add_argument("--workers", type=int, default=0)
     ap.add_argument("--fifo-steps", type=int, default=3)
     ap.add_argument("--state-store-bytes", type=int, default=0, help="state store bytes (0 = library default)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05_c2_generate.json"))
-    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_r05_c2_generate.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05c_c2_generate.json"))
+    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_r05c_c2_generate.json"))
     ap.add_argument("--no-extra", action="store_true", help="skip the scale_workload / variants measurements")
     args = ap.parse_args()
 

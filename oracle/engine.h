@@ -284,6 +284,7 @@ inline Result bfs(const Spec& sp, const Cfg& cfg, const Options& o) {
     r.depth = frontier.empty() ? 0 : 1;
     std::vector<Succ> succs;
     int32_t level = 1;
+    const int succ_debug = std::getenv("ORACLE_SUCC_DEBUG") ? std::atoi(std::getenv("ORACLE_SUCC_DEBUG")) : 0;
     while (!frontier.empty()) {
       if (o.max_depth && level >= o.max_depth) { r.left_on_queue = (int64_t)frontier.size(); break; }
       std::vector<int64_t> nextf;
@@ -391,6 +392,8 @@ inline Result bfs(const Spec& sp, const Cfg& cfg, const Options& o) {
           goto finish;
         }
         r.generated += (int64_t)succs.size();
+        if (succ_debug && level >= succ_debug)   // (debugging aid: every parent and its successor count, stderr)
+          std::fprintf(stderr, "P\t%d\t%s\t%zu\n", (int)level, state_text(sp, cur).c_str(), succs.size());
         if (succs.empty() && o.check_deadlock) {
           r.verdict = "DEADLOCK"; build_trace(idx, -1, nullptr);
           r.left_on_queue = (int64_t)(frontier.size() - fi - 1 + nextf.size());

@@ -392,13 +392,21 @@ struct RaftMembership : Spec {
         State u = t; ReplyDirect(u, s, r, m); out.push_back({u, A_HandleCatchupResponse});
       }
     }
-    if (!succ || ((mmi == ci || mmi == mi) && mmi != ci) || !isLeader || !termEq || inCfg) {
+    // TLC's getNextStates enumerates each true disjunct of this list as a branch of its own, so the
+    // discard successor is generated once per true disjunct (:783-789; the inner disjunct
+    // `mmi = ci \/ mmi = mi` is followed by `mmi /= ci`, which only its second branch passes)
+    const int copies = (!succ) + (mmi == mi && mmi != ci) + (!isLeader) + (!termEq) + inCfg;
+    for (int q = 0; q < copies; ++q) {
       State t = s; DiscardDirect(t, s, m); out.push_back({t, A_HandleCatchupResponse});
     }
   }
   void HandleCheckOldConfig(const State& s, const V& i, const V& m, std::vector<Succ>& out) const {                  // :795-822  G6
     bool isLeader = eq(ap(s[state], i), Leader), termEq = eq(ap(m, "mterm"), ap(s[currentTerm], i));
-    if (!isLeader || termEq) { State t = s; DiscardDirect(t, s, m); out.push_back({t, A_HandleCheckOldConfig}); }
+    // :796 `state[i] /= Leader \/ m.mterm = currentTerm[i]`: TLC enumerates each true disjunct as a
+    // branch, so a non-leader receiving a current-term message generates the discard twice
+    for (int q = 0; q < (int)(!isLeader) + (int)termEq; ++q) {
+      State t = s; DiscardDirect(t, s, m); out.push_back({t, A_HandleCheckOldConfig});
+    }
     if (isLeader && termEq) {
       int64_t mci = GetMaxConfigIndex(s, i), ci = as_int(ap(s[commitIndex], i));
       if (mci <= ci) {

@@ -101,8 +101,10 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
         W t;
         const int act = S::template apply<false>(s, k, sub, t, err, a.rt);
         if (act >= 0) {
-          ++nsucc;
-          atomicAdd(&lds_cnt[act], 1u);
+          // TLC's generated counters: the copies a disjunctive guard enumerates (S::tlc_copies)
+          const int cp = (act == MA_HandleCheckOldConfig || act == MA_HandleCatchupResponse) ? S::tlc_copies(s, k, sub, a.rt) : 1;
+          nsucc += (u32)cp;
+          atomicAdd(&lds_cnt[act], (unsigned)cp);
           if (S::in_model(t, s, a.rt)) {
             if (t.bag.v[S::MK] != S::EMPTY) err |= ME_CAP;           // bag domain beyond the compiled capacity
             need = true;
@@ -440,7 +442,12 @@ __device__ __forceinline__ void stop_group(typename S::Work& s, const MembRuntim
       S::launder(s);
       W t;
       const int act = S::template apply<false>(s, k, sub, t, err, rt);
-      if (act >= 0 && (whole || S::slot_of(k, sub) <= stop_slot)) atomicAdd(&lds_cnt[act], 1u);
+      const int slot = S::slot_of(k, sub);
+      if (act >= 0 && (whole || slot <= stop_slot)) {
+        // a successor's TLC copies follow it in TLC's order: counted unless it is the event itself
+        const int cp = (act == MA_HandleCheckOldConfig || act == MA_HandleCatchupResponse) ? S::tlc_copies(s, k, sub, rt) : 1;
+        atomicAdd(&lds_cnt[act], (whole || slot < stop_slot) ? (unsigned)cp : 1u);
+      }
     }
   }
 }

@@ -803,6 +803,34 @@ struct Memb {
   }
 
   // ReceiveDirect(m) :842-863: UpdateTerm first, then the type handler's successors in disjunct order.
+  // How many times TLC's getNextStates generates the successor of instance k, sub-slot sub (>= 1 when
+  // there is one): it enumerates every true disjunct of a disjunction inside an action as a branch of
+  // its own, so a guard written as a disjunction yields the same successor once per true disjunct.
+  // In this module that happens to two discards: HandleCheckOldConfig's `state[i] /= Leader \/
+  // m.mterm = currentTerm[i]` (raft.tla:796) and HandleCatchupResponse's five-way list (:783-789).
+  // The copies are one state, so only TLC's generated counters see them (distinct states, levels and
+  // traces do not); the generic front end, which follows the text, counts them the same way.
+  RMC_HD static int tlc_copies(const Work& s, int k, int sub, const MembRuntime& rt) {
+    if (k < G_RECV || k >= G_TO) return 1;
+    const u64 ent = sel(s.bag, k - G_RECV);
+    if (ent == EMPTY) return 1;
+    const u64 m = mcode(ent);
+    const int cls = mcls(m);
+    if (cls != K_COC && cls != K_CRP) return 1;
+    const u64 dp = mdesc_packed(cls);
+    const int i = (int)fld(m, (int)(dp & 127), SB), j = (int)fld(m, (int)((dp >> 7) & 127), SB);
+    const int mt = (int)fld(m, (int)((dp >> 14) & 127), TB), ct = g_term(s, i);
+    if (sub != (mt > ct ? 1 : 0)) return 1;   // (UpdateTerm, when enabled, takes the first sub-slot)
+    const bool isLeader = g_st(s, i) == (int)L, termEq = mt == ct;
+    if (cls == K_COC) return (!isLeader || termEq) ? (int)!isLeader + (int)termEq : 1;
+    const LogV li = getlog(s, i);
+    const int mmi = (int)fld(m, O_CRP_MMI, IB), ci = g_commit(s, i), mi = g_match(s, i, j);
+    const bool succ = fld(m, O_CRP_SUC, 1);
+    const bool inCfg = (config_of<MAXLOG>(li, llen(li), rt.init_cfg, rt.cfg_type, nullptr) >> j) & 1u;
+    const bool c1 = succ && ((mmi != ci && mmi != mi) || mmi == ci) && isLeader && termEq && !inCfg;
+    if (c1) return 1;
+    return (int)!succ + (int)(mmi == mi && mmi != ci) + (int)!isLeader + (int)!termEq + (int)inCfg;
+  }
 #define RMC_EMIT(cond) if ((cond) && (idx++ == sub))
   RMC_HD static int receive(const Work& s, u64 m, int sub, Work& t, Delta& d, u32& err, const MembRuntime& rt) {
     const int cls = mcls(m);
@@ -1682,6 +1710,18 @@ struct Memb {
 #ifndef RMC_TLC_CFG_MASK
 #define RMC_TLC_CFG_MASK 1
 #endif
+// the one-pass narrowing's loop over a state's messages (RMC_TLC_QU: its unroll factor, so a lane has several LDS
+// reads of bag entries in flight instead of one per iteration)
+#ifndef RMC_TLC_QU
+#define RMC_TLC_QU 1
+#endif
+#if RMC_TLC_QU == 4
+#define RMC_QLOOP _Pragma("unroll 4")
+#elif RMC_TLC_QU == 2
+#define RMC_QLOOP _Pragma("unroll 2")
+#else
+#define RMC_QLOOP _Pragma("unroll 1")
+#endif
   // cfgm: the entries whose message carries a ConfigEntry (the only ones perm_entries changes;
   // with RMC_TLC_CFG_MASK 0 every entry of a state with config entries anywhere, as in round 4)
   struct BagRef {
@@ -1821,7 +1861,7 @@ struct Memb {
         const int p = __builtin_ctz(m);
         const u32 pi = perm_of(p);
         u64 k0 = ~0ull, k1 = ~0ull, k2 = ~0ull, h = 0;
-#pragma unroll 1
+RMC_QLOOP
         for (int q = 0; q < len; ++q) {
           const u64 e = bag[q];
           const u64 c = perm_code(mcode(e), pi, ce && bag.cfg(q), cfgt);

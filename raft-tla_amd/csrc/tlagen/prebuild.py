@@ -36,6 +36,8 @@ SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing
           ("memb_nosym_gen", "configs/raft_membership_mc.tla", "configs/memb_nosym.cfg"),
           ("memb_shipped_gen", "configs/raft_membership_mc.tla", "configs/membership_shipped.cfg"),
           ("memb_two_gen", "configs/raft_membership_mc.tla", "configs/memb_two.cfg"),
+          # C3 (BASELINE configs[2]): 4 servers, NextDynamic -- the hand path's full-size run cross-checked
+          ("memb_four_gen", "configs/raft_membership_mc.tla", "configs/memb_four.cfg"),
           # the punctuated searches: golden-trace prefix constraints, an ACTION_CONSTRAINT
           ("memb_morc_gen", "configs/raft_membership_mc.tla", "configs/scen_MajorityOfClusterRestarts_punct.cfg"),
           ("memb_cwcl_gen", "configs/raft_membership_mc.tla", "configs/scen_CommitWhenConcurrentLeaders_punct.cfg"),

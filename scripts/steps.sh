@@ -19,6 +19,7 @@ O=${1:?OUT}; shift
 mkdir -p "$O"
 export TMPDIR=/tmp
 R=$(pwd)
+pyn=0
 for step in "$@"; do
   name=${step%%=*}; arg=${step#*=}; [ "$arg" = "$step" ] && arg=""
   echo "== $step ($(date +%T))"
@@ -70,8 +71,10 @@ for l in open('$O/memb_$n.json').read().strip().splitlines():
       bash scripts/memb_prof.sh "${O#$R/}/memb_prof" "${arg:-r05}"; rc=$? ;;
     py)
       IFS=':' read -r -a a <<< "$arg"
-      timeout -k 10 900 python3 -u "${a[@]}" > "$O/py_$(basename "${a[0]}" .py).log" 2>&1
-      rc=$?; tail -3 "$O/py_$(basename "${a[0]}" .py).log" ;;
+      pyn=$((pyn + 1)); lg="$O/py_$(basename "${a[0]}" .py).log"
+      [ "$pyn" -gt 1 ] && lg="$O/py_$(basename "${a[0]}" .py)_$pyn.log"   # (later py steps: _2, _3, ...)
+      timeout -k 10 900 python3 -u "${a[@]}" > "$lg" 2>&1
+      rc=$?; tail -3 "$lg" ;;
     *) echo "unknown step $name"; rc=2 ;;
   esac
   echo "== $step rc=$rc"

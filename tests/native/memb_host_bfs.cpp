@@ -73,7 +73,7 @@ int main(int argc, char** argv) {
       // TLC (oracle) counts a state's whole successor list before checking any of them
       for (int k = 0; k < S::NI; ++k) {
         if (!S::group_enabled(k, rt.next)) continue;
-        for (int sub = 0; sub < S::nsub(k); ++sub) { W t; if (S::apply(s, k, sub, t, err, rt) >= 0) generated++; }
+        for (int sub = 0; sub < S::nsub(k); ++sub) { W t; if (S::apply(s, k, sub, t, err, rt) >= 0) generated += S::tlc_copies(s, k, sub, rt); }
       }
       for (int k = 0; k < S::NI && verdict == "OK"; ++k) {
         if (!S::group_enabled(k, rt.next)) continue;
@@ -102,6 +102,7 @@ int main(int argc, char** argv) {
               break;
             }
           }
+          gen_act[act] += S::tlc_copies(s, k, sub, rt) - 1;   // TLC's copies of it (they follow it in the list)
         }
       }
     }

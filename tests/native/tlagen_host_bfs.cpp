@@ -112,6 +112,7 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[i], "--trace")) want_trace = true;
     else if (!std::strcmp(argv[i], "--dump") && i + 1 < argc) dump_path = argv[++i];
   }
+  const int succ_debug = std::getenv("TLG_SUCC_DEBUG") ? std::atoi(std::getenv("TLG_SUCC_DEBUG")) : 0;
   static u32 words[1 << 22], hs[1 << 16];
   tlv::Ar A;
   tlv::init(A, words, 1 << 22, hs, 1 << 16);
@@ -178,6 +179,8 @@ int main(int argc, char** argv) {
       tlg::next_states(c, em);
       if (A.err) { err |= A.err; verdict = (A.err & tlv::E_OVF) ? "CAPACITY" : "EVAL_ERROR"; break; }
       generated += (long long)succ.size();
+      if (succ_debug && depth >= succ_debug)   // (debugging aid: every parent and its successor count, stderr)
+        std::fprintf(stderr, "P\t%d\t%s\t%zu\n", depth, state_text(all[frontier[fi]]).c_str(), succ.size());
       if (succ.empty() && deadlock) { verdict = "DEADLOCK"; break; }
       for (auto& s : succ) {
         if (s.cerr) { verdict = "EVAL_ERROR"; break; }
