@@ -3,7 +3,7 @@
 #   bash scripts/steps.sh OUT STEP [STEP ...]
 # Every step has its own time limit and writes under OUT; the first failing step ends the session
 # (after a GPU fault, abort, timeout or hang nothing else touches the GPU in that call).
-#   tests[=EXPR]        pytest -m gpu (optionally -k EXPR)
+#   tests[=EXPR]        pytest -m gpu -x (optionally -k EXPR); testsall[=EXPR]: without -x
 #   smoke               __graft_entry__.smoke()
 #   bench               bench.py with its defaults (the driver's line)
 #   c2[=NAME[=LIB]]     bench.py C2 only (no extras, no CPU baseline) with library LIB (default: the
@@ -24,9 +24,10 @@ for step in "$@"; do
   name=${step%%=*}; arg=${step#*=}; [ "$arg" = "$step" ] && arg=""
   echo "== $step ($(date +%T))"
   case $name in
-    tests)
+    tests|testsall)
       k=(); [ -n "$arg" ] && k=(-k "$arg")
-      timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" > "$O/pytest.log" 2>&1
+      x=(-x); [ "$name" = testsall ] && x=()   # testsall: every test, not stopping at the first failure
+      timeout -k 10 1500 python -u -m pytest tests -m gpu "${x[@]}" -v --timeout 300 --timeout-method thread "${k[@]}" > "$O/pytest.log" 2>&1
       rc=$?; tail -3 "$O/pytest.log" ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1

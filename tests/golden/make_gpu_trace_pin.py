@@ -7,6 +7,7 @@ case's "oracle_pin" and must equal the GPU's.  The trace itself is validated by 
 
     python tests/golden/make_gpu_trace_pin.py CASE [--workers T] [--sym view|tlc]
 """
+import fcntl
 import json
 import os
 import subprocess
@@ -26,10 +27,13 @@ def main():
     cmd = [build_oracle(), "bfs", "--tla", MEMB_MC, "--cfg", os.path.join(CONFIGS, case + ".cfg"), "--sym", sym,
            "--lean", "--workers", workers]
     r = json.loads(subprocess.run(cmd, stdout=subprocess.PIPE, text=True, check=True).stdout.strip().splitlines()[-1])
+    lock = open(INDEX + ".lock", "w")
+    fcntl.flock(lock, fcntl.LOCK_EX)   # the two SYMMETRY modes run side by side and finish in any order
     doc = json.load(open(INDEX))
     pin = {k: r[k] for k in KEYS}
     assert pin == {k: doc["cases"][case][k] for k in KEYS}, (pin, doc["cases"][case])
-    doc["cases"][case]["oracle_pin"] = dict(pin, sym=sym, oracle_seconds=round(r["seconds"], 1), oracle_workers=int(workers))
+    key = "oracle_pin" if sym == "view" else "oracle_pin_" + sym   # (the test runs "tlc" against oracle_pin_tlc)
+    doc["cases"][case][key] = dict(pin, sym=sym, oracle_seconds=round(r["seconds"], 1), oracle_workers=int(workers))
     json.dump(doc, open(INDEX, "w"), indent=1, sort_keys=True)
     print(case, pin)
 

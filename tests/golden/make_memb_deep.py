@@ -36,7 +36,7 @@ def main():
     fcntl.flock(lock, fcntl.LOCK_EX)   # the two modes run side by side and finish in any order
     doc = json.load(open(OUT)) if os.path.exists(OUT) else {}
     doc[case] = {k: r[k] for k in ("verdict", "violated", "generated", "distinct", "depth", "left_on_queue", "levels", "actions")}
-    doc[case].update(cfg="memb_four", sym=mode, max_depth=depth, oracle_seconds=round(r["seconds"], 1),
+    doc[case].update(cfg="memb_four", sym=mode, max_depth=depth, oracle_seconds=round(r["seconds"], 1), tlc_copies=True,
                      oracle_workers=int(workers),
                      source="oracle/engine.h bfs_lean on configs/memb_four.cfg (tests/golden/make_memb_deep.py)")
     json.dump(doc, open(OUT, "w"), indent=1, sort_keys=True)
