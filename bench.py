@@ -122,8 +122,9 @@ def main():
     ap.add_argument("--workers", type=int, default=0)
     ap.add_argument("--fifo-steps", type=int, default=3)
     ap.add_argument("--state-store-bytes", type=int, default=0, help="state store bytes (0 = library default)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05c_c2_generate.json"))
-    ap.add_argument("--valu-json", default=os.path.join(ROOT, "profiles", "valu_r05c_c2_generate.json"))
+    # committed rocprofv3 summaries of the dominant kernel (default: the one for whichever kernel dominates)
+    ap.add_argument("--traffic-json", default=None)
+    ap.add_argument("--valu-json", default=None)
     ap.add_argument("--no-extra", action="store_true", help="skip the scale_workload / variants measurements")
     args = ap.parse_args()
 
@@ -296,15 +297,21 @@ def main():
         achieved = bytes_per_launch / avg_s / 1e9
         wl_key = os.path.basename(args.config) + ("@%d" % args.max_depth if args.max_depth else "")
 
-        def pmc_summary(path):
+        # the library's kernel names -> rocprofv3's (orig_merge_probe is the fused orig_dedup_plain)
+        rocprof_name = {"orig_merge_probe": "orig_dedup_plain"}.get(kname, kname)
+        defaults = {"orig_generate": ("traffic_r05c_c2_generate.json", "valu_r05c_c2_generate.json"),
+                    "orig_merge_probe": ("traffic_r05c_c2_dedup.json", None)}.get(kname, (None, None))
+
+        def pmc_summary(path, default):
             """a committed rocprofv3 summary of this kernel on this workload, else None"""
+            path = path or (os.path.join(ROOT, "profiles", default) if default else None)
             try:
                 doc = json.load(open(path))
-            except (OSError, ValueError):
+            except (OSError, ValueError, TypeError):
                 return None
-            return doc if doc.get("kernel_name") == kname and doc.get("workload") == wl_key else None
+            return doc if doc.get("kernel_name") in (kname, rocprof_name) and doc.get("workload") == wl_key else None
 
-        tj = pmc_summary(args.traffic_json)
+        tj = pmc_summary(args.traffic_json, defaults[0])
         ded = [v for k, v in kernels.items() if k in ("orig_merge_probe", "orig_dedup")]
         ded_s = sum(v["ms"] for v in ded) / 1e3
         line = {
@@ -356,7 +363,7 @@ def main():
                                           "run by the instrumented dedup kernel (RAFTMC_COUNT_PROBES), rates over the timed runs' time"}
         # VALU issue fraction of the dominant kernel: PMC instruction count per launch from profiles/, live
         # launch time; MI355X_MICROARCH.md: 4 SIMD-32 per CU, a wave64 VALU instruction issues in 2 cycles
-        vj = pmc_summary(args.valu_json)
+        vj = pmc_summary(args.valu_json, defaults[1])
         if vj:
             line["roofline"]["valu_issue_frac"] = vj["valu_insts_per_launch"] / (avg_s * 256 * 2 * 2.4e9)
         line.update(extra)
