@@ -33,9 +33,26 @@ def one(path, frontend, depth):
     return d
 
 
+# the front end labels a successor by the defined operator it came from; the hand kernels by handler
+GROUPS = {"ReceiveDirect": ("HandleRequestVoteRequest", "DropStaleResponse", "HandleRequestVoteResponse",
+                            "HandleAppendEntriesRequest", "HandleAppendEntriesResponse", "HandleCatchupRequest",
+                            "HandleCatchupResponse", "HandleCheckOldConfig"),
+          "NextUnreliable": ("DuplicateMessage", "DropMessage")}
+
+
+def grouped(actions):
+    out = {}
+    for a, (g, d) in actions.items():
+        a = next((k for k, v in GROUPS.items() if a in v), a)
+        if g or d:
+            out[a] = [out.get(a, [0, 0])[0] + g, out.get(a, [0, 0])[1] + d]
+    return out
+
+
 for depth in [int(x) for x in sys.argv[1:]] or [14]:
     h = one(HAND, "hand", depth)
     g = one(GEN, "generated", depth)
+    h["actions"], g["actions"] = grouped(h["actions"]), grouped(g["actions"])
     keys = ("verdict", "violated", "distinct", "generated", "depth", "left", "levels", "actions", "trace_states")
     print(json.dumps({"max_depth": depth, "agree": all(h[k] == g[k] for k in keys),
                       "differ": [k for k in keys if h[k] != g[k]]}), flush=True)
