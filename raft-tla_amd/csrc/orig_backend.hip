@@ -68,14 +68,19 @@ enum {
 };
 enum { EV_NEXT_ERROR = 0, EV_DEADLOCK = 1, EV_INV_ERROR = 2, EV_VIOLATION = 3 };
 enum { OE_CAP_STORE = 0x100, OE_TABLE_FULL = 0x200 };
+// Seen-set batches and the LDS filter (round 5, profiles/r05_dedup_ab.txt r5x-r6a): 4 probes in flight
+// per thread at 50 VGPRs and a 2048-slot filter (18.4 KB of LDS) give 8 workgroups per CU, the wave
+// limit, where 8 probes at 92 VGPRs and 4096 slots (34.8 KB) gave 4: orig_dedup_plain 11.5 -> 10.4 ms
+// per C2 run although 3.5% more fingerprints get past the smaller filter (351M probes, not 339M); the
+// FIFO path 35.9 -> 34.8 ms.  16 per thread (183 VGPRs) 16.4 ms, 1024 slots 11.1 ms.
 #ifndef RMC_DEDUP_PER
-#define RMC_DEDUP_PER 8
+#define RMC_DEDUP_PER 4
 #endif
 #ifndef RMC_DEDUP_PIPE
 #define RMC_DEDUP_PIPE 0    // 1: orig_dedup_pipe (software-pipelined probes) instead of orig_dedup_plain
 #endif
 #ifndef RMC_LDS_SLOTS
-#define RMC_LDS_SLOTS 4096
+#define RMC_LDS_SLOTS 2048
 #endif
 constexpr int DEDUP_PER = RMC_DEDUP_PER;      // probes in flight per dedup thread
 constexpr int BS = 256;                       // workgroup size of every kernel (4 waves)
@@ -928,7 +933,7 @@ __global__ void __launch_bounds__(BS) orig_probe_plain(DedupArgs a) {
 }
 
 // Fused variant for TLC -workers N (what the pipeline runs): records through a first-come LDS
-// filter (lds_first: an LDS CAS claims each empty slot, 32 KB; a full window lets a record through to the
+// filter (lds_first: an LDS CAS claims each empty slot, 16 KB; a full window lets a record through to the
 // seen-set, never drop a state), the survivors probe the 8-B seen-set DEDUP_PER at a time, and
 // the new states' producers go out parent-major as in orig_probe_plain.  COUNT: also count the
 // fingerprints that reach the seen-set (ctr[K_PROBES], one atomic per workgroup) -- a separate

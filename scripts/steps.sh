@@ -8,6 +8,7 @@
 #   bench               bench.py with its defaults (the driver's line)
 #   c2[=NAME[=LIB]]     bench.py C2 only (no extras, no CPU baseline) with library LIB (default: the
 #                       in-tree build), 8 timed steps; prints ms/step, kernels, seen-set probes
+#   c2f[=NAME[=LIB]]    the C2 line and the FIFO (-workers 1) run beside it
 #   c2t=GIB             the C2 line with a GIB-GiB seen-set (--fp-table-bytes), 8 timed steps
 #   memb[=NAME[=LIB]]   scripts/memb_probe.py memb_four (C3, TLC's symmetry rule) with library LIB, twice
 #   prof                rocprofv3 --kernel-trace --stats of a short C2 bench
@@ -45,6 +46,16 @@ import json
 d = json.loads(open('$O/c2_$n.json').read().strip().splitlines()[-1])
 print('$n', round(d['ms_per_step'], 2), {k: round(v['ms'], 2) for k, v in d['kernels'].items()}, d['config']['distinct_per_run'],
       'probes', d.get('dedup_set', {}).get('probes_per_run'))" ;;
+    c2f)   # c2f[=NAME[=LIB]]: the C2 line and TLC -workers 1 (FIFO order) beside it
+      n=${arg%%=*}; lib=${arg#*=}; [ "$lib" = "$arg" ] && lib=""; n=${n:-base}
+      timeout -k 10 300 env ${lib:+RAFTMC_LIB=$lib} python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-extra --fifo-steps 3 \
+        > "$O/c2f_$n.json" 2> "$O/c2f_$n.err"
+      rc=$?
+      [ $rc -eq 0 ] && python3 -c "
+import json
+d = json.loads(open('$O/c2f_$n.json').read().strip().splitlines()[-1])
+f = d['tlc_workers_1']
+print('$n', round(d['ms_per_step'], 2), 'fifo', round(f['ms_per_step'], 2), {k: round(v, 2) for k, v in f['kernels_ms'].items()})" ;;
     c2t)
       timeout -k 10 200 python3 bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-extra --fifo-steps 0 \
         --fp-table-bytes $((arg << 30)) > "$O/c2t_$arg.json" 2> "$O/c2t_$arg.err"
