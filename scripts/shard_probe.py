@@ -3,7 +3,7 @@ per-rank cost of the sharded kernels, with the Python level loop (torch transpor
 communication at world 1) and with the library's native RCCL loop (a one-rank communicator:
 self-exchanges are device copies).  A development tool.
 
-    python scripts/shard_probe.py [CFG]
+    python scripts/shard_probe.py [CFG] [--lib LIBRAFTMC]     (--lib: an experiment build, RAFTMC_LIB)
 """
 import importlib
 import json
@@ -13,6 +13,10 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+if "--lib" in sys.argv:
+    k = sys.argv.index("--lib")
+    os.environ["RAFTMC_LIB"] = os.path.join(ROOT, sys.argv[k + 1])
+    del sys.argv[k:k + 2]
 raftmc = importlib.import_module("raft-tla_amd")
 shard = importlib.import_module("raft-tla_amd.shard")
 cfg = os.path.join(ROOT, "configs", (sys.argv[1] if len(sys.argv) > 1 else "c2") + ".cfg")
