@@ -138,7 +138,10 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
 // Phase 1: successors, constraints and TLC "generated" counts; in-model (and, for the
 // invariant check, out-of-model) cells are appended with one atomic per wave and slot.
 template <class S>
-__global__ void __launch_bounds__(BS) memb_expand(MGenArgs a) {
+#ifndef RMC_MEXP_WAVES
+#define RMC_MEXP_WAVES 1   // amdgpu_waves_per_eu hint of memb_expand (1: none; 3 spills 214 VGPRs)
+#endif
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MEXP_WAVES))) memb_expand(MGenArgs a) {
   using W = typename S::Work;
   constexpr int NWP = S::NWP;
   __shared__ unsigned int lds_cnt[MA_NACT + 1];
@@ -221,7 +224,10 @@ __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
 // Out-of-model successors: TLC still checks the invariants on them ([ext] switch (ii)); the
 // first violation / evaluation error in key order becomes the level's event.
 template <class S>
-__global__ void __launch_bounds__(BS) memb_oom_check(MGenArgs a) {
+#ifndef RMC_MOOM_WAVES
+#define RMC_MOOM_WAVES 1
+#endif
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MOOM_WAVES))) memb_oom_check(MGenArgs a) {
   using W = typename S::Work;
   constexpr int NWP = S::NWP;
   const u32 n = a.cell_count[2 * blockIdx.x + 1];

@@ -167,7 +167,8 @@ def memb_actions_as_generated(acts):
 
 @needs_tool
 @needs_ref
-@pytest.mark.parametrize("case", ["memb_nosym@13", "tlc:membership_shipped@16", "tlc:memb_two@16"])
+@pytest.mark.parametrize("case", ["memb_nosym@13", "tlc:membership_shipped@16", "tlc:memb_two@16", "tlc:memb_dynamic3@14",
+                                  "tlc:memb_four@13"])
 def test_generated_membership_matches_oracle(case):
     """The unmodified tlc_membership/raft.tla (through configs/raft_membership_mc.tla) on the generated
     path with TLC's semantics in full -- VIEW vars, SYMMETRY perms by TLC's rule (the least permuted
@@ -183,14 +184,11 @@ def test_generated_membership_matches_oracle(case):
     want = memb_actions_as_generated(g["actions"])
     got = {k: v for k, v in r["actions"].items() if v[0]}
     assert {k: v[1] for k, v in got.items()} == {k: v[1] for k, v in want.items()}   # distinct: FIFO-sensitive
-    # generated: the front end enumerates every true disjunct of an infix \/ inside an action, as
-    # TLC's getNextStates does for a disjunction, so HandleCheckOldConfig's guard
-    # `state[i] /= Leader \/ m.mterm = currentTerm[i]` (raft.tla:796) yields its Discard successor
-    # twice when both hold; the oracle evaluates that guard as one boolean.  Only that handler differs.
-    extra = r["generated"] - g["generated"]
-    assert 0 <= extra <= g["actions"]["HandleCheckOldConfig"][0]
-    assert {k: v[0] for k, v in got.items() if k != "ReceiveDirect"} == {k: v[0] for k, v in want.items() if k != "ReceiveDirect"}
-    assert got.get("ReceiveDirect", [0, 0])[0] - want.get("ReceiveDirect", [0, 0])[0] == extra
+    # generated: the front end enumerates every true disjunct of a disjunction inside an action, as
+    # TLC's getNextStates does; since round 5 the oracle emits those copies too
+    # (HandleCheckOldConfig :796, HandleCatchupResponse :783-789), so every generated count is equal
+    assert r["generated"] == g["generated"]
+    assert {k: v[0] for k, v in got.items()} == {k: v[0] for k, v in want.items()}
 
 
 @needs_tool
