@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
 // first violation / evaluation error in key order becomes the level's event.
 template <class S>
 #ifndef RMC_MOOM_WAVES
-#define RMC_MOOM_WAVES 1
+#define RMC_MOOM_WAVES 3   // memb_oom_check at 3 waves per SIMD (148 VGPRs, no spill): C3 0.88-0.92 vs 0.89-0.94 s
 #endif
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MOOM_WAVES))) memb_oom_check(MGenArgs a) {
   using W = typename S::Work;
