@@ -37,9 +37,13 @@
 extern "C" {
 #endif
 
-/* 2: mc_summary_t gained seen_set_probes and a reserved tail (a caller built against version 1
- * passes a smaller struct, so mc_open refuses version-1 opts rather than let mc_summary write past it) */
-#define RAFTMC_ABI_VERSION 2
+/* 2: mc_summary_t gained a reserved tail (a caller built against version 1 passes a smaller struct,
+ *    so mc_open refuses version-1 opts rather than let mc_summary write past it).
+ * 3: the version in mc_opts is the CALLER's: mc_default_opts is an inline wrapper in this header that
+ *    passes RAFTMC_ABI_VERSION as the caller was compiled with it to mc_opts_init (version 2's
+ *    library-side mc_default_opts stamped the library's own version, so a version-1 caller passed
+ *    mc_open's check).  Layouts are unchanged from version 2. */
+#define RAFTMC_ABI_VERSION 3
 
 /* error codes */
 #define MC_OK 0
@@ -67,6 +71,13 @@ extern "C" {
  * cleared, SYMMETRY + VIEW identify states whose VIEWs lie in one orbit (the opt-in "orbit" mode,
  * CLI -symmetry orbit: faster, fewer distinct states when histories differ).  tlc_membership only. */
 #define MC_COMPAT_SYM_TLC 0x2u
+/* TLC's getNextStates enumerates every true disjunct of a disjunctive guard inside an action as a branch
+ * of its own, so the one successor such a guard admits is GENERATED once per true disjunct
+ * (tlc_membership/raft.tla:796 HandleCheckOldConfig, :783-789 HandleCatchupResponse's discard).  Set by
+ * mc_default_opts (TLC's counters); cleared, that successor counts once.  Only generated counters (and
+ * TLC's counters at a stop point) see it: the state is the same.  raft_original has no overlapping
+ * disjuncts (no effect); the generated path follows the text and refuses the flag cleared. */
+#define MC_COMPAT_DISJUNCT_COPIES 0x4u
 
 typedef struct mc_ctx mc_ctx;
 
@@ -88,7 +99,7 @@ typedef struct mc_opts {
   uint64_t state_store_bytes; /* bytes for the per-state store (packed states + parents); 0 = auto */
   int64_t max_depth;          /* 0 = unbounded (TLC -dfid/-depth analogue for BFS)        */
   uint64_t seed;              /* fingerprint seed (0 = default)                           */
-  uint32_t tlc_compat_flags;  /* MC_COMPAT_* (default MC_COMPAT_INV_OUT_OF_MODEL | MC_COMPAT_SYM_TLC) */
+  uint32_t tlc_compat_flags;  /* MC_COMPAT_* (default INV_OUT_OF_MODEL | SYM_TLC | DISJUNCT_COPIES) */
   int32_t check_deadlock;     /* 1 = report states without successors (TLC default; -deadlock disables) */
   int32_t block_size;         /* expand kernel workgroup size (0 = 256)                   */
   int32_t same_device;        /* n_gpus > 1 only: 1 = every rank on `device` (the ranks exchange through
@@ -143,8 +154,16 @@ typedef struct mc_summary_t {
   int64_t reserved[8];        /* zero; later fields come out of this tail (the size stays)  */
 } mc_summary_t;
 
-/* Fill opts with defaults. */
-void mc_default_opts(mc_opts* o);
+/* Fill opts with defaults and stamp caller_abi_version (the RAFTMC_ABI_VERSION the caller was built
+ * against) into o->abi_version; mc_open refuses versions whose struct layouts this library does not
+ * have.  MC_E_INVALID (opts still filled) for such a version, MC_OK otherwise. */
+int mc_opts_init(mc_opts* o, int32_t caller_abi_version);
+/* Fill opts with defaults (this header's ABI version).  The library also exports a function of this
+ * name for binaries built before version 3: it leaves abi_version 0 ("unstated"), which mc_open
+ * refuses, since those callers cannot say which layout they were built with. */
+#ifndef RAFTMC_BUILDING_LIBRARY
+static inline void mc_default_opts(mc_opts* o) { (void)mc_opts_init(o, RAFTMC_ABI_VERSION); }
+#endif
 
 /* Load a spec module (.tla) and a TLC model config (.cfg); no GPU work yet. */
 int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx** out);

@@ -158,6 +158,9 @@ struct Spec {
 struct Options {
   bool inv_out_of_model = true;     // [ext] switch (ii)
   std::string sym_mode = "tlc";     // [ext] switch (iv): "tlc" | "view"
+  bool disjunct_copies = true;      // [ext] switch (vi): a successor is generated once per true disjunct
+                                    // of a disjunctive guard inside an action (TLC's getNextStates;
+                                    // tlc_membership/raft.tla:783-789, :796); false: once
   int64_t max_depth = 0;            // 0 = unbounded; depth counts init as 1
   int64_t max_states = 0;           // stop after this many distinct (sample mode)
   bool check_deadlock = false;

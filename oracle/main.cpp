@@ -66,6 +66,7 @@ int main(int argc, char** argv) {
     else if (k == "--dump") o.dump_states = nxt();
     else if (k == "--sym") o.sym_mode = nxt();
     else if (k == "--no-inv-oom") o.inv_out_of_model = false;
+    else if (k == "--no-disjunct-copies") o.disjunct_copies = false;
     else if (k == "--deadlock") o.check_deadlock = true;
     else if (k == "--golden") golden = nxt();
     else if (k == "--golden-cwcl") gc = nxt();
@@ -85,6 +86,7 @@ int main(int argc, char** argv) {
     else if (family == "apalache") sp.reset(new RaftApalache(cfg));
     else {
       auto* m = new RaftMembership(cfg);
+      m->disjunct_copies = o.disjunct_copies;
       if (!gc.empty()) m->golden_cwcl = load_golden_global(gc);
       if (!gm.empty()) m->golden_morc = load_golden_global(gm);
       sp.reset(m);

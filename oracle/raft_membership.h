@@ -27,6 +27,7 @@ struct RaftMembership : Spec {
   V RVReq, RVResp, AEReq, AEResp, CReq, CResp, COC;
   std::vector<std::string> vn;
   bool use_async = true, use_crash = false, use_unreliable = false, use_dynamic = false;
+  bool disjunct_copies = true;   // engine.h Options::disjunct_copies, [ext] switch (vi)
   std::vector<V> golden_cwcl, golden_morc;   // punctuated-search prefixes (raft.tla:1201, :1231)
 
   // Constraint bounds (raft.tla:23-30)
@@ -395,7 +396,9 @@ struct RaftMembership : Spec {
     // TLC's getNextStates enumerates each true disjunct of this list as a branch of its own, so the
     // discard successor is generated once per true disjunct (:783-789; the inner disjunct
     // `mmi = ci \/ mmi = mi` is followed by `mmi /= ci`, which only its second branch passes)
-    const int copies = (!succ) + (mmi == mi && mmi != ci) + (!isLeader) + (!termEq) + inCfg;
+    // (switch (vi) off: once)
+    int copies = (!succ) + (mmi == mi && mmi != ci) + (!isLeader) + (!termEq) + inCfg;
+    if (!disjunct_copies) copies = std::min(copies, 1);
     for (int q = 0; q < copies; ++q) {
       State t = s; DiscardDirect(t, s, m); out.push_back({t, A_HandleCatchupResponse});
     }
@@ -404,7 +407,8 @@ struct RaftMembership : Spec {
     bool isLeader = eq(ap(s[state], i), Leader), termEq = eq(ap(m, "mterm"), ap(s[currentTerm], i));
     // :796 `state[i] /= Leader \/ m.mterm = currentTerm[i]`: TLC enumerates each true disjunct as a
     // branch, so a non-leader receiving a current-term message generates the discard twice
-    for (int q = 0; q < (int)(!isLeader) + (int)termEq; ++q) {
+    const int copies = disjunct_copies ? (int)(!isLeader) + (int)termEq : (int)(!isLeader || termEq);
+    for (int q = 0; q < copies; ++q) {
       State t = s; DiscardDirect(t, s, m); out.push_back({t, A_HandleCheckOldConfig});
     }
     if (isLeader && termEq) {

@@ -20,6 +20,7 @@ struct RunOpts {
   uint64_t seed = 0;
   bool inv_out_of_model = true;
   bool sym_tlc = false;   // MC_COMPAT_SYM_TLC
+  bool disjunct_copies = true;   // MC_COMPAT_DISJUNCT_COPIES
   bool check_deadlock = false;
   int block_size = 256;
   // TLC -workers: 1 = TLC's single-worker FIFO order (order-dependent outputs — which parent of a

@@ -67,6 +67,18 @@ constexpr u64 P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full, P3 = 0x165
               P4 = 0x85EBCA77C2B2AE63ull, P5 = 0x27D4EB2F165667C5ull;
 RMC_HD u64 rotl64(u64 x, int r) { return (x << r) | (x >> (64 - r)); }
 RMC_HD u64 fmix64(u64 h) { h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32; return h; }
+// the fingerprint from the sum of the per-word terms.  RMC_FP_NOFINAL (experiment): the sum itself --
+// the final mix is a bijection, so it changes no collision, only the bits the seen-set indexes by
+template <int NW32>
+RMC_HD u64 fp_final(u64 acc, u64 seed) {
+#ifdef RMC_FP_NOFINAL
+  (void)seed;
+  const u64 h = acc;
+#else
+  const u64 h = fmix64(acc ^ seed ^ ((u64)NW32 * P4));
+#endif
+  return h ? h : 1ull;
+}
 template <int NW32>
 RMC_HD u64 fp64(const u32 (&w)[NW32], u64 seed) {
   // per 64-bit word a bijective mix keyed by its position, summed, then a final mix: equal
@@ -77,8 +89,7 @@ RMC_HD u64 fp64(const u32 (&w)[NW32], u64 seed) {
     const u64 v = (u64)w[k] | (k + 1 < NW32 ? (u64)w[k + 1] << 32 : 0ull);
     acc += fmix64(v ^ (seed + (u64)(k / 2 + 1) * P1));
   }
-  const u64 h = fmix64(acc ^ seed ^ ((u64)NW32 * P4));
-  return h ? h : 1ull;
+  return fp_final<NW32>(acc, seed);
 }
 
 // The same fingerprint, incrementally: fp64 is a sum of per-word terms, so a successor's
@@ -101,14 +112,21 @@ struct FpBase {
   }
   // fp64(w, seed) given the parent's words `base` (from which init() was computed)
   RMC_HD u64 fp(const u32 (&w)[NW32], const u32 (&base)[NW32], u64 seed) const {
+    bool changed;
+    return fp(w, base, seed, changed);
+  }
+  // ... and whether w differs from base at all (false: the successor is its parent)
+  RMC_HD u64 fp(const u32 (&w)[NW32], const u32 (&base)[NW32], u64 seed, bool& changed) const {
     u64 acc = sum;
+    changed = false;
 #pragma unroll
     for (int k = 0; k < NW64; ++k) {
       const u64 v = word(w, k);
-      if (v != word(base, k)) acc += fmix64(v ^ key(seed, k)) - term[k];
+      const bool d = v != word(base, k);
+      changed |= d;
+      if (d) acc += fmix64(v ^ key(seed, k)) - term[k];
     }
-    const u64 h = fmix64(acc ^ seed ^ ((u64)NW32 * P4));
-    return h ? h : 1ull;
+    return fp_final<NW32>(acc, seed);
   }
   // fp64 of the parent's words `base` plus d * 2^P (P a compile-time bit offset into the packed
   // state, d = +-1): the successor that changes one small field by one, where the field does not
@@ -126,8 +144,7 @@ struct FpBase {
         acc += fmix64(nhi ^ key(seed, K + 1)) - term[K + 1];
       }
     }
-    const u64 h = fmix64(acc ^ seed ^ ((u64)NW32 * P4));
-    return h ? h : 1ull;
+    return fp_final<NW32>(acc, seed);
   }
 };
 

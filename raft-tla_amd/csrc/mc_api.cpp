@@ -10,6 +10,7 @@
 #include <thread>
 #include <vector>
 
+#define RAFTMC_BUILDING_LIBRARY 1   // the header's inline mc_default_opts is for callers
 #include "../../include/raftmc.h"
 #include "backend.h"
 #include "model.h"
@@ -87,15 +88,30 @@ std::string trace_text(const mc_ctx* c, const rmc::RunResult& r) {
 
 extern "C" {
 
-void mc_default_opts(mc_opts* o) {
-  if (!o) return;
+namespace {
+bool abi_supported(int32_t v) { return v == 2 || v == RAFTMC_ABI_VERSION; }   // 2 and 3 share the layouts
+void fill_default_opts(mc_opts* o) {
   std::memset(o, 0, sizeof *o);
-  o->abi_version = RAFTMC_ABI_VERSION;
   o->n_gpus = 1;
   o->workers = 1;
-  o->tlc_compat_flags = MC_COMPAT_INV_OUT_OF_MODEL | MC_COMPAT_SYM_TLC;   // TLC's defaults: the drop-in semantics
+  o->tlc_compat_flags = MC_COMPAT_INV_OUT_OF_MODEL | MC_COMPAT_SYM_TLC | MC_COMPAT_DISJUNCT_COPIES;   // TLC's: the drop-in semantics
   o->check_deadlock = 1;
   o->block_size = 256;
+}
+}  // namespace
+
+int mc_opts_init(mc_opts* o, int32_t caller_abi_version) {
+  if (!o) return MC_E_INVALID;
+  fill_default_opts(o);
+  o->abi_version = caller_abi_version;
+  return abi_supported(caller_abi_version) ? MC_OK : MC_E_INVALID;
+}
+
+// binaries built before ABI 3 call this symbol: their layout is unknown, so the version stays 0 and
+// mc_open refuses the opts (include/raftmc.h)
+void mc_default_opts(mc_opts* o) {
+  if (!o) return;
+  fill_default_opts(o);
 }
 
 int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx** out) {
@@ -103,9 +119,9 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
   *out = nullptr;
   auto* c = new mc_ctx();
   c->tla_path = tla_path; c->cfg_path = cfg_path;
-  mc_opts d; mc_default_opts(&d);
+  mc_opts d; mc_opts_init(&d, RAFTMC_ABI_VERSION);
   if (!o) o = &d;
-  if (o->abi_version != RAFTMC_ABI_VERSION) { delete c; return MC_E_INVALID; }
+  if (!abi_supported(o->abi_version)) { delete c; return MC_E_INVALID; }
   if (o->n_gpus < 1 || o->n_gpus > 8) { delete c; return MC_E_INVALID; }
   c->n_gpus = o->n_gpus;
   c->same_device = o->same_device != 0;
@@ -116,6 +132,7 @@ int mc_open(const char* tla_path, const char* cfg_path, const mc_opts* o, mc_ctx
   c->ro.seed = o->seed;
   c->ro.inv_out_of_model = (o->tlc_compat_flags & MC_COMPAT_INV_OUT_OF_MODEL) != 0;
   c->ro.sym_tlc = (o->tlc_compat_flags & MC_COMPAT_SYM_TLC) != 0;
+  c->ro.disjunct_copies = (o->tlc_compat_flags & MC_COMPAT_DISJUNCT_COPIES) != 0;
   c->ro.check_deadlock = o->check_deadlock != 0;
   c->ro.block_size = o->block_size ? o->block_size : 256;
   c->ro.workers = o->workers;

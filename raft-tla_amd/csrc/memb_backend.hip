@@ -860,6 +860,7 @@ class MembGpu : public Backend {
     if (int rc = ensure_alloc(o, err)) return rc;
     if (int rc = prepare_prefixes(err)) return rc;
     rt_host_.sym_tlc = rt_dev_.sym_tlc = (o.sym_tlc && m_.rt.symmetry) ? 1u : 0u;
+    rt_host_.disjunct_copies = rt_dev_.disjunct_copies = o.disjunct_copies ? 1u : 0u;
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
@@ -1327,6 +1328,7 @@ class MembGpu : public Backend {
     if (int rc = ensure_alloc(so, err)) return rc;
     if (int rc = prepare_prefixes(err)) return rc;
     rt_host_.sym_tlc = rt_dev_.sym_tlc = (o.sym_tlc && m_.rt.symmetry) ? 1u : 0u;
+    rt_host_.disjunct_copies = rt_dev_.disjunct_copies = o.disjunct_copies ? 1u : 0u;
     sopts_ = o; s_rank_ = rank; s_world_ = world; s_finished_ = false; have_viol_ = false; sres_err_ = 0; sharded_ = true;
     // level records / sorted winners / newrec: lvl_cap_ entries each, plus the sort's scratch
     const u64 sb = so.state_store_bytes;

@@ -80,6 +80,7 @@ MembModel resolve_memb_model(const CfgFile& cfg) {
   else if (cfg.next == "Next") m.rt.next = MN_ASYNC | MN_CRASH | MN_UNRELIABLE;
   else if (cfg.next == "NextDynamic") m.rt.next = MN_ASYNC | MN_CRASH | MN_UNRELIABLE | MN_DYNAMIC;
   else throw CfgError(MC_E_UNSUPPORTED, "NEXT '" + cfg.next + "' is not one of the Next relations of raft.tla:909-943");
+  m.rt.disjunct_copies = 1;   // TLC's counting (MC_COMPAT_DISJUNCT_COPIES); the run's opts decide
   if (cfg.symmetry == "perms") m.rt.symmetry = 1;
   else if (!cfg.symmetry.empty()) throw CfgError(MC_E_UNSUPPORTED, "SYMMETRY must be perms (raft.tla:1281)");
   if (cfg.view != "vars")

@@ -133,6 +133,7 @@ struct MembRuntime {
   u32 plen0, plen1;
   u32 preg1_off;            // h1 bit offset of region 1's dead-binding mask
   u32 sym_tlc;              // SYMMETRY in TLC's mode (MC_COMPAT_SYM_TLC): least permuted full state, then VIEW
+  u32 disjunct_copies;      // MC_COMPAT_DISJUNCT_COPIES: TLC's generated count of a disjunctive guard (tlc_copies)
 };
 
 // ------------------------------------------------------------------ small constexpr tables
@@ -811,7 +812,7 @@ struct Memb {
   // The copies are one state, so only TLC's generated counters see them (distinct states, levels and
   // traces do not); the generic front end, which follows the text, counts them the same way.
   RMC_HD static int tlc_copies(const Work& s, int k, int sub, const MembRuntime& rt) {
-    if (k < G_RECV || k >= G_TO) return 1;
+    if (!rt.disjunct_copies || k < G_RECV || k >= G_TO) return 1;
     const u64 ent = sel(s.bag, k - G_RECV);
     if (ent == EMPTY) return 1;
     const u64 m = mcode(ent);

@@ -157,6 +157,9 @@ template <class S>
 #ifndef RMC_GEN_UCOUNT
 #define RMC_GEN_UCOUNT 0    // 1: per-action counts of the uniform-action instances aggregated per wave
 #endif
+#ifndef RMC_GEN_SELFLOOP
+#define RMC_GEN_SELFLOOP 1  // successors equal to their parent leave no record (A/B: 0)
+#endif
 #ifndef RMC_GEN_DD_LOOP
 #define RMC_GEN_DD_LOOP 0   // 1: DuplicateMessage / DropMessage through the generic loop (apply + pack), A/B only
 #endif
@@ -336,8 +339,15 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
           } else {
             S::pack(t, pw);
           }
-          if constexpr (INC) fp = fb.fp(pw, bw, a.seed);
-          else fp = fp64(pw, a.seed);
+          if constexpr (INC) {
+            // a successor equal to its parent (Restart(i) of a server already in the reset state,
+            // allLogs' = allLogs) is in the seen-set under an older key: no record, no probe
+            bool changed;
+            fp = fb.fp(pw, bw, a.seed, changed);
+            if (RMC_GEN_SELFLOOP) have = changed;
+          } else {
+            fp = fp64(pw, a.seed);
+          }
 #ifdef RMC_EXP_DOUBLE_PACKFP
           {   // cost-attribution experiment: pack + fingerprint a second time (laundered, same value)
             W t2 = t;
@@ -385,7 +395,11 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
     wcount += (u32)__popcll(mask);
   }
 #ifndef RMC_GEN_BINNED
+#ifdef RMC_EXP_NO_DD
+  if constexpr (false) {   // cost attribution only: the DuplicateMessage / DropMessage section left out
+#else
   if constexpr (KEND < S::NI) {
+#endif
     // DuplicateMessage(m) / DropMessage(m) (raft_original.tla:442-449) for bag slot q, in instance
     // order, unrolled (q is a compile-time constant): the successor is the parent (allLogs' applied)
     // with one message count +-1 — the count field is the low CNTB bits of bag entry q, at the
@@ -532,8 +546,13 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
         if constexpr (INC && RMC_GEN_PATCH) S::pack_patch(t, S::dirty_static(k), bw, pw);   // k uniform: static groups
         else S::pack(t, pw);
         u64 fp;
-        if constexpr (INC) fp = fb.fp(pw, bw, a.seed);
-        else fp = fp64(pw, a.seed);
+        if constexpr (INC) {
+          bool changed;   // AdvanceCommitIndex(i) without an advance is its parent: no record
+          fp = fb.fp(pw, bw, a.seed, changed);
+          if (RMC_GEN_SELFLOOP && !changed) continue;
+        } else {
+          fp = fp64(pw, a.seed);
+        }
         const u32 idx = atomicAdd(wcnt, 1u);
         a.rfp[wreg + idx] = fp;
         a.rkey[wreg + idx] = (unsigned short)((plane << 8) | (unsigned)k);

@@ -1,6 +1,6 @@
 // raftmc — command-line front end mirroring TLC's flags:
 //   raftmc [-config F.cfg] [-workers N] [-deadlock] [-depth D] [-device K]
-//          [-fptable BYTES] [-store BYTES] [-seed S] [-no-inv-oom] [-dump FILE] [-json]
+//          [-fptable BYTES] [-store BYTES] [-seed S] [-no-inv-oom] [-no-disjunct-copies] [-dump FILE] [-json]
 //          [-checkpoint LEVELS] [-checkpoint-file FILE] [-recover FILE] [-symmetry tlc|orbit]
 //          [-gpus N] [-countfinal] F.tla
 // (-countfinal, with -depth D and -workers N: the states at depth D are counted and checked, not
@@ -46,6 +46,7 @@ int main(int argc, char** argv) {
     else if (k == "-store") o.state_store_bytes = std::strtoull(val(), nullptr, 10);
     else if (k == "-seed") o.seed = std::strtoull(val(), nullptr, 0);
     else if (k == "-no-inv-oom") o.tlc_compat_flags &= ~MC_COMPAT_INV_OUT_OF_MODEL;
+    else if (k == "-no-disjunct-copies") o.tlc_compat_flags &= ~MC_COMPAT_DISJUNCT_COPIES;   // a disjunctive guard's successor counted once
     else if (k == "-symmetry") {   // "tlc" (default): TLC's least-permuted-state rule; "orbit": the faster orbit mode
       const std::string v = val();
       if (v == "tlc") o.tlc_compat_flags |= MC_COMPAT_SYM_TLC;

@@ -306,6 +306,10 @@ struct TlagenBackend : Backend {
       err = "checkpoint / recover are not implemented on the generated path";
       return MC_E_UNSUPPORTED;
     }
+    if (!o.disjunct_copies) {   // the generated code enumerates disjuncts as TLC does (MC_COMPAT_DISJUNCT_COPIES)
+      err = "the generated path counts TLC's disjunct copies; MC_COMPAT_DISJUNCT_COPIES cannot be cleared on it";
+      return MC_E_UNSUPPORTED;
+    }
     // TLC -workers 1: the single-worker FIFO order (two passes per level, tlagen_kernels.h); any
     // other -workers: first-come insertion, every count TLC prints is order independent, and an
     // event is searched again in FIFO order for TLC's counterexample and stop point

@@ -16,14 +16,15 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RAFTMC_LIB") or os.path.join(_HERE, "_build", "libraftmc.so")   # RAFTMC_LIB: experiment builds only
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 VERDICTS = {0: "OK", 1: "INVARIANT_VIOLATION", 2: "EVAL_ERROR", 3: "CAPACITY_OVERFLOW", 4: "DEADLOCK", 5: "DEPTH_LIMIT"}
 MC_COMPAT_INV_OUT_OF_MODEL = 0x1
 MC_COMPAT_SYM_TLC = 0x2
+MC_COMPAT_DISJUNCT_COPIES = 0x4
 
 # every symbol include/raftmc.h declares
-EXPORTS = ["mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stats", "mc_level_stats", "mc_kernel_stats",
+EXPORTS = ["mc_opts_init", "mc_default_opts", "mc_open", "mc_run", "mc_summary", "mc_action_stats", "mc_level_stats", "mc_kernel_stats",
            "mc_trace", "mc_report", "mc_dump_states", "mc_describe", "mc_exit_code", "mc_free",
            "mc_close", "mc_last_error", "mc_shard_open", "mc_shard_record_bytes", "mc_shard_frontier",
            "mc_shard_generate", "mc_shard_fill", "mc_shard_dedup", "mc_shard_materialize", "mc_shard_store",
@@ -102,6 +103,7 @@ def load_library(path=LIB_PATH):
                               "(make -C raft-tla_amd)" % (path, got, want))
     P = ctypes.c_void_p
     lib.mc_default_opts.argtypes = [ctypes.POINTER(McOpts)]
+    lib.mc_opts_init.argtypes = [ctypes.POINTER(McOpts), ctypes.c_int32]
     lib.mc_open.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(McOpts), ctypes.POINTER(P)]
     lib.mc_run.argtypes = [P]
     lib.mc_summary.argtypes = [P, ctypes.POINTER(McSummary)]
@@ -143,8 +145,9 @@ class ModelChecker:
     """One raftmc handle: mc_open on construction, mc_run in run()."""
 
     # sym_tlc: SYMMETRY as TLC applies it (the default, MC_COMPAT_SYM_TLC); False = the orbit mode
+    # disjunct_copies: TLC's generated count of a disjunctive guard (MC_COMPAT_DISJUNCT_COPIES, default)
     def __init__(self, spec, config=None, workers=1, deadlock=True, device=0, max_depth=0,
-                 fp_table_bytes=0, state_store_bytes=0, seed=0, inv_out_of_model=True, sym_tlc=True, n_gpus=1,
+                 fp_table_bytes=0, state_store_bytes=0, seed=0, inv_out_of_model=True, sym_tlc=True, disjunct_copies=True, n_gpus=1,
                  same_device=False, frontend="auto", count_final_level=False):
         """n_gpus > 1: one search over the GPUs device .. device + n_gpus - 1 (owner-partitioned
         fingerprints, one host thread per GPU inside the library, in-process RCCL); same_device: all
@@ -157,14 +160,17 @@ class ModelChecker:
         if config is None:
             config = spec[:-4] + ".cfg" if spec.endswith(".tla") else spec + ".cfg"
         o = McOpts()
-        self.lib.mc_default_opts(ctypes.byref(o))
+        # the binding's own ABI version (the header it mirrors), not the library's (include/raftmc.h)
+        if self.lib.mc_opts_init(ctypes.byref(o), ABI_VERSION):
+            raise RaftMCError(-1, "libraftmc.so does not implement ABI version %d" % ABI_VERSION)
         o.device, o.workers, o.max_depth = device, workers, max_depth
         o.n_gpus, o.same_device = n_gpus, 1 if same_device else 0
         o.frontend = {"auto": 0, "generated": 1, "hand": 2}[frontend]
         o.count_final_level = 1 if count_final_level else 0
         o.fp_table_bytes, o.state_store_bytes, o.seed = fp_table_bytes, state_store_bytes, seed
         o.check_deadlock = 1 if deadlock else 0
-        o.tlc_compat_flags = (MC_COMPAT_INV_OUT_OF_MODEL if inv_out_of_model else 0) | (MC_COMPAT_SYM_TLC if sym_tlc else 0)
+        o.tlc_compat_flags = ((MC_COMPAT_INV_OUT_OF_MODEL if inv_out_of_model else 0) | (MC_COMPAT_SYM_TLC if sym_tlc else 0) |
+                              (MC_COMPAT_DISJUNCT_COPIES if disjunct_copies else 0))
         self.h = ctypes.c_void_p()
         rc = self.lib.mc_open(spec.encode(), config.encode(), ctypes.byref(o), ctypes.byref(self.h))
         if rc:

@@ -12,7 +12,7 @@ HEADER = os.path.join(ROOT, "include", "raftmc.h")
 
 def declared_functions():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(mc_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:static inline )?(?:int|void|const char\*)\s+(mc_\w+)\s*\(", text, re.M)))
 
 
 def test_header_and_python_mirror_agree(raftmc):
@@ -58,12 +58,44 @@ def test_abi_version_mismatch_refused(raftmc):
     lib = raftmc.load_library()
     rm = __import__("importlib").import_module("raft-tla_amd.raftmc")
     o = rm.McOpts()
-    lib.mc_default_opts(ctypes.byref(o))
-    assert o.abi_version == raftmc.ABI_VERSION == 2
+    assert lib.mc_opts_init(ctypes.byref(o), raftmc.ABI_VERSION) == 0
+    assert o.abi_version == raftmc.ABI_VERSION == 3
     o.abi_version = 1
     h = ctypes.c_void_p()
     rc = lib.mc_open(ORIG_MC.encode(), os.path.join(CONFIGS, "c2.cfg").encode(), ctypes.byref(o), ctypes.byref(h))
     assert rc == -1 and not h
+
+
+def test_default_opts_path_stamps_the_callers_version(raftmc, tmp_path):
+    """the version in mc_opts is the caller's, also through the documented
+    mc_default_opts -> mc_open sequence.  A C caller compiled against include/raftmc.h gets the header's
+    version from the inline mc_default_opts and is accepted; a caller built against an older header,
+    which reaches the library's exported mc_default_opts symbol, gets version 0 and is refused; the
+    version-1 layout is refused by mc_opts_init itself.  (mc_open only parses: no GPU work.)"""
+    import ctypes
+    lib = raftmc.load_library()
+    rm = __import__("importlib").import_module("raft-tla_amd.raftmc")
+    cfg = os.path.join(CONFIGS, "c2.cfg").encode()
+    o = rm.McOpts()
+    lib.mc_default_opts(ctypes.byref(o))            # the pre-v3 symbol
+    assert o.abi_version == 0 and o.workers == 1 and o.n_gpus == 1
+    h = ctypes.c_void_p()
+    assert lib.mc_open(ORIG_MC.encode(), cfg, ctypes.byref(o), ctypes.byref(h)) == -1 and not h
+    o = rm.McOpts()
+    assert lib.mc_opts_init(ctypes.byref(o), 1) == -1 and o.abi_version == 1
+    # a C caller through the header's inline wrapper
+    src = tmp_path / "caller.c"
+    src.write_text('#include <stdio.h>\n#include "raftmc.h"\n'
+                   'int main(int argc, char** argv) {\n  mc_opts o; mc_default_opts(&o);\n  mc_ctx* c = 0;\n'
+                   '  int rc = mc_open(argv[1], argv[2], &o, &c);\n  printf("%d %d\\n", o.abi_version, rc);\n'
+                   '  if (c) mc_close(c);\n  return 0;\n}\n')
+    import subprocess
+    libdir = os.path.join(ROOT, "raft-tla_amd", "_build")
+    exe = tmp_path / "caller"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src), "-L", libdir, "-lraftmc",
+                    "-Wl,-rpath," + libdir], check=True)
+    out = subprocess.run([str(exe), ORIG_MC, os.path.join(CONFIGS, "c2.cfg")], capture_output=True, text=True, check=True)
+    assert out.stdout.split() == [str(raftmc.ABI_VERSION), "0"], out
 
 
 @pytest.mark.parametrize("spec,cfg,kw", [

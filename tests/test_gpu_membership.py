@@ -305,3 +305,19 @@ def test_c3_deep_oracle_pin(raftmc, case):
     if g.get("tlc_copies"):
         assert r.generated == g["generated"]
         assert r.actions == g["actions"]
+
+
+@pytest.mark.parametrize("mode", ["copies", "once"])
+def test_disjunct_copies_switch(raftmc, mode):
+    """MC_COMPAT_DISJUNCT_COPIES (the default) counts a disjunctive guard's successor once per true
+    disjunct as TLC's getNextStates does (raft.tla:796, :783-789); cleared, once.  Either way the GPU
+    equals the oracle's run with the same switch (tests/golden/disjunct_copies.json, NextDynamic to
+    depth 16): counts, levels and per-action generated and distinct counts."""
+    fx = json.load(open(os.path.join(GOLDEN, "disjunct_copies.json")))
+    g = fx[mode]
+    r = raftmc.check(MEMB_MC, os.path.join(CONFIGS, fx["cfg"]), max_depth=fx["max_depth"], deadlock=False,
+                     disjunct_copies=mode == "copies", **SMALL)
+    assert r.verdict in ("OK", "DEPTH_LIMIT"), r.error
+    assert (r.generated, r.distinct, r.depth, r.left_on_queue) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
+    assert [lv[0] for lv in r.levels] == g["levels"]
+    assert r.actions == {k: tuple(v) for k, v in g["actions"].items()} or r.actions == g["actions"]

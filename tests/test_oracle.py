@@ -190,3 +190,22 @@ def test_deadlock_verdict_and_no_deadlock_in_shipped_next_relations():
         r = run_oracle("bfs", MEMB_MC, os.path.join(CONFIGS, f["cfg"] + ".cfg"), "--sym", f.get("sym", "view"), "--deadlock",
                        "--max-depth", f["max_depth"])
         assert (r["verdict"], r["generated"], r["distinct"], r["actions"]) == ("OK", f["generated"], f["distinct"], f["actions"])
+
+
+def test_disjunct_copies_switch_oracle():
+    """[ext] switch (vi), TLC's disjunct copies (oracle/engine.h Options::disjunct_copies, default on,
+    --no-disjunct-copies): the committed fixture of both settings (tests/golden/make_disjunct_copies.py)
+    differs only in the GENERATED counters of the two handlers whose guards are disjunctions
+    (tlc_membership/raft.tla:796 HandleCheckOldConfig, :783-789 HandleCatchupResponse): the state space,
+    its levels and every distinct count are the same; and a live run at depth 14 shows the same shape."""
+    fx = json.load(open(os.path.join(GOLDEN, "disjunct_copies.json")))
+    a, b = fx["copies"], fx["once"]
+    copied = {"HandleCheckOldConfig", "HandleCatchupResponse"}
+    for x, y in ((a, b), (run_oracle("bfs", MEMB_MC, os.path.join(CONFIGS, fx["cfg"]), "--max-depth", 14),
+                         run_oracle("bfs", MEMB_MC, os.path.join(CONFIGS, fx["cfg"]), "--max-depth", 14, "--no-disjunct-copies"))):
+        assert (x["distinct"], x["levels"], x["depth"]) == (y["distinct"], y["levels"], y["depth"])
+        diff = {k: x["actions"][k][0] - y["actions"][k][0] for k in x["actions"]}
+        assert {k for k, v in diff.items() if v} <= copied and min(diff.values()) == 0
+        assert x["generated"] - y["generated"] == sum(diff.values()) > 0
+        assert all(x["actions"][k][1] == y["actions"][k][1] for k in x["actions"])
+    assert {k for k, v in a["actions"].items() if v[0] != b["actions"][k][0]} == copied   # both fire by depth 16
