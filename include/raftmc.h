@@ -311,6 +311,12 @@ int mc_shard_run_loopback(mc_ctx* const* ctxs, int32_t world);
  * compile time.  The Python binding compares it with the sources next to the library and refuses
  * a stale build, so a GPU run provably executes the tree it was shipped with. */
 const char* mc_source_hash(void);
+
+/* Test support: in the next sharded run (n_gpus > 1, mc_shard_run_*), rank `rank` leaves the native
+ * level loop with MC_E_STATE when the search reaches `depth` -- a rank failure at a known point, to test
+ * that its peers are released.  rank < 0 disables (the default).  Nothing else reads
+ * it, and no environment variable does: a production run cannot trigger it by accident. */
+int mc_set_fault_injection(mc_ctx* ctx, int32_t rank, int64_t depth);
 int mc_shard_layout(mc_ctx* ctx, const int64_t* frontier_counts);
 int mc_shard_select(mc_ctx* ctx, int64_t* reply_counts);
 int mc_shard_event_stats(mc_ctx* ctx, const int64_t* global_stats, int64_t* stats);

@@ -21,6 +21,9 @@ struct RunOpts {
   bool inv_out_of_model = true;
   bool sym_tlc = false;   // MC_COMPAT_SYM_TLC
   bool disjunct_copies = true;   // MC_COMPAT_DISJUNCT_COPIES
+  // mc_set_fault_injection (tests only): rank test_fail_rank leaves the sharded loop at that depth
+  int test_fail_rank = -1;
+  int64_t test_fail_depth = -1;
   bool check_deadlock = false;
   int block_size = 256;
   // TLC -workers: 1 = TLC's single-worker FIFO order (order-dependent outputs — which parent of a

@@ -58,8 +58,8 @@ RMC_HD int popc32(u32 x) {
 }
 
 // ---------------------------------------------------------------------------
-// FP64 of raftmc: xxHash64-style rounds over the packed state words (two
-// 64-bit multiplies per 8 bytes) plus the xxh64 avalanche.  The seed is fixed
+// FP64 of raftmc: a sum of xxHash64-style per-word mixes over the packed state words (two
+// 64-bit multiplies per 8 bytes, keyed by the word's position and the seed).  The seed is fixed
 // per run and recorded in the summary.  0 is the empty-slot marker of the
 // seen-set, so a fingerprint of 0 is remapped to 1 (documented bias 2^-64).
 // ---------------------------------------------------------------------------
@@ -67,22 +67,25 @@ constexpr u64 P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full, P3 = 0x165
               P4 = 0x85EBCA77C2B2AE63ull, P5 = 0x27D4EB2F165667C5ull;
 RMC_HD u64 rotl64(u64 x, int r) { return (x << r) | (x >> (64 - r)); }
 RMC_HD u64 fmix64(u64 h) { h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32; return h; }
-// the fingerprint from the sum of the per-word terms.  RMC_FP_NOFINAL (experiment): the sum itself --
-// the final mix is a bijection, so it changes no collision, only the bits the seen-set indexes by
+// the fingerprint from the sum of the per-word terms: the sum itself.  (Rounds 1-5 followed it with
+// xxh64's avalanche, fmix64(acc ^ seed ^ NW * P4): a bijection, so it changed no collision -- two states
+// collide iff their sums do -- only the bits the seen-set indexes by, and a sum of fmix64 outputs is as
+// uniform in every bit.  Dropping it saves one fmix64 per successor: orig_generate 11.67 -> 11.14 ms
+// per C2 run, round 6, profiles/r06_generate_ab.txt.)  RMC_FP_FINALMIX restores it (A/B only).
 template <int NW32>
 RMC_HD u64 fp_final(u64 acc, u64 seed) {
-#ifdef RMC_FP_NOFINAL
+#ifdef RMC_FP_FINALMIX
+  const u64 h = fmix64(acc ^ seed ^ ((u64)NW32 * P4));
+#else
   (void)seed;
   const u64 h = acc;
-#else
-  const u64 h = fmix64(acc ^ seed ^ ((u64)NW32 * P4));
 #endif
   return h ? h : 1ull;
 }
 template <int NW32>
 RMC_HD u64 fp64(const u32 (&w)[NW32], u64 seed) {
-  // per 64-bit word a bijective mix keyed by its position, summed, then a final mix: equal
-  // fingerprints need equal words or a 2^-64 coincidence of mixes
+  // per 64-bit word a bijective mix keyed by its position, summed: equal fingerprints need equal
+  // words or a 2^-64 coincidence of mixes
   u64 acc = 0;
 #pragma unroll
   for (int k = 0; k < NW32; k += 2) {

@@ -88,7 +88,7 @@ struct FifoShardLoop {
     }
     for (int k = 0; k < n; ++k) h_small[32 + NST + k] = mx[k];
     FSL_HIP(hipMemcpyAsync(d_sum, h_small + 32, 2 * NST * 8, hipMemcpyHostToDevice, s));
-    if (W > 1 && T.allreduce(d_sum, n, d_max, nmax ? n : 1, s, err)) return MC_E_NO_DEVICE;
+    if ((W > 1 || T.allreduce_at_world1()) && T.allreduce(d_sum, n, d_max, nmax ? n : 1, s, err)) return MC_E_NO_DEVICE;
     FSL_HIP(hipMemcpyAsync(h_small + 32, d_sum, 2 * NST * 8, hipMemcpyDeviceToHost, s));
     FSL_HIP(hipStreamSynchronize(s));
     for (int k = 0; k < n; ++k) h[k] = is_max && is_max[k] ? h_small[32 + NST + k] : h_small[32 + k];

@@ -219,6 +219,13 @@ int mc_set_recover(mc_ctx* c, const char* path) {
   return MC_OK;
 }
 
+int mc_set_fault_injection(mc_ctx* c, int32_t rank, int64_t depth) {
+  if (!c) return MC_E_INVALID;
+  c->ro.test_fail_rank = rank < 0 ? -1 : rank;
+  c->ro.test_fail_depth = rank < 0 ? -1 : depth;
+  return MC_OK;
+}
+
 namespace {
 // mc_opts.n_gpus > 1: the sharded BFS (owner-partitioned fingerprints) inside this
 // process, one host thread per GPU running the backend's native level loop (raft_original:
@@ -245,8 +252,8 @@ int run_multi(mc_ctx* c) {
   bool use_rccl = !c->same_device && rmc::rccl().load(err) == 0;
   if (use_rccl && (int)c->local_comms.size() != W) {
     for (ncclComm_t x : c->local_comms) if (x) (void)rmc::rccl().CommDestroy(x);
-    c->local_comms.assign(W, nullptr);
-    if (rmc::rccl().CommInitAll(c->local_comms.data(), W, dev.data()) != ncclSuccess) { c->local_comms.clear(); use_rccl = false; }
+    std::string e;   // non-blocking communicators where RCCL has them (rccl_api.h rccl_init_all)
+    if (rmc::rccl_init_all(c->local_comms, dev, e)) { c->local_comms.clear(); use_rccl = false; }
   }
   if (!use_rccl && !c->same_device) {   // loopback between devices: device copies over xGMI peer access
     for (int a = 0; a < W; ++a)
@@ -612,14 +619,21 @@ int mc_shard_run_rccl(mc_ctx* c, int32_t rank, int32_t world, const void* unique
     if (c->comm) { (void)rmc::rccl().CommDestroy(c->comm); c->comm = nullptr; }
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof id);
-    ncclResult_t r = rmc::rccl().CommInitRank(&c->comm, world, id, rank);
-    if (r != ncclSuccess) { c->comm = nullptr; c->last_error = std::string("ncclCommInitRank: ") + rmc::rccl().GetErrorString(r); return MC_E_NO_DEVICE; }
+    if (rmc::rccl_init_rank(&c->comm, world, id, rank, err)) { c->comm = nullptr; c->last_error = err; return MC_E_NO_DEVICE; }
     c->comm_rank = rank; c->comm_world = world;
     std::memcpy(c->comm_id, unique_id, sizeof(ncclUniqueId));
   }
   rmc::RcclTransport t(c->comm);
   rc = c->be->shard_run_native(t, err);
-  if (rc) { c->last_error = err; return rc; }
+  if (rc) {
+    // the loop left early (a peer's failure seen through the communicator's asynchronous error, or a
+    // local one): abort the communicator, which stops this rank's pending transfers; the next run
+    // builds a fresh one
+    (void)rmc::rccl().CommAbort(c->comm);
+    c->comm = nullptr;
+    c->last_error = err;
+    return rc;
+  }
   c->res = *c->be->shard_result();
   c->ran = true;
   c->last_error = c->res.error;

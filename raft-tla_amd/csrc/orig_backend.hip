@@ -202,6 +202,11 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
 #pragma unroll
     for (int q = 0; q < S::AW; ++q) al[q] = 0;
   }
+  // bw = the parent with allLogs' (what every successor carries); a successor whose words equal bw is
+  // the parent itself only when allLogs' = allLogs (no log of the parent is new to allLogs)
+  bool al_same = true;
+#pragma unroll
+  for (int q = 0; q < S::AW; ++q) al_same &= al[q] == s.allLogs[q];
   if constexpr (INC) {
     W b = s;
 #pragma unroll
@@ -344,7 +349,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
             // allLogs' = allLogs) is in the seen-set under an older key: no record, no probe
             bool changed;
             fp = fb.fp(pw, bw, a.seed, changed);
-            if (RMC_GEN_SELFLOOP) have = changed;
+            if (RMC_GEN_SELFLOOP) have = changed || !al_same;
           } else {
             fp = fp64(pw, a.seed);
           }
@@ -519,6 +524,9 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
     }
     u32 bw[INC ? NW : 1];
     FpBase<INC ? NW : 2> fb;
+    bool al_same = true;   // allLogs' = allLogs: a successor equal to bw is the parent (orig_generate)
+#pragma unroll
+    for (int q = 0; q < S::AW; ++q) al_same &= al[q] == s.allLogs[q];
     if constexpr (INC) {
       W b = s;
 #pragma unroll
@@ -549,7 +557,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
         if constexpr (INC) {
           bool changed;   // AdvanceCommitIndex(i) without an advance is its parent: no record
           fp = fb.fp(pw, bw, a.seed, changed);
-          if (RMC_GEN_SELFLOOP && !changed) continue;
+          if (RMC_GEN_SELFLOOP && !changed && al_same) continue;
         } else {
           fp = fp64(pw, a.seed);
         }
@@ -2773,7 +2781,7 @@ class OrigGpu : public Backend {
       h_max[3] = g[3]; h_max[4] = g[4]; h_max[5] = g[5]; h_max[6] = next_chunks;
       for (int b = 0; b < 32; ++b) h_max[8 + b] = (g[3] >> b) & 1;
       HIPCHK(hipMemcpyAsync(d_sum, h_sum, 2 * MC_SHARD_NSTAT * 8, hipMemcpyHostToDevice, stream_));
-      if (W > 1 && T.allreduce(d_sum, MC_SHARD_NSTAT, d_max, 8 + 32, stream_, err)) return MC_E_NO_DEVICE;
+      if ((W > 1 || T.allreduce_at_world1()) && T.allreduce(d_sum, MC_SHARD_NSTAT, d_max, 8 + 32, stream_, err)) return MC_E_NO_DEVICE;
       HIPCHK(hipMemcpyAsync(h_sum, d_sum, 2 * MC_SHARD_NSTAT * 8, hipMemcpyDeviceToHost, stream_));
       HIPCHK(hipStreamSynchronize(stream_));
       for (int k = 0; k < MC_SHARD_NSTAT; ++k) g[k] = h_sum[k];
@@ -2801,17 +2809,41 @@ class OrigGpu : public Backend {
     for (;;) {
       const u64 front = sh_level_count_;
       const bool last = count_last && sres_.depth + 1 >= sopts_.max_depth;
-      if (const char* inj = std::getenv("RAFTMC_TEST_SHARD_FAIL")) {   // test hook: "rank:depth" leaves the loop there
-        int fr = -1, fd = -1;
-        if (std::sscanf(inj, "%d:%d", &fr, &fd) == 2 && fr == me && (int64_t)fd == sres_.depth) {
-          err = "injected failure (RAFTMC_TEST_SHARD_FAIL) at depth " + std::to_string(fd);
-          return MC_E_STATE;
-        }
+      if (sopts_.test_fail_rank == me && sopts_.test_fail_depth == sres_.depth) {   // mc_set_fault_injection (tests)
+        err = "injected failure (mc_set_fault_injection) at depth " + std::to_string(sres_.depth);
+        return MC_E_STATE;
       }
       for (int64_t c = 0; c < nchunks; ++c) {
         const u64 begin = std::min<u64>((u64)c * chunk, front);
         const u64 count = std::min<u64>(chunk, front - begin);
         sh_chunk_begin_ = sh_level_begin_ + begin; sh_chunk_count_ = count;
+        if (W == 1) {
+          // World 1: every fingerprint is this rank's, so the route pass, both counts exchanges (the
+          // chunk's two host synchronisations) and the acknowledged re-derivation collapse into the
+          // single-GPU -workers N kernels: orig_dedup_plain's first-come LDS filter is the route's, its
+          // probes the owner's, orig_materialize_plain stores the new states behind the level; the
+          // counts stay on the device (orig_advance), the host waits once per level
+          if (count == 0) continue;
+          const GenArgs g = gen_args(sh_chunk_begin_, count, sh_chunk_begin_, sres_.seed, sopts_);
+          const unsigned nblk = (unsigned)((count + BS - 1) / BS);
+          HIPCHK(hipMemsetAsync(d_ctr_ + K_LEAD, 0, 8, stream_));
+          NAT_TIMED(0, launch_generate(g, nblk));
+          sres_.kernels[0].algo_bytes += (double)count * NWP * 4;
+          DedupArgs d;
+          d.rfp = d_rfp_; d.rkey = d_rkey_; d.rcnt = d_rcnt_blk_; d.region = (u64)BS * S::NI; d.gid0 = sh_chunk_begin_;
+          d.urec = (ulonglong2*)d_urec_; d.ucnt = d_ucnt_;
+          d.table = d_table_; d.table_mask = sh_table_mask(); d.newpos = d_newrec_; d.ctr = (unsigned long long*)d_ctr_;
+          d.prof = 0;
+          NAT_TIMED(2, hipLaunchKernelGGL((orig_dedup_plain<WW, false>), dim3(nblk), dim3(BS), 0, stream_, d));
+          MatPlainArgs m;
+          m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.base = 0; m.dst_base = sh_next_write_;
+          m.cap = cap_; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.store = last ? 0u : 1u;
+          NAT_TIMED(3, hipLaunchKernelGGL((orig_materialize_plain<S>), dim3((unsigned)std::min<u64>(4096, (count * 2 + BS - 1) / BS)),
+                                          dim3(BS), 0, stream_, m));
+          hipLaunchKernelGGL(orig_advance, dim3(1), dim3(64), 0, stream_, (unsigned long long*)d_ctr_);
+          HIPCHK(hipGetLastError());
+          continue;
+        }
         HIPCHK(hipMemsetAsync(d_rcnt_, 0, 16 * 8, stream_));
         if (count > 0) {
           const GenArgs g = gen_args(sh_chunk_begin_, count, sh_chunk_begin_, sres_.seed, sopts_);
@@ -2916,8 +2948,18 @@ class OrigGpu : public Backend {
       }
       HIPCHK(hipStreamSynchronize(stream_));
       harvest();
+      if (W == 1) {   // the level's new states (orig_advance's running count), stored behind the level
+        u64 lvl_new = 0;
+        HIPCHK(hipMemcpy(&lvl_new, d_ctr_ + K_LEVEL_NEW, 8, hipMemcpyDeviceToHost));
+        sh_new_ = lvl_new;
+        if (!last) sh_next_write_ += lvl_new;
+      }
       int64_t g[MC_SHARD_NSTAT];
       if (int rc = shard_level_stats(g, err)) return rc;
+      if (W == 1) {   // SURVEY.md §8(d) bytes of the fused kernels (the W > 1 ones count per exchange)
+        sres_.kernels[2].algo_bytes += (double)g[2] * (10 + 8) + (double)sh_new_ * (16 + 8);
+        sres_.kernels[3].algo_bytes += (double)sh_new_ * (2.0 * NWP * 4 + 8);
+      }
       int64_t next_chunks = 0;
       if (int rc = allreduce_level(g, rounds(sh_new_), next_chunks)) return rc;
       if (last) unstored_ = sh_new_;   // this rank's share of the final level: counted, not in the store

@@ -30,16 +30,19 @@ struct ShardTransport {
   virtual int exchange(int me, int W, const char* const* src, const uint64_t* sbytes, char* const* dst,
                        const uint64_t* rbytes, hipStream_t s, std::string& err) = 0;
   virtual int allreduce(int64_t* d_sum, int n_sum, int64_t* d_max, int n_max, hipStream_t s, std::string& err) = 0;
+  virtual bool allreduce_at_world1() const { return false; }   // run allreduce() with one rank too
 };
 
 // Abort coordination of the in-process multi-GPU run (mc_api.cpp run_multi): the ranks' RcclTransports
-// share one RcclAbort.  Every RCCL call of a rank is bracketed by its `busy` flag, raised BEFORE the
-// `aborted` flag is read (both sequentially consistent), so the aborting thread either sees the rank
-// inside a call and waits for it to leave, or the rank sees `aborted` and returns an error without
-// touching its communicator.  Only then is the communicator aborted (ncclCommAbort frees it and stops
-// its pending kernels, which releases a peer blocked in a stream synchronisation on them): no rank
-// uses a freed communicator.  A rank blocked inside an RCCL call for longer than the grace period
-// (a connection setup waiting for the failed peer) is aborted anyway: that call cannot return otherwise.
+// share one RcclAbort.  The communicators are non-blocking (rccl_api.h rccl_init_all): no RCCL call
+// blocks its thread, a rank waits for its exchanges by polling (RcclTransport::complete) and sees
+// `aborted` between two polls.  Every RCCL call of a rank is bracketed by its `busy` flag, raised BEFORE
+// the `aborted` flag is read (both sequentially consistent), so the aborting thread either sees the
+// rank inside a call (which returns at once) and waits for it to leave, or the rank sees `aborted` and
+// returns an error without touching its communicator.  Only then is the communicator aborted
+// (ncclCommAbort frees it and stops its pending kernels): no rank uses a freed communicator.  (With
+// an RCCL without non-blocking communicators the calls block; a rank still inside one after the grace
+// period is aborted anyway, as that call cannot return otherwise.)
 struct RcclAbort {
   explicit RcclAbort(int w) : busy(w) { for (auto& b : busy) b.store(false); }
   std::vector<std::atomic<bool>> busy;   // [rank] inside an RCCL call
@@ -55,20 +58,27 @@ struct RcclAbort {
     std::lock_guard<std::mutex> lk(mu);
     if (done) return;
     done = true;
+    const int grace_ms = rccl().nonblocking() ? 60000 : 5000;   // non-blocking: calls return at once
     for (size_t r = 0; r < comms.size(); ++r) {
-      for (int spin = 0; busy[r].load() && spin < 5000; ++spin) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      for (int spin = 0; busy[r].load() && spin < grace_ms; ++spin) std::this_thread::sleep_for(std::chrono::milliseconds(1));
       if (comms[r]) (void)rccl().CommAbort(comms[r]);
       comms[r] = nullptr;                // freed by the abort: never destroyed again
     }
   }
 };
 
-// RCCL over xGMI: grouped ncclSend/ncclRecv straight between the kernels' buffers
+// RCCL over xGMI: grouped ncclSend/ncclRecv straight between the kernels' buffers.  Each call
+// returns once its transfers are done: the group is polled out of ncclInProgress (non-blocking
+// communicator), an event recorded behind it on the stream is polled to completion, and between polls
+// the communicator's asynchronous error (a peer's failure) and the in-process abort flag are checked
+// -- so a rank never waits in a stream synchronisation on a transfer a failed peer will not serve.
 struct RcclTransport : ShardTransport {
   ncclComm_t comm;
   RcclAbort* ab;   // the in-process run's abort coordination (nullptr: one rank per process)
   int rank;
+  hipEvent_t done_ev = nullptr;
   explicit RcclTransport(ncclComm_t c, RcclAbort* a = nullptr, int r = 0) : comm(c), ab(a), rank(r) {}
+  ~RcclTransport() override { if (done_ev) (void)hipEventDestroy(done_ev); }
   // raise busy, then check aborted (see RcclAbort); false = aborted, the call must not run
   bool enter(std::string& err) {
     if (!ab) return true;
@@ -77,6 +87,43 @@ struct RcclTransport : ShardTransport {
     return true;
   }
   void leave() { if (ab) ab->busy[rank].store(false); }
+  bool stopped() const { return ab && ab->aborted.load(); }
+  // the group just ended: wait for it to be enqueued and then to finish on the stream
+  int complete(hipStream_t s, const char* what, std::string& err) {
+    RcclApi& R = rccl();
+    if (!R.nonblocking()) return 0;   // blocking communicator: the caller's stream synchronisation waits
+    for (;;) {   // out of ncclInProgress: the group's work is on the stream
+      if (!enter(err)) return -5;
+      ncclResult_t st = ncclSuccess;
+      const ncclResult_t r = R.CommGetAsyncError(comm, &st);
+      leave();
+      if (r != ncclSuccess || (st != ncclSuccess && st != ncclInProgress)) {
+        err = std::string(what) + ": " + R.GetErrorString(r != ncclSuccess ? r : st);
+        return -5;
+      }
+      if (st == ncclSuccess) break;
+      std::this_thread::yield();
+    }
+    if (!done_ev && hipEventCreateWithFlags(&done_ev, hipEventDisableTiming) != hipSuccess) { err = std::string(what) + ": hipEventCreate"; return -5; }
+    if (hipEventRecord(done_ev, s) != hipSuccess) { err = std::string(what) + ": hipEventRecord"; return -5; }
+    for (unsigned spin = 0;; ++spin) {
+      const hipError_t q = hipEventQuery(done_ev);
+      if (q == hipSuccess) return 0;
+      if (q != hipErrorNotReady) { err = std::string(what) + ": " + hipGetErrorString(q); return -5; }
+      if (stopped()) { err = std::string(what) + ": another rank left the loop (communicators aborted)"; return -5; }
+      if ((spin & 1023) == 1023) {   // now and then: has a peer failed?
+        if (!enter(err)) return -5;
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t r = R.CommGetAsyncError(comm, &st);
+        leave();
+        if (r != ncclSuccess || (st != ncclSuccess && st != ncclInProgress)) {
+          err = std::string(what) + ": " + R.GetErrorString(r != ncclSuccess ? r : st);
+          return -5;
+        }
+      }
+      std::this_thread::yield();
+    }
+  }
   int exchange(int me, int W, const char* const* src, const uint64_t* sbytes, char* const* dst, const uint64_t* rbytes,
                hipStream_t s, std::string& err) override {
     RcclApi& R = rccl();
@@ -88,21 +135,26 @@ struct RcclTransport : ShardTransport {
       if (sbytes[p]) r = R.Send(src[p], sbytes[p], ncclUint8, p, comm, s);
       if (r == ncclSuccess && rbytes[p]) r = R.Recv(dst[p], rbytes[p], ncclUint8, p, comm, s);
     }
-    const ncclResult_t r2 = R.GroupEnd();
+    ncclResult_t r2 = R.GroupEnd();
     leave();
+    if (r2 == ncclInProgress) r2 = ncclSuccess;   // non-blocking: complete() waits
     if (r != ncclSuccess || r2 != ncclSuccess) { err = std::string("RCCL exchange: ") + R.GetErrorString(r != ncclSuccess ? r : r2); return -5; }
-    return 0;
+    return complete(s, "RCCL exchange", err);
   }
+  // also at world 1 (a one-rank all-reduce): the mc_shard_run_rccl path runs its communicator, the
+  // non-blocking group and the completion polling at every level on a one-GPU machine too
+  bool allreduce_at_world1() const override { return true; }
   int allreduce(int64_t* d_sum, int n_sum, int64_t* d_max, int n_max, hipStream_t s, std::string& err) override {
     RcclApi& R = rccl();
     if (!enter(err)) return -5;
     ncclResult_t r = R.GroupStart();
     if (r == ncclSuccess) r = R.AllReduce(d_sum, d_sum, n_sum, ncclInt64, ncclSum, comm, s);
     if (r == ncclSuccess) r = R.AllReduce(d_max, d_max, n_max, ncclInt64, ncclMax, comm, s);
-    const ncclResult_t r2 = R.GroupEnd();
+    ncclResult_t r2 = R.GroupEnd();
     leave();
+    if (r2 == ncclInProgress) r2 = ncclSuccess;
     if (r != ncclSuccess || r2 != ncclSuccess) { err = std::string("RCCL all-reduce: ") + R.GetErrorString(r != ncclSuccess ? r : r2); return -5; }
-    return 0;
+    return complete(s, "RCCL all-reduce", err);
   }
 };
 

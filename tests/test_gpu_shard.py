@@ -419,21 +419,21 @@ def test_native_loop_store_overflow(raftmc):
     assert out[0].distinct == sum(lv[0] for lv in out[0].levels) < 54426066
 
 
-def test_n_gpus_rank_failure_releases_peers(raftmc, monkeypatch):
+def test_n_gpus_rank_failure_releases_peers(raftmc):
     """A rank that leaves the native loop early (here an injected failure of rank 1 at depth 5,
-    RAFTMC_TEST_SHARD_FAIL) releases its peers instead of leaving them in the next collective: mc_run
+    mc_set_fault_injection) releases its peers instead of leaving them in the next collective: mc_run
     returns the failing rank's error, naming it, within seconds; the same handle then runs the model to
     completion (fresh communicators on a node: the aborted ones are never reused)."""
     cfg = os.path.join(CONFIGS, "c2.cfg")
     kw = dict(workers=0, fp_table_bytes=2 << 30, state_store_bytes=2 << 30)
     with raftmc.ModelChecker(ORIG_MC, cfg, n_gpus=2, same_device=torch.cuda.device_count() < 2, **kw) as mc:
-        monkeypatch.setenv("RAFTMC_TEST_SHARD_FAIL", "1:5")
+        mc.set_fault_injection(1, 5)
         t0 = time.time()
         with pytest.raises(raftmc.RaftMCError) as e:
             mc.run()
         assert time.time() - t0 < 60
         assert "rank 1" in str(e.value) and "injected failure" in str(e.value), str(e.value)
-        monkeypatch.delenv("RAFTMC_TEST_SHARD_FAIL")
+        mc.set_fault_injection(-1, 0)
         r = mc.run()
     g = json.load(open(os.path.join(GOLDEN, "c2_exact.json")))
     assert (r.verdict, r.generated, r.distinct, r.depth) == ("OK", g["generated"], g["distinct"], g["depth"]), r.error
