@@ -71,16 +71,11 @@ RMC_HD u64 fmix64(u64 h) { h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h 
 // xxh64's avalanche, fmix64(acc ^ seed ^ NW * P4): a bijection, so it changed no collision -- two states
 // collide iff their sums do -- only the bits the seen-set indexes by, and a sum of fmix64 outputs is as
 // uniform in every bit.  Dropping it saves one fmix64 per successor: orig_generate 11.67 -> 11.14 ms
-// per C2 run, round 6, profiles/r06_generate_ab.txt.)  RMC_FP_FINALMIX restores it (A/B only).
+// per C2 run, round 6, profiles/r06_generate_ab.txt.)
 template <int NW32>
 RMC_HD u64 fp_final(u64 acc, u64 seed) {
-#ifdef RMC_FP_FINALMIX
-  const u64 h = fmix64(acc ^ seed ^ ((u64)NW32 * P4));
-#else
   (void)seed;
-  const u64 h = acc;
-#endif
-  return h ? h : 1ull;
+  return acc ? acc : 1ull;
 }
 template <int NW32>
 RMC_HD u64 fp64(const u32 (&w)[NW32], u64 seed) {

@@ -401,14 +401,7 @@ struct Orig {
       return OA_Timeout;
     }
     k -= N;
-    if (k < N * N) {                                               // RequestVote(i, j) :189-198
-      const int i = k / N, j = k % N;
-      if (g_st(s, i) != C) return -1;
-      if ((row_bits(s.vresp, i) >> j) & 1u) return -1;
-      const u32 li = sel(s.log, i);
-      with_msg(t.bag, m_rvq(g_term(s, i), last_term(li), llen(li), i, j), err);
-      return OA_RequestVote;
-    }
+    if (k < N * N) return request_vote(s, k / N, k % N, t, err);   // RequestVote(i, j) :189-198
     k -= N * N;
     if (k < N) {                                                   // BecomeLeader(i) :228-242
       const int i = k;
@@ -489,6 +482,16 @@ struct Orig {
       bag_add_at(t.bag, k, -1, err);                               // WithoutMessage (G1)
       return OA_DropMessage;
     }
+  }
+
+  // RequestVote(i, j) (raft_original.tla:189-198) into t (= s on entry); i, j may differ per lane
+  // (orig_generate's per-lane RequestVote section)
+  RMC_HD static int request_vote(const Work& s, int i, int j, Work& t, u32& err) {
+    if (g_st(s, i) != C) return -1;
+    if ((row_bits(s.vresp, i) >> j) & 1u) return -1;
+    const u32 li = sel(s.log, i);
+    with_msg(t.bag, m_rvq(g_term(s, i), last_term(li), llen(li), i, j), err);
+    return OA_RequestVote;
   }
 
   // the evoterLog field of an election record from voterLog[i]'s row (see ECOMPACT)

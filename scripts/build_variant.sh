@@ -2,6 +2,8 @@
 # Experiment builds (C2 shape only): raft-tla_amd/_build_var/NAME/libraftmc.so with extra -D flags.
 #   scripts/build_variant.sh NAME "-DRMC_DEDUP_PER=8 -DRMC_LDS_SLOTS=2048"
 # Select one at run time with RAFTMC_LIB=raft-tla_amd/_build_var/NAME/libraftmc.so.
+# The rejected experiment switches live in scripts/variants/orig_backend_experiments.hip (third argument):
+#   scripts/build_variant.sh binned "-DRMC_GEN_BINNED" scripts/variants/orig_backend_experiments.hip
 set -e
 NAME=$1; DEFS=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)

@@ -1,3 +1,12 @@
+// ARCHIVE of experiments (not built by the product; round 6 hygiene): raft-tla_amd/csrc/orig_backend.hip
+// as it stood in round 6 before its rejected experiment switches were removed -- every RMC_* switch
+// below (RMC_GEN_BINNED, RMC_GEN_PATCH, RMC_GEN_UCOUNT, RMC_GEN_WAVE_COUNTS, RMC_GEN_DD_LOOP,
+// RMC_EXP_DOUBLE_*, RMC_EXP_SKIP_*, RMC_EXP_NO_DD, RMC_DBG_*, RMC_LDS_PLAIN, RMC_DEDUP_PIPE, ...) and the
+// kernels orig_dedup_pipe / orig_dedup_queue / orig_merge_plain / orig_probe_plain, with the measurements
+// that rejected them in DESIGN.md §4a/§5 and profiles/r0*_*_ab.txt.  Build one for an A/B against the
+// product's headers:
+//   scripts/build_variant.sh NAME "-DRMC_GEN_BINNED" scripts/variants/orig_backend_experiments.hip
+// (RMC_GEN_RVC=1, RMC_GEN_SELFLOOP=1 and no RMC_FP_FINALMIX are what the product adopted.)
 // raftmc — gfx950 BFS backend for thirdparty/raft_original.tla.
 //
 // TLC's single-worker FIFO order, reproduced on a data-parallel GPU.  Every successor has the
@@ -73,9 +82,18 @@ enum { OE_CAP_STORE = 0x100, OE_TABLE_FULL = 0x200 };
 // limit, where 8 probes at 92 VGPRs and 4096 slots (34.8 KB) gave 4: orig_dedup_plain 11.5 -> 10.4 ms
 // per C2 run although 3.5% more fingerprints get past the smaller filter (351M probes, not 339M); the
 // FIFO path 35.9 -> 34.8 ms.  16 per thread (183 VGPRs) 16.4 ms, 1024 slots 11.1 ms.
-constexpr int DEDUP_PER = 4;                  // probes in flight per dedup thread
+#ifndef RMC_DEDUP_PER
+#define RMC_DEDUP_PER 4
+#endif
+#ifndef RMC_DEDUP_PIPE
+#define RMC_DEDUP_PIPE 0    // 1: orig_dedup_pipe (software-pipelined probes) instead of orig_dedup_plain
+#endif
+#ifndef RMC_LDS_SLOTS
+#define RMC_LDS_SLOTS 2048
+#endif
+constexpr int DEDUP_PER = RMC_DEDUP_PER;      // probes in flight per dedup thread
 constexpr int BS = 256;                       // workgroup size of every kernel (4 waves)
-constexpr int LDS_FP_SLOTS = 2048;            // workgroup-local fingerprint set (8 B fp + 4 B key per slot)
+constexpr int LDS_FP_SLOTS = RMC_LDS_SLOTS;   // workgroup-local fingerprint set (8 B fp + 4 B key per slot)
 constexpr int MAT_CAP = 2048;      // winners staged in LDS per materialize round
 constexpr int SCAN_BS = 1024;      // orig_scan workgroup
 
@@ -105,26 +123,59 @@ struct GenArgs {
   u32* lead;                   // [chunk] parents with leader work (chunk index | 1 << 31 if no other successor)
 };
 
-// One lane per frontier state; successor, constraints, TLC generated counts, out-of-model invariants,
-// canonical pack and FP64 in one pass.  (A split expand + full-lane fingerprint pipeline measured
-// 51.4 vs 49.4 ms/run on C2: apply, not the pack + hash, dominates this spec.)  Three sections:
-//  * RequestVote(i, j): each lane's enabled instances one per trip (per-lane instance);
-//  * a wave-uniform loop over the other instances (Restart, Timeout, Receive; the leader instances
-//    [LEAD_LO, LEAD_HI) are orig_generate_lead's): k is a scalar, so the instance decode and the bag
-//    slot selects are scalar work;
-//  * DuplicateMessage / DropMessage unrolled per bag slot, without apply or pack.
-// In-model successors leave as compacted records: per instance a wave ballot and consecutive stores
-// into the wave's own region (only ~21% of C2's instance slots carry an in-model successor).
-// Rejected designs (measured on MI355X; scripts/variants/orig_backend_experiments.hip builds them):
-// instances binned by family for every family (19.5 vs 14.5 ms, round 4: a per-lane instance turns
-// apply's whole dispatch into vector work), patch packing from the parent's words (14.45 vs 13.37 ms,
-// round 5), per-wave aggregated action counts (+1.3 ms, round 2), DuplicateMessage / DropMessage
-// through apply (13.37 -> 14.71 ms).
-// 4 waves per SIMD (<= 128 VGPRs, no spill): 11.7 vs 13.4 ms per C2 run at 3 (round 5); 5 spills.
-// Larger states (C5: 24 words) get no hint and keep the plain hash (the base terms would cost them
-// occupancy: 45 vs 38 ms of expand time for C5 to depth 12).
+#if defined(RMC_EXP_DOUBLE_PACKFP) || defined(RMC_EXP_DOUBLE_APPLY)
+// opaque redefinition of a Work's registers (cost-attribution experiments only)
 template <class S>
-__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 15 ? 4 : 1))) orig_generate(GenArgs a) {
+__device__ __forceinline__ void exp_launder(typename S::Work& s) {
+  asm volatile("" : "+v"(s.term), "+v"(s.st), "+v"(s.voted), "+v"(s.commit), "+v"(s.vresp), "+v"(s.vgrant));
+#pragma unroll
+  for (int i = 0; i < S::N; ++i) asm volatile("" : "+v"(s.nexti.v[i]), "+v"(s.matchi.v[i]), "+v"(s.log.v[i]), "+v"(s.vl.v[i]));
+#pragma unroll
+  for (int q = 0; q < S::AW; ++q) asm volatile("" : "+v"(s.allLogs[q]));
+#pragma unroll
+  for (int q = 0; q < S::EMAX; ++q) asm volatile("" : "+v"(s.el[q]));
+#pragma unroll
+  for (int q = 0; q < S::MK + 1; ++q) asm volatile("" : "+v"(s.bag.v[q]));
+}
+#endif
+
+// One lane per frontier state, a wave-uniform loop over the action instances; successor,
+// constraints, TLC generated counts, out-of-model invariants, canonical pack and FP64 in one
+// pass.  (A split expand + full-lane fingerprint pipeline measured 51.4 vs 49.4 ms/run on C2:
+// apply, not the pack + hash, dominates this spec.  Unrolling the ~50-instance loop is refused
+// by the compiler at this body size.)  In-model successors leave as compacted records: per
+// instance a wave ballot, one LDS atomic per wave for the base, and consecutive stores
+// (only ~21% of C2's instance slots carry an in-model successor).
+template <class S>
+// 4 waves per SIMD (<= 128 VGPRs, no spill since the Dup/Drop section stopped going through apply):
+// 11.7 vs 13.4 ms of orig_generate per C2 run at 3 (round 5, profiles/r05_generate_ab.txt; round 2
+// measured 3 at 19.9 vs 22.3 ms without the hint); 5 spills.  Larger states (C5: 24 words) get no hint.
+#ifndef RMC_GEN_WAVES
+#define RMC_GEN_WAVES 4
+#endif
+#ifndef RMC_GEN_INC
+#define RMC_GEN_INC 1
+#endif
+#ifndef RMC_GEN_PATCH
+// in-model successors packed by patching the parent's words (S::pack_patch) instead of a whole pack:
+// 1 = every instance (Receive: the wave's union of changed groups, one ballot per group), 2 = only the
+// instances whose changed groups are static (Receive packs whole), 0 = whole packs (the default:
+// round 5 measured mode 1 at 14.45 vs 13.37 ms of orig_generate per C2 run, profiles/r05_generate_ab.txt)
+#define RMC_GEN_PATCH 0
+#endif
+#ifndef RMC_GEN_UCOUNT
+#define RMC_GEN_UCOUNT 0    // 1: per-action counts of the uniform-action instances aggregated per wave
+#endif
+#ifndef RMC_GEN_RVC
+#define RMC_GEN_RVC 0       // 1: RequestVote instances per lane (the RequestVote section below)
+#endif
+#ifndef RMC_GEN_SELFLOOP
+#define RMC_GEN_SELFLOOP 1  // successors equal to their parent leave no record (A/B: 0)
+#endif
+#ifndef RMC_GEN_DD_LOOP
+#define RMC_GEN_DD_LOOP 0   // 1: DuplicateMessage / DropMessage through the generic loop (apply + pack), A/B only
+#endif
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 15 ? RMC_GEN_WAVES : 1))) orig_generate(GenArgs a) {
   using W = typename S::Work;
   constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
   __shared__ unsigned int lds_cnt[OA_NACT + 1];   // per-action generated, in-model total
@@ -146,7 +197,9 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
   unsigned long long ev = ~0ull;
   // the parent's packed words with allLogs' (every successor carries allLogs \cup {log[i]},
   // raft_original.tla:464) and their fingerprint terms: successors re-hash changed words only
-  constexpr bool INC = NW <= 16;
+  // (C5-sized states keep the plain hash: the base terms would cost them occupancy, measured
+  // 45 vs 38 ms of expand time for C5 to depth 12)
+  constexpr bool INC = RMC_GEN_INC && NW <= 16;
   u32 bw[INC ? NW : 1];
   FpBase<INC ? NW : 2> fb;
   if (active) {
@@ -173,43 +226,17 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
     S::pack(b, bw);
     fb.init(bw, a.seed);
   }
-  // an in-model successor t (allLogs' applied): its fingerprint, and whether it leaves a record -- a
-  // successor equal to its parent (Restart(i) of a server already in the reset state, allLogs' =
-  // allLogs) is in the seen-set under an older key: no record, no probe (C2: 351M -> 313M seen-set
-  // probes per run, round 6)
-  auto fingerprint = [&](const W& t, u64& fp) -> bool {
-    u32 pw[NW];
-    S::pack(t, pw);
-    if constexpr (INC) {
-      bool changed;
-      fp = fb.fp(pw, bw, a.seed, changed);
-      return changed || !al_same;
-    } else {
-      fp = fp64(pw, a.seed);
-      return true;
-    }
-  };
-  // this wave's in-model successors of one trip into its record region (one ballot, consecutive stores)
-  auto append = [&](bool have, u64 fp, int k) {
-    const u64 mask = __ballot(have);
-    if (have) {
-      const u32 idx = wcount + __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
-      rfp[idx] = fp;
-      rkey[idx] = (unsigned short)((threadIdx.x << 8) | (unsigned)k);
-    }
-    wcount += (u32)__popcll(mask);
-  };
   // leader work (S::leader_work: a Leader or a Candidate with a quorum, ~1% of C2's states) is
   // left to orig_generate_lead, which runs those instances on full waves of just such parents: here
   // a wave with one leader lane would pay all of [LEAD_LO, LEAD_HI) for it (measured: a third of
   // this kernel's time for 0.7% of C2's successors)
   const bool lead = active && S::leader_work(s);
-  {
+  if constexpr (RMC_GEN_RVC != 0) {
     // RequestVote(i, j) [2N, 2N + N*N) (raft_original.tla:189-198): each lane's enabled instances one
     // per trip (S::request_vote_mask), so the wave runs as often as its busiest lane has RequestVote
     // instances instead of N*N times (C2: 6.3 trips per wave against 9, tests/native/orig_host_bfs.cpp
-    // WAVE=64 "rv_waves"; orig_generate 11.1 -> 9.8 ms per run, round 6).  The handler is one short
-    // function of (i, j) (S::request_vote), so a per-lane instance costs a few VALU ops here.
+    // WAVE=64 "rv_waves").  The handler is one short function of (i, j) (S::request_vote), so a per-lane
+    // instance costs a few VALU ops here, unlike the whole apply dispatch (RMC_GEN_BINNED).
     u32 rvm = active ? S::request_vote_mask(s) : 0u;
 #pragma unroll 1
     while (__ballot(rvm != 0u)) {
@@ -229,24 +256,104 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
           atomicAdd(&lds_cnt[act], 1u);
           if (S::in_model(t, a.rt)) {
             ++nin;
-            have = fingerprint(t, fp);
+            u32 pw[NW];
+            S::pack(t, pw);
+            if constexpr (INC) {
+              bool changed;
+              fp = fb.fp(pw, bw, a.seed, changed);
+              have = changed || !al_same;
+            } else {
+              fp = fp64(pw, a.seed);
+              have = true;
+            }
+          } else if (a.inv_oom && S::violated(t, a.rt.invariants & S::inv_frame(OA_RequestVote))) {
+            const u64 e = ev_word(gid, (u32)k, EV_VIOLATION);   // (RequestVote writes only the bag: no invariant reads it)
+            ev = e < ev ? e : ev;
           }
-          // out of the model: RequestVote writes only the bag, which no invariant reads (S::inv_frame)
         }
       }
-      append(have, fp, k);
+      const u64 mask = __ballot(have);
+      if (have) {
+        const u32 idx = wcount + __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
+        rfp[idx] = fp;
+        rkey[idx] = (unsigned short)((threadIdx.x << 8) | (unsigned)k);
+      }
+      wcount += (u32)__popcll(mask);
     }
   }
+#ifndef RMC_GEN_BINNED
+  // A wave-uniform loop over the instances: k is a scalar, so the instance decode and the bag slot
+  // selects are scalar work, and the successor's pack + fingerprint + record append run once per
+  // slot for all lanes.  (RMC_GEN_BINNED below bins each lane's enabled instances by family
+  // instead -- SURVEY.md §7 hard part 8 -- and measured 19.5 vs 14.5 ms of orig_generate per C2 run
+  // on MI355X, round 4: the per-lane instance index turns the decode and selects into vector work
+  // and the saved iterations do not pay for it.)
   // DuplicateMessage / DropMessage [I_DUP, NI) change one message count and nothing else: with the
   // incremental fingerprint they are the unrolled section after this loop (no apply, no pack)
-  constexpr int KEND = INC ? S::I_DUP : S::NI;
+  constexpr int KEND = (INC && !RMC_GEN_DD_LOOP) ? S::I_DUP : S::NI;
 #pragma unroll 1
   for (int kk = 0; kk < KEND; ++kk) {
-    if (kk == 2 * S::N) kk = S::LEAD_HI;   // RequestVote: the section above; leader work: orig_generate_lead
-    const int k = kk;                      // wave-uniform
-    const bool on = active;
+    if (RMC_GEN_RVC != 0 && kk == 2 * S::N) kk = S::LEAD_LO;   // RequestVote: the per-lane section above
+#ifndef RMC_DBG_NO_SKIP
+    if (kk == S::LEAD_LO) kk = S::LEAD_HI;      // wave-uniform
+#endif
+#ifdef RMC_EXP_SKIP_HI
+    if (kk >= RMC_EXP_SKIP_LO && kk < RMC_EXP_SKIP_HI) continue;   // cost-attribution experiment only
+#endif
+    const int k = kk;
+#else
+  // Experiment (see above): instances binned by family (SURVEY.md §7 hard part 8): the lane's enabled instances of one
+  // family, one per iteration, every lane at once -- the lanes of an iteration share one handler,
+  // and the wave iterates as often as its busiest lane has instances of the family instead of once
+  // per instance slot.  Families: Restart, Timeout, RequestVote, Receive per message class
+  // (UpdateTerm, then one handler per message type), DuplicateMessage/DropMessage (those out of the
+  // model counted at once, below).  Successor records carry their instance, so the order they are
+  // produced in is immaterial (the seen-set keeps minimum keys, events are minima over keys).
+  constexpr int NFAM = 4 + S::RECV_CLASSES;
+  u32 fm_to = 0, fm_rv = 0, fm_dd = 0, fm_rc[S::RECV_CLASSES];
+#pragma unroll
+  for (int c = 0; c < S::RECV_CLASSES; ++c) fm_rc[c] = 0u;
+  if (active) {
+    fm_to = S::timeout_mask(s);
+    fm_rv = S::request_vote_mask(s);
+#pragma unroll
+    for (int q = 0; q < S::MK; ++q) {
+      const int cls = S::recv_class(s, q);
+#pragma unroll
+      for (int c = 0; c < S::RECV_CLASSES; ++c) fm_rc[c] |= (cls == c ? 1u : 0u) << q;
+    }
+    u32 ndup = 0, ndrop = 0;
+#pragma unroll
+    for (int q = 0; q < 2 * S::MK; ++q) {
+      if (s.bag.v[q < S::MK ? q : q - S::MK] == S::BEMPTY) continue;
+      if (S::quick_out_of_model(s, S::I_DUP + q, a.rt) >= 0) { if (q < S::MK) ++ndup; else ++ndrop; }
+      else fm_dd |= 1u << q;
+    }
+    nsucc += ndup + ndrop;
+    if (ndup) atomicAdd(&lds_cnt[OA_DuplicateMessage], ndup);
+    if (ndrop) atomicAdd(&lds_cnt[OA_DropMessage], ndrop);
+  }
+  // family f (wave-uniform): this lane's mask and the family's first instance
+  auto fam_mask = [&](int f) -> u32 {
+    u32 m = f == 0 ? (active ? (u32)lomask(S::N) : 0u) : f == 1 ? fm_to : f == 2 ? fm_rv : f == NFAM - 1 ? fm_dd : 0u;
+#pragma unroll
+    for (int c = 0; c < S::RECV_CLASSES; ++c) m = f == 3 + c ? fm_rc[c] : m;
+    return m;
+  };
+  auto fam_base = [&](int f) -> int { return f == 0 ? 0 : f == 1 ? S::N : f == 2 ? 2 * S::N : f == NFAM - 1 ? S::I_DUP : S::I_RECV; };
+  int fam = 0;
+  u32 fmask = fam_mask(0);
+#pragma unroll 1
+  for (;;) {
+    while (fam < NFAM && !__ballot(fmask != 0u)) { ++fam; fmask = fam < NFAM ? fam_mask(fam) : 0u; }   // wave-uniform
+    if (fam == NFAM) break;
+    int k = -1;   // none for this lane in this iteration (it still takes part in the wave's ballots)
+    if (fmask) { k = fam_base(fam) + __builtin_ctz(fmask); fmask &= fmask - 1u; }
+#endif
+    const bool on = active && k >= 0;
     u64 fp = 0;
     bool have = false;
+    int cnt_act = -1;   // this lane's successor action (RMC_GEN_WAVE_COUNTS: counted per wave)
     const int qa = on ? S::quick_out_of_model(s, k, a.rt) : -1;
     if (qa >= 0) {      // generated, out of the model, no invariant to check: counted only
       ++nsucc;
@@ -254,14 +361,71 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
     } else if (on) {
       W t;
       const int act = S::apply(s, k, t, err);
+#ifdef RMC_EXP_DOUBLE_APPLY
+#ifdef RMC_EXP_DOUBLE_HI
+      if (k >= RMC_EXP_DOUBLE_LO && k < RMC_EXP_DOUBLE_HI)   // only the instances [LO, HI)
+#endif
+      {   // cost-attribution experiment: apply a second time on a laundered copy (same result)
+        W s2 = s, t2;
+        exp_launder<S>(s2);
+        u32 e2 = 0;
+        if (S::apply(s2, k, t2, e2) != act) err |= e2 | 1u;
+      }
+#endif
       if (act >= 0) {
 #pragma unroll
         for (int q = 0; q < S::AW; ++q) t.allLogs[q] = al[q];
         ++nsucc;
-        atomicAdd(&lds_cnt[act], 1u);
+#ifdef RMC_GEN_WAVE_COUNTS
+        cnt_act = act;
+#else
+        // instances before Receive have one action for every state (Restart, Timeout, RequestVote):
+        // counted per wave below, one LDS atomic instead of 64 conflicting ones
+        if (RMC_GEN_UCOUNT && k < S::I_RECV) cnt_act = act;
+        else atomicAdd(&lds_cnt[act], 1u);
+#endif
         if (S::in_model(t, a.rt)) {
           ++nin;
-          have = fingerprint(t, fp);
+          have = true;
+          u32 pw[NW];
+          if constexpr (INC && RMC_GEN_PATCH) {
+            // the parent's words with the groups the action changed re-inserted (S::pack_patch): the
+            // groups are known from the wave-uniform instance, except for Receive, whose handler depends
+            // on the message: there the union over the wave's in-model successors (one ballot per group)
+            u32 du = S::dirty_static(k);
+            if (du != ~0u) {
+              S::pack_patch(t, du, bw, pw);
+            } else if (RMC_GEN_PATCH == 1) {
+              const u32 d = S::dirty_of(s, t);
+              du = 0;
+#pragma unroll
+              for (int g = 0; g < S::NPG; ++g) du |= __ballot((d >> g) & 1u) ? 1u << g : 0u;
+              S::pack_patch(t, __builtin_amdgcn_readfirstlane(du), bw, pw);
+            } else {
+              S::pack(t, pw);
+            }
+          } else {
+            S::pack(t, pw);
+          }
+          if constexpr (INC) {
+            // a successor equal to its parent (Restart(i) of a server already in the reset state,
+            // allLogs' = allLogs) is in the seen-set under an older key: no record, no probe
+            bool changed;
+            fp = fb.fp(pw, bw, a.seed, changed);
+            if (RMC_GEN_SELFLOOP) have = changed || !al_same;
+          } else {
+            fp = fp64(pw, a.seed);
+          }
+#ifdef RMC_EXP_DOUBLE_PACKFP
+          {   // cost-attribution experiment: pack + fingerprint a second time (laundered, same value)
+            W t2 = t;
+            exp_launder<S>(t2);
+            u32 pw2[NW];
+            S::pack(t2, pw2);
+            const u64 fp2 = INC ? fb.fp(pw2, bw, a.seed) : fp64(pw2, a.seed);
+            if (fp2 != fp) fp = 0;
+          }
+#endif
         } else if (a.inv_oom && S::violated(t, a.rt.invariants & S::inv_frame(act))) {
           // TLC checks invariants on out-of-model successors ([ext] switch (ii)); first in key order wins
           // (only those the action can change: the parent satisfies all of them, S::inv_frame)
@@ -270,9 +434,40 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
         }
       }
     }
-    append(have, fp, k);
+#ifdef RMC_GEN_WAVE_COUNTS
+    {   // per-action generated counts: one LDS atomic per wave when its lanes agree on the action
+      const u64 am = __ballot(cnt_act >= 0);
+      if (am) {
+        const int first = __ffsll((unsigned long long)am) - 1;
+        const int a0 = __shfl(cnt_act, first);
+        if (__ballot(cnt_act == a0) == am) { if (lane == first) atomicAdd(&lds_cnt[a0], (unsigned)__popcll(am)); }
+        else if (cnt_act >= 0) atomicAdd(&lds_cnt[cnt_act], 1u);
+      }
+    }
+#else
+    if (RMC_GEN_UCOUNT && k < S::I_RECV) {   // wave-uniform branch: one action for every lane
+      const u64 am = __ballot(cnt_act >= 0);
+      if (am) {
+        const int first = __ffsll((unsigned long long)am) - 1;
+        const int a0 = __shfl(cnt_act, first);
+        if (lane == first) atomicAdd(&lds_cnt[a0], (unsigned)__popcll(am));
+      }
+    }
+#endif
+    const u64 mask = __ballot(have);
+    if (have) {
+      const u32 idx = wcount + __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
+      rfp[idx] = fp;
+      rkey[idx] = (unsigned short)((threadIdx.x << 8) | (unsigned)k);
+    }
+    wcount += (u32)__popcll(mask);
   }
+#ifndef RMC_GEN_BINNED
+#ifdef RMC_EXP_NO_DD
+  if constexpr (false) {   // cost attribution only: the DuplicateMessage / DropMessage section left out
+#else
   if constexpr (KEND < S::NI) {
+#endif
     // DuplicateMessage(m) / DropMessage(m) (raft_original.tla:442-449) for bag slot q, in instance
     // order, unrolled (q is a compile-time constant): the successor is the parent (allLogs' applied)
     // with one message count +-1 — the count field is the low CNTB bits of bag entry q, at the
@@ -312,13 +507,21 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
         if (om && lane == __ffsll((unsigned long long)om) - 1)
           atomicAdd(&lds_cnt[dup ? OA_DuplicateMessage : OA_DropMessage], (unsigned)__popcll(om));
       }
-      append(have, fp, k);
+      const u64 mask = __ballot(have);
+      if (have) {
+        const u32 idx = wcount + __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u));
+        rfp[idx] = fp;
+        rkey[idx] = (unsigned short)((threadIdx.x << 8) | (unsigned)k);
+      }
+      wcount += (u32)__popcll(mask);
     });
   }
+#endif
   if (active) {
     if (err & OE_EVAL_LOG_INDEX) { const u64 e = ev_word(gid, 0, EV_NEXT_ERROR); ev = e < ev ? e : ev; }
     if (nsucc == 0 && a.deadlock && !lead) { const u64 e = ev_word(gid, 0, EV_DEADLOCK); ev = e < ev ? e : ev; }
   }
+#ifndef RMC_DBG_NO_PUSH
   {   // leader-work parents to the chunk's list: one global atomic per wave
     const u64 lm = __ballot(lead);
     if (lm) {
@@ -329,6 +532,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
       if (lead) a.lead[base + (u32)__popcll(lm & ((1ull << lane) - 1ull))] = (u32)tid | (nsucc == 0 ? 0x80000000u : 0u);
     }
   }
+#endif
   const u32 cap_err = err & ~(u32)OE_EVAL_LOG_INDEX;   // compiled-capacity limits, not TLC semantics
   if (cap_err) {
     atomicOr(&a.ctr[K_ERR], (unsigned long long)cap_err);
@@ -350,14 +554,14 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
 // record order inside a region is immaterial: the FIFO merge keeps the minimum key, the -workers N
 // filter decides by key).
 template <class S>
-__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 15 ? 4 : 1))) orig_generate_lead(GenArgs a) {
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <= 15 ? RMC_GEN_WAVES : 1))) orig_generate_lead(GenArgs a) {
   using W = typename S::Work;
   constexpr int NW = S::NW, NWP = (S::NW + 3) & ~3;
   __shared__ unsigned int lds_cnt[OA_NACT + 1];
   for (int t = threadIdx.x; t < OA_NACT + 1; t += BS) lds_cnt[t] = 0;
   __syncthreads();
   const u64 n = a.ctr[K_LEAD];
-  constexpr bool INC = NW <= 16;
+  constexpr bool INC = RMC_GEN_INC && NW <= 16;
   u32 err = 0, nin = 0;
   unsigned long long ev = ~0ull;
   // grid-stride with a wave-uniform trip count (every lane of a wave runs the same instance loop)
@@ -410,12 +614,13 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
       if (S::in_model(t, a.rt)) {
         ++nin;
         u32 pw[NW];
-        S::pack(t, pw);
+        if constexpr (INC && RMC_GEN_PATCH) S::pack_patch(t, S::dirty_static(k), bw, pw);   // k uniform: static groups
+        else S::pack(t, pw);
         u64 fp;
         if constexpr (INC) {
           bool changed;   // AdvanceCommitIndex(i) without an advance is its parent: no record
           fp = fb.fp(pw, bw, a.seed, changed);
-          if (!changed && al_same) continue;
+          if (RMC_GEN_SELFLOOP && !changed && al_same) continue;
         } else {
           fp = fp64(pw, a.seed);
         }
@@ -460,25 +665,31 @@ struct WaveRegions {
 
 // Workgroup-local first-come fingerprint filter: answers only "certainly produced here before"
 // (a full probe window lets the record through: the seen-set decides).  An empty slot is claimed
-// by LDS CAS, so the set is exact up to the window: with plain stores (the round-4
-// form, scripts/variants/orig_backend_experiments.hip RMC_LDS_PLAIN) two lanes inserting different fingerprints into one slot at once left one of them out of
+// by LDS CAS, so the set is exact up to the window: with plain stores (RMC_LDS_PLAIN, the round-4
+// form) two lanes inserting different fingerprints into one slot at once left one of them out of
 // the set, and two lanes with the same fingerprint both passed.  Measured on C2 (round 5,
 // profiles/r05_dedup_ab.txt): 339.5M seen-set probes per run instead of 367.0M, orig_dedup_plain
 // 11.30 vs 11.51 ms; a 16-slot window changed nothing (366.5M: overflow is not the leak) and an
 // 8192-slot set (64 KB) cost occupancy (14.96 ms).
-constexpr int LDS_WIN = 8;   // probe window of the LDS filter
+#ifndef RMC_LDS_WIN
+#define RMC_LDS_WIN 8
+#endif
 template <int SLOTS = LDS_FP_SLOTS>
 __device__ __forceinline__ bool lds_first(unsigned long long* set, u64 fp) {
   u32 h = (u32)(fp >> 20) & (SLOTS - 1);
 #pragma unroll 1
-  for (int p = 0; p < LDS_WIN; ++p) {
+  for (int p = 0; p < RMC_LDS_WIN; ++p) {
     unsigned long long cur = set[h];
     if (cur == fp) return false;            // produced here before
+#ifndef RMC_LDS_PLAIN
     if (cur == 0ull) {                      // claim the slot; a lane that loses the race looks at the winner's fp
       cur = atomicCAS(&set[h], 0ull, (unsigned long long)fp);
       if (cur == 0ull) return true;
       if (cur == fp) return false;
     }
+#else
+    if (cur == 0ull) { set[h] = fp; return true; }
+#endif
     h = (h + 1) & (SLOTS - 1);
   }
   return true;                              // window full: let the seen-set decide
@@ -698,10 +909,124 @@ __global__ void __launch_bounds__(BS) orig_probe(DedupArgs a) {
 // TLC's own workers).  8-B seen-set entries, first-come LDS filter, no keys, no winner pass: the
 // inserting thread numbers its new state directly.
 
+// workgroup b: generate-workgroup b's records through an exact LDS set (CAS); the first record of
+// each fingerprint (and every record whose probe window is full) is written compacted as
+// (fp, global key) to the workgroup's region
+__global__ void __launch_bounds__(BS) orig_merge_plain(DedupArgs a) {
+  __shared__ unsigned long long lfp[LDS_FP_SLOTS];
+  __shared__ u32 out_cnt;
+  for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lfp[t] = 0ull;
+  if (threadIdx.x == 0) out_cnt = 0;
+  __syncthreads();
+  const WaveRegions wr(a.rcnt + 4 * blockIdx.x, a.region / 4);
+  const u32 n = wr.n;
+  const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
+  const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
+  ulonglong2* out = a.urec + (u64)blockIdx.x * a.region;
+  const int lane = __lane_id();
+  constexpr int P1 = 8;
+#pragma unroll 1
+  for (u32 i0 = 0; i0 < n; i0 += P1 * BS) {
+    u64 fp[P1];
+    u32 lk[P1];
+#pragma unroll
+    for (int j = 0; j < P1; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      const u64 at = wr.at(i);
+      fp[j] = i < n ? fps[at] : 0ull;
+      lk[j] = i < n ? (u32)keys[at] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < P1; ++j) {
+      bool keep = false;
+      if (fp[j]) {
+        keep = true;                                   // window full: keep (the seen-set decides)
+        u32 h = (u32)(fp[j] >> 20) & (LDS_FP_SLOTS - 1);
+#pragma unroll 1
+        for (int p = 0; p < 8; ++p) {
+          unsigned long long c = lfp[h];
+          if (c == 0ull) c = atomicCAS(&lfp[h], 0ull, (unsigned long long)fp[j]);
+          if (c == 0ull) break;                        // first here
+          if (c == fp[j]) { keep = false; break; }     // produced here before
+          h = (h + 1) & (LDS_FP_SLOTS - 1);
+        }
+      }
+      const u64 m = __ballot(keep);
+      if (m) {
+        const int leader = __ffsll((unsigned long long)m) - 1;
+        u32 base = 0;
+        if (lane == leader) base = atomicAdd(&out_cnt, (u32)__popcll(m));
+        base = __shfl(base, leader);
+        if (keep)
+          out[base + (u32)__popcll(m & ((1ull << lane) - 1ull))] =
+              make_ulonglong2((unsigned long long)fp[j], (unsigned long long)~nkey_of(a.gid0, blockIdx.x, lk[j]));
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) a.ucnt[blockIdx.x] = out_cnt;
+}
+
+// workgroup b probes the 8-B seen-set once per record of region b (DEDUP_PER in flight per
+// thread); the new states' producers are marked in an LDS (parent, instance) mask and written in
+// parent-major, instance order (one global atomic per workgroup): the next level keeps siblings
+// adjacent, so its diamonds land in one workgroup again and its waves hold similar states
+template <int WW, bool COUNT>
+__global__ void __launch_bounds__(BS) orig_probe_plain(DedupArgs a) {
+  __shared__ u32 wave_tot[BS / 64];
+  __shared__ unsigned long long base_sh;
+  __shared__ unsigned long long win[BS * WW];
+  for (int t = threadIdx.x; t < BS * WW; t += BS) win[t] = 0ull;
+  __syncthreads();
+  const u32 n = a.ucnt[blockIdx.x];
+  const ulonglong2* in = a.urec + (u64)blockIdx.x * a.region;
+  const u64 pgid0 = a.gid0 + (u64)blockIdx.x * BS;   // global id of this workgroup's first parent
+  u32 err = 0;
+  if (COUNT && threadIdx.x == 0 && n) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)n);
+#pragma unroll 1
+  for (u32 i0 = 0; i0 < n; i0 += DEDUP_PER * BS) {
+    u64 fp[DEDUP_PER], key[DEDUP_PER], pos[DEDUP_PER];
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      const ulonglong2 r = i < n ? in[i] : make_ulonglong2(0ull, 0ull);
+      fp[j] = r.x; key[j] = r.y;
+    }
+    const u32 ins = probe_batch<DEDUP_PER, false, 1>(a.table, a.table_mask, fp, key, pos, err);
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j)
+      if ((ins >> j) & 1u) {
+        const u32 p = (u32)((key[j] >> 8) - pgid0), k = (u32)(key[j] & 255);
+        atomicOr(&win[p * WW + (k >> 6)], 1ull << (k & 63));
+      }
+  }
+  __syncthreads();
+  u64 wm[WW];
+  u32 mine = 0;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) { wm[q] = win[threadIdx.x * WW + q]; mine += (u32)__popcll(wm[q]); }
+  u32 total = 0;
+  const u32 off = block_excl_scan(mine, wave_tot, &total);
+  if (threadIdx.x == 0) base_sh = total ? atomicAdd(&a.ctr[K_CHUNK_NEW], (unsigned long long)total) : 0ull;
+  __syncthreads();
+  u64 o = base_sh + off;
+  const u64 pg = pgid0 + threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) {
+    u64 m = wm[q];
+    while (m) {
+      const int k = q * 64 + __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      a.newpos[o++] = (pg << 8) | (u64)k;
+    }
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+}
+
 // Fused variant for TLC -workers N (what the pipeline runs): records through a first-come LDS
 // filter (lds_first: an LDS CAS claims each empty slot, 16 KB; a full window lets a record through to the
 // seen-set, never drop a state), the survivors probe the 8-B seen-set DEDUP_PER at a time, and
-// the new states' producers go out parent-major (an LDS winner mask per parent).  COUNT: also count the
+// the new states' producers go out parent-major as in orig_probe_plain.  COUNT: also count the
 // fingerprints that reach the seen-set (ctr[K_PROBES], one atomic per workgroup) -- a separate
 // instantiation, because even one extra same-address atomic per wave costs ~3 ms of C2's
 // 11 ms here (round 4, measured), so timed runs leave it off (RAFTMC_COUNT_PROBES).
@@ -738,6 +1063,13 @@ __global__ void __launch_bounds__(BS) orig_dedup_plain(DedupArgs a) {
       for (int j = 0; j < DEDUP_PER; ++j) probes += fp[j] ? 1u : 0u;
     }
     const u32 ins = probe_batch<DEDUP_PER, false, 1>(a.table, a.table_mask, fp, key, pos, err);
+#ifdef RMC_EXP_DOUBLE_PROBE
+    {   // cost attribution only: the same probes again (now all present: lookups, no CAS)
+      u64 pos2[DEDUP_PER];
+      u32 e2 = 0;
+      if (probe_batch<DEDUP_PER, false, 1>(a.table, a.table_mask, fp, key, pos2, e2)) err |= OE_TABLE_FULL;
+    }
+#endif
 #pragma unroll
     for (int j = 0; j < DEDUP_PER; ++j)
       if ((ins >> j) & 1u) atomicOr(&win[(key[j] >> 8) * WW + ((key[j] & 255) >> 6)], 1ull << (key[j] & 63));
@@ -758,6 +1090,238 @@ __global__ void __launch_bounds__(BS) orig_dedup_plain(DedupArgs a) {
       if (t) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)t);
     }
   }
+  u64 wm[WW];
+  u32 mine = 0;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) { wm[q] = win[threadIdx.x * WW + q]; mine += (u32)__popcll(wm[q]); }
+  u32 total = 0;
+  const u32 off = block_excl_scan(mine, wave_tot, &total);
+  if (threadIdx.x == 0) base_sh = total ? atomicAdd(&a.ctr[K_CHUNK_NEW], (unsigned long long)total) : 0ull;
+  __syncthreads();
+  u64 o = base_sh + off;
+  const u64 pg = a.gid0 + (u64)blockIdx.x * BS + threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) {
+    u64 m = wm[q];
+    while (m) {
+      const int k = q * 64 + __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      a.newpos[o++] = (pg << 8) | (u64)k;
+    }
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+}
+
+// The same kernel software-pipelined (RMC_DEDUP_PIPE): a wave's seen-set probes of batch t are in
+// flight while it loads and LDS-filters batch t + 1.  Vector-memory loads complete in issue order
+// (one vmcnt counter), so the order of issue is what lets them overlap: per iteration the record
+// loads of batch t + 2 are issued BEFORE the probes of batch t + 1, and waiting for those records
+// (older) does not wait for the probes (newer).
+//   prologue: records 0; filter 0; records 1; probes 0
+//   iteration t: filter t + 1 (its records arrived) | finish probes t (compare, CAS the empty slots,
+//                walk the rare collisions, mark winners) | records t + 2; probes t + 1
+template <int WW, bool COUNT>
+__global__ void __launch_bounds__(BS) orig_dedup_pipe(DedupArgs a) {
+  constexpr int P = DEDUP_PER;
+  __shared__ unsigned long long lfp[LDS_FP_SLOTS];
+  __shared__ u32 wave_tot[BS / 64];
+  __shared__ unsigned long long base_sh;
+  __shared__ unsigned long long win[BS * WW];
+  for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lfp[t] = 0ull;
+  for (int t = threadIdx.x; t < BS * WW; t += BS) win[t] = 0ull;
+  __syncthreads();
+  const WaveRegions wr(a.rcnt + 4 * blockIdx.x, a.region / 4);
+  const u32 n = wr.n;
+  const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
+  const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
+  const u64* table = a.table;
+  const u64 mask = a.table_mask;
+  u32 err = 0;
+  u32 probes = 0;
+  auto load_records = [&](u32 i0, u64 (&fp)[P], u64 (&key)[P]) {
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      const u64 at = wr.at(i);
+      fp[j] = i < n ? fps[at] : 0ull;
+      key[j] = i < n ? (u64)keys[at] : 0ull;
+    }
+  };
+  auto filter = [&](u64 (&fp)[P]) {
+#pragma unroll
+    for (int j = 0; j < P; ++j)
+      if (fp[j] && !lds_first(lfp, fp[j])) fp[j] = 0ull;
+    if constexpr (COUNT) {
+#pragma unroll
+      for (int j = 0; j < P; ++j) probes += fp[j] ? 1u : 0u;
+    }
+  };
+  auto issue = [&](const u64 (&fp)[P], u64 (&cur)[P]) {
+#pragma unroll
+    for (int j = 0; j < P; ++j) cur[j] = fp[j] ? table[fp[j] & mask] : ~0ull;
+  };
+  // probe_batch's second half over pre-loaded first slots (8-B entries, no keys)
+  auto finish = [&](const u64 (&fp)[P], const u64 (&key)[P], u64 (&cur)[P]) {
+    u32 ins = 0, done = 0;
+    u64 pos[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      pos[j] = fp[j] & mask;
+      if (fp[j] && cur[j] == 0ull) {
+        cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[pos[j]], 0ull, (unsigned long long)fp[j]);
+        if (cur[j] == 0ull) { ins |= 1u << j; done |= 1u << j; }
+      }
+      if (!fp[j] || cur[j] == fp[j]) done |= 1u << j;
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      if ((done >> j) & 1u) continue;
+      u64 slot = (pos[j] + 1) & mask;
+      for (u64 probe = 0;; ++probe) {
+        if (probe > mask || probe >= (1u << 20)) { err |= OE_TABLE_FULL; break; }
+        const u64 c = a.table[slot];
+        if (c == fp[j]) break;
+        if (c == 0ull) {
+          const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[slot], 0ull, (unsigned long long)fp[j]);
+          if (old == 0ull) { ins |= 1u << j; break; }
+          if (old == fp[j]) break;
+        }
+        slot = (slot + 1) & mask;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j)
+      if ((ins >> j) & 1u) atomicOr(&win[(key[j] >> 8) * WW + ((key[j] & 255) >> 6)], 1ull << (key[j] & 63));
+  };
+  constexpr u32 STEP = (u32)P * BS;
+  u64 fpA[P], keyA[P], curA[P], fpB[P], keyB[P];
+  if (n) {
+    load_records(0, fpA, keyA);
+    filter(fpA);
+    load_records(STEP, fpB, keyB);   // (zeros past the end)
+    issue(fpA, curA);
+  }
+#pragma unroll 1
+  for (u32 i0 = 0; i0 < n; i0 += STEP) {
+    const bool more = i0 + STEP < n;   // workgroup-uniform
+    if (more) filter(fpB);             // its records arrived; the probes of batch A are in flight
+    finish(fpA, keyA, curA);
+    if (more) {
+#pragma unroll
+      for (int j = 0; j < P; ++j) { fpA[j] = fpB[j]; keyA[j] = keyB[j]; }
+      load_records(i0 + 2 * STEP, fpB, keyB);
+      issue(fpA, curA);
+    }
+  }
+  __shared__ u32 wave_probes[BS / 64];
+  if constexpr (COUNT) {
+    u32 wp = probes;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) wp += __shfl_xor(wp, d);
+    if (__lane_id() == 0) wave_probes[threadIdx.x >> 6] = wp;
+  }
+  __syncthreads();
+  if constexpr (COUNT) {
+    if (threadIdx.x == 0) {
+      u32 t = 0;
+#pragma unroll
+      for (int w = 0; w < BS / 64; ++w) t += wave_probes[w];
+      if (t) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)t);
+    }
+  }
+  u64 wm[WW];
+  u32 mine = 0;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) { wm[q] = win[threadIdx.x * WW + q]; mine += (u32)__popcll(wm[q]); }
+  u32 total = 0;
+  const u32 off = block_excl_scan(mine, wave_tot, &total);
+  if (threadIdx.x == 0) base_sh = total ? atomicAdd(&a.ctr[K_CHUNK_NEW], (unsigned long long)total) : 0ull;
+  __syncthreads();
+  u64 o = base_sh + off;
+  const u64 pg = a.gid0 + (u64)blockIdx.x * BS + threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < WW; ++q) {
+    u64 m = wm[q];
+    while (m) {
+      const int k = q * 64 + __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      a.newpos[o++] = (pg << 8) | (u64)k;
+    }
+  }
+  if (err) atomicOr(&a.ctr[K_ERR], (unsigned long long)err);
+}
+
+// The same, with full probe lanes: about half of the records repeat a successor of the same 256
+// parents, so probing straight after the LDS filter leaves half of every probe batch empty (the
+// probes in flight per thread that hide the HBM latency are really ~4 of 8).  Here each wave
+// pushes its filter survivors into its own LDS queue (ballot + mbcnt, no atomics) and probes only
+// full batches of 64 * DEDUP_PER fingerprints; the partial rest goes out at the end.  The wave's
+// actual probes are counted into ctr[K_PROBES] (the probes/s the bench reports).
+constexpr int DQ_P = 4;                                  // records loaded per lane per round
+constexpr int DQ_CAP = 64 * (DEDUP_PER + DQ_P);          // per-wave queue entries
+template <int WW>
+__global__ void __launch_bounds__(BS) orig_dedup_queue(DedupArgs a) {
+  __shared__ unsigned long long lfp[LDS_FP_SLOTS];
+  __shared__ u32 wave_tot[BS / 64];
+  __shared__ unsigned long long base_sh;
+  __shared__ unsigned long long win[BS * WW];
+  __shared__ unsigned long long qfp[BS / 64][DQ_CAP];
+  __shared__ unsigned short qkey[BS / 64][DQ_CAP];
+  for (int t = threadIdx.x; t < LDS_FP_SLOTS; t += BS) lfp[t] = 0ull;
+  for (int t = threadIdx.x; t < BS * WW; t += BS) win[t] = 0ull;
+  __syncthreads();
+  const WaveRegions wr(a.rcnt + 4 * blockIdx.x, a.region / 4);
+  const u32 n = wr.n;
+  const u64* fps = a.rfp + (u64)blockIdx.x * a.region;
+  const unsigned short* keys = a.rkey + (u64)blockIdx.x * a.region;
+  const int lane = __lane_id(), wv = threadIdx.x >> 6;
+  unsigned long long* qf = qfp[wv];
+  unsigned short* qk = qkey[wv];
+  u32 qn = 0;            // wave-uniform queue length
+  u64 probes = 0;        // wave-uniform
+  u32 err = 0;
+  // probe the top `take` (<= 64 * DEDUP_PER) queue entries, DEDUP_PER per lane
+  auto drain = [&](u32 take) {
+    u64 fp[DEDUP_PER], key[DEDUP_PER], pos[DEDUP_PER];
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j) {
+      const u32 q = (u32)j * 64 + (u32)lane;
+      fp[j] = q < take ? (u64)qf[qn - take + q] : 0ull;
+      key[j] = q < take ? (u64)qk[qn - take + q] : 0ull;
+    }
+    const u32 ins = probe_batch<DEDUP_PER, false, 1>(a.table, a.table_mask, fp, key, pos, err);
+#pragma unroll
+    for (int j = 0; j < DEDUP_PER; ++j)
+      if ((ins >> j) & 1u) atomicOr(&win[(key[j] >> 8) * WW + ((key[j] & 255) >> 6)], 1ull << (key[j] & 63));
+    probes += take;
+    qn -= take;
+    __builtin_amdgcn_wave_barrier();   // the next pushes reuse these queue entries
+  };
+#pragma unroll 1
+  for (u32 i0 = 0; i0 < n; i0 += DQ_P * BS) {
+#pragma unroll
+    for (int j = 0; j < DQ_P; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      const u64 at = wr.at(i);
+      const u64 fp = i < n ? fps[at] : 0ull;
+      const unsigned short k = i < n ? keys[at] : (unsigned short)0;
+      const bool keep = fp && lds_first(lfp, fp);   // else produced by this workgroup's parents before
+      const u64 m = __ballot(keep);
+      if (keep) {
+        const u32 slot = qn + (u32)__popcll(m & ((1ull << lane) - 1ull));
+        qf[slot] = (unsigned long long)fp;
+        qk[slot] = k;
+      }
+      qn += (u32)__popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();   // the queue writes of every lane before the reads below
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    while (qn >= 64u * DEDUP_PER) drain(64u * DEDUP_PER);
+  }
+  if (qn) drain(qn);
+  if (lane == 0 && probes) atomicAdd(&a.ctr[K_PROBES], (unsigned long long)probes);
+  __syncthreads();
   u64 wm[WW];
   u32 mine = 0;
 #pragma unroll
@@ -1413,7 +1977,7 @@ class OrigGpu : public Backend {
   void launch_generate(const GenArgs& g, unsigned nblk) {
     hipLaunchKernelGGL((orig_generate<S>), dim3(nblk), dim3(BS), 0, stream_, g);
     const unsigned lblk = std::min<unsigned>(nblk, std::max<unsigned>(64u, nblk / 8));
-    hipLaunchKernelGGL((orig_generate_lead<S>), dim3(lblk), dim3(BS), 0, stream_, g);
+    if (!dbg_no_lead_) hipLaunchKernelGGL((orig_generate_lead<S>), dim3(lblk), dim3(BS), 0, stream_, g);
   }
 
   RouteArgs route_args(u32 world) const {
@@ -1524,7 +2088,17 @@ class OrigGpu : public Backend {
           if (count_probes) hipLaunchKernelGGL((orig_probe<true>), dim3(nblk), dim3(BS), 0, stream_, d);
           else hipLaunchKernelGGL((orig_probe<false>), dim3(nblk), dim3(BS), 0, stream_, d);
         } else {
-          if (count_probes) {
+          if (split_plain_) {
+            hipLaunchKernelGGL(orig_merge_plain, dim3(nblk), dim3(BS), 0, stream_, d);
+            HIPCHK(hipGetLastError());
+            if (count_probes) hipLaunchKernelGGL((orig_probe_plain<WW, true>), dim3(nblk), dim3(BS), 0, stream_, d);
+            else hipLaunchKernelGGL((orig_probe_plain<WW, false>), dim3(nblk), dim3(BS), 0, stream_, d);
+          } else if (dedup_queue_) {
+            hipLaunchKernelGGL((orig_dedup_queue<WW>), dim3(nblk), dim3(BS), 0, stream_, d);
+          } else if (RMC_DEDUP_PIPE) {
+            if (count_probes) hipLaunchKernelGGL((orig_dedup_pipe<WW, true>), dim3(nblk), dim3(BS), 0, stream_, d);
+            else hipLaunchKernelGGL((orig_dedup_pipe<WW, false>), dim3(nblk), dim3(BS), 0, stream_, d);
+          } else if (count_probes) {
             hipLaunchKernelGGL((orig_dedup_plain<WW, true>), dim3(nblk), dim3(BS), 0, stream_, d);
           } else {
             hipLaunchKernelGGL((orig_dedup_plain<WW, false>), dim3(nblk), dim3(BS), 0, stream_, d);
@@ -2487,9 +3061,12 @@ class OrigGpu : public Backend {
   u64 sviol_parent_ = 0; u32 sviol_bad_ = 0; std::string sviol_act_, sviol_text_;
   u64 sh_event_ = ~0ull;
   bool last_fifo_ = true;   // seen-set layout of the last single-GPU run (16-B keyed / 8-B entries)
+  const bool split_plain_ = std::getenv("RAFTMC_SPLIT_PLAIN") != nullptr;          // experiment: merge + probe kernels
+  const bool dedup_queue_ = std::getenv("RAFTMC_DEDUP_QUEUE") != nullptr;   // experiment: full-lane probes from per-wave LDS queues
   // RAFTMC_PROF=1: per-phase wall-clock ticks (100 MHz) of orig_dedup, summed over workgroups
   const bool prof_ = std::getenv("RAFTMC_PROF") != nullptr;
   const bool progress_ = std::getenv("RAFTMC_PROGRESS") != nullptr;
+  const bool dbg_no_lead_ = std::getenv("RAFTMC_DBG_NO_LEAD") != nullptr;   // debugging only: leader work dropped
   u64 prof_acc_[5] = {0, 0, 0, 0, 0};
   // native (RCCL) level loop buffers
   u64* d_nat_ = nullptr; u64* h_nat_ = nullptr;
