@@ -77,11 +77,6 @@ constexpr int DEDUP_PER = 4;                  // probes in flight per dedup thre
 constexpr int BS = 256;                       // workgroup size of every kernel (4 waves)
 constexpr int LDS_FP_SLOTS = 2048;            // workgroup-local fingerprint set (8 B fp + 4 B key per slot)
 constexpr int MAT_CAP = 2048;      // winners staged in LDS per materialize round
-#ifndef RMC_PIPE_CHUNKS
-#define RMC_PIPE_CHUNKS 4
-#endif
-constexpr int PIPE_CHUNKS = RMC_PIPE_CHUNKS;   // -workers N: chunks of a large level, generate overlapping dedup (0: off)
-constexpr u64 PIPE_MIN = 1u << 18;             // levels below this many states stay one chunk
 constexpr int SCAN_BS = 1024;      // orig_scan workgroup
 
 // f(std::integral_constant<int, Q>) for Q = B .. E-1: a loop whose index is a compile-time constant
@@ -108,7 +103,6 @@ struct GenArgs {
   u32 inv_oom, deadlock;
   unsigned long long* ctr;
   u32* lead;                   // [chunk] parents with leader work (chunk index | 1 << 31 if no other successor)
-  unsigned long long* lead_cnt;   // their count (&ctr[K_LEAD], or the pipelined run's per-buffer word)
 };
 
 // One lane per frontier state; successor, constraints, TLC generated counts, out-of-model invariants,
@@ -330,7 +324,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
     if (lm) {
       const int first = __ffsll((unsigned long long)lm) - 1;
       u32 base = 0;
-      if (lane == first) base = (u32)atomicAdd(a.lead_cnt, (unsigned long long)__popcll(lm));
+      if (lane == first) base = (u32)atomicAdd(&a.ctr[K_LEAD], (unsigned long long)__popcll(lm));
       base = __shfl(base, first);
       if (lead) a.lead[base + (u32)__popcll(lm & ((1ull << lane) - 1ull))] = (u32)tid | (nsucc == 0 ? 0x80000000u : 0u);
     }
@@ -362,7 +356,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
   __shared__ unsigned int lds_cnt[OA_NACT + 1];
   for (int t = threadIdx.x; t < OA_NACT + 1; t += BS) lds_cnt[t] = 0;
   __syncthreads();
-  const u64 n = *a.lead_cnt;
+  const u64 n = a.ctr[K_LEAD];
   constexpr bool INC = NW <= 16;
   u32 err = 0, nin = 0;
   unsigned long long ev = ~0ull;
@@ -1386,16 +1380,6 @@ class OrigGpu : public Backend {
       HIPCHK(hipMalloc(&d_route_, (u64)world * nrec * 16));
       HIPCHK(hipMalloc(&d_rcnt_, 2 * 8 * 8));
     }
-    pipe_ok_ = false;
-    if (world == 0 && PIPE_CHUNKS > 1) {   // the pipelined -workers N levels' second record buffer (run)
-      HIPCHK(hipMalloc(&d_rfp2_, nrec * 8));
-      HIPCHK(hipMalloc(&d_rkey2_, nrec * 2));
-      HIPCHK(hipMalloc(&d_rcnt_blk2_, nblk * 16));
-      HIPCHK(hipMalloc(&d_lead2_, chunk_states_ * 4));
-      HIPCHK(hipMalloc(&d_leadcnt_, 2 * 8));
-      HIPCHK(hipStreamCreateWithFlags(&stream2_, hipStreamNonBlocking));
-      pipe_ok_ = true;
-    }
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
     dev_ = o.device; req_table_ = o.fp_table_bytes; req_store_ = o.state_store_bytes; alloc_world_ = world;
@@ -1420,7 +1404,6 @@ class OrigGpu : public Backend {
     g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.deadlock = o.check_deadlock ? 1u : 0u;
     g.ctr = (unsigned long long*)d_ctr_;
     g.lead = d_lead_;
-    g.lead_cnt = (unsigned long long*)(d_ctr_ + K_LEAD);
     return g;
   }
 
@@ -1518,39 +1501,19 @@ class OrigGpu : public Backend {
       // stay on the device (grid-stride / scanned offsets), so the host synchronises once per
       // level, for the counters
       int nch = 0;
-      // TLC -workers N: a large level goes in PIPE_CHUNKS chunks whose successor pass (VALU-bound) on
-      // stream_ overlaps the previous chunk's seen-set dedup + materialize (HBM-latency-bound) on
-      // stream2_, through two record buffers (chunk c's generate waits until chunk c - 2's dedup has
-      // read its buffer: that dedup's end event); the dedup / materialize / advance chain of the chunks
-      // stays in chunk order on stream2_, so the store order and the counts are the one-stream ones
-      const bool pipe = !fifo && pipe_ok_ && level_count >= PIPE_MIN;
-      u64 chunk = chunk_states_;
-      if (pipe) chunk = std::min<u64>(chunk_states_, ((level_count + PIPE_CHUNKS - 1) / PIPE_CHUNKS + BS - 1) / BS * BS);
-      hipStream_t sd = pipe ? stream2_ : stream_;   // the dedup / materialize stream
-      for (u64 cb = level_begin; cb < level_end; cb += chunk, ++nch) {
-        const u64 cnt = std::min<u64>(chunk, level_end - cb);
+      for (u64 cb = level_begin; cb < level_end; cb += chunk_states_, ++nch) {
+        const u64 cnt = std::min<u64>(chunk_states_, level_end - cb);
         const unsigned nblk = (unsigned)((cnt + BS - 1) / BS);
         if (int rc = lvl_events(nch)) { err = "hipEventCreate failed"; return rc; }
-        const int slot = pipe ? (nch & 1) : 0;
-        // kernels index the device store (global id - base_); keys and parent pointers are global
-        GenArgs g = gen_args(cb - base_, cnt, cb, r.seed, o);
-        if (slot) { g.rfp = d_rfp2_; g.rkey = d_rkey2_; g.rcnt = d_rcnt_blk2_; g.lead = d_lead2_; }
-        if (pipe) {
-          g.lead_cnt = (unsigned long long*)(d_leadcnt_ + slot);
-          if (nch >= 2) HIPCHK(hipStreamWaitEvent(stream_, lvl_ev_[8 * (nch - 2) + 3], 0));   // buffer read by then
-          HIPCHK(hipMemsetAsync(d_leadcnt_ + slot, 0, 8, stream_));
-        }
         hipEvent_t* e = &lvl_ev_[8 * nch];
+        // kernels index the device store (global id - base_); keys and parent pointers are global
+        const GenArgs g = gen_args(cb - base_, cnt, cb, r.seed, o);
         HIPCHK(hipEventRecord(e[0], stream_));
         launch_generate(g, nblk);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(e[1], stream_));
-        if (pipe) {
-          HIPCHK(hipStreamWaitEvent(sd, e[1], 0));
-          HIPCHK(hipEventRecord(e[2], sd));
-        }
         DedupArgs d;
-        d.rfp = g.rfp; d.rkey = g.rkey; d.rcnt = g.rcnt; d.region = (u64)BS * S::NI; d.gid0 = cb;
+        d.rfp = d_rfp_; d.rkey = d_rkey_; d.rcnt = d_rcnt_blk_; d.region = (u64)BS * S::NI; d.gid0 = cb;
         d.urec = (ulonglong2*)d_urec_; d.ucnt = d_ucnt_;
         d.table = d_table_; d.table_mask = tmask; d.newpos = d_newrec_; d.ctr = (unsigned long long*)d_ctr_;
         d.prof = prof_ ? 1u : 0u;
@@ -1562,13 +1525,13 @@ class OrigGpu : public Backend {
           else hipLaunchKernelGGL((orig_probe<false>), dim3(nblk), dim3(BS), 0, stream_, d);
         } else {
           if (count_probes) {
-            hipLaunchKernelGGL((orig_dedup_plain<WW, true>), dim3(nblk), dim3(BS), 0, sd, d);
+            hipLaunchKernelGGL((orig_dedup_plain<WW, true>), dim3(nblk), dim3(BS), 0, stream_, d);
           } else {
-            hipLaunchKernelGGL((orig_dedup_plain<WW, false>), dim3(nblk), dim3(BS), 0, sd, d);
+            hipLaunchKernelGGL((orig_dedup_plain<WW, false>), dim3(nblk), dim3(BS), 0, stream_, d);
           }
         }
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(e[3], sd));
+        HIPCHK(hipEventRecord(e[3], stream_));
         if (fifo) {
           MarkArgs mk;
           mk.newpos = d_newrec_; mk.table = d_table_; mk.gid0 = cb; mk.chunk_count = cnt; mk.winmask = d_winmask_;
@@ -1591,27 +1554,27 @@ class OrigGpu : public Backend {
           MatPlainArgs m;
           m.states = d_states_; m.meta = d_meta_; m.newrec = d_newrec_; m.base = base_; m.dst_base = level_end - base_;
           m.cap = cap_; m.rt = m_.rt; m.ctr = (unsigned long long*)d_ctr_; m.store = last ? 0u : 1u;
-          hipLaunchKernelGGL((orig_materialize_plain<S>), dim3((unsigned)std::min<u64>(4096, (cnt * 2 + BS - 1) / BS)), dim3(BS), 0, sd, m);
+          hipLaunchKernelGGL((orig_materialize_plain<S>), dim3((unsigned)std::min<u64>(4096, (cnt * 2 + BS - 1) / BS)), dim3(BS), 0, stream_, m);
         }
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(e[7], sd));
-        hipLaunchKernelGGL(orig_advance, dim3(1), dim3(64), 0, sd, (unsigned long long*)d_ctr_);
+        HIPCHK(hipEventRecord(e[7], stream_));
+        hipLaunchKernelGGL(orig_advance, dim3(1), dim3(64), 0, stream_, (unsigned long long*)d_ctr_);
         HIPCHK(hipGetLastError());
         for (size_t q = 0; q < r.kernels.size(); ++q) if (fifo || q != 2) r.kernels[q].launches += 1;
         r.kernels[0].algo_bytes += (double)cnt * S_B;        // + G_in * 10 record bytes per level below
       }
       u64* const c = h_ctr_;   // pinned: the readback is one direct copy
-      HIPCHK(hipMemcpyAsync(c, d_ctr_, K_NCTR * 8, hipMemcpyDeviceToHost, sd));
-      hipLaunchKernelGGL(orig_reset_ctr, dim3(1), dim3(64), 0, sd, (unsigned long long*)d_ctr_);
+      HIPCHK(hipMemcpyAsync(c, d_ctr_, K_NCTR * 8, hipMemcpyDeviceToHost, stream_));
+      hipLaunchKernelGGL(orig_reset_ctr, dim3(1), dim3(64), 0, stream_, (unsigned long long*)d_ctr_);
       HIPCHK(hipGetLastError());
       ctr_clean_ = true;
-      HIPCHK(hipStreamSynchronize(sd));   // (pipelined: stream_'s kernels precede stream2_'s last ones)
+      HIPCHK(hipStreamSynchronize(stream_));
       double level_ms = 0;
       for (int q = 0; q < nch; ++q) {
-        // event pairs per kernel: generate (e0, e1), dedup (e1, e3; pipelined: e2 on stream2_, e3),
-        // mark/scan (e3, e5; FIFO only), materialize (e5 or e3, e7)
+        // event pairs per kernel: generate (e0, e1), dedup (e1, e3), mark/scan (e3, e5; FIFO only),
+        // materialize (e5 or e3, e7)
         const hipEvent_t* e = &lvl_ev_[8 * q];
-        const std::pair<int, int> pr[4] = {{0, 1}, {pipe ? 2 : 1, 3}, {3, fifo ? 5 : 3}, {fifo ? 5 : 3, 7}};
+        const std::pair<int, int> pr[4] = {{0, 1}, {1, 3}, {3, fifo ? 5 : 3}, {fifo ? 5 : 3, 7}};
         for (int k = 0; k < 4; ++k) {
           float ms = 0;
           if (pr[k].first != pr[k].second) (void)hipEventElapsedTime(&ms, e[pr[k].first], e[pr[k].second]);
@@ -2508,12 +2471,6 @@ class OrigGpu : public Backend {
   u64* d_winmask_ = nullptr; u32* d_wcnt_ = nullptr; u64* d_woff_ = nullptr; u64* d_urec_ = nullptr; u32* d_ucnt_ = nullptr;
   u64* d_route_ = nullptr; u64* d_rcnt_ = nullptr; u32* d_stout_ = nullptr; u64 stout_cap_ = 0;
   u32* d_lead_ = nullptr;      // [chunk] the chunk's leader-work parents (orig_generate -> orig_generate_lead)
-  // pipelined -workers N levels (run): the second record buffer, its leader list, both lists' counts,
-  // and the dedup / materialize stream
-  u64* d_rfp2_ = nullptr; unsigned short* d_rkey2_ = nullptr; u32* d_rcnt_blk2_ = nullptr; u32* d_lead2_ = nullptr;
-  u64* d_leadcnt_ = nullptr;
-  hipStream_t stream2_ = nullptr;
-  bool pipe_ok_ = false;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_[9] = {};
   u64 table_mask_ = 0, cap_ = 0, total_ = 0, chunk_states_ = 0;
@@ -2547,12 +2504,8 @@ class OrigGpu : public Backend {
   void release() {
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_stop_, (void*)d_rfp_, (void*)d_rkey_,
                     (void*)d_rcnt_blk_, (void*)d_newrec_, (void*)d_winmask_, (void*)d_wcnt_, (void*)d_woff_, (void*)d_urec_, (void*)d_ucnt_,
-                    (void*)d_route_, (void*)d_rcnt_, (void*)d_stout_, (void*)d_lead_, (void*)d_rfp2_, (void*)d_rkey2_,
-                    (void*)d_rcnt_blk2_, (void*)d_lead2_, (void*)d_leadcnt_})
+                    (void*)d_route_, (void*)d_rcnt_, (void*)d_stout_, (void*)d_lead_})
       if (p) (void)hipFree(p);
-    d_rfp2_ = nullptr; d_rkey2_ = nullptr; d_rcnt_blk2_ = nullptr; d_lead2_ = nullptr; d_leadcnt_ = nullptr; pipe_ok_ = false;
-    if (stream2_) (void)hipStreamDestroy(stream2_);
-    stream2_ = nullptr;
     for (void* p : {(void*)d_nat_, nat_recv_, nat_acks_, nat_stin_})
       if (p) (void)hipFree(p);
     if (h_nat_) (void)hipHostFree(h_nat_);
