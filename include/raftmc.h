@@ -223,6 +223,13 @@ int mc_collision_observed(mc_ctx* ctx, double* val);
 int mc_set_checkpoint(mc_ctx* ctx, const char* path, int32_t every_levels);
 int mc_set_recover(mc_ctx* ctx, const char* path);
 
+/* Free the device memory the handle keeps between runs (state store, seen-set, work buffers; the
+ * generated path keeps its whole working set, up to state_store_bytes, so that a second run of the
+ * same model does not pay ~2.5 s of hipMalloc for a 200 GiB store).  The summary, the trace and the
+ * report of the last run stay readable; mc_dump_states and mc_collision_observed, which read the
+ * device store, return MC_E_STATE until the next mc_run, which allocates again. */
+int mc_release_device_memory(mc_ctx* ctx);
+
 /* Full TLC-style report (summary + trace) as text; caller frees with mc_free. */
 int mc_report(const mc_ctx* ctx, char** text, size_t* len);
 

@@ -69,6 +69,8 @@ struct Backend {
   virtual std::string describe_json() const = 0;
   virtual int run(const RunOpts& o, RunResult& r, std::string& err) = 0;
   virtual int dump_states(const std::string& path, std::string& err) = 0;
+  // mc_release_device_memory: free the device buffers kept between runs (the next run allocates again)
+  virtual void release_device() = 0;
   // TLC's "based on the actual fingerprints" estimate: 1 / min gap of the seen-set (fp_gap.h)
   virtual int observed_collision(double& v, std::string& err) { (void)v; err = "not available"; return -4; }
   // punctuated-search prefix constraints whose golden history trace is data (tla_value.h)

@@ -126,6 +126,21 @@ struct FpBase {
     }
     return fp_final<NW32>(acc, seed);
   }
+  // fp(w, base, seed, changed) when w can differ from base only in the 64-bit words [K0, NW64)
+  // (compile-time: a successor that changes a known tail of the packed state, e.g. the message bag)
+  template <int K0>
+  RMC_HD u64 fp_tail(const u32 (&w)[NW32], const u32 (&base)[NW32], u64 seed, bool& changed) const {
+    u64 acc = sum;
+    changed = false;
+#pragma unroll
+    for (int k = K0; k < NW64; ++k) {
+      const u64 v = word(w, k);
+      const bool d = v != word(base, k);
+      changed |= d;
+      if (d) acc += fmix64(v ^ key(seed, k)) - term[k];
+    }
+    return fp_final<NW32>(acc, seed);
+  }
   // fp64 of the parent's words `base` plus d * 2^P (P a compile-time bit offset into the packed
   // state, d = +-1): the successor that changes one small field by one, where the field does not
   // carry out of its own bits (so at most the two 64-bit words holding bits P.. change)

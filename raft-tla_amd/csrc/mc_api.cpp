@@ -23,6 +23,7 @@ struct mc_ctx {
   rmc::RunOpts ro;
   rmc::RunResult res;
   bool ran = false;
+  bool released = false;   // mc_release_device_memory since the last run
   std::string last_error, tla_path, cfg_path;
   mutable std::map<std::string, std::string> action_loc;   // action name -> TLC location text ("" if none)
   const std::string& location_of(const std::string& act) const {
@@ -331,6 +332,7 @@ int run_multi(mc_ctx* c) {
 int mc_run(mc_ctx* c) {
   if (!c) return MC_E_INVALID;
   if (!c->be) return MC_E_STATE;
+  c->released = false;
   if (c->n_gpus > 1) { c->ran = false; return run_multi(c); }
   std::string err;
   int rc = c->be->run(c->ro, c->res, err);
@@ -444,9 +446,18 @@ int mc_action_location(const mc_ctx* c, const char* action, char** text, size_t*
   return *text ? MC_OK : MC_E_OOM;
 }
 
+int mc_release_device_memory(mc_ctx* c) {
+  if (!c) return MC_E_INVALID;
+  if (!c->be) return MC_E_STATE;
+  c->be->release_device();
+  for (auto& p : c->peers) if (p) p->release_device();
+  c->released = true;   // the last run's stored states are gone: mc_dump_states / mc_collision_observed refuse
+  return MC_OK;
+}
+
 int mc_collision_observed(mc_ctx* c, double* val) {
   if (!c || !val) return MC_E_INVALID;
-  if (!c->ran) return MC_E_STATE;
+  if (!c->ran || c->released) return MC_E_STATE;
   std::string err;
   double v = -1;
   const int rc = c->be->observed_collision(v, err);
@@ -458,7 +469,7 @@ int mc_collision_observed(mc_ctx* c, double* val) {
 
 int mc_dump_states(const mc_ctx* c, const char* path) {
   if (!c || !path) return MC_E_INVALID;
-  if (!c->ran) return MC_E_STATE;
+  if (!c->ran || c->released) return MC_E_STATE;
   std::string err;
   if (c->n_gpus > 1) {
     // every rank's partition of the state space: one file per rank, path.rank<r> (as shard.py writes)

@@ -1758,6 +1758,7 @@ class MembGpu : public Backend {
   }
   unsigned long long* d_prof_ = nullptr;   // RMC_FP_PROF builds (printed to stderr by release)
 
+  void release_device() override { release(); }
   void release() {
     if (d_prof_) {
       unsigned long long h[8] = {0};

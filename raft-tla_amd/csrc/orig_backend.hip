@@ -77,6 +77,12 @@ constexpr int DEDUP_PER = 4;                  // probes in flight per dedup thre
 constexpr int BS = 256;                       // workgroup size of every kernel (4 waves)
 constexpr int LDS_FP_SLOTS = 2048;            // workgroup-local fingerprint set (8 B fp + 4 B key per slot)
 constexpr int MAT_CAP = 2048;      // winners staged in LDS per materialize round
+#ifndef RMC_RV_PATCH
+#define RMC_RV_PATCH 0
+#endif
+#ifndef RMC_RV_WCOUNT
+#define RMC_RV_WCOUNT 0
+#endif
 constexpr int SCAN_BS = 1024;      // orig_scan workgroup
 
 // f(std::integral_constant<int, Q>) for Q = B .. E-1: a loop whose index is a compile-time constant
@@ -226,13 +232,31 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(S::NW <
 #pragma unroll
           for (int w2 = 0; w2 < S::AW; ++w2) t.allLogs[w2] = al[w2];
           ++nsucc;
-          atomicAdd(&lds_cnt[act], 1u);
+          if (!RMC_RV_WCOUNT) atomicAdd(&lds_cnt[act], 1u);
           if (S::in_model(t, a.rt)) {
             ++nin;
+#if RMC_RV_PATCH
+            if constexpr (INC) {
+              // RequestVote changes only the bag: the parent's words with the bag re-packed, and only the
+              // 64-bit words from the bag's first one re-hashed (both compile-time ranges)
+              u32 pw[NW];
+              S::pack_patch(t, 1u << S::PG_BAG, bw, pw);
+              bool changed;
+              fp = fb.template fp_tail<S::BAG_OFF / 64>(pw, bw, a.seed, changed);
+              have = changed || !al_same;
+            } else {
+              have = fingerprint(t, fp);
+            }
+#else
             have = fingerprint(t, fp);
+#endif
           }
           // out of the model: RequestVote writes only the bag, which no invariant reads (S::inv_frame)
         }
+      }
+      if (RMC_RV_WCOUNT) {   // every lane of the trip generates one RequestVote: one LDS atomic per wave
+        const u64 gm = __ballot(on);
+        if (lane == __ffsll((unsigned long long)gm) - 1) atomicAdd(&lds_cnt[OA_RequestVote], (unsigned)__popcll(gm));
       }
       append(have, fp, k);
     }
@@ -2501,6 +2525,7 @@ class OrigGpu : public Backend {
   u64 base_ = 0;
   HostStore host_{NWP};
 
+  void release_device() override { release(); }
   void release() {
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_stop_, (void*)d_rfp_, (void*)d_rkey_,
                     (void*)d_rcnt_blk_, (void*)d_newrec_, (void*)d_winmask_, (void*)d_wcnt_, (void*)d_woff_, (void*)d_urec_, (void*)d_ucnt_,

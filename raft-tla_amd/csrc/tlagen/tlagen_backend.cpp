@@ -222,6 +222,7 @@ struct TlagenBackend : Backend {
     key = hex(fnv64(k));
   }
   ~TlagenBackend() override { release(); }
+  void release_device() override { release(); }
   void release() {
     pool.free_all();
     d_words = nullptr; d_offs = nullptr;

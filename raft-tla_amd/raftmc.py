@@ -31,7 +31,7 @@ EXPORTS = ["mc_opts_init", "mc_default_opts", "mc_open", "mc_run", "mc_summary",
            "mc_shard_level_stats", "mc_shard_level_commit", "mc_shard_read_state", "mc_shard_violation",
            "mc_set_history_prefix", "mc_shard_layout", "mc_shard_select", "mc_shard_event_stats",
            "mc_collision_observed", "mc_rccl_unique_id", "mc_shard_run_rccl", "mc_shard_run_loopback",
-           "mc_set_checkpoint", "mc_set_recover", "mc_action_location", "mc_source_hash", "mc_set_fault_injection"]
+           "mc_set_checkpoint", "mc_set_recover", "mc_action_location", "mc_source_hash", "mc_set_fault_injection", "mc_release_device_memory"]
 
 
 class McOpts(ctypes.Structure):
@@ -122,6 +122,7 @@ def load_library(path=LIB_PATH):
     lib.mc_set_checkpoint.argtypes = [P, ctypes.c_char_p, ctypes.c_int32]
     lib.mc_set_recover.argtypes = [P, ctypes.c_char_p]
     lib.mc_set_fault_injection.argtypes = [P, ctypes.c_int32, ctypes.c_int64]
+    lib.mc_release_device_memory.argtypes = [P]
     lib.mc_exit_code.argtypes = [P]
     lib.mc_free.argtypes = [P]
     lib.mc_close.argtypes = [P]
@@ -204,6 +205,12 @@ class ModelChecker:
     def set_recover(self, path):
         """TLC -recover: the next run() resumes the search saved in `path`."""
         rc = self.lib.mc_set_recover(self.h, path.encode() if path else None)
+        if rc:
+            raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
+
+    def release_device_memory(self):
+        """Free the device buffers this handle keeps between runs (the next run() allocates again)."""
+        rc = self.lib.mc_release_device_memory(self.h)
         if rc:
             raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
 

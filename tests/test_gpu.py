@@ -482,3 +482,26 @@ def test_collision_estimates_and_tlc_summary_lines(raftmc):
     with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, "memb_two.cfg"), max_depth=14, deadlock=False) as mc:
         mc.run()
         assert 0 < mc.collision_observed() < 1
+
+
+@pytest.mark.parametrize("frontend", ["hand", "generated"])
+def test_release_device_memory(raftmc, frontend, tmp_path):
+    """mc_release_device_memory (a handle keeps its device buffers between runs -- the generated
+    path its whole working set): after it the last run's summary and trace stay readable, mc_dump_states is
+    refused (MC_E_STATE), and the next run allocates again and gives the same result."""
+    cfg = os.path.join(CONFIGS, "parity_pair.cfg")
+    spec = ORIG_MC
+    if frontend == "generated":   # the front end's prebuilt source (the GPU box has no reference checkout)
+        from test_gpu_tlagen import gen_source
+        spec = gen_source("parity_pair")
+    with raftmc.ModelChecker(spec, cfg, frontend=frontend, fp_table_bytes=1 << 24, state_store_bytes=1 << 28) as mc:
+        a = mc.run()
+        mc.release_device_memory()
+        assert mc.summary().distinct == a.distinct
+        with pytest.raises(raftmc.RaftMCError) as e:
+            mc.dump_states(str(tmp_path / "x.txt"))
+        assert e.value.code == -7
+        b = mc.run()
+        mc.dump_states(str(tmp_path / "y.txt"))
+    assert (a.verdict, a.generated, a.distinct, a.depth) == (b.verdict, b.generated, b.distinct, b.depth)
+    assert sum(1 for _ in open(tmp_path / "y.txt")) == b.distinct
