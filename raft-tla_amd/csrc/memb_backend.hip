@@ -68,9 +68,10 @@ struct MGenArgs {
   const u32* states;
   u64 chunk_begin, chunk_count, rank0;     // first state of the chunk: gid and rank in its level
   u64* cand;                               // [NSLOT][chunk] fingerprints, 0 = none
-  u32* cells;                              // per workgroup: BS*NSLOT cells (slot * chunk + state) of in-model successors
+  u32* cells;                              // per workgroup: BS*NSLOT cells (slot * chunk + state) of in-model successors,
+                                           // in four per-wave regions of 64*NSLOT
   u32* cells_oom;                          // ... of out-of-model successors (TLC checks their invariants, [ext] (ii))
-  u32* cell_count;                         // per workgroup: [in-model, out-of-model] cell counts
+  u32* cell_count;                         // per workgroup: in-model cells of waves 0-3, out-of-model cells of waves 0-3
   unsigned short* nsucc;                   // [chunk] successors per state (TLC "generated")
   u64 seed;
   MembRuntime rt;
@@ -84,11 +85,14 @@ struct MGenArgs {
 // loop body (hoisting them over ~100 instances exhausts the register file).
 template <class S, int K0, int K1, int NS>
 __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs& a, bool active, u64 tid, u32& err,
-                                             u32& nsucc, u32& nin, unsigned int* lds_cnt, unsigned int* lds_cells) {
+                                             u32& nsucc, u32& nin, unsigned int* lds_cnt, u32& wcin, u32& wcoom) {
   using W = typename S::Work;
-  const int lane = __lane_id();
-  u32* cells = a.cells + (u64)blockIdx.x * (BS * S::NSLOT);
-  u32* cells_oom = a.cells_oom + (u64)blockIdx.x * (BS * S::NSLOT);
+  // this wave's own regions of the workgroup's cell lists (64 * NSLOT cells each): a wave's cells stay
+  // together, parent group by parent group (memb_fingerprint's lanes then share the 64 parents of one
+  // expand wave, not the workgroup's 256: fewer parent lines re-fetched past L2)
+  const u64 wreg = (u64)blockIdx.x * (BS * S::NSLOT) + (u64)(threadIdx.x >> 6) * (64 * S::NSLOT);
+  u32* cells = a.cells + wreg;
+  u32* cells_oom = a.cells_oom + wreg;
   for (int k = K0; k < K1; ++k) {
     const bool en = S::group_enabled(k, a.rt.next);                 // wave-uniform
     for (int sub = 0; sub < NS; ++sub) {
@@ -115,25 +119,30 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
         }
       }
       const u32 cell = (u32)((u64)slot * a.chunk_count + tid);
+      // one ballot per list, consecutive stores at the wave's running count (wave-uniform: no atomic)
       const u64 mask = __ballot(need);
-      if (mask) {
-        const int leader = __ffsll((unsigned long long)mask) - 1;
-        u32 base = 0;
-        if (lane == leader) base = atomicAdd(&lds_cells[0], (unsigned int)__popcll(mask));   // LDS: no global contention
-        base = __shfl(base, leader);
-        if (need) cells[base + __popcll(mask & ((1ull << lane) - 1ull))] = cell;
-      }
+      if (need) cells[wcin + __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u))] = cell;
+      wcin += (u32)__popcll(mask);
       const u64 omask = __ballot(oom);
-      if (omask) {
-        const int leader = __ffsll((unsigned long long)omask) - 1;
-        u32 base = 0;
-        if (lane == leader) base = atomicAdd(&lds_cells[1], (unsigned int)__popcll(omask));
-        base = __shfl(base, leader);
-        if (oom) cells_oom[base + __popcll(omask & ((1ull << lane) - 1ull))] = cell;
-      }
+      if (oom) cells_oom[wcoom + __builtin_amdgcn_mbcnt_hi((u32)(omask >> 32), __builtin_amdgcn_mbcnt_lo((u32)omask, 0u))] = cell;
+      wcoom += (u32)__popcll(omask);
     }
   }
 }
+
+// A workgroup's cells: its four waves' regions (wave w's at w * 64 * NSLOT, cnt[w] cells each),
+// concatenated in wave order.
+struct CellRegions {
+  u32 p1, p2, p3, n, wreg;
+  __device__ CellRegions(const u32* cnt, u32 wave_region) {
+    p1 = cnt[0]; p2 = p1 + cnt[1]; p3 = p2 + cnt[2]; n = p3 + cnt[3]; wreg = wave_region;
+  }
+  __device__ u32 at(u32 i) const {
+    const u32 w = (i >= p1) + (i >= p2) + (i >= p3);
+    const u32 base = w == 0 ? 0u : w == 1 ? p1 : w == 2 ? p2 : p3;
+    return w * wreg + (i - base);
+  }
+};
 
 // Phase 1: successors, constraints and TLC "generated" counts; in-model (and, for the
 // invariant check, out-of-model) cells are appended with one atomic per wave and slot.
@@ -145,9 +154,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MEX
   using W = typename S::Work;
   constexpr int NWP = S::NWP;
   __shared__ unsigned int lds_cnt[MA_NACT + 1];
-  __shared__ unsigned int lds_cells[2];
   for (int t = threadIdx.x; t < MA_NACT + 1; t += BS) lds_cnt[t] = 0;
-  if (threadIdx.x < 2) lds_cells[threadIdx.x] = 0;
   __syncthreads();
   const u64 tid = (u64)blockIdx.x * BS + threadIdx.x;
   const bool active = tid < a.chunk_count;
@@ -162,12 +169,12 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MEX
   } else {
     S::init(s);
   }
-  u32 err = 0, nsucc = 0, nin = 0;
+  u32 err = 0, nsucc = 0, nin = 0, wcin = 0, wcoom = 0;
   // three loops (instances before Receive, Receive with its two successor slots, the rest): the
   // compile-time ranges prune apply's dispatch while keeping the kernel within short-branch range
-  expand_group<S, S::G_RV, S::G_RECV, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, lds_cells);
-  expand_group<S, S::G_RECV, S::G_TO, 2>(s, a, active, tid, err, nsucc, nin, lds_cnt, lds_cells);
-  expand_group<S, S::G_TO, S::NI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, lds_cells);
+  expand_group<S, S::G_RV, S::G_RECV, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom);
+  expand_group<S, S::G_RECV, S::G_TO, 2>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom);
+  expand_group<S, S::G_TO, S::NI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom);
   unsigned long long ev = ~0ull;
   if (active) {
     a.nsucc[tid] = (unsigned short)nsucc;
@@ -183,10 +190,10 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MEX
   __syncthreads();
   for (int t = threadIdx.x; t < MA_NACT; t += BS)
     if (lds_cnt[t]) atomicAdd(&a.ctr[C_ACT + t], (unsigned long long)lds_cnt[t]);
-  if (threadIdx.x == 0) {
-    if (lds_cnt[MA_NACT]) atomicAdd(&a.ctr[C_GEN_IN], (unsigned long long)lds_cnt[MA_NACT]);
-    a.cell_count[2 * blockIdx.x] = lds_cells[0];
-    a.cell_count[2 * blockIdx.x + 1] = lds_cells[1];
+  if (threadIdx.x == 0 && lds_cnt[MA_NACT]) atomicAdd(&a.ctr[C_GEN_IN], (unsigned long long)lds_cnt[MA_NACT]);
+  if (__lane_id() == 0) {   // per wave: [in-model x 4 waves, out-of-model x 4 waves]
+    a.cell_count[8 * blockIdx.x + (threadIdx.x >> 6)] = wcin;
+    a.cell_count[8 * blockIdx.x + 4 + (threadIdx.x >> 6)] = wcoom;
   }
 }
 
@@ -197,10 +204,11 @@ template <class S, bool TLC>
 __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
   using W = typename S::Work;
   constexpr int NWP = S::NWP;
-  const u32 n = a.cell_count[2 * blockIdx.x];
+  const CellRegions cr(a.cell_count + 8 * blockIdx.x, 64 * S::NSLOT);
+  const u32 n = cr.n;
   const u32* cells = a.cells + (u64)blockIdx.x * (BS * S::NSLOT);
   for (u32 i = threadIdx.x; i < n; i += BS) {
-  const u32 cell = cells[i];
+  const u32 cell = cells[cr.at(i)];
   const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
   int k, sub;
   S::inst_of_slot((int)slot, k, sub);
@@ -230,10 +238,11 @@ template <class S>
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MOOM_WAVES))) memb_oom_check(MGenArgs a) {
   using W = typename S::Work;
   constexpr int NWP = S::NWP;
-  const u32 n = a.cell_count[2 * blockIdx.x + 1];
+  const CellRegions cr(a.cell_count + 8 * blockIdx.x + 4, 64 * S::NSLOT);
+  const u32 n = cr.n;
   const u32* cells = a.cells_oom + (u64)blockIdx.x * (BS * S::NSLOT);
   for (u32 i = threadIdx.x; i < n; i += BS) {
-  const u32 cell = cells[i];
+  const u32 cell = cells[cr.at(i)];
   const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
   int k, sub;
   S::inst_of_slot((int)slot, k, sub);
@@ -837,7 +846,7 @@ class MembGpu : public Backend {
     HIPCHK(hipMalloc(&d_nsucc_, chunk_ * 2));
     HIPCHK(hipMalloc(&d_cells_, chunk_ * S::NSLOT * 4));
     HIPCHK(hipMalloc(&d_cells_oom_, chunk_ * S::NSLOT * 4));
-    HIPCHK(hipMalloc(&d_cell_count_, 2 * ((chunk_ + BS - 1) / BS) * 4));
+    HIPCHK(hipMalloc(&d_cell_count_, 8 * ((chunk_ + BS - 1) / BS) * 4));
     HIPCHK(hipMalloc(&d_woff_, chunk_ * 4));
     HIPCHK(hipMalloc(&d_bsum_, SCAN_MAX_BLOCKS * 8));
     HIPCHK(hipMalloc(&d_ctr_, C_NCTR * 8));

@@ -77,6 +77,14 @@ for l in open('$O/memb_$n.json').read().strip().splitlines():
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_stats" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extra --fifo-steps 0 > "$O/prof_stats.log" 2>&1
       rc=$? ;;
+    gaps)   # gaps[=EXTRA]: a C2 kernel trace (csv) and the device's idle time per run (scripts/kernel_gaps.py)
+      timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$O/gaps" -o run -- python3 bench.py --steps 3 --warmup 1 \
+        --no-cpu-baseline --no-extra --fifo-steps 0 > "$O/gaps.log" 2>&1
+      rc=$?
+      if [ $rc -eq 0 ]; then
+        f=$(find "$O/gaps" -name '*kernel_trace.csv' | sort | tail -n 1)
+        python3 scripts/kernel_gaps.py "$f" "$O/kernel_gaps.json"; rc=$?
+      fi ;;
     c2_prof)
       bash scripts/c2_prof.sh "${O#$R/}/c2_prof" "${arg:-r05}"; rc=$? ;;
     memb_prof)

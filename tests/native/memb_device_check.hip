@@ -124,15 +124,15 @@ int main(int argc, char** argv) {
     u32 *dcells, *dcells_oom, *dcount;
     (void)hipMalloc(&dcells, nblk * 256 * S::NSLOT * 4);
     (void)hipMalloc(&dcells_oom, nblk * 256 * S::NSLOT * 4);
-    (void)hipMalloc(&dcount, nblk * 2 * 4);
+    (void)hipMalloc(&dcount, nblk * 8 * 4);
     g.states = dst4; g.chunk_begin = 0; g.chunk_count = n; g.rank0 = 0; g.cand = dcand; g.cells = dcells; g.cells_oom = dcells_oom;
     g.cell_count = dcount; g.nsucc = dns; g.seed = seed; g.rt = rt; g.inv_oom = 1; g.deadlock = 0; g.ctr = (unsigned long long*)dctr;
     hipLaunchKernelGGL((memb_expand<S>), dim3((unsigned)nblk), dim3(256), 0, 0, g);
     if (hipDeviceSynchronize() != hipSuccess) { std::printf("{\"error\": \"expand kernel\"}\n"); return 1; }
     // validate every workgroup's two cell lists on the host before any kernel dereferences them
     {
-      std::vector<u32> cnts(nblk * 2);
-      (void)hipMemcpy(cnts.data(), dcount, nblk * 2 * 4, hipMemcpyDeviceToHost);
+      std::vector<u32> cnts(nblk * 8);   // per workgroup: in-model cells of waves 0-3, out-of-model cells of waves 0-3
+      (void)hipMemcpy(cnts.data(), dcount, nblk * 8 * 4, hipMemcpyDeviceToHost);
       u64 nbad = 0, nwant_in = 0, nwant_oom = 0, ncells = 0, noom = 0;
       std::vector<char> seen_cell(np, 0);
       auto check = [&](u32 c, bool want_in, u64 blk) {
@@ -147,10 +147,17 @@ int main(int argc, char** argv) {
         if (!ok) { if (!nbad) std::fprintf(stderr, "bad cell %08x (in-model list: %d)\n", c, (int)want_in); ++nbad; }
       };
       for (u64 b = 0; b < nblk; ++b) {
-        if (cnts[2 * b] > 256u * S::NSLOT || cnts[2 * b + 1] > 256u * S::NSLOT) { std::printf("{\"error\": \"cell count out of range\"}\n"); return 4; }
-        std::vector<u32> cl(cnts[2 * b]), co(cnts[2 * b + 1]);
-        if (!cl.empty()) (void)hipMemcpy(cl.data(), dcells + b * 256 * S::NSLOT, cl.size() * 4, hipMemcpyDeviceToHost);
-        if (!co.empty()) (void)hipMemcpy(co.data(), dcells_oom + b * 256 * S::NSLOT, co.size() * 4, hipMemcpyDeviceToHost);
+        std::vector<u32> cl, co;
+        for (int w = 0; w < 4; ++w) {
+          const u32 ci = cnts[8 * b + w], coo = cnts[8 * b + 4 + w];
+          if (ci > 64u * S::NSLOT || coo > 64u * S::NSLOT) { std::printf("{\"error\": \"cell count out of range\"}\n"); return 4; }
+          std::vector<u32> x(ci), y(coo);
+          const u64 reg = b * 256 * S::NSLOT + (u64)w * 64 * S::NSLOT;
+          if (ci) (void)hipMemcpy(x.data(), dcells + reg, ci * 4, hipMemcpyDeviceToHost);
+          if (coo) (void)hipMemcpy(y.data(), dcells_oom + reg, coo * 4, hipMemcpyDeviceToHost);
+          cl.insert(cl.end(), x.begin(), x.end());
+          co.insert(co.end(), y.begin(), y.end());
+        }
         for (u32 c : cl) check(c, true, b);
         for (u32 c : co) check(c, false, b);
         ncells += cl.size(); noom += co.size();
