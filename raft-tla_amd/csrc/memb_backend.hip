@@ -134,13 +134,12 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
 // concatenated in wave order.
 struct CellRegions {
   u32 p1, p2, p3, n, wreg;
-  __device__ CellRegions(const u32* cnt, u32 wave_region) {
-    p1 = cnt[0]; p2 = p1 + cnt[1]; p3 = p2 + cnt[2]; n = p3 + cnt[3]; wreg = wave_region;
+  __device__ CellRegions(const u32* cnt, u32 wave_region) {   // (uniform: kept in SGPRs)
+    p1 = __builtin_amdgcn_readfirstlane(cnt[0]); p2 = p1 + __builtin_amdgcn_readfirstlane(cnt[1]);
+    p3 = p2 + __builtin_amdgcn_readfirstlane(cnt[2]); n = p3 + __builtin_amdgcn_readfirstlane(cnt[3]); wreg = wave_region;
   }
-  __device__ u32 at(u32 i) const {
-    const u32 w = (i >= p1) + (i >= p2) + (i >= p3);
-    const u32 base = w == 0 ? 0u : w == 1 ? p1 : w == 2 ? p2 : p3;
-    return w * wreg + (i - base);
+  __device__ u32 at(u32 i) const {   // w * wreg + (i - p_w), as three selects (no indexed table)
+    return i + (i >= p1 ? wreg - p1 : 0u) + (i >= p2 ? wreg - (p2 - p1) : 0u) + (i >= p3 ? wreg - (p3 - p2) : 0u);
   }
 };
 
