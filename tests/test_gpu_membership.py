@@ -300,8 +300,8 @@ def test_c3_deep_oracle_pin(raftmc, case):
     assert (r.distinct, r.depth, r.left_on_queue) == (g["distinct"], g["depth"], g["left_on_queue"])
     assert {a: v[1] for a, v in r.actions.items()} == {a: v[1] for a, v in g["actions"].items()}   # distinct per action
     # Generated counters: compared for a pin made by the oracle that counts TLC's copies of disjunctive
-    # guards (round 5, "tlc_copies").  An older pin predates that count (its hours-long
-    # oracle run was not repeated): its distinct side above still holds, its generated side does not apply.
+    # guards ("tlc_copies") -- every pin since round 6 (the orbit-mode depth-18 pin was
+    # re-made then); a pin without the flag would predate that count and keep only its distinct side.
     if g.get("tlc_copies"):
         assert r.generated == g["generated"]
         assert r.actions == g["actions"]
