@@ -54,6 +54,7 @@ namespace rmc {
 namespace {
 enum {
   C_CELLS = 0, C_ERR = 1, C_EVENT = 2, C_NEW = 3, C_ERRGID = 4, C_GEN_IN = 5, C_CELLS_OOM = 6,
+  C_BIG = 7,   // the chunk's cells memb_fingerprint_lds left to memb_fingerprint_list (zeroed by memb_expand)
   C_ACT = 8, C_SHARD = C_ACT + 2 * MA_NACT, C_NCTR = C_SHARD + 8   // C_SHARD: per-rank bucket counters
 };
 enum { EV_NEXT_ERROR = 0, EV_DEADLOCK = 1, EV_INV_ERROR = 2, EV_VIOLATION = 3 };
@@ -78,6 +79,7 @@ struct MGenArgs {
   u32 inv_oom, deadlock;
   unsigned long long* ctr;
   unsigned long long* prof;                // RMC_FP_PROF builds: wave cycles per fingerprint stage (else null)
+  u32* big;                                // TLC mode: cells whose parent's bag exceeds memb_fingerprint_lds's slice
 };
 
 // Phase 1 for the instances [K0, K1) with NS successors each.  The bounds are compile-time so
@@ -154,6 +156,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MEX
   constexpr int NWP = S::NWP;
   __shared__ unsigned int lds_cnt[MA_NACT + 1];
   for (int t = threadIdx.x; t < MA_NACT + 1; t += BS) lds_cnt[t] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(&a.ctr[C_BIG], 0ull);   // (the previous chunk's list kernel is done)
   __syncthreads();
   const u64 tid = (u64)blockIdx.x * BS + threadIdx.x;
   const bool active = tid < a.chunk_count;
@@ -225,6 +228,81 @@ __global__ void __launch_bounds__(BS) memb_fingerprint(MGenArgs a) {
   { W t2; u32 e2 = 0; int k2 = k; asm volatile("" : "+v"(k2)); S::template apply<TLC>(s, k2, sub, t2, e2, a.rt); asm volatile("" :: "v"((u32)t2.hr0), "v"(t2.term), "v"(e2)); }
 #endif
   a.cand[cell] = TLC ? S::fingerprint_tlc(t, a.seed, a.rt, a.prof) : S::fingerprint_orbit(t, a.seed, a.rt);
+  }
+}
+
+// TLC's symmetry rule (the drop-in default) at 3 waves per SIMD: the same fingerprints as
+// memb_fingerprint<S, true>, with the bag out of the registers.  The parent's bag entries go from the
+// store straight to the lane's LDS slice (sorted, non-empty ones only: C3 states carry 3 messages on
+// average), the re-derivation leaves the bag change to the caller (S::apply_nobag) and it is made on
+// the slice (S::slice_with_msg / slice_without_msg), and the symmetry search and the view hash read the
+// slice (S::fingerprint_tlc_slice).  Each Work is then ~70 VGPRs smaller: 168 VGPRs and a 24-entry slice
+// (48 KB of LDS per workgroup) give 3 waves per SIMD where memb_fingerprint's 240 VGPRs and 64-KB bag
+// stage gave 2.  A parent whose bag could overflow the slice leaves its cell to memb_fingerprint_list.
+template <class S>
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(3))) memb_fingerprint_lds(MGenArgs a) {
+  using W = typename S::Work;
+  constexpr int SL = S::MK + 1 < 24 ? S::MK + 1 : 24;   // slice entries: any parent bag that fits, plus one insertion
+  __shared__ u64 sbag[SL * BS];
+  u64* const p = sbag + threadIdx.x;                    // lane-interleaved: entry q at p[q * BS]
+  const CellRegions cr(a.cell_count + 8 * blockIdx.x, 64 * S::NSLOT);
+  const u32 n = cr.n;
+  const u32* cells = a.cells + (u64)blockIdx.x * (BS * S::NSLOT);
+  for (u32 i = threadIdx.x; i < n; i += BS) {
+    const u32 cell = cells[cr.at(i)];
+    const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
+    int k, sub;
+    S::inst_of_slot((int)slot, k, sub);
+    const uint2* src = reinterpret_cast<const uint2*>(a.states + (a.chunk_begin + st) * S::NWP);
+    u32 w[S::BAGW];
+#pragma unroll
+    for (int q = 0; q < S::BAGW / 2; ++q) { const uint2 v = src[q]; w[2 * q] = v.x; w[2 * q + 1] = v.y; }
+    int len = 0;
+    bool big = false;
+#pragma unroll 1
+    for (int q = 0; q < S::MK; ++q) {   // packed entries are sorted, empty (0) ones last
+      const uint2 v = src[S::BAGW / 2 + q];
+      const u64 x = (u64)v.x | (u64)v.y << 32;
+      if (!x) break;
+      if (len < SL - 1) p[len * BS] = x; else big = true;
+      ++len;
+    }
+    if (big) { a.big[atomicAdd(&a.ctr[C_BIG], 1ull)] = cell; continue; }
+    W s, t;
+    S::unpack_nobag(w, s);
+    const int bi = k >= S::G_RECV && k < S::G_TO ? k - S::G_RECV : k >= S::G_DUP && k < S::G_DROP ? k - S::G_DUP
+                 : k >= S::G_DROP && k < S::G_ADD ? k - S::G_DROP : -1;
+    const u64 xent = bi >= 0 && bi < len ? p[bi * BS] : S::EMPTY;
+    u32 err = 0;
+    typename S::Delta d;
+    S::template apply_nobag<true>(s, k, sub, xent, t, d, err, a.rt);
+    if (d.a) S::slice_with_msg(p, BS, len, SL, d.add);
+    if (d.r) S::slice_without_msg(p, BS, len, d.rem);
+    a.cand[cell] = S::fingerprint_tlc_slice(t, p, BS, len, a.seed, a.rt);
+  }
+}
+
+// The cells memb_fingerprint_lds left (a parent bag longer than its slice): memb_fingerprint's
+// TLC-mode path, grid-stride over the list (its length on the device; usually none)
+template <class S>
+__global__ void __launch_bounds__(BS) memb_fingerprint_list(MGenArgs a) {
+  using W = typename S::Work;
+  constexpr int NWP = S::NWP;
+  const u64 n = a.ctr[C_BIG];
+  for (u64 i = (u64)blockIdx.x * BS + threadIdx.x; i < n; i += (u64)gridDim.x * BS) {
+    const u32 cell = a.big[i];
+    const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
+    int k, sub;
+    S::inst_of_slot((int)slot, k, sub);
+    u32 w[NWP];
+    const uint4* src = reinterpret_cast<const uint4*>(a.states + (a.chunk_begin + st) * NWP);
+#pragma unroll
+    for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+    W s, t;
+    S::unpack(w, s);
+    u32 err = 0;
+    S::template apply<true>(s, k, sub, t, err, a.rt);
+    a.cand[cell] = S::fingerprint_tlc(t, a.seed, a.rt);
   }
 }
 
@@ -846,6 +924,7 @@ class MembGpu : public Backend {
     HIPCHK(hipMalloc(&d_cells_, chunk_ * S::NSLOT * 4));
     HIPCHK(hipMalloc(&d_cells_oom_, chunk_ * S::NSLOT * 4));
     HIPCHK(hipMalloc(&d_cell_count_, 8 * ((chunk_ + BS - 1) / BS) * 4));
+    HIPCHK(hipMalloc(&d_big_, chunk_ * S::NSLOT * 4));
     HIPCHK(hipMalloc(&d_woff_, chunk_ * 4));
     HIPCHK(hipMalloc(&d_bsum_, SCAN_MAX_BLOCKS * 8));
     HIPCHK(hipMalloc(&d_ctr_, C_NCTR * 8));
@@ -1716,7 +1795,7 @@ class MembGpu : public Backend {
   MembText<S> text_;
   u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr;
   u64* d_cand_ = nullptr; u64* d_newrec_ = nullptr; unsigned short* d_nsucc_ = nullptr; unsigned int* d_woff_ = nullptr;
-  u32* d_cells_ = nullptr; u32* d_cells_oom_ = nullptr; u32* d_cell_count_ = nullptr;
+  u32* d_cells_ = nullptr; u32* d_cells_oom_ = nullptr; u32* d_cell_count_ = nullptr; u32* d_big_ = nullptr;
   u64* d_bsum_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_[9] = {};
@@ -1759,8 +1838,16 @@ class MembGpu : public Backend {
     if (!d_prof_) { HIPCHK(hipMalloc(&d_prof_, 8 * 8)); HIPCHK(hipMemset(d_prof_, 0, 8 * 8)); }
     g.prof = d_prof_;
 #endif
-    if (rt_dev_.sym_tlc) hipLaunchKernelGGL((memb_fingerprint<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
-    else hipLaunchKernelGGL((memb_fingerprint<S, false>), dim3(nblk), dim3(BS), 0, stream_, g);
+    g.big = d_big_;
+    if (rt_dev_.sym_tlc && !g.prof) {
+      hipLaunchKernelGGL((memb_fingerprint_lds<S>), dim3(nblk), dim3(BS), 0, stream_, g);
+      HIPCHK(hipGetLastError());
+      hipLaunchKernelGGL((memb_fingerprint_list<S>), dim3(std::min<u32>(nblk, 256u)), dim3(BS), 0, stream_, g);
+    } else if (rt_dev_.sym_tlc) {   // (RMC_FP_PROF builds: the stage timers are memb_fingerprint's)
+      hipLaunchKernelGGL((memb_fingerprint<S, true>), dim3(nblk), dim3(BS), 0, stream_, g);
+    } else {
+      hipLaunchKernelGGL((memb_fingerprint<S, false>), dim3(nblk), dim3(BS), 0, stream_, g);
+    }
     HIPCHK(hipGetLastError());
     return 0;
   }
@@ -1780,12 +1867,12 @@ class MembGpu : public Backend {
     for (void* q : {(void*)d_lvl_, (void*)d_sorted_, (void*)d_newrec_lvl_, (void*)d_sort_tmp_, (void*)d_nsucc_lvl_}) if (q) (void)hipFree(q);
     d_lvl_ = nullptr; d_sorted_ = nullptr; d_newrec_lvl_ = nullptr; d_sort_tmp_ = nullptr; d_nsucc_lvl_ = nullptr; lvl_cap_ = 0;
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_cand_, (void*)d_newrec_,
-                    (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_, (void*)d_cells_oom_, (void*)d_cell_count_})
+                    (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_, (void*)d_cells_oom_, (void*)d_cell_count_, (void*)d_big_})
       if (p) (void)hipFree(p);
     for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
     if (stream_) (void)hipStreamDestroy(stream_);
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_cand_ = nullptr; d_newrec_ = nullptr;
-    d_nsucc_ = nullptr; d_woff_ = nullptr; d_bsum_ = nullptr; d_cells_ = nullptr; d_cells_oom_ = nullptr; d_cell_count_ = nullptr; stream_ = nullptr;
+    d_nsucc_ = nullptr; d_woff_ = nullptr; d_bsum_ = nullptr; d_cells_ = nullptr; d_cells_oom_ = nullptr; d_cell_count_ = nullptr; d_big_ = nullptr; stream_ = nullptr;
   }
   // stored state `gid` (global id) and its parent pointer, from the host part or the device
   void read_state(u64 gid, W& s, u64* meta = nullptr) const {

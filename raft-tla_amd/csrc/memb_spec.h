@@ -668,7 +668,10 @@ struct Memb {
     }
     return act;
   }
-  RMC_HD static int apply_inner(const Work& s, int k, int sub, Work& t, Delta& d, u32& err, const MembRuntime& rt) {
+  // XE: the bag entry of the instance's slot (Receive / DuplicateMessage / DropMessage) is xent, not read
+  // from s.bag (memb_fingerprint_lds keeps the bag in LDS; EMPTY when the slot is past the bag's end)
+  template <bool XE = false>
+  RMC_HD static int apply_inner(const Work& s, int k, int sub, Work& t, Delta& d, u32& err, const MembRuntime& rt, u64 xent = EMPTY) {
     const u32 cfgt = rt.cfg_type;
     if (k < G_BL) {                                                   // RequestVote(i, j) :431-440
       const int i = k / N, j = k % N;
@@ -739,7 +742,7 @@ struct Memb {
       return MA_AppendEntries;
     }
     if (k < G_TO) {                                                   // Receive(m) :842-863
-      const u64 ent = sel(s.bag, k - G_RECV);
+      const u64 ent = XE ? xent : sel(s.bag, k - G_RECV);
       if (ent == EMPTY) return -1;
       return receive(s, mcode(ent), sub, t, d, err, rt);
     }
@@ -768,13 +771,13 @@ struct Memb {
       return MA_Restart;
     }
     if (k < G_DROP) {                                                 // DuplicateMessage(m), messages[m] = 1 :892-896, :926-928
-      const u64 ent = sel(s.bag, k - G_DUP);
+      const u64 ent = XE ? xent : sel(s.bag, k - G_DUP);
       if (ent == EMPTY || mcount(ent) != 1) return -1;
       d.add = mcode(ent); d.a = true;
       return MA_DuplicateMessage;
     }
     if (k < G_ADD) {                                                  // DropMessage(m), messages[m] = 1 :900-904, :930-932
-      const u64 ent = sel(s.bag, k - G_DROP);
+      const u64 ent = XE ? xent : sel(s.bag, k - G_DROP);
       if (ent == EMPTY || mcount(ent) != 1) return -1;
       d.rem = mcode(ent); d.r = true;
       return MA_DropMessage;
@@ -801,6 +804,45 @@ struct Memb {
       send(t, d, m_coc(false, i, j, i, g_term(s, i), err), err);
       return MA_DeleteServer;
     }
+  }
+
+  // The TLC-mode fingerprint kernel's re-derivation without the bag in registers (memb_fingerprint_lds):
+  // apply's successor with the bag change left in d for the caller to make on its LDS copy of the
+  // parent's bag (xent: the entry at the instance's bag slot).  Nothing after the bag change in apply
+  // reads the bag (prefix_step reads d, tlc_refine the histories), so the order is apply's.
+  template <bool HR = true>
+  RMC_HD static int apply_nobag(const Work& s, int k, int sub, u64 xent, Work& t, Delta& d, u32& err, const MembRuntime& rt) {
+    t = s;
+    d = Delta{0, 0, HK_NONE, false, false};
+    const int act = apply_inner<true>(s, k, sub, t, d, err, rt, xent);
+    if (act >= 0) {
+      if (rt.plen0 | rt.plen1) prefix_step(s, t, d, rt);
+      if (HR && rt.sym_tlc) tlc_refine(s, t, d, rt.cfg_type);
+    }
+    return act;
+  }
+  // with_msg / without_msg on a bag kept as len sorted entries p[q * stride] (a per-lane LDS slice of
+  // cap entries): the same sorted order (entry value = code << CNTB | count, codes unique) and counts
+  RMC_HD static void slice_with_msg(u64* p, int stride, int& len, int cap, u64 code) {
+    int q = 0;
+#pragma unroll 1
+    while (q < len && mcode(p[q * stride]) < code) ++q;
+    if (q < len && mcode(p[q * stride]) == code) { p[q * stride] += 1; return; }
+    if (len >= cap) return;   // (the kernel sends parents that could overflow the slice elsewhere)
+#pragma unroll 1
+    for (int r = len; r > q; --r) p[r * stride] = p[(r - 1) * stride];
+    p[q * stride] = (code << CNTB) | 1ull;
+    ++len;
+  }
+  RMC_HD static void slice_without_msg(u64* p, int stride, int& len, u64 code) {
+    int q = 0;
+#pragma unroll 1
+    while (q < len && mcode(p[q * stride]) != code) ++q;
+    if (q == len) return;
+    if (mcount(p[q * stride]) > 1) { p[q * stride] -= 1; return; }
+#pragma unroll 1
+    for (int r = q; r + 1 < len; ++r) p[r * stride] = p[(r + 1) * stride];
+    --len;
   }
 
   // ReceiveDirect(m) :842-863: UpdateTerm first, then the type handler's successors in disjunct order.
@@ -1248,7 +1290,7 @@ struct Memb {
     }
     return any;
   }
-  RMC_HD static bool has_config_entries(const Work& t, u32 cfgt) {
+  RMC_HD static bool logs_have_config(const Work& t, u32 cfgt) {
     bool any = false;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
@@ -1256,6 +1298,10 @@ struct Memb {
 #pragma unroll
       for (int p = 0; p < MAXLOG; ++p) if (p < llen(l) && etype(lent(l, p)) == cfgt) any = true;
     }
+    return any;
+  }
+  RMC_HD static bool has_config_entries(const Work& t, u32 cfgt) {
+    bool any = logs_have_config(t, cfgt);
 #pragma unroll 1
     for (int q = 0; q < MK; ++q) {
       const u64 e = sel(t.bag, q);
@@ -1370,6 +1416,32 @@ struct Memb {
     for (int q = 0; q < MK; ++q) {
       const u64 e = sel(t.bag, q);
       if (e == EMPTY) break;
+      const u64 dp = mdesc_packed(mcls(mcode(e)));
+      const int sd = CODEB + CNTB - (int)(dp & 127) - SB, ss = CODEB + CNTB - (int)((dp >> 7) & 127) - SB;
+      const int ov = (int)((dp >> 21) & 127), sv = CODEB + CNTB - ov - SB;
+      u64 x = e & ~(lomask(SB) << sd) & ~(lomask(SB) << ss);
+      if (ov) x &= ~(lomask(SB) << sv);
+      if (CE) x = (perm_entries(mcode(x), pi, cfgt) << CNTB) | (x & lomask(CNTB));
+      x |= (u64)pi_of(pi, (int)((e >> sd) & lomask(SB))) << sd | (u64)pi_of(pi, (int)((e >> ss) & lomask(SB))) << ss;
+      if (ov) x |= (u64)pi_of(pi, (int)((e >> sv) & lomask(SB))) << sv;
+      acc += fmix(x ^ seed ^ K_MSG);
+    }
+    return acc;
+  }
+  // view_hash1 with the bag read through an accessor (fingerprint_tlc: the per-lane LDS copy, so the
+  // successor's bag registers are dead once staged and a runtime entry index is one LDS read instead of
+  // a select chain over MK + 1 registers)
+  template <bool CE, class Bag>
+  RMC_HD static u64 view_hash1_bag(const Work& t, const Bag& bag, int len, u32 pi, u64 seed, u32 cfgt) {
+    u64 acc = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const LogV l = getlog(t, i);
+      acc += fmix(server_word(t, i, pi) ^ log_hash(CE ? perm_log(l, pi, cfgt) : l, seed));
+    }
+#pragma unroll 1
+    for (int q = 0; q < len; ++q) {
+      const u64 e = bag[q];
       const u64 dp = mdesc_packed(mcls(mcode(e)));
       const int sd = CODEB + CNTB - (int)(dp & 127) - SB, ss = CODEB + CNTB - (int)((dp >> 7) & 127) - SB;
       const int ov = (int)((dp >> 21) & 127), sv = CODEB + CNTB - ov - SB;
@@ -2007,9 +2079,10 @@ RMC_QLOOP
       if (ce && t.bag.v[q] != EMPTY && (!RMC_TLC_CFG_MASK || msg_has_config(mcode(t.bag.v[q]), rt.cfg_type))) cfgm |= 1u << q;
     }
     RMC_PROF_ADD(prof, 1, pt);
-    const u32 pi = tlc_min_perm(t, BagRef{base, stride, cfgm}, len, ce, rt.cfg_type, prof);
+    const BagRef bref{base, stride, cfgm};
+    const u32 pi = tlc_min_perm(t, bref, len, ce, rt.cfg_type, prof);
     pt = RMC_PROF_T();
-    const u64 best = ce ? view_hash1<true>(t, pi, seed, rt.cfg_type) : view_hash1<false>(t, pi, seed, rt.cfg_type);
+    const u64 best = ce ? view_hash1_bag<true>(t, bref, len, pi, seed, rt.cfg_type) : view_hash1_bag<false>(t, bref, len, pi, seed, rt.cfg_type);
     RMC_PROF_ADD(prof, 6, pt);
 #if defined(__HIP_DEVICE_COMPILE__) && defined(RMC_FP_DUP_MINPERM)   // timing experiment: the search twice
     { int l2 = len; asm volatile("" : "+v"(l2)); const u32 p2 = tlc_min_perm(t, BagRef{base, stride, cfgm}, l2, ce, rt.cfg_type); asm volatile("" :: "v"(p2)); }
@@ -2020,6 +2093,30 @@ RMC_QLOOP
     const u64 fp = fmix(best ^ seed);
     return fp ? fp : 1ull;
   }
+
+  // fingerprint_tlc of t whose bag is the len sorted entries p[q * stride] (memb_fingerprint_lds)
+  RMC_HD static u64 fingerprint_tlc_slice(const Work& t, u64* p, int stride, int len, u64 seed, const MembRuntime& rt) {
+    u32 cfgm = 0;
+#pragma unroll 1
+    for (int q = 0; q < len; ++q) if (msg_has_config(mcode(p[q * stride]), rt.cfg_type)) cfgm |= 1u << q;
+    const bool ce = cfgm != 0 || logs_have_config(t, rt.cfg_type);
+    const BagRef bref{p, stride, cfgm};
+    const u32 pi = tlc_min_perm(t, bref, len, ce, rt.cfg_type);
+    const u64 best = ce ? view_hash1_bag<true>(t, bref, len, pi, seed, rt.cfg_type) : view_hash1_bag<false>(t, bref, len, pi, seed, rt.cfg_type);
+    const u64 fp = fmix(best ^ seed);
+    return fp ? fp : 1ull;
+  }
+  // unpack without the bag (its words: NW - 2 * MK onwards)
+  template <int M>
+  RMC_HD static void unpack_nobag(const u32 (&w)[M], Work& t) {
+    t.term = w[0]; t.st = w[1]; t.voted = w[2]; t.commit = w[3]; t.vr = w[4]; t.vg = w[5];
+    t.nexti = (u64)w[6] | (u64)w[7] << 32; t.matchi = (u64)w[8] | (u64)w[9] << 32;
+#pragma unroll
+    for (int i = 0; i < N; ++i) { const LogV l = log_load((u64)w[10 + 2 * i] | (u64)w[11 + 2 * i] << 32); t.la.v[i] = l.a; t.lb.v[i] = l.b; }
+    t.h0 = (u64)w[10 + 2 * N] | (u64)w[11 + 2 * N] << 32; t.h1 = (u64)w[12 + 2 * N] | (u64)w[13 + 2 * N] << 32;
+    t.hr0 = (u64)w[14 + 2 * N] | (u64)w[15 + 2 * N] << 32; t.hr1 = (u64)w[16 + 2 * N] | (u64)w[17 + 2 * N] << 32;
+  }
+  static constexpr int BAGW = 18 + 2 * N;   // first packed word of the bag
 
   // ------------------------------------------------------------ pack / unpack (word aligned)
   RMC_HD static u64 log_store(LogV l) { return (l.a & lomask(MAXLOG * EW)) | ((u64)llen(l) << 60); }
