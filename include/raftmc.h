@@ -324,6 +324,13 @@ const char* mc_source_hash(void);
  * that its peers are released.  rank < 0 disables (the default).  Nothing else reads
  * it, and no environment variable does: a production run cannot trigger it by accident. */
 int mc_set_fault_injection(mc_ctx* ctx, int32_t rank, int64_t depth);
+
+/* Test support: tlc_membership's fingerprint kernel in TLC's symmetry rule keeps a parent's bag in a
+ * per-lane LDS slice and leaves a parent whose bag could overflow it to a fallback kernel (DESIGN.md
+ * §4b); this caps the slice at `entries` (0: every parent to the fallback; < 0: the compiled slice, the
+ * default) so a test drives both kernels with a shipped config.  The fingerprints are the same either
+ * way; nothing else reads it. */
+int mc_set_fp_slice(mc_ctx* ctx, int32_t entries);
 int mc_shard_layout(mc_ctx* ctx, const int64_t* frontier_counts);
 int mc_shard_select(mc_ctx* ctx, int64_t* reply_counts);
 int mc_shard_event_stats(mc_ctx* ctx, const int64_t* global_stats, int64_t* stats);

@@ -23,6 +23,7 @@ struct RunOpts {
   bool disjunct_copies = true;   // MC_COMPAT_DISJUNCT_COPIES
   // mc_set_fault_injection (tests only): rank test_fail_rank leaves the sharded loop at that depth
   int test_fail_rank = -1;
+  int test_fp_slice = -1;        // mc_set_fp_slice (tests only): tlc_membership's LDS bag slice cap
   int64_t test_fail_depth = -1;
   bool check_deadlock = false;
   int block_size = 256;

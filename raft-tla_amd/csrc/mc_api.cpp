@@ -227,6 +227,12 @@ int mc_set_fault_injection(mc_ctx* c, int32_t rank, int64_t depth) {
   return MC_OK;
 }
 
+int mc_set_fp_slice(mc_ctx* c, int32_t entries) {
+  if (!c) return MC_E_INVALID;
+  c->ro.test_fp_slice = entries < 0 ? -1 : entries;
+  return MC_OK;
+}
+
 namespace {
 // mc_opts.n_gpus > 1: the sharded BFS (owner-partitioned fingerprints) inside this
 // process, one host thread per GPU running the backend's native level loop (raft_original:

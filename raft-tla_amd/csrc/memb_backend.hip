@@ -80,6 +80,7 @@ struct MGenArgs {
   unsigned long long* ctr;
   unsigned long long* prof;                // RMC_FP_PROF builds: wave cycles per fingerprint stage (else null)
   u32* big;                                // TLC mode: cells whose parent's bag exceeds memb_fingerprint_lds's slice
+  u32 slice_cap;                           // parent bag entries memb_fingerprint_lds keeps (<= its slice - 1)
 };
 
 // Phase 1 for the instances [K0, K1) with NS successors each.  The bounds are compile-time so
@@ -243,6 +244,7 @@ template <class S>
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(3))) memb_fingerprint_lds(MGenArgs a) {
   using W = typename S::Work;
   constexpr int SL = S::MK + 1 < 24 ? S::MK + 1 : 24;   // slice entries: any parent bag that fits, plus one insertion
+                                                        // (a.slice_cap <= SL - 1 of them hold the parent's)
   __shared__ u64 sbag[SL * BS];
   u64* const p = sbag + threadIdx.x;                    // lane-interleaved: entry q at p[q * BS]
   const CellRegions cr(a.cell_count + 8 * blockIdx.x, 64 * S::NSLOT);
@@ -264,7 +266,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(3))) me
       const uint2 v = src[S::BAGW / 2 + q];
       const u64 x = (u64)v.x | (u64)v.y << 32;
       if (!x) break;
-      if (len < SL - 1) p[len * BS] = x; else big = true;
+      if (len < (int)a.slice_cap) p[len * BS] = x; else big = true;
       ++len;
     }
     if (big) { a.big[atomicAdd(&a.ctr[C_BIG], 1ull)] = cell; continue; }
@@ -947,6 +949,7 @@ class MembGpu : public Backend {
     if (int rc = ensure_alloc(o, err)) return rc;
     if (int rc = prepare_prefixes(err)) return rc;
     rt_host_.sym_tlc = rt_dev_.sym_tlc = (o.sym_tlc && m_.rt.symmetry) ? 1u : 0u;
+    fp_slice_test_ = o.test_fp_slice;
     rt_host_.disjunct_copies = rt_dev_.disjunct_copies = o.disjunct_copies ? 1u : 0u;
     auto t0 = std::chrono::steady_clock::now();
     HIPCHK(hipMemsetAsync(d_table_, 0, (table_mask_ + 1) * 16, stream_));
@@ -1415,6 +1418,7 @@ class MembGpu : public Backend {
     if (int rc = ensure_alloc(so, err)) return rc;
     if (int rc = prepare_prefixes(err)) return rc;
     rt_host_.sym_tlc = rt_dev_.sym_tlc = (o.sym_tlc && m_.rt.symmetry) ? 1u : 0u;
+    fp_slice_test_ = o.test_fp_slice;
     rt_host_.disjunct_copies = rt_dev_.disjunct_copies = o.disjunct_copies ? 1u : 0u;
     sopts_ = o; s_rank_ = rank; s_world_ = world; s_finished_ = false; have_viol_ = false; sres_err_ = 0; sharded_ = true;
     // level records / sorted winners / newrec: lvl_cap_ entries each, plus the sort's scratch
@@ -1796,6 +1800,7 @@ class MembGpu : public Backend {
   u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr;
   u64* d_cand_ = nullptr; u64* d_newrec_ = nullptr; unsigned short* d_nsucc_ = nullptr; unsigned int* d_woff_ = nullptr;
   u32* d_cells_ = nullptr; u32* d_cells_oom_ = nullptr; u32* d_cell_count_ = nullptr; u32* d_big_ = nullptr;
+  int fp_slice_test_ = -1;   // RunOpts::test_fp_slice of the current run
   u64* d_bsum_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t ev_[9] = {};
@@ -1839,6 +1844,11 @@ class MembGpu : public Backend {
     g.prof = d_prof_;
 #endif
     g.big = d_big_;
+    {   // room for one insertion; mc_set_fp_slice (tests) lowers the cap
+      const int full = (S::MK + 1 < 24 ? S::MK + 1 : 24) - 1;
+      const int t = fp_slice_test_;
+      g.slice_cap = (u32)(t >= 0 && t < full ? t : full);
+    }
     if (rt_dev_.sym_tlc && !g.prof) {
       hipLaunchKernelGGL((memb_fingerprint_lds<S>), dim3(nblk), dim3(BS), 0, stream_, g);
       HIPCHK(hipGetLastError());

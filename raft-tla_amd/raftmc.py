@@ -31,7 +31,7 @@ EXPORTS = ["mc_opts_init", "mc_default_opts", "mc_open", "mc_run", "mc_summary",
            "mc_shard_level_stats", "mc_shard_level_commit", "mc_shard_read_state", "mc_shard_violation",
            "mc_set_history_prefix", "mc_shard_layout", "mc_shard_select", "mc_shard_event_stats",
            "mc_collision_observed", "mc_rccl_unique_id", "mc_shard_run_rccl", "mc_shard_run_loopback",
-           "mc_set_checkpoint", "mc_set_recover", "mc_action_location", "mc_source_hash", "mc_set_fault_injection", "mc_release_device_memory"]
+           "mc_set_checkpoint", "mc_set_recover", "mc_action_location", "mc_source_hash", "mc_set_fault_injection", "mc_release_device_memory", "mc_set_fp_slice"]
 
 
 class McOpts(ctypes.Structure):
@@ -122,6 +122,7 @@ def load_library(path=LIB_PATH):
     lib.mc_set_checkpoint.argtypes = [P, ctypes.c_char_p, ctypes.c_int32]
     lib.mc_set_recover.argtypes = [P, ctypes.c_char_p]
     lib.mc_set_fault_injection.argtypes = [P, ctypes.c_int32, ctypes.c_int64]
+    lib.mc_set_fp_slice.argtypes = [P, ctypes.c_int32]
     lib.mc_release_device_memory.argtypes = [P]
     lib.mc_exit_code.argtypes = [P]
     lib.mc_free.argtypes = [P]
@@ -217,6 +218,12 @@ class ModelChecker:
     def set_fault_injection(self, rank, depth):
         """Tests only: in the next sharded run rank `rank` leaves the level loop at `depth` (rank < 0: off)."""
         rc = self.lib.mc_set_fault_injection(self.h, rank, depth)
+        if rc:
+            raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
+
+    def set_fp_slice(self, entries):
+        """Tests only: cap tlc_membership's LDS bag slice (0: every parent to the fallback kernel; < 0: default)."""
+        rc = self.lib.mc_set_fp_slice(self.h, entries)
         if rc:
             raise RaftMCError(rc, self.lib.mc_last_error(self.h).decode())
 

@@ -323,6 +323,24 @@ def test_disjunct_copies_switch(raftmc, mode):
     assert r.actions == g["actions"]
 
 
+@pytest.mark.parametrize("cap", [0, 2])
+def test_fp_slice_fallback(raftmc, cap):
+    """TLC-mode fingerprints come from memb_fingerprint_lds, which keeps a parent's bag in an LDS slice and
+    leaves a parent whose bag could overflow it to memb_fingerprint_list (the register-bag path).  No
+    shipped config fills the slice, so mc_set_fp_slice caps it: 0 sends every parent to the fallback, 2 those
+    with more than two messages (a mix of both kernels in every chunk).  Counts, levels and per-action
+    counts equal the oracle's NextDynamic fixture (tests/golden/disjunct_copies.json) either way."""
+    fx = json.load(open(os.path.join(GOLDEN, "disjunct_copies.json")))
+    g = fx["copies"]
+    with raftmc.ModelChecker(MEMB_MC, os.path.join(CONFIGS, fx["cfg"]), max_depth=fx["max_depth"], deadlock=False, **SMALL) as mc:
+        mc.set_fp_slice(cap)
+        r = mc.run()
+    assert r.verdict in ("OK", "DEPTH_LIMIT"), r.error
+    assert (r.generated, r.distinct, r.depth, r.left_on_queue) == (g["generated"], g["distinct"], g["depth"], g["left_on_queue"])
+    assert [lv[0] for lv in r.levels] == g["levels"]
+    assert r.actions == g["actions"]
+
+
 def test_cwcl_count_claim(raftmc):
     """The reference's count claim, tlc_membership/raft.tla:1188-1191: "there are over 1.2 million traces
     of length 20 that satisfy CommitWhenConcurrentLeaders_constraint".  The shipped model with that
