@@ -19,7 +19,7 @@ db() { find $1 -name "*.db" | head -1; }
 cd $R
 python3 scripts/rocpd_summary.py stats $(db $O/stats) $O/${TAG}_c3_memb_kernel_stats.csv &&
 python3 scripts/rocpd_summary.py traffic $(db $O/fetch) $(db $O/write) memb_fingerprint $O/traffic_${TAG}_c3_fingerprint.json memb_four.cfg &&
-python3 scripts/rocpd_summary.py traffic $(db $O/fetch) $(db $O/write) memb_dedup $O/traffic_${TAG}_c3_dedup.json memb_four.cfg &&
+python3 scripts/rocpd_summary.py traffic $(db $O/fetch) $(db $O/write) memb_dedup $O/traffic_${TAG}_c3_dedup.json memb_four.cfg --random &&
 python3 scripts/rocpd_summary.py valu $(db $O/sq) memb_fingerprint $O/valu_${TAG}_c3_fingerprint.json memb_four.cfg &&
 python3 scripts/rocpd_summary.py valu $(db $O/sq) memb_expand $O/valu_${TAG}_c3_expand.json memb_four.cfg &&
 python3 scripts/pmc_table.py $(db $O/sq) > $O/${TAG}_c3_sq_table.txt
