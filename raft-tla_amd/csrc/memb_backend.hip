@@ -105,15 +105,20 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
       S::launder(s);
       bool need = false, oom = false;
       if (active) {
+        // the successor without its bag (round 6): the constraints read the bag's total and RequestVote
+        // counts, which S::in_model_delta takes from the parent's bag and the change d, so no successor
+        // bag is built (with_msg's sorted insertion over MK + 1 registers)
         W t;
-        const int act = S::template apply<false>(s, k, sub, t, err, a.rt);
+        typename S::Delta d;
+        const int bi = S::bag_slot_of(k);
+        const u64 xent = bi >= 0 ? sel(s.bag, bi) : S::EMPTY;
+        const int act = S::template apply_nobag<false>(s, k, sub, xent, t, d, err, a.rt);
         if (act >= 0) {
           // TLC's generated counters: the copies a disjunctive guard enumerates (S::tlc_copies)
-          const int cp = (act == MA_HandleCheckOldConfig || act == MA_HandleCatchupResponse) ? S::tlc_copies(s, k, sub, a.rt) : 1;
+          const int cp = (act == MA_HandleCheckOldConfig || act == MA_HandleCatchupResponse) ? S::template tlc_copies<true>(s, k, sub, a.rt, xent) : 1;
           nsucc += (u32)cp;
           atomicAdd(&lds_cnt[act], (unsigned)cp);
-          if (S::in_model(t, s, a.rt)) {
-            if (t.bag.v[S::MK] != S::EMPTY) err |= ME_CAP;           // bag domain beyond the compiled capacity
+          if (S::in_model_delta(t, s, d, a.rt, err)) {   // (also flags a bag beyond the compiled capacity)
             need = true;
             ++nin;
           } else if (a.inv_oom) {
@@ -272,8 +277,7 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(3))) me
     if (big) { a.big[atomicAdd(&a.ctr[C_BIG], 1ull)] = cell; continue; }
     W s, t;
     S::unpack_nobag(w, s);
-    const int bi = k >= S::G_RECV && k < S::G_TO ? k - S::G_RECV : k >= S::G_DUP && k < S::G_DROP ? k - S::G_DUP
-                 : k >= S::G_DROP && k < S::G_ADD ? k - S::G_DROP : -1;
+    const int bi = S::bag_slot_of(k);
     const u64 xent = bi >= 0 && bi < len ? p[bi * BS] : S::EMPTY;
     u32 err = 0;
     typename S::Delta d;
@@ -312,7 +316,7 @@ __global__ void __launch_bounds__(BS) memb_fingerprint_list(MGenArgs a) {
 // first violation / evaluation error in key order becomes the level's event.
 template <class S>
 #ifndef RMC_MOOM_WAVES
-#define RMC_MOOM_WAVES 3   // memb_oom_check at 3 waves per SIMD (148 VGPRs, no spill): C3 0.88-0.92 vs 0.89-0.94 s
+#define RMC_MOOM_WAVES 4   // memb_oom_check at 4 waves per SIMD (round 6, without the bag: 128 VGPRs, no spill)
 #endif
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MOOM_WAVES))) memb_oom_check(MGenArgs a) {
   using W = typename S::Work;
@@ -325,14 +329,19 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MOO
   const u64 slot = cell / a.chunk_count, st = cell - slot * a.chunk_count;
   int k, sub;
   S::inst_of_slot((int)slot, k, sub);
-  u32 w[NWP];
-  const uint4* src = reinterpret_cast<const uint4*>(a.states + (a.chunk_begin + st) * NWP);
+  // no invariant reads the bag: the parent's words before it and the one entry the instance reads
+  const uint2* src = reinterpret_cast<const uint2*>(a.states + (a.chunk_begin + st) * NWP);
+  u32 w[S::BAGW];
 #pragma unroll
-  for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+  for (int q = 0; q < S::BAGW / 2; ++q) { const uint2 v = src[q]; w[2 * q] = v.x; w[2 * q + 1] = v.y; }
+  const int bi = S::bag_slot_of(k);
+  u64 xent = S::EMPTY;
+  if (bi >= 0) { const uint2 v = src[S::BAGW / 2 + bi]; const u64 x = (u64)v.x | (u64)v.y << 32; xent = x ? x : S::EMPTY; }
   W s, t;
-  S::unpack(w, s);
+  S::unpack_nobag(w, s);
   u32 err = 0;
-  S::template apply<false>(s, k, sub, t, err, a.rt);
+  typename S::Delta d;
+  S::template apply_nobag<false>(s, k, sub, xent, t, d, err, a.rt);
   const u32 r = S::check_invariants(t, a.rt);
   if (r) {
     const u64 e = (((a.rank0 + st) * (u64)S::NSLOT + slot) << 2) | ((r >> 8) == IV_BAD ? EV_VIOLATION : EV_INV_ERROR);

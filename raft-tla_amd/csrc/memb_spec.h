@@ -821,6 +821,10 @@ struct Memb {
     }
     return act;
   }
+  // the bag slot instance k reads (Receive / DuplicateMessage / DropMessage), -1 for the others
+  RMC_HD static int bag_slot_of(int k) {
+    return k >= G_RECV && k < G_TO ? k - G_RECV : k >= G_DUP && k < G_DROP ? k - G_DUP : k >= G_DROP && k < G_ADD ? k - G_DROP : -1;
+  }
   // with_msg / without_msg on a bag kept as len sorted entries p[q * stride] (a per-lane LDS slice of
   // cap entries): the same sorted order (entry value = code << CNTB | count, codes unique) and counts
   RMC_HD static void slice_with_msg(u64* p, int stride, int& len, int cap, u64 code) {
@@ -853,9 +857,10 @@ struct Memb {
   // m.mterm = currentTerm[i]` (raft.tla:796) and HandleCatchupResponse's five-way list (:783-789).
   // The copies are one state, so only TLC's generated counters see them (distinct states, levels and
   // traces do not); the generic front end, which follows the text, counts them the same way.
-  RMC_HD static int tlc_copies(const Work& s, int k, int sub, const MembRuntime& rt) {
+  template <bool XE = false>
+  RMC_HD static int tlc_copies(const Work& s, int k, int sub, const MembRuntime& rt, u64 xent = EMPTY) {
     if (!rt.disjunct_copies || k < G_RECV || k >= G_TO) return 1;
-    const u64 ent = sel(s.bag, k - G_RECV);
+    const u64 ent = XE ? xent : sel(s.bag, k - G_RECV);
     if (ent == EMPTY) return 1;
     const u64 m = mcode(ent);
     const int cls = mcls(m);
@@ -1008,15 +1013,44 @@ struct Memb {
 
   // ------------------------------------------------------------ constraints (cfg CONSTRAINTS) and action constraints
   RMC_HD static bool in_model(const Work& t, const Work& s, const MembRuntime& rt) {
-    const u32 c = rt.constraints;
-    bool ok = true;
-    int tot = 0, sumr = 0, sumt = 0, cand = 0;
-    bool rv1 = true, anyr = false;
+    int tot = 0;
+    bool rv1 = true;
 #pragma unroll
     for (int q = 0; q < MK + 1; ++q) {
       const u64 e = t.bag.v[q];
       if (e != EMPTY) { tot += mcount(e); if (mcls(mcode(e)) == K_RVQ && mcount(e) > 1) rv1 = false; }
     }
+    return in_model_bag(t, s, rt, tot, rv1);
+  }
+  // in_model of t = (s's successor by apply_nobag, bag change d) from s's bag and d, without t's bag:
+  // the message total and RequestVote singleness of t's bag (with_msg then without_msg, as apply).  err
+  // gets what apply and the expand kernel flag: a count beyond its field (with_msg, any successor) and,
+  // for an in-model successor, a bag of more than MK messages (the expand kernel's check of entry MK)
+  RMC_HD static bool in_model_delta(const Work& t, const Work& s, const Delta& d, const MembRuntime& rt, u32& err) {
+    int tot = 0, n = 0;
+    bool rv1 = true, found = false;
+#pragma unroll
+    for (int q = 0; q < MK; ++q) {
+      const u64 e = s.bag.v[q];
+      if (e == EMPTY) continue;
+      const u64 code = mcode(e);
+      int c = mcount(e);
+      if (d.a && code == d.add) { found = true; if (c + 1 > (int)lomask(CNTB)) err |= ME_CAP; ++c; }
+      if (d.r && code == d.rem) --c;
+      tot += c;
+      n += c > 0;   // (without_msg removes a message whose count reaches zero)
+      if (mcls(code) == K_RVQ && c > 1) rv1 = false;
+    }
+    if (d.a && !found && !(d.r && d.rem == d.add)) { ++tot; ++n; }
+    const bool ok = in_model_bag(t, s, rt, tot, rv1);
+    if (ok && n > MK) err |= ME_CAP;
+    return ok;
+  }
+  RMC_HD static bool in_model_bag(const Work& t, const Work& s, const MembRuntime& rt, int tot, bool rv1) {
+    const u32 c = rt.constraints;
+    bool ok = true;
+    int sumr = 0, sumt = 0, cand = 0;
+    bool anyr = false;
 #pragma unroll
     for (int i = 0; i < N; ++i) {
       sumr += restarted(t, i); sumt += timeouts(t, i); anyr |= restarted(t, i) != 0;
