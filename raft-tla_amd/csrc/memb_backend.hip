@@ -500,21 +500,31 @@ __global__ void __launch_bounds__(BS) memb_materialize(MMatArgs a) {
     const int slot = (int)(rec & 1023);
     int k, sub;
     S::inst_of_slot(slot, k, sub);
-    u32 w[NWP];
-    const uint4* src = reinterpret_cast<const uint4*>(a.states + gid * NWP);
+    // the state without its bag in registers (round 6): the words before the bag and the one entry the
+    // instance reads; the successor's bag goes from the parent's packed entries to the store in one merge
+    // pass with the change (S::bag_merge), its other words packed (no invariant reads the bag)
+    const u32* src = a.states + gid * NWP;
+    u32 w[S::BAGW];
 #pragma unroll
-    for (int q = 0; q < NWP / 4; ++q) { const uint4 v = src[q]; w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w; }
+    for (int q = 0; q < S::BAGW / 2; ++q) { const uint2 v = reinterpret_cast<const uint2*>(src)[q]; w[2 * q] = v.x; w[2 * q + 1] = v.y; }
+    const u64* pbag = reinterpret_cast<const u64*>(src + S::BAGW);
+    const int bi = S::bag_slot_of(k);
+    u64 xent = S::EMPTY;
+    if (bi >= 0) { const u64 x = pbag[bi]; xent = x ? x : S::EMPTY; }
     W s, t;
-    S::unpack(w, s);
-    const int act = S::template apply<TLC>(s, k, sub, t, err, a.rt);
+    S::unpack_nobag(w, s);
+    typename S::Delta d;
+    const int act = S::template apply_nobag<TLC>(s, k, sub, xent, t, d, err, a.rt);
     const u64 dst = a.dst_base + i;
     if (act >= 0 && dst < a.cap) {
-      u32 pw[NW];
-      S::pack(t, pw);
-      uint4* o = reinterpret_cast<uint4*>(a.states + dst * NWP);
+      u32 pw[S::BAGW];
+      S::pack_nobag(t, pw);
+      u32* o = a.states + dst * NWP;
 #pragma unroll
-      for (int q = 0; q < NWP / 4; ++q)
-        o[q] = make_uint4(pw[4 * q], 4 * q + 1 < NW ? pw[4 * q + 1] : 0u, 4 * q + 2 < NW ? pw[4 * q + 2] : 0u, 4 * q + 3 < NW ? pw[4 * q + 3] : 0u);
+      for (int q = 0; q < S::BAGW / 2; ++q) reinterpret_cast<uint2*>(o)[q] = make_uint2(pw[2 * q], pw[2 * q + 1]);
+      S::bag_merge(pbag, reinterpret_cast<u64*>(o + S::BAGW), d, err);
+#pragma unroll
+      for (int q = NW; q < NWP; ++q) o[q] = 0u;
       a.meta[dst] = ((gid | a.gid_tag) << 20) | ((u64)act << 10) | (u64)slot;
       atomicAdd(&lds_cnt[act], 1u);
       const u32 r = S::check_invariants(t, a.rt);

@@ -2151,6 +2151,37 @@ RMC_QLOOP
     t.hr0 = (u64)w[14 + 2 * N] | (u64)w[15 + 2 * N] << 32; t.hr1 = (u64)w[16 + 2 * N] | (u64)w[17 + 2 * N] << 32;
   }
   static constexpr int BAGW = 18 + 2 * N;   // first packed word of the bag
+  // pack without the bag (words [0, BAGW))
+  RMC_HD static void pack_nobag(const Work& t, u32 (&w)[BAGW]) {
+    w[0] = t.term; w[1] = t.st; w[2] = t.voted; w[3] = t.commit; w[4] = t.vr; w[5] = t.vg;
+    w[6] = (u32)t.nexti; w[7] = (u32)(t.nexti >> 32); w[8] = (u32)t.matchi; w[9] = (u32)(t.matchi >> 32);
+#pragma unroll
+    for (int i = 0; i < N; ++i) { const u64 x = log_store(LogV{t.la.v[i], t.lb.v[i]}); w[10 + 2 * i] = (u32)x; w[11 + 2 * i] = (u32)(x >> 32); }
+    w[10 + 2 * N] = (u32)t.h0; w[11 + 2 * N] = (u32)(t.h0 >> 32); w[12 + 2 * N] = (u32)t.h1; w[13 + 2 * N] = (u32)(t.h1 >> 32);
+    w[14 + 2 * N] = (u32)t.hr0; w[15 + 2 * N] = (u32)(t.hr0 >> 32); w[16 + 2 * N] = (u32)t.hr1; w[17 + 2 * N] = (u32)(t.hr1 >> 32);
+  }
+  // the successor's packed bag from the parent's (MK sorted entries, 0 = empty, last) and apply's change
+  // d: with_msg then without_msg as one merge pass, entry by entry (the bag never held in registers).
+  // err: with_msg's count overflow and an (MK+1)-th message (that entry is dropped: expand reports it too)
+  RMC_HD static void bag_merge(const u64* in, u64* out, const Delta& d, u32& err) {
+    const u64 xa = (d.add << CNTB) | 1ull;
+    bool pend = d.a;   // the new message not yet placed (or counted into its existing entry)
+    int o = 0;
+    auto emit = [&](u64 x) { if (o < MK) out[o] = x; else err |= ME_CAP; ++o; };
+#pragma unroll 1
+    for (int q = 0; q < MK; ++q) {
+      u64 x = in[q];
+      if (!x) break;
+      const u64 code = mcode(x);
+      if (pend && d.add < code) { if (!(d.r && d.rem == d.add)) emit(xa); pend = false; }
+      if (pend && code == d.add) { if (mcount(x) + 1 > (int)lomask(CNTB)) err |= ME_CAP; x += 1; pend = false; }
+      if (d.r && code == d.rem) { if (mcount(x) <= 1) continue; x -= 1; }
+      emit(x);
+    }
+    if (pend && !(d.r && d.rem == d.add)) emit(xa);
+#pragma unroll 1
+    for (; o < MK; ++o) out[o] = 0ull;
+  }
 
   // ------------------------------------------------------------ pack / unpack (word aligned)
   RMC_HD static u64 log_store(LogV l) { return (l.a & lomask(MAXLOG * EW)) | ((u64)llen(l) << 60); }
