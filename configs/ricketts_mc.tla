@@ -16,4 +16,7 @@ BoundedMessages == BagCardinality(messages) <= MaxMsgs
 
 \* Test-only scenario invariant (reachable): no leader ever.
 NoLeader == ~ \E i \in Server : state[i] = Leader
+
+\* Test-only negative control of TypeOK's function-set form: terms stay in 0..1 (false after the first Timeout).
+BadTerm == currentTerm \in [Server -> 0..1]
 =============================================================================

@@ -28,6 +28,11 @@ SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing
           ("ricketts_election_safety", "configs/ricketts_mc.tla", "configs/ricketts_election_safety.cfg"),
           ("ricketts_safety", "configs/ricketts_mc.tla", "configs/ricketts_safety.cfg"),
           ("toy_ring_view", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing_view.cfg"),
+          ("funsets", "configs/tlagen/FunSets.tla", "configs/tlagen/FunSets.cfg"),
+          ("funsets_fbelow2", "configs/tlagen/FunSets.tla", "configs/tlagen/FunSets_FBelow2.cfg"),
+          ("funsets_qempty", "configs/tlagen/FunSets.tla", "configs/tlagen/FunSets_QEmpty.cfg"),
+          ("ricketts_typeok", "configs/ricketts_mc.tla", "configs/ricketts_typeok.cfg"),
+          ("ricketts_badterm", "configs/ricketts_mc.tla", "configs/ricketts_badterm.cfg"),
           ("rec_fun", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun.cfg"),
           ("rec_fun_fact", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_fact.cfg"),
           ("rec_fun_sum", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_sum.cfg"),

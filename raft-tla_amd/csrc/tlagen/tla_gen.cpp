@@ -511,6 +511,17 @@ struct Gen {
         return "apply(A, " + ex(n.a[0], sc) + ", " + ex(n.a[1], sc) + ")";
       }
       case K::Dot: return "apply(A, " + ex(n.a[0], sc) + ", mk_atom(A, " + std::to_string(str_atom(n.s)) + "u))";
+      case K::FunSet: return "fun_set(A, " + ex(n.a[0], sc) + ", " + ex(n.a[1], sc) + ")";
+      case K::RecordSet: {
+        const std::string m = fresh("m");
+        std::string o = "[&]() -> u32 { const u32 " + m + " = A.htop;\n";
+        for (size_t i = 0; i < n.fields.size(); ++i) {
+          const std::string kv = fresh("k");
+          o += " { const u32 " + kv + " = mk_atom(A, " + std::to_string(str_atom(n.fields[i])) + "u); const u32 v_ = " + ex(n.a[i], sc) +
+               "; hpush(A, " + kv + "); hpush(A, v_); }\n";
+        }
+        return o + " return rec_set(A, " + m + ");\n}()";
+      }
       case K::Record: {
         const std::string m = fresh("m");
         const bool big = node_count(e) >= kOutlineCtor;
@@ -552,10 +563,103 @@ struct Gen {
     return o + " } }\n";
   }
 
+  // Sets a membership test should not build: function sets, record sets, Seq(S), Nat / Int, and unions,
+  // filters, SUBSET and definitions of them (TypeOK-style predicates: raft_dricketts.tla:482-492)
+  bool lazy_set(const NP& r, int depth = 0) {
+    if (!r || depth > 32) return false;
+    switch (r->k) {
+      case K::FunSet: case K::RecordSet: return true;
+      case K::Ident:
+        if (r->s == "Nat" || r->s == "Int") return !global(r->s);
+        if (auto d = global(r->s)) return d->params.empty() && d->body && !recursive_fun(*d) && lazy_set(d->body, depth + 1);
+        return false;
+      case K::OpApp: return r->s == "Seq" && r->a.size() == 1 && !global(r->s);
+      case K::Binary: return r->s == "\\cup" && (lazy_set(r->a[0], depth + 1) || lazy_set(r->a[1], depth + 1));
+      case K::SetFilter: return r->binds.size() == 1 && r->binds[0].names.size() == 1 && lazy_set(r->binds[0].set, depth + 1);
+      case K::Unary: return r->s == "SUBSET" && lazy_set(r->a[0], depth + 1);
+      default: return false;
+    }
+  }
+  // the elements of a set or sequence value xv, one at a time as `el` (a loop statement)
+  std::string coll_loop(const std::string& xv, const std::string& el, const std::string& body) {
+    const std::string i = fresh("i"), n = fresh("n"), st = fresh("t");
+    return "{ u32 " + el + " = first(" + xv + ");\n for (u32 " + i + " = 0, " + n + " = count(A, " + xv + "); " + i + " < " + n + "; ++" +
+           i + ", " + el + " = nextv(A, " + el + ")) {\n const u32 " + st + " = A.top;\n" + body + " A.top = " + st + ";\n } }\n";
+  }
+  // x \in r as a C++ bool expression, x an evaluated value handle (a C++ name).  The lazy_set forms are
+  // tested without being built, as TLC evaluates such a membership (x \in [S -> Nat] works although
+  // [S -> Nat] is infinite): a function set by its domain and then every value against the range, a
+  // record set field by field, Seq(S) element by element, a union by either side, a filter by its base
+  // set and predicate, SUBSET S element by element, a definition by its body
+  std::string member_of(const std::string& xv, const NP& r, Scope& sc, int depth = 0) {
+    if (r->k == K::Ident && !find(sc, r->s) && !global(r->s)) {
+      if (r->s == "Nat") return "(tg(A, " + xv + ") == T_INT && ival(A, " + xv + ") >= 0)";
+      if (r->s == "Int") return "(tg(A, " + xv + ") == T_INT)";
+    }
+    if (depth < 32 && lazy_set(r)) {
+      if (r->k == K::Ident && !find(sc, r->s)) {   // a definition: its body, in the module's scope
+        Scope top;
+        return member_of(xv, global(r->s)->body, top, depth + 1);
+      }
+      if (r->k == K::Binary && r->s == "\\cup")
+        return "(" + member_of(xv, r->a[0], sc, depth + 1) + " || " + member_of(xv, r->a[1], sc, depth + 1) + ")";
+      if (r->k == K::SetFilter) {
+        Scope s2 = sc;
+        Sym b; b.cxx = xv;
+        s2.push_back({r->binds[0].names[0], b});
+        return "(" + member_of(xv, r->binds[0].set, sc, depth + 1) + " && truth(A, " + ex(r->a[0], s2) + "))";
+      }
+      if (r->k == K::OpApp && r->s == "Seq") {
+        const std::string el = fresh("e");
+        return "[&]() -> bool { if (tg(A, " + xv + ") != T_SEQ) return false;\n" +
+               coll_loop(xv, el, " if (!(" + member_of(el, r->a[0], sc, depth + 1) + ")) return false;\n") + " return true; }()";
+      }
+      if (r->k == K::Unary && r->s == "SUBSET") {
+        const std::string el = fresh("e");
+        return "[&]() -> bool { if (tg(A, " + xv + ") != T_SET) return false;\n" +
+               coll_loop(xv, el, " if (!(" + member_of(el, r->a[0], sc, depth + 1) + ")) return false;\n") + " return true; }()";
+      }
+    }
+    if (r->k == K::Unary && r->s == "DOMAIN") return "in_dom(A, " + ex(r->a[0], sc) + ", " + xv + ")";
+    if (r->k == K::Unary && r->s == "SUBSET") return "(tg(A, " + xv + ") == T_SET && set_subseteq(A, " + xv + ", " + ex(r->a[0], sc) + "))";
+    if (r->k == K::Binary && r->s == "..")
+      return "[&]() -> bool { if (tg(A, " + xv + ") != T_INT) return false; const i64 v_ = ival(A, " + xv + "); return v_ >= ival(A, " +
+             ex(r->a[0], sc) + ") && v_ <= ival(A, " + ex(r->a[1], sc) + "); }()";
+    if (r->k == K::FunSet) {   // [S -> T]: a function (or sequence) with domain S and every value in T
+      const std::string k = fresh("e"), v = fresh("v");
+      const std::string body = " { const u32 " + v + " = apply(A, " + xv + ", " + k + "); if (!(" + member_of(v, r->a[1], sc, depth + 1) +
+                               ")) return false; }\n";
+      return "[&]() -> bool { const u32 t_ = tg(A, " + xv + "); if (t_ != T_FUN && t_ != T_SEQ) return false;\n"
+             " if (!eqv(A, dom(A, " + xv + "), " + ex(r->a[0], sc) + ")) return false;\n" +
+             set_loop("dom(A, " + xv + ")", k, body, true) + " return true; }()";
+    }
+    if (r->k == K::RecordSet) {   // [f1 : S1, ...]: a record with exactly these fields, each in its set
+      std::string o = "[&]() -> bool { if (tg(A, " + xv + ") != T_FUN || coll_card(A, " + xv + ") != " +
+                      std::to_string(r->fields.size()) + "u) return false;\n";
+      for (size_t i = 0; i < r->fields.size(); ++i) {
+        const std::string key = "mk_atom(A, " + std::to_string(str_atom(r->fields[i])) + "u)", v = fresh("v");
+        o += " { const u32 k_ = " + key + "; if (!in_dom(A, " + xv + ", k_)) return false; const u32 " + v + " = apply(A, " + xv +
+             ", k_); if (!(" + member_of(v, r->a[i], sc, depth + 1) + ")) return false; }\n";
+      }
+      return o + " return true; }()";
+    }
+    return "set_in(A, " + xv + ", " + ex(r, sc) + ")";
+  }
+
   std::string binary(const Node& n, Scope& sc) {
     const std::string& op = n.s;
     const NP& l = n.a[0];
     const NP& r = n.a[1];
+    if (op == "\\subseteq" && lazy_set(r)) {   // x \subseteq S: every element of x in S (S never built)
+      const std::string xv = fresh("x"), el = fresh("e");
+      return "[&]() -> u32 { const u32 " + xv + " = " + ex(l, sc) + "; if (tg(A, " + xv + ") != T_SET) { A.err |= E_TYPE; return 0u; }\n" +
+             coll_loop(xv, el, " if (!(" + member_of(el, r, sc) + ")) return 0u;\n") + " return 2u; }()";
+    }
+    if ((op == "\\in" || op == "\\notin") && lazy_set(r) && !(r->k == K::Ident && (r->s == "Nat" || r->s == "Int"))) {
+      const std::string xv = fresh("x");
+      return "[&]() -> u32 { const u32 " + xv + " = " + ex(l, sc) + "; return mk_bool(" + (op == "\\notin" ? "!" : "") +
+             member_of(xv, r, sc) + "); }()";
+    }
     if (op == "\\in" || op == "\\notin") {
       const std::string neg = op == "\\notin" ? "!" : "";
       if (r->k == K::Ident && !find(sc, r->s) && !global(r->s)) {

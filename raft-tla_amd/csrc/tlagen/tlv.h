@@ -332,6 +332,61 @@ TLV_NI u32 union_all(Ar& a, u32 s) {   // UNION s
   return set_end(a, mark);
 }
 
+// [S -> T]: every function from S to T, |T|^|S| of them (more than 2^20: E_UNSUP).  A membership test
+// x \in [S -> T] never builds it (the generated code tests the domain and each value instead).
+TLV_NI u32 fun_set(Ar& a, u32 s, u32 t) {
+  if (tg(a, s) != T_SET || tg(a, t) != T_SET) { a.err |= E_TYPE; return s; }
+  const u32 n = count(a, s), m = count(a, t);
+  u64 total = 1;
+  for (u32 i = 0; i < n; ++i) { total *= m; if (total > (1ull << 20)) { a.err |= E_UNSUP; return s; } }
+  const u32 base = a.htop;   // the elements of S, then of T, as indexable handles
+  u32 e = first(s);
+  for (u32 i = 0; i < n; ++i, e = nextv(a, e)) hpush(a, e);
+  e = first(t);
+  for (u32 j = 0; j < m; ++j, e = nextv(a, e)) hpush(a, e);
+  if (a.err & E_OVF) { a.htop = base; return s; }
+  const u32 outer = a.htop;
+  for (u64 idx = 0; idx < total; ++idx) {
+    const u32 mark = a.htop;
+    u64 r = idx;
+    for (u32 i = 0; i < n; ++i, r /= m) { hpush(a, a.hs[base + i]); hpush(a, a.hs[base + n + (u32)(r % m)]); }
+    const u32 f = fun_end(a, mark);
+    hpush(a, f);
+  }
+  const u32 res = set_end(a, outer);
+  a.htop = base;
+  return res;
+}
+// [f1 : S1, ..., fk : Sk] from (field atom, set) handle pairs hs[mark..htop): every record with field
+// fi in Si (more than 2^20: E_UNSUP)
+TLV_NI u32 rec_set(Ar& a, u32 mark) {
+  const u32 k = (a.htop - mark) / 2;
+  u64 total = 1;
+  for (u32 i = 0; i < k; ++i) {
+    const u32 si = a.hs[mark + 2 * i + 1];
+    if (tg(a, si) != T_SET) { a.err |= E_TYPE; a.htop = mark; return 0; }
+    total *= count(a, si);
+    if (total > (1ull << 20)) { a.err |= E_UNSUP; a.htop = mark; return 0; }
+  }
+  const u32 outer = a.htop;
+  for (u64 idx = 0; idx < total; ++idx) {
+    const u32 m2 = a.htop;
+    u64 r = idx;
+    for (u32 i = 0; i < k; ++i) {
+      const u32 si = a.hs[mark + 2 * i + 1], c = count(a, si);
+      u32 e = first(si);
+      for (u32 q = (u32)(r % c); q > 0; --q) e = nextv(a, e);
+      r /= c;
+      hpush(a, a.hs[mark + 2 * i]); hpush(a, e);
+    }
+    const u32 f = fun_end(a, m2);
+    hpush(a, f);
+  }
+  const u32 res = set_end(a, outer);
+  a.htop = mark;
+  return res;
+}
+
 // ---- functions, records, sequences
 TLV_NI u32 dom(Ar& a, u32 f) {
   const u32 t = tg(a, f);

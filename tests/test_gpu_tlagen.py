@@ -101,6 +101,34 @@ def test_generated_deadlock_and_eval_error(raftmc, cfg, verdict, depth, code):
     assert "/\\ x = %d" % (0 if verdict == "DEADLOCK" else 1) in r.trace_text.split("State %d:" % depth)[1]
 
 
+def test_function_and_record_sets_on_gpu(raftmc):
+    """[S -> T] / [f : S, ...] as values and as lazily tested sets (configs/tlagen/FunSets.tla) on the GPU:
+    the Python restatement's counts for the whole space (TypeOK holding), a negative control's depth;
+    Ricketts' TypeOK to depth 12 with the oracle's counts, and its negative control BadTerm."""
+    from test_tlagen import RICKETTS_D12, funsets_model
+    want = funsets_model()
+    for workers in (1, 0):
+        with raftmc.ModelChecker(os.path.join(CONFIGS, "tlagen", "FunSets.tla"), os.path.join(CONFIGS, "tlagen", "FunSets.cfg"),
+                                 workers=workers, **SMALL) as mc:
+            r = mc.run()
+        assert r.verdict == "OK", r.error
+        assert (r.generated, r.distinct, r.depth, [lv[0] for lv in r.levels]) == (want["generated"], want["distinct"], want["depth"], want["levels"])
+    for inv in ("FBelow2", "QEmpty"):
+        with raftmc.ModelChecker(os.path.join(CONFIGS, "tlagen", "FunSets.tla"), os.path.join(CONFIGS, "tlagen", "FunSets_%s.cfg" % inv),
+                                 workers=1, **SMALL) as mc:
+            r = mc.run()
+        assert (r.verdict, r.violated, r.depth) == ("INVARIANT_VIOLATION", inv, want["first_violation"][inv]), r.error
+    with raftmc.ModelChecker(gen_source("ricketts_typeok"), os.path.join(CONFIGS, "ricketts_typeok.cfg"), frontend="generated",
+                             workers=1, max_depth=12, **SMALL) as mc:
+        r = mc.run()
+    assert r.verdict == "DEPTH_LIMIT", r.error
+    assert {"generated": r.generated, "distinct": r.distinct, "levels": [lv[0] for lv in r.levels]} == RICKETTS_D12
+    with raftmc.ModelChecker(gen_source("ricketts_badterm"), os.path.join(CONFIGS, "ricketts_badterm.cfg"), frontend="generated",
+                             workers=1, **SMALL) as mc:
+        r = mc.run()
+    assert (r.verdict, r.violated, r.depth) == ("INVARIANT_VIOLATION", "BadTerm", 2), r.error
+
+
 def test_ricketts_on_gpu(raftmc):
     """thirdparty/raft_dricketts.tla (Bags module, TLAPS-only in the reference) through the generated
     path, pinned by the oracle's restatement (tests/golden/ricketts_oracle.json): to depth 12 with

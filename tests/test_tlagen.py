@@ -271,6 +271,80 @@ def test_countdown_verdicts(cfg, verdict, depth):
     assert (r["verdict"], r["depth"], r["distinct"]) == (verdict, depth, depth)
 
 
+FUNSETS = os.path.join(CONFIGS, "tlagen", "FunSets.tla")
+
+
+def funsets_model():
+    """configs/tlagen/FunSets.tla restated in Python (S = {s1, s2}): TLC's generated / distinct counts and
+    level sizes of the whole space, and the BFS depth at which each negative control first fails."""
+    def succ(st):
+        f, r, q = st
+        out = []
+        for i in range(2):
+            if f[i] < 2:
+                out.append((tuple(x + (j == i) for j, x in enumerate(f)), r, q))
+        if r[0] < 2:
+            out.append((f, (r[0] + 1, r[1]), q))
+        out.append(((1, 1), r, q))
+        if len(q) < 2:
+            out.append((f, r, q + (r,)))
+        return out
+    ok = {"FBelow2": lambda st: max(st[0]) <= 1, "RBelow2": lambda st: st[1][0] <= 1, "QEmpty": lambda st: not st[2]}
+    level = [((0, 0), (0, b), ()) for b in (False, True)]
+    seen, gen, levels, first, depth = set(level), len(level), [len(level)], {}, 1
+    while level:
+        nxt = []
+        for st in level:
+            for t in succ(st):
+                gen += 1
+                if t not in seen:
+                    seen.add(t)
+                    nxt.append(t)
+        depth += 1
+        for k, f in ok.items():
+            if k not in first and any(not f(t) for t in nxt):
+                first[k] = depth
+        if nxt:
+            levels.append(len(nxt))
+        level = nxt
+    return {"generated": gen, "distinct": len(seen), "depth": len(levels), "levels": levels, "first_violation": first}
+
+
+@needs_tool
+def test_function_and_record_sets():
+    """[S -> T] and [f : S, ...] on the generated path: as values (Init's choices, \\E over a function
+    set: fun_set / rec_set) and in membership tests that never build the set (TypeOK-style: [S -> Nat],
+    Seq([a : 0..2, b : {FALSE, TRUE}]), a filter over Nat, \\subseteq a record set over Nat, \\notin).
+    TypeOK holds in every state, and the whole space equals the Python restatement's counts."""
+    want = funsets_model()
+    r = host_bfs(generate(FUNSETS, os.path.join(CONFIGS, "tlagen", "FunSets.cfg")))
+    assert (r["verdict"], r["err"]) == ("OK", 0)
+    assert {k: r[k] for k in ("generated", "distinct", "depth", "levels")} == {k: want[k] for k in ("generated", "distinct", "depth", "levels")}
+
+
+@needs_tool
+@pytest.mark.parametrize("inv", ["FBelow2", "RBelow2", "QEmpty"])
+def test_function_set_negative_controls(inv):
+    """Each negative control (f \\in [S -> 0..1], r \\in [a : 0..1, b : BOOLEAN], q \\in [{} -> Cell]) is
+    violated at the first depth where the Python restatement has a state outside it."""
+    r = host_bfs(generate(FUNSETS, os.path.join(CONFIGS, "tlagen", "FunSets_%s.cfg" % inv)))
+    assert (r["verdict"], r["violated"], r["depth"]) == ("INVARIANT_VIOLATION", inv, funsets_model()["first_violation"][inv])
+
+
+@needs_tool
+@needs_ref
+def test_ricketts_type_invariant():
+    """Ricketts' full type invariant (raft_dricketts.tla:482-492, the TLAPS proof's TypeOK: [Server -> Nat],
+    Seq([term : Nat, value : Value]), [Server -> [Server -> {n \\in Nat : 1 <= n}]], SUBSET Server, and the
+    messages' record types under \\subseteq) checked by the generated code: it holds in every state to depth
+    12, whose counts stay the oracle's; its negative control BadTerm fails at the first Timeout."""
+    r = host_bfs(generate(os.path.join(CONFIGS, "ricketts_mc.tla"), os.path.join(CONFIGS, "ricketts_typeok.cfg")), "--max-depth", "12")
+    assert (r["verdict"], r["err"]) == ("DEPTH_LIMIT", 0)
+    assert {k: r[k] for k in RICKETTS_D12} == RICKETTS_D12
+    r = host_bfs(generate(os.path.join(CONFIGS, "ricketts_mc.tla"), os.path.join(CONFIGS, "ricketts_badterm.cfg")))
+    assert (r["verdict"], r["violated"], r["depth"]) == ("INVARIANT_VIOLATION", "BadTerm", 2)
+
+
 def strip_history_global(state_line):
     """The oracle's membership state text leaves out history["global"] (its dump_line; the record
     it keeps per state is the rank summary, oracle/raft_membership.h): drop the field to compare."""
