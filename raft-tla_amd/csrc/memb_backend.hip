@@ -17,11 +17,13 @@
 //                     symmetric FP64 of the view (min over Permutations(Server))
 //                     into cand[slot][state]
 //  1c memb_oom_check  lane per out-of-model successor: invariants (TLC [ext] (ii))
-//  2. memb_dedup      16 independent seen-set probes per thread over 16-B
-//                     entries (fp, ~level|key); insert-if-absent with CAS,
-//                     then atomicMax of ~(level << 40 | key); cand := entry+1
-//  3. memb_select     lane per state: which of its slots won its fingerprint
-//                     (entry still holds its own key), per-block exclusive scan
+//  2. memb_dedup_cells workgroup b takes expand-workgroup b's in-model cells, 8
+//                     independent seen-set probes per thread over 16-B entries
+//                     (fp, ~level|key); insert-if-absent with CAS, then
+//                     atomicMax of ~(level << 40 | key); cand := entry+1
+//  3. memb_select     lane per state: which of its in-model slots (the slot
+//                     mask memb_expand wrote) won its fingerprint (entry still
+//                     holds its own key), per-block exclusive scan
 //  4. memb_scan_blocks exclusive scan of the block totals (one workgroup)
 //  5. memb_compact    lane per state: winners' (parent, slot) records in key order
 //  6. memb_materialize lane per new state: re-derive, store packed state and
@@ -81,6 +83,8 @@ struct MGenArgs {
   unsigned long long* prof;                // RMC_FP_PROF builds: wave cycles per fingerprint stage (else null)
   u32* big;                                // TLC mode: cells whose parent's bag exceeds memb_fingerprint_lds's slice
   u32 slice_cap;                           // parent bag entries memb_fingerprint_lds keeps (<= its slice - 1)
+  u64* smask;                              // [SMW][chunk] each state's in-model slots (bit per slot); null: the
+                                           // dense form, every cand slot written (the sharded loop reads it so)
 };
 
 // Phase 1 for the instances [K0, K1) with NS successors each.  The bounds are compile-time so
@@ -88,7 +92,8 @@ struct MGenArgs {
 // loop body (hoisting them over ~100 instances exhausts the register file).
 template <class S, int K0, int K1, int NS>
 __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs& a, bool active, u64 tid, u32& err,
-                                             u32& nsucc, u32& nin, unsigned int* lds_cnt, u32& wcin, u32& wcoom) {
+                                             u32& nsucc, u32& nin, unsigned int* lds_cnt, u32& wcin, u32& wcoom,
+                                             u64 (&smk)[(S::NSLOT + 63) / 64]) {
   using W = typename S::Work;
   // this wave's own regions of the workgroup's cell lists (64 * NSLOT cells each): a wave's cells stay
   // together, parent group by parent group (memb_fingerprint's lanes then share the 64 parents of one
@@ -100,7 +105,7 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
     const bool en = S::group_enabled(k, a.rt.next);                 // wave-uniform
     for (int sub = 0; sub < NS; ++sub) {
       const int slot = S::slot_of(k, sub);
-      if (active) a.cand[(u64)slot * a.chunk_count + tid] = 0;
+      if (active && !a.smask) a.cand[(u64)slot * a.chunk_count + tid] = 0;   // (dense form only)
       if (!en) continue;
       S::launder(s);
       bool need = false, oom = false;
@@ -127,6 +132,7 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
         }
       }
       const u32 cell = (u32)((u64)slot * a.chunk_count + tid);
+      smk[slot >> 6] |= (u64)need << (slot & 63);   // (slot is wave-uniform)
       // one ballot per list, consecutive stores at the wave's running count (wave-uniform: no atomic)
       const u64 mask = __ballot(need);
       if (need) cells[wcin + __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u))] = cell;
@@ -178,11 +184,16 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MEX
     S::init(s);
   }
   u32 err = 0, nsucc = 0, nin = 0, wcin = 0, wcoom = 0;
+  u64 smk[(S::NSLOT + 63) / 64] = {};
   // three loops (instances before Receive, Receive with its two successor slots, the rest): the
   // compile-time ranges prune apply's dispatch while keeping the kernel within short-branch range
-  expand_group<S, S::G_RV, S::G_RECV, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom);
-  expand_group<S, S::G_RECV, S::G_TO, 2>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom);
-  expand_group<S, S::G_TO, S::NI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom);
+  expand_group<S, S::G_RV, S::G_RECV, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom, smk);
+  expand_group<S, S::G_RECV, S::G_TO, 2>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom, smk);
+  expand_group<S, S::G_TO, S::NI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom, smk);
+  if (active && a.smask) {
+#pragma unroll
+    for (int w = 0; w < (S::NSLOT + 63) / 64; ++w) a.smask[(u64)w * a.chunk_count + tid] = smk[w];
+  }
   unsigned long long ev = ~0ull;
   if (active) {
     a.nsucc[tid] = (unsigned short)nsucc;
@@ -351,6 +362,8 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MOO
 }
 
 struct MDedupArgs {
+  const u32* cells;            // the in-model cells, per expand workgroup and wave (memb_dedup_cells)
+  const u32* cell_count;
   u64* cand;
   u64 nslots, chunk_count, rank0, nslot, level;
   u64* table;                  // [2 * slots] (fp, ~(level << 40 | key)); zero = empty
@@ -358,53 +371,64 @@ struct MDedupArgs {
   unsigned long long* ctr;
 };
 
-__global__ void __launch_bounds__(BS) memb_dedup(MDedupArgs a) {
-  const u64 tile = (u64)blockIdx.x * (BS * DPER);
-  u64 fp[DPER], cur[DPER], pos[DPER];
-#pragma unroll
-  for (int j = 0; j < DPER; ++j) {
-    const u64 idx = tile + (u64)j * BS + threadIdx.x;
-    fp[j] = idx < a.nslots ? a.cand[idx] : 0ull;
-    pos[j] = fp[j] & a.table_mask;
-  }
-#pragma unroll
-  for (int j = 0; j < DPER; ++j) cur[j] = fp[j] ? a.table[2 * pos[j]] : ~0ull;
-#pragma unroll
-  for (int j = 0; j < DPER; ++j)
-    if (fp[j] && cur[j] == 0ull)
-      cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[2 * pos[j]], 0ull, (unsigned long long)fp[j]);
+// memb_dedup over the in-model cells only: workgroup b takes expand-workgroup b's cell lists, DPER_C
+// cells in flight per thread (round 6: the cand array is no longer zeroed, dedup'd, selected and
+// compacted densely over every (slot, state) -- ~2% of C3's slots hold a successor)
+constexpr int DPER_C = 8;
+__global__ void __launch_bounds__(BS) memb_dedup_cells(MDedupArgs a) {
+  const CellRegions cr(a.cell_count + 8 * blockIdx.x, 64 * (u32)a.nslot);
+  const u32 n = cr.n;
+  const u32* cells = a.cells + (u64)blockIdx.x * (BS * a.nslot);
   u32 err = 0;
+  for (u32 i0 = 0; i0 < n; i0 += BS * DPER_C) {
+    u64 fp[DPER_C], cur[DPER_C], pos[DPER_C];
+    u32 cell[DPER_C];
 #pragma unroll
-  for (int j = 0; j < DPER; ++j) {
-    if (!fp[j]) continue;
-    if (cur[j] == 0ull || cur[j] == fp[j]) continue;          // inserted here, or already present
-    u64 slot = (pos[j] + 1) & a.table_mask;
-    for (int probe = 0;; ++probe) {
-      if (probe >= (1 << 20)) { err |= MERR_TABLE_FULL; break; }
-      const u64 c = a.table[2 * slot];
-      if (c == fp[j]) break;
-      if (c == 0ull) {
-        const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[2 * slot], 0ull, (unsigned long long)fp[j]);
-        if (old == 0ull || old == fp[j]) break;
-      }
-      slot = (slot + 1) & a.table_mask;
+    for (int j = 0; j < DPER_C; ++j) {
+      const u32 i = i0 + (u32)j * BS + threadIdx.x;
+      cell[j] = i < n ? cells[cr.at(i)] : 0u;
+      fp[j] = i < n ? a.cand[cell[j]] : 0ull;
+      pos[j] = fp[j] & a.table_mask;
     }
-    pos[j] = slot;
-  }
-  // FIFO first-found: keep the minimum (level, key) per fingerprint (older levels always win)
 #pragma unroll
-  for (int j = 0; j < DPER; ++j) {
-    if (!fp[j]) continue;
-    const u64 idx = tile + (u64)j * BS + threadIdx.x;
-    const u64 sl = idx / a.chunk_count, st = idx - sl * a.chunk_count;
-    const u64 key = (a.rank0 + st) * a.nslot + sl;
-    atomicMax((unsigned long long*)&a.table[2 * pos[j] + 1], (unsigned long long)~((a.level << 40) | key));
-    a.cand[idx] = pos[j] + 1;
+    for (int j = 0; j < DPER_C; ++j) cur[j] = fp[j] ? a.table[2 * pos[j]] : ~0ull;
+#pragma unroll
+    for (int j = 0; j < DPER_C; ++j)
+      if (fp[j] && cur[j] == 0ull)
+        cur[j] = (u64)atomicCAS((unsigned long long*)&a.table[2 * pos[j]], 0ull, (unsigned long long)fp[j]);
+#pragma unroll
+    for (int j = 0; j < DPER_C; ++j) {
+      if (!fp[j]) continue;
+      if (cur[j] == 0ull || cur[j] == fp[j]) continue;          // inserted here, or already present
+      u64 slot = (pos[j] + 1) & a.table_mask;
+      for (int probe = 0;; ++probe) {
+        if (probe >= (1 << 20)) { err |= MERR_TABLE_FULL; break; }
+        const u64 c = a.table[2 * slot];
+        if (c == fp[j]) break;
+        if (c == 0ull) {
+          const u64 old = (u64)atomicCAS((unsigned long long*)&a.table[2 * slot], 0ull, (unsigned long long)fp[j]);
+          if (old == 0ull || old == fp[j]) break;
+        }
+        slot = (slot + 1) & a.table_mask;
+      }
+      pos[j] = slot;
+    }
+    // FIFO first-found: keep the minimum (level, key) per fingerprint (older levels always win)
+#pragma unroll
+    for (int j = 0; j < DPER_C; ++j) {
+      if (!fp[j]) continue;
+      const u64 sl = cell[j] / a.chunk_count, st = cell[j] - sl * a.chunk_count;
+      const u64 key = (a.rank0 + st) * a.nslot + sl;
+      atomicMax((unsigned long long*)&a.table[2 * pos[j] + 1], (unsigned long long)~((a.level << 40) | key));
+      a.cand[cell[j]] = pos[j] + 1;
+    }
   }
   if (err) atomicOr(&a.ctr[C_ERR], (unsigned long long)err);
 }
 
 struct MSelArgs {
+  const u64* smask;            // [smw][chunk] in-model slots per state (memb_expand)
+  u32 smw;
   u64* cand;
   u64 chunk_count, rank0, nslot, level;
   const u64* table;
@@ -419,11 +443,15 @@ __global__ void __launch_bounds__(BS) memb_select(MSelArgs a) {
   unsigned int mine = 0;
   if (tid < a.chunk_count) {
     const u64 kb = (a.rank0 + tid) * a.nslot;
-    for (u64 sl = 0; sl < a.nslot; ++sl) {
-      const u64 c = a.cand[sl * a.chunk_count + tid];
-      if (!c) continue;
-      const u64 want = ~((a.level << 40) | (kb + sl));
-      if (a.table[2 * (c - 1) + 1] == want) { a.cand[sl * a.chunk_count + tid] = c | WINBIT; ++mine; }
+    for (u32 w = 0; w < a.smw; ++w) {   // only the state's in-model slots
+      u64 m = a.smask[(u64)w * a.chunk_count + tid];
+      while (m) {
+        const u64 sl = (u64)w * 64 + (u64)__builtin_ctzll(m);
+        m &= m - 1;
+        const u64 c = a.cand[sl * a.chunk_count + tid];
+        const u64 want = ~((a.level << 40) | (kb + sl));
+        if (a.table[2 * (c - 1) + 1] == want) { a.cand[sl * a.chunk_count + tid] = c | WINBIT; ++mine; }
+      }
     }
   }
   unsigned int incl = mine;
@@ -459,6 +487,8 @@ __global__ void __launch_bounds__(BS) memb_scan_blocks(unsigned long long* bsum,
 }
 
 struct MCompArgs {
+  const u64* smask;
+  u32 smw;
   const u64* cand;
   u64 chunk_count, chunk_begin, nslot;
   const unsigned int* woff;
@@ -471,8 +501,14 @@ __global__ void __launch_bounds__(BS) memb_compact(MCompArgs a) {
   if (tid >= a.chunk_count) return;
   u64 o = a.bsum[blockIdx.x] + a.woff[tid];
   const u64 gid = a.chunk_begin + tid;
-  for (u64 sl = 0; sl < a.nslot; ++sl)
-    if (a.cand[sl * a.chunk_count + tid] & WINBIT) a.newrec[o++] = (gid << 10) | sl;
+  for (u32 w = 0; w < a.smw; ++w) {   // in-model slots in slot order: the winners in key order
+    u64 m = a.smask[(u64)w * a.chunk_count + tid];
+    while (m) {
+      const u64 sl = (u64)w * 64 + (u64)__builtin_ctzll(m);
+      m &= m - 1;
+      if (a.cand[sl * a.chunk_count + tid] & WINBIT) a.newrec[o++] = (gid << 10) | sl;
+    }
+  }
 }
 
 struct MMatArgs {
@@ -946,6 +982,7 @@ class MembGpu : public Backend {
     HIPCHK(hipMalloc(&d_cells_oom_, chunk_ * S::NSLOT * 4));
     HIPCHK(hipMalloc(&d_cell_count_, 8 * ((chunk_ + BS - 1) / BS) * 4));
     HIPCHK(hipMalloc(&d_big_, chunk_ * S::NSLOT * 4));
+    HIPCHK(hipMalloc(&d_smask_, chunk_ * SMW * 8));
     HIPCHK(hipMalloc(&d_woff_, chunk_ * 4));
     HIPCHK(hipMalloc(&d_bsum_, SCAN_MAX_BLOCKS * 8));
     HIPCHK(hipMalloc(&d_ctr_, C_NCTR * 8));
@@ -1048,13 +1085,17 @@ class MembGpu : public Backend {
         g.states = sp; g.chunk_begin = cb; g.chunk_count = cnt; g.rank0 = rank0; g.cand = d_cand_; g.cells = d_cells_;
         g.cells_oom = d_cells_oom_; g.cell_count = d_cell_count_; g.nsucc = d_nsucc_;
         g.seed = r.seed; g.rt = rt_dev_; g.inv_oom = o.inv_out_of_model ? 1u : 0u; g.deadlock = o.check_deadlock ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_;
+        g.smask = d_smask_;
         MDedupArgs d;
+        d.cells = d_cells_; d.cell_count = d_cell_count_;
         d.cand = d_cand_; d.nslots = nslots; d.chunk_count = cnt; d.rank0 = rank0; d.nslot = S::NSLOT; d.level = level + 1;
         d.table = d_table_; d.table_mask = table_mask_; d.ctr = (unsigned long long*)d_ctr_;
         MSelArgs sa;
+        sa.smask = d_smask_; sa.smw = (u32)SMW;
         sa.cand = d_cand_; sa.chunk_count = cnt; sa.rank0 = rank0; sa.nslot = S::NSLOT; sa.level = level + 1; sa.table = d_table_;
         sa.woff = d_woff_; sa.bsum = (unsigned long long*)d_bsum_;
         MCompArgs ca;
+        ca.smask = d_smask_; ca.smw = (u32)SMW;
         ca.cand = d_cand_; ca.chunk_count = cnt; ca.chunk_begin = cb; ca.nslot = S::NSLOT; ca.woff = d_woff_;
         ca.bsum = (const unsigned long long*)d_bsum_; ca.newrec = d_newrec_;
         HIPCHK(hipEventRecord(ev_[7], stream_));
@@ -1066,7 +1107,7 @@ class MembGpu : public Backend {
         HIPCHK(hipEventRecord(ev_[0], stream_));
         if (int rc = launch_fingerprint(g, nblk, err)) return rc;
         HIPCHK(hipEventRecord(ev_[1], stream_));
-        hipLaunchKernelGGL(memb_dedup, dim3((unsigned)((nslots + BS * DPER - 1) / (BS * DPER))), dim3(BS), 0, stream_, d);
+        hipLaunchKernelGGL(memb_dedup_cells, dim3(nblk), dim3(BS), 0, stream_, d);
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ev_[2], stream_));
         hipLaunchKernelGGL(memb_select, dim3(nblk), dim3(BS), 0, stream_, sa);
@@ -1528,6 +1569,7 @@ class MembGpu : public Backend {
     g.cand = d_cand_; g.cells = d_cells_; g.cells_oom = d_cells_oom_; g.cell_count = d_cell_count_; g.nsucc = d_nsucc_;
     g.seed = sres_.seed; g.rt = rt_dev_; g.inv_oom = sopts_.inv_out_of_model ? 1u : 0u;
     g.deadlock = sopts_.check_deadlock ? 1u : 0u; g.ctr = (unsigned long long*)d_ctr_;
+    g.smask = nullptr;   // the dense cand form: memb_route / memb_dedup_sh / memb_select_sh read every slot
     HIPCHK(hipEventRecord(ev_[0], stream_));
     hipLaunchKernelGGL((memb_expand<S>), dim3(nblk), dim3(BS), 0, stream_, g);
     HIPCHK(hipGetLastError());
@@ -1819,6 +1861,8 @@ class MembGpu : public Backend {
   u64* d_table_ = nullptr; u32* d_states_ = nullptr; u64* d_meta_ = nullptr; u64* d_ctr_ = nullptr;
   u64* d_cand_ = nullptr; u64* d_newrec_ = nullptr; unsigned short* d_nsucc_ = nullptr; unsigned int* d_woff_ = nullptr;
   u32* d_cells_ = nullptr; u32* d_cells_oom_ = nullptr; u32* d_cell_count_ = nullptr; u32* d_big_ = nullptr;
+  u64* d_smask_ = nullptr;   // [SMW][chunk] in-model slot masks (single-GPU loop)
+  static constexpr int SMW = (S::NSLOT + 63) / 64;
   int fp_slice_test_ = -1;   // RunOpts::test_fp_slice of the current run
   u64* d_bsum_ = nullptr;
   hipStream_t stream_ = nullptr;
@@ -1896,12 +1940,12 @@ class MembGpu : public Backend {
     for (void* q : {(void*)d_lvl_, (void*)d_sorted_, (void*)d_newrec_lvl_, (void*)d_sort_tmp_, (void*)d_nsucc_lvl_}) if (q) (void)hipFree(q);
     d_lvl_ = nullptr; d_sorted_ = nullptr; d_newrec_lvl_ = nullptr; d_sort_tmp_ = nullptr; d_nsucc_lvl_ = nullptr; lvl_cap_ = 0;
     for (void* p : {(void*)d_table_, (void*)d_states_, (void*)d_meta_, (void*)d_ctr_, (void*)d_cand_, (void*)d_newrec_,
-                    (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_, (void*)d_cells_oom_, (void*)d_cell_count_, (void*)d_big_})
+                    (void*)d_nsucc_, (void*)d_woff_, (void*)d_bsum_, (void*)d_cells_, (void*)d_cells_oom_, (void*)d_cell_count_, (void*)d_big_, (void*)d_smask_})
       if (p) (void)hipFree(p);
     for (auto& e : ev_) { if (e) (void)hipEventDestroy(e); e = nullptr; }
     if (stream_) (void)hipStreamDestroy(stream_);
     d_table_ = nullptr; d_states_ = nullptr; d_meta_ = nullptr; d_ctr_ = nullptr; d_cand_ = nullptr; d_newrec_ = nullptr;
-    d_nsucc_ = nullptr; d_woff_ = nullptr; d_bsum_ = nullptr; d_cells_ = nullptr; d_cells_oom_ = nullptr; d_cell_count_ = nullptr; d_big_ = nullptr; stream_ = nullptr;
+    d_nsucc_ = nullptr; d_woff_ = nullptr; d_bsum_ = nullptr; d_cells_ = nullptr; d_cells_oom_ = nullptr; d_cell_count_ = nullptr; d_big_ = nullptr; d_smask_ = nullptr; stream_ = nullptr;
   }
   // stored state `gid` (global id) and its parent pointer, from the host part or the device
   void read_state(u64 gid, W& s, u64* meta = nullptr) const {
