@@ -93,7 +93,7 @@ struct MGenArgs {
 template <class S, int K0, int K1, int NS>
 __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs& a, bool active, u64 tid, u32& err,
                                              u32& nsucc, u32& nin, unsigned int* lds_cnt, u32& wcin, u32& wcoom,
-                                             u64 (&smk)[(S::NSLOT + 63) / 64]) {
+                                             u64& mcur, int& mwi) {
   using W = typename S::Work;
   // this wave's own regions of the workgroup's cell lists (64 * NSLOT cells each): a wave's cells stay
   // together, parent group by parent group (memb_fingerprint's lanes then share the 64 parents of one
@@ -106,6 +106,12 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
     for (int sub = 0; sub < NS; ++sub) {
       const int slot = S::slot_of(k, sub);
       if (active && !a.smask) a.cand[(u64)slot * a.chunk_count + tid] = 0;   // (dense form only)
+      // the slot mask one 64-bit word at a time: slots come in increasing order (slot_of), every one of them
+      if ((slot >> 6) != mwi) {   // (wave-uniform)
+        if (active && a.smask && mwi >= 0) a.smask[(u64)mwi * a.chunk_count + tid] = mcur;
+        mcur = 0;
+        mwi = slot >> 6;
+      }
       if (!en) continue;
       S::launder(s);
       bool need = false, oom = false;
@@ -132,7 +138,7 @@ __device__ __forceinline__ void expand_group(typename S::Work& s, const MGenArgs
         }
       }
       const u32 cell = (u32)((u64)slot * a.chunk_count + tid);
-      smk[slot >> 6] |= (u64)need << (slot & 63);   // (slot is wave-uniform)
+      mcur |= (u64)need << (slot & 63);
       // one ballot per list, consecutive stores at the wave's running count (wave-uniform: no atomic)
       const u64 mask = __ballot(need);
       if (need) cells[wcin + __builtin_amdgcn_mbcnt_hi((u32)(mask >> 32), __builtin_amdgcn_mbcnt_lo((u32)mask, 0u))] = cell;
@@ -184,16 +190,14 @@ __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(RMC_MEX
     S::init(s);
   }
   u32 err = 0, nsucc = 0, nin = 0, wcin = 0, wcoom = 0;
-  u64 smk[(S::NSLOT + 63) / 64] = {};
+  u64 mcur = 0;
+  int mwi = -1;
   // three loops (instances before Receive, Receive with its two successor slots, the rest): the
   // compile-time ranges prune apply's dispatch while keeping the kernel within short-branch range
-  expand_group<S, S::G_RV, S::G_RECV, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom, smk);
-  expand_group<S, S::G_RECV, S::G_TO, 2>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom, smk);
-  expand_group<S, S::G_TO, S::NI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom, smk);
-  if (active && a.smask) {
-#pragma unroll
-    for (int w = 0; w < (S::NSLOT + 63) / 64; ++w) a.smask[(u64)w * a.chunk_count + tid] = smk[w];
-  }
+  expand_group<S, S::G_RV, S::G_RECV, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom, mcur, mwi);
+  expand_group<S, S::G_RECV, S::G_TO, 2>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom, mcur, mwi);
+  expand_group<S, S::G_TO, S::NI, 1>(s, a, active, tid, err, nsucc, nin, lds_cnt, wcin, wcoom, mcur, mwi);
+  if (active && a.smask) a.smask[(u64)mwi * a.chunk_count + tid] = mcur;   // the last word
   unsigned long long ev = ~0ull;
   if (active) {
     a.nsucc[tid] = (unsigned short)nsucc;
