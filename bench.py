@@ -299,8 +299,8 @@ def main():
 
         # the library's kernel names -> rocprofv3's (orig_merge_probe is the fused orig_dedup_plain)
         rocprof_name = {"orig_merge_probe": "orig_dedup_plain"}.get(kname, kname)
-        defaults = {"orig_generate": ("traffic_r05d_c2_generate.json", "valu_r05d_c2_generate.json"),
-                    "orig_merge_probe": ("traffic_r05d_c2_dedup.json", None)}.get(kname, (None, None))
+        defaults = {"orig_generate": ("traffic_r06f_c2_generate.json", "valu_r06f_c2_generate.json"),
+                    "orig_merge_probe": ("traffic_r06f_c2_dedup.json", None)}.get(kname, (None, None))
 
         def pmc_summary(path, default):
             """a committed rocprofv3 summary of this kernel on this workload, else None"""
