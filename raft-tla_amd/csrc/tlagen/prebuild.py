@@ -33,6 +33,8 @@ SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing
           ("funsets_qempty", "configs/tlagen/FunSets.tla", "configs/tlagen/FunSets_QEmpty.cfg"),
           ("ricketts_typeok", "configs/ricketts_mc.tla", "configs/ricketts_typeok.cfg"),
           ("ricketts_badterm", "configs/ricketts_mc.tla", "configs/ricketts_badterm.cfg"),
+          ("higher_order", "configs/tlagen/HigherOrder.tla", "configs/tlagen/HigherOrder.cfg"),
+          ("higher_order_fewzeros", "configs/tlagen/HigherOrder.tla", "configs/tlagen/HigherOrder_FewZeros.cfg"),
           ("rec_fun", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun.cfg"),
           ("rec_fun_fact", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_fact.cfg"),
           ("rec_fun_sum", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_sum.cfg"),

@@ -28,6 +28,7 @@ enum class K {
   And, Or,                            // junction lists and infix /\ \/
   If, Case, Let, Forall, Exists, Choose,
   SetEnum, SetFilter, SetMap, FunCons, FunApp, Except, At, Record, RecordSet, FunSet, Tuple, Dot,
+  Lambda,                             // LAMBDA x, y : e (fields = parameters, a[0] = body): an operator argument
   Unsupported
 };
 
@@ -52,6 +53,7 @@ struct Node {
 struct Def {
   std::string name;
   std::vector<std::string> params;
+  std::vector<int> arity;              // per parameter: 0 for a value, k for an operator parameter F(_, .., _)
   NP body;                            // null if the body failed to parse (error kept in `error`)
   std::string error;
   std::string module;

@@ -87,6 +87,12 @@ struct Gen {
     return *d;
   }
 
+  static int arity_of(const Def& d, size_t i) { return i < d.arity.size() ? d.arity[i] : 0; }
+  static bool higher_order(const Def& d) {
+    for (size_t i = 0; i < d.params.size(); ++i) if (arity_of(d, i)) return true;
+    return false;
+  }
+
   // ---- level: does a definition (transitively) contain primes / UNCHANGED?
   bool has_action(const NP& e, std::set<std::string>& visiting) {
     if (!e) return false;
@@ -284,6 +290,7 @@ struct Gen {
         out += "auto " + s.cxx + " = [&](auto& " + self.cxx + ", u32 " + arg + ") -> u32 {\n " + rec_body(*d, inner, arg) + "};\n";
         continue;
       }
+      if (higher_order(*d)) unsup(*e, "LET operator " + d->name + " with an operator parameter");
       Sym s; s.kind = Sym::LetOp; s.def = d; s.cxx = fresh("L");
       s.scope = std::make_shared<Scope>(sc);   // recursion is outside the subset
       Scope inner = sc;
@@ -402,10 +409,15 @@ struct Gen {
       case K::OpApp: {
         if (n.s == "Cardinality" && n.a.size() == 1 && n.a[0]->k == K::Unary && n.a[0]->s == "DOMAIN" && !find(sc, n.s) && !global(n.s))
           return "mk_int(A, coll_card(A, " + ex(n.a[0]->a[0], sc) + "))";
+        if (!find(sc, n.s)) {
+          if (auto d = global(n.s)) { if (higher_order(*d)) return apply_higher(n, sc, *d); }
+          else if (n.s == "SelectSeq") return select_seq(n, sc);
+        }
         std::vector<std::string> args;
         for (auto& a : n.a) args.push_back(ex(a, sc));
         return ident(n, sc, args);
       }
+      case K::Lambda: unsup(n, "LAMBDA other than as an operator argument");
       case K::Prime: {
         if (n.a[0]->k != K::Ident || !var_idx.count(n.a[0]->s)) unsup(n, "priming a non-variable expression");
         const std::string X = std::to_string(var_idx[n.a[0]->s]);
@@ -709,6 +721,7 @@ struct Gen {
         if (!args.empty()) unsup(n, "applying a value as an operator");
         return s->cxx;
       }
+      if (s->def && s->def->params.size() != args.size()) unsup(n, "operator " + nm + " with " + std::to_string(args.size()) + " arguments");
       std::string o = s->cxx + "(";
       for (size_t i = 0; i < args.size(); ++i) o += (i ? ", " : "") + args[i];
       return o + ")";
@@ -880,6 +893,10 @@ struct Gen {
         if (auto d = global(n.s)) {
           body_of(d, n);
           const bool action = is_action(d);
+          if (higher_order(*d)) {
+            if (action) unsup(n, "action operator " + d->name + " with an operator parameter");
+            break;   // a predicate: evaluated by ex (apply_higher)
+          }
           if (action || init_mode) return inline_op(n, sc, *d, Scope(), k, split, split && action ? action_id(d->name) : label, split && action);
         }
         break;
@@ -891,6 +908,85 @@ struct Gen {
   }
 
   bool is_action_body(const std::shared_ptr<Def>& d) { std::set<std::string> v; return has_action(d->body, v); }
+
+  // ---- higher-order operators (Op(F(_), x) == .. F(x) ..) and LAMBDA.  An operator argument
+  // becomes a C++ lambda of the caller's scope: a LAMBDA (its body over its parameters), a LET
+  // operator (its own lambda), or a global / standard-module operator by name (a wrapper calling
+  // it).  A global operator with an operator parameter is expanded at each application, as an
+  // immediately invoked lambda whose body sees only its parameters (the module scope), with the
+  // operator parameters bound to those lambdas (Sym::LetOp).
+  std::set<std::string> expanding;   // higher-order operators being expanded (recursion is refused)
+  std::shared_ptr<Def> lambda_def(const Node& l) {
+    auto d = std::make_shared<Def>();
+    d->name = "LAMBDA"; d->params = l.fields; d->arity.assign(l.fields.size(), 0); d->body = l.a[0]; d->module = l.module; d->line = l.line;
+    return d;
+  }
+  Sym op_arg(const NP& a, Scope& sc, int arity, std::string& decl) {
+    Sym s; s.kind = Sym::LetOp; s.cxx = fresh("L");
+    s.scope = std::make_shared<Scope>(sc);
+    std::string params;
+    std::vector<std::string> qs;
+    for (int i = 0; i < arity; ++i) { qs.push_back(fresh("q")); params += (i ? ", u32 " : "u32 ") + qs.back(); }
+    if (a->k == K::Lambda) {
+      if ((int)a->fields.size() != arity) unsup(*a, "a LAMBDA of " + std::to_string(a->fields.size()) + " parameters for an operator of " + std::to_string(arity));
+      s.def = lambda_def(*a);
+      Scope inner = sc;
+      for (int i = 0; i < arity; ++i) { Sym v; v.cxx = qs[i]; inner.push_back({a->fields[i], v}); }
+      decl += "auto " + s.cxx + " = [&](" + params + ") -> u32 { return " + ex(a->a[0], inner) + "; };\n";
+      return s;
+    }
+    if (a->k != K::Ident) unsup(*a, "an operator argument that is not a name or a LAMBDA");
+    if (const Sym* b = find(sc, a->s)) {
+      if (b->kind != Sym::LetOp) unsup(*a, "a value (" + a->s + ") passed as an operator argument");
+      if (b->def && (int)b->def->params.size() != arity) unsup(*a, "operator " + a->s + " passed for an operator of " + std::to_string(arity) + " arguments");
+      return *b;
+    }
+    if (auto d = global(a->s)) {
+      if (higher_order(*d)) unsup(*a, "a higher-order operator (" + a->s + ") passed as an operator argument");
+      if ((int)d->params.size() != arity) unsup(*a, "operator " + a->s + " passed for an operator of " + std::to_string(arity) + " arguments");
+      s.def = d;
+      s.scope = std::make_shared<Scope>();
+    } else {
+      s.def = std::make_shared<Def>();   // a standard-module operator (Len, Append, ..): its arity is checked by ident
+      s.def->name = a->s; s.def->params = qs; s.def->arity.assign(arity, 0);
+      s.def->body = std::make_shared<Node>(*a);
+      s.def->body->k = K::OpApp;
+      for (auto& q : qs) { auto id = std::make_shared<Node>(*a); id->s = q; s.def->body->a.push_back(id); }
+    }
+    Node call = *a;
+    call.k = K::OpApp;
+    decl += "auto " + s.cxx + " = [&](" + params + ") -> u32 { return " + ident(call, sc, qs) + "; };\n";
+    return s;
+  }
+  std::string apply_higher(const Node& n, Scope& sc, const Def& d) {
+    if (n.a.size() != d.params.size()) unsup(n, "operator " + d.name + " with " + std::to_string(n.a.size()) + " arguments");
+    if (!d.body) unsup(n, "definition " + d.name + " does not parse: " + d.error);
+    if (expanding.count(d.name)) unsup(n, "recursive higher-order operator " + d.name);
+    std::string decl;
+    Scope inner;
+    for (size_t i = 0; i < d.params.size(); ++i) {
+      if (arity_of(d, i)) { inner.push_back({d.params[i], op_arg(n.a[i], sc, arity_of(d, i), decl)}); continue; }
+      if (n.a[i]->k == K::Lambda) unsup(*n.a[i], "a LAMBDA for the value parameter " + d.params[i] + " of " + d.name);
+      Sym v; v.cxx = fresh("p");
+      decl += "const u32 " + v.cxx + " = " + ex(n.a[i], sc) + ";\n";
+      inner.push_back({d.params[i], v});
+    }
+    expanding.insert(d.name);
+    const std::string body = ex(d.body, inner);
+    expanding.erase(d.name);
+    return "[&]() -> u32 {\n" + decl + "return " + body + ";\n}()";
+  }
+  // SelectSeq(s, Test) (Sequences): the elements of s, in order, for which Test holds
+  std::string select_seq(const Node& n, Scope& sc) {
+    if (n.a.size() != 2) unsup(n, "SelectSeq with " + std::to_string(n.a.size()) + " arguments");
+    std::string decl;
+    const Sym t = op_arg(n.a[1], sc, 1, decl);
+    const std::string S = fresh("S"), m = fresh("m"), e = fresh("e"), i = fresh("i"), c = fresh("n"), tp = fresh("t"), kp = fresh("k");
+    return "[&]() -> u32 {\n" + decl + "const u32 " + S + " = " + ex(n.a[0], sc) + ";\n if (tg(A, " + S + ") != T_SEQ) { A.err |= E_TYPE; return " + S +
+           "; }\n const u32 " + m + " = A.htop; u32 " + e + " = first(" + S + ");\n for (u32 " + i + " = 0, " + c + " = count(A, " + S + "); " + i + " < " + c +
+           "; ++" + i + ", " + e + " = nextv(A, " + e + ")) {\n  const u32 " + tp + " = A.top; const bool " + kp + " = truth(A, " + t.cxx + "(" + e + ")); A.top = " + tp +
+           ";\n  if (" + kp + ") hpush(A, " + e + ");\n }\n return seq_end(A, " + m + ");\n}()";
+  }
 
   std::string inline_op(const Node& n, Scope& sc, const Def& d, const Scope& defscope, const std::string& k, bool split, int label, bool set_label) {
     if (n.a.size() != d.params.size()) unsup(n, "operator " + d.name + " with " + std::to_string(n.a.size()) + " arguments");

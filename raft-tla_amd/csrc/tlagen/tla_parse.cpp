@@ -295,6 +295,13 @@ struct Parser {
       n->a.push_back(expr(0));
       return n;
     }
+    if (s == "LAMBDA") {   // LAMBDA x, y : e — SequencesExt's Remove (SelectSeq(s, LAMBDA t : t # e))
+      ++p; NP n = mk(K::Lambda, t);
+      do n->fields.push_back(ident()); while (is(",") && (++p, true));
+      expect(":");
+      n->a.push_back(expr(0));
+      return n;
+    }
     if (s == "CHOOSE") {
       ++p; NP n = mk(K::Choose, t);
       n->binds = binds();
@@ -467,7 +474,7 @@ struct Parser {
     ++p;
     if (raw().t == T::Op && raw().s != "==" && raw().s != "(" && raw().s != "[" && tk[p + 1].t == T::Id &&
         tk[p + 2].t == T::Op && tk[p + 2].s == "==") {                 // infix definition a (+) b == ...
-      d->name = raw().s; ++p; d->params = {first, ident()};
+      d->name = raw().s; ++p; d->params = {first, ident()}; d->arity = {0, 0};
     } else {
       d->name = first;
       if (is("(")) {
@@ -475,8 +482,15 @@ struct Parser {
         if (!is(")")) {
           do {
             std::string q = ident();
-            if (is("(")) { ++p; while (!is(")")) ++p; ++p; }   // operator parameter Op(_): arity ignored
+            int k = 0;
+            if (is("(")) {   // operator parameter F(_, _)
+              ++p;
+              while (!is(")")) { if (raw().s == "_") ++k; ++p; }
+              ++p;
+              if (!k) fail("operator parameter without an argument");
+            }
             d->params.push_back(q);
+            d->arity.push_back(k);
           } while (is(",") && (++p, true));
         }
         expect(")");

@@ -101,6 +101,22 @@ def test_generated_deadlock_and_eval_error(raftmc, cfg, verdict, depth, code):
     assert "/\\ x = %d" % (0 if verdict == "DEADLOCK" else 1) in r.trace_text.split("State %d:" % depth)[1]
 
 
+def test_higher_order_operators_on_gpu(raftmc):
+    """Operator parameters, LAMBDA and SelectSeq (configs/tlagen/HigherOrder.tla) on the GPU, both
+    pipelines: the Python restatement's counts for the whole space, and a negative control's depth."""
+    from test_tlagen import higher_order_model
+    want = higher_order_model()
+    spec = os.path.join(CONFIGS, "tlagen", "HigherOrder.tla")
+    for workers in (1, 0):
+        with raftmc.ModelChecker(spec, os.path.join(CONFIGS, "tlagen", "HigherOrder.cfg"), workers=workers, **SMALL) as mc:
+            r = mc.run()
+        assert r.verdict == "OK", r.error
+        assert (r.generated, r.distinct, r.depth, [lv[0] for lv in r.levels]) == (want["generated"], want["distinct"], want["depth"], want["levels"])
+    with raftmc.ModelChecker(spec, os.path.join(CONFIGS, "tlagen", "HigherOrder_FewZeros.cfg"), workers=1, **SMALL) as mc:
+        r = mc.run()
+    assert (r.verdict, r.depth) == ("INVARIANT_VIOLATION", want["first_violation"]["FewZeros"])
+
+
 def test_function_and_record_sets_on_gpu(raftmc):
     """[S -> T] / [f : S, ...] as values and as lazily tested sets (configs/tlagen/FunSets.tla) on the GPU:
     the Python restatement's counts for the whole space (TypeOK holding), a negative control's depth;
