@@ -35,6 +35,8 @@ SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing
           ("ricketts_badterm", "configs/ricketts_mc.tla", "configs/ricketts_badterm.cfg"),
           ("higher_order", "configs/tlagen/HigherOrder.tla", "configs/tlagen/HigherOrder.cfg"),
           ("higher_order_fewzeros", "configs/tlagen/HigherOrder.tla", "configs/tlagen/HigherOrder_FewZeros.cfg"),
+          ("recursive_ops", "configs/tlagen/Recursive.tla", "configs/tlagen/Recursive.cfg"),
+          ("recursive_ops_runaway", "configs/tlagen/Recursive.tla", "configs/tlagen/Recursive_Runaway.cfg"),
           ("rec_fun", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun.cfg"),
           ("rec_fun_fact", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_fact.cfg"),
           ("rec_fun_sum", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_sum.cfg"),

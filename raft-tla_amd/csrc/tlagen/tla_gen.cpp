@@ -215,8 +215,33 @@ struct Gen {
     const std::string body = ex(d->body, sc);
     init_mode = save;
     fn_protos.push_back(sig + ";");
-    fn_bodies.push_back(sig + " {\n  Ar& A = *c.A; (void)A;\n  return " + body + ";\n}\n");
+    if (recursive_op(d))   // a RECURSIVE operator (or one of a mutually recursive group): bounded like TLC's stack
+      fn_bodies.push_back(sig + " {\n  Ar& A = *c.A; (void)A;\n  if (A.rdepth >= kMaxRecDepth) { A.err |= E_UNSUP; return 0u; }\n"
+                          "  ++A.rdepth; const u32 r_ = " + body + ";\n  --A.rdepth; return r_;\n}\n");
+    else
+      fn_bodies.push_back(sig + " {\n  Ar& A = *c.A; (void)A;\n  return " + body + ";\n}\n");
     return fn;
+  }
+
+  // does a global operator reach itself through the global operators its body applies?
+  std::map<std::string, bool> rec_memo;
+  void reached(const NP& e, std::set<std::string>& seen) {
+    if (!e) return;
+    if (e->k == K::Ident || e->k == K::OpApp || e->k == K::Binary) {
+      auto d = global(e->s);
+      if (d && d->body && seen.insert(d->name).second) reached(d->body, seen);
+    }
+    for (auto& c : e->a) reached(c, seen);
+    for (auto& b : e->binds) reached(b.set, seen);
+    for (auto& u : e->ups) { reached(u.rhs, seen); for (auto& st : u.path) reached(st.idx, seen); }
+    for (auto& d : e->defs) reached(d->body, seen);
+  }
+  bool recursive_op(const std::shared_ptr<Def>& d) {
+    auto it = rec_memo.find(d->name);
+    if (it != rec_memo.end()) return it->second;
+    std::set<std::string> seen;
+    reached(d->body, seen);
+    return rec_memo[d->name] = seen.count(d->name) != 0;
   }
 
   // ---- recursive function definitions  f[x \in S] == e  whose body applies f (TypedBags' Sum:

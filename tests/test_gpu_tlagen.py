@@ -117,6 +117,22 @@ def test_higher_order_operators_on_gpu(raftmc):
     assert (r.verdict, r.depth) == ("INVARIANT_VIOLATION", want["first_violation"]["FewZeros"])
 
 
+def test_recursive_operators_on_gpu(raftmc):
+    """RECURSIVE operators (configs/tlagen/Recursive.tla: self- and mutually recursive) on the GPU, both
+    pipelines: the Python restatement's counts; a runaway recursion ends as an evaluation error."""
+    from test_tlagen import recursive_ops_model
+    want = recursive_ops_model()
+    spec = os.path.join(CONFIGS, "tlagen", "Recursive.tla")
+    for workers in (1, 0):
+        with raftmc.ModelChecker(spec, os.path.join(CONFIGS, "tlagen", "Recursive.cfg"), workers=workers, **SMALL) as mc:
+            r = mc.run()
+        assert r.verdict == "OK", r.error
+        assert (r.generated, r.distinct, r.depth, [lv[0] for lv in r.levels]) == (want["generated"], want["distinct"], want["depth"], want["levels"])
+    with raftmc.ModelChecker(spec, os.path.join(CONFIGS, "tlagen", "Recursive_Runaway.cfg"), workers=1, **SMALL) as mc:
+        r = mc.run()
+    assert (r.verdict, r.violated, r.depth) == ("EVAL_ERROR", "Runaway", 1)
+
+
 def test_function_and_record_sets_on_gpu(raftmc):
     """[S -> T] / [f : S, ...] as values and as lazily tested sets (configs/tlagen/FunSets.tla) on the GPU:
     the Python restatement's counts for the whole space (TypeOK holding), a negative control's depth;

@@ -518,3 +518,44 @@ def test_sequences_ext_remove(tmp_path, cfg, verdict, depth, distinct):
     assert r.returncode == 0, r.stderr
     r = host_bfs(out)
     assert (r["verdict"], r["depth"], r["distinct"], r["err"]) == (verdict, depth, distinct, 0)
+
+
+RECURSIVE_OPS = os.path.join(CONFIGS, "tlagen", "Recursive.tla")
+
+
+def recursive_ops_model():
+    """configs/tlagen/Recursive.tla restated in Python: s grows by one of 0..3 up to length 3, then drops
+    its head; TLC's generated / distinct counts and level sizes, and SumBelow4's first failing depth."""
+    level = [()]
+    seen, gen, levels, first, depth = set(level), 1, [1], None, 1
+    while level:
+        nxt = []
+        for st in level:
+            for t in ([st + (v,) for v in range(4)] if len(st) < 3 else [st[1:]]):
+                gen += 1
+                if t not in seen:
+                    seen.add(t)
+                    nxt.append(t)
+        depth += 1
+        if first is None and any(sum(t) >= 4 for t in nxt):
+            first = depth
+        if nxt:
+            levels.append(len(nxt))
+        level = nxt
+    return {"generated": gen, "distinct": len(seen), "depth": len(levels), "levels": levels, "sum_below4": first}
+
+
+@needs_tool
+def test_recursive_operators():
+    """RECURSIVE operators: self-recursive (SumSeq over a sequence, Fact) and mutually recursive (IsEven /
+    IsOdd) on the generated path; Inv's identities hold in every state and the whole space equals the
+    Python restatement's; the negative control fails at its depth; a runaway recursion (Fact(-1)) is an
+    evaluation error at the recursion bound (kMaxRecDepth), like TLC's stack overflow, never a hang."""
+    want = recursive_ops_model()
+    r = host_bfs(generate(RECURSIVE_OPS, os.path.join(CONFIGS, "tlagen", "Recursive.cfg")))
+    assert (r["verdict"], r["err"]) == ("OK", 0)
+    assert {k: r[k] for k in ("generated", "distinct", "depth", "levels")} == {k: want[k] for k in ("generated", "distinct", "depth", "levels")}
+    r = host_bfs(generate(RECURSIVE_OPS, os.path.join(CONFIGS, "tlagen", "Recursive_SumBelow4.cfg")))
+    assert (r["verdict"], r["violated"], r["depth"]) == ("INVARIANT_VIOLATION", "SumBelow4", want["sum_below4"])
+    r = host_bfs(generate(RECURSIVE_OPS, os.path.join(CONFIGS, "tlagen", "Recursive_Runaway.cfg")))
+    assert (r["verdict"], r["violated"], r["depth"]) == ("EVAL_ERROR", "Runaway", 1)
