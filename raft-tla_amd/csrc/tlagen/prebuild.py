@@ -37,6 +37,7 @@ SPECS += [("toy_ring", "configs/tlagen/TokenRing.tla", "configs/tlagen/TokenRing
           ("higher_order_fewzeros", "configs/tlagen/HigherOrder.tla", "configs/tlagen/HigherOrder_FewZeros.cfg"),
           ("recursive_ops", "configs/tlagen/Recursive.tla", "configs/tlagen/Recursive.cfg"),
           ("recursive_ops_runaway", "configs/tlagen/Recursive.tla", "configs/tlagen/Recursive_Runaway.cfg"),
+          ("product", "configs/tlagen/Product.tla", "configs/tlagen/Product.cfg"),
           ("rec_fun", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun.cfg"),
           ("rec_fun_fact", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_fact.cfg"),
           ("rec_fun_sum", "configs/tlagen/RecFun.tla", "configs/tlagen/RecFun_sum.cfg"),

@@ -32,7 +32,7 @@ enum class K {
   Unsupported
 };
 
-struct Bind { std::vector<std::string> names; NP set; };
+struct Bind { std::vector<std::string> names; NP set; bool tuple = false; };   // tuple: <<a, b>> \in S
 struct PathStep { bool field = false; std::string name; NP idx; };   // ![idx] or !.name
 struct Update { std::vector<PathStep> path; NP rhs; };
 struct Def;

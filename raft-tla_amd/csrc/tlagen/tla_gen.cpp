@@ -265,7 +265,7 @@ struct Gen {
   // check, then the value of e; `sc` must already map the function's name to its RecFn symbol
   std::string rec_body(const Def& d, Scope& sc, const std::string& arg) {
     const Node& fc = *d.body;
-    if (fc.binds.size() != 1 || fc.binds[0].names.size() != 1) unsup(fc, "recursive function " + d.name + " of more than one argument");
+    if (fc.binds.size() != 1 || fc.binds[0].names.size() != 1 || fc.binds[0].tuple) unsup(fc, "recursive function " + d.name + " of more than one argument");
     Scope inner = sc;
     Sym x; x.cxx = arg;
     inner.push_back({fc.binds[0].names[0], x});
@@ -345,6 +345,17 @@ struct Gen {
                          const std::function<std::string(Scope&)>& inner) {
     if (bi == bs.size()) return inner(sc);
     const Bind& b = bs[bi];
+    if (b.tuple) {   // <<a, b>> \in S: each element of S is a tuple of exactly that many components
+      const std::string el = fresh("e");
+      Scope s2 = sc;
+      std::string hd = " if (tg(A, " + el + ") != T_SEQ || count(A, " + el + ") != " + std::to_string(b.names.size()) + "u) { A.err |= E_TYPE; } else {\n";
+      for (size_t i = 0; i < b.names.size(); ++i) {
+        Sym v; v.cxx = fresh("c");
+        hd += " const u32 " + v.cxx + " = apply(A, " + el + ", mk_int(A, " + std::to_string(i + 1) + "));\n";
+        s2.push_back({b.names[i], v});
+      }
+      return set_loop(ex(b.set, sc), el, hd + bind_loops(bs, bi + 1, 0, s2, restore, inner) + " }\n", restore);
+    }
     // the set of a multi-name bind is evaluated once
     if (ni == 0 && b.names.size() > 1) {
       const std::string sv = fresh("B");
@@ -515,6 +526,7 @@ struct Gen {
         const std::string m = fresh("m");
         Scope s2 = sc;
         const bool filt = n.k == K::SetFilter;
+        if (filt && n.binds[0].tuple) unsup(n, "a set filter over a tuple binding");
         const std::string loops = bind_loops(n.binds, 0, 0, s2, false, [&](Scope& s3) {
           if (filt) return " if (truth(A, " + ex(n.a[0], s3) + ")) hpush(A, " + find(s3, n.binds[0].names[0])->cxx + ");\n";
           return " hpush(A, " + ex(n.a[0], s3) + ");\n";
@@ -522,6 +534,7 @@ struct Gen {
         return "[&]() -> u32 { const u32 " + m + " = A.htop;\n" + loops + " return set_end(A, " + m + ");\n}()";
       }
       case K::FunCons: {
+        for (auto& b : n.binds) if (b.tuple) unsup(n, "a function constructor over a tuple binding");
         const std::string m = fresh("m");
         Scope s2 = sc;
         const std::string loops = bind_loops(n.binds, 0, 0, s2, false, [&](Scope& s3) {
@@ -685,6 +698,17 @@ struct Gen {
 
   std::string binary(const Node& n, Scope& sc) {
     const std::string& op = n.s;
+    if (op == "\\X") {   // S1 \X .. \X Sk: the set of k-tuples
+      std::string o = "[&]() -> u32 {\n";
+      std::vector<std::string> sets, els;
+      for (auto& a : n.a) { sets.push_back(fresh("S")); els.push_back(fresh("e")); o += " const u32 " + sets.back() + " = " + ex(a, sc) + ";\n"; }
+      const std::string m = fresh("m"), tm = fresh("m");
+      std::string body = " { const u32 " + tm + " = A.htop;";
+      for (auto& e : els) body += " hpush(A, " + e + ");";
+      body += " const u32 t_ = seq_end(A, " + tm + "); hpush(A, t_); }\n";
+      for (size_t i = sets.size(); i-- > 0;) body = set_loop(sets[i], els[i], body, false);
+      return o + " const u32 " + m + " = A.htop;\n" + body + " return set_end(A, " + m + ");\n}()";
+    }
     const NP& l = n.a[0];
     const NP& r = n.a[1];
     if (op == "\\subseteq" && lazy_set(r)) {   // x \subseteq S: every element of x in S (S never built)

@@ -121,6 +121,7 @@ std::string canon_op(const std::string& s) {   // synonyms
   if (s == "#") return "/=";
   if (s == "\\circ") return "\\o";
   if (s == "\\equiv") return "<=>";
+  if (s == "\\times") return "\\X";
   return s;
 }
 
@@ -131,7 +132,7 @@ int infix_prec(const std::string& s) {
       {"=", 5}, {"/=", 5}, {"<", 5}, {">", 5}, {"<=", 5}, {">=", 5}, {"\\in", 5}, {"\\notin", 5},
       {"\\subseteq", 5}, {"\\subset", 5}, {"\\supseteq", 5}, {"~>", 2},
       {"@@", 6}, {":>", 7}, {"\\cup", 8}, {"\\cap", 8}, {"\\", 8}, {"(+)", 10}, {"(-)", 11},
-      {"..", 9}, {"+", 10}, {"-", 11}, {"%", 11}, {"*", 13}, {"\\div", 13}, {"\\o", 13}, {"^", 14}};
+      {"..", 9}, {"\\X", 10}, {"+", 10}, {"-", 11}, {"%", 11}, {"*", 13}, {"\\div", 13}, {"\\o", 13}, {"^", 14}};
   auto it = p.find(s);
   return it == p.end() ? -1 : it->second;
 }
@@ -202,12 +203,18 @@ struct Parser {
     std::vector<Bind> out;
     do {
       Bind b;
-      if (is("<<")) fail("tuple bindings are outside the subset");
-      b.names.push_back(ident());
-      while (is(",")) {
-        const size_t save = p; ++p;
-        if (peek().t == T::Id && (tk[p + 1].s == "," || canon_op(tk[p + 1].s) == "\\in")) b.names.push_back(ident());
-        else { p = save; break; }
+      if (is("<<")) {   // \E <<a, b>> \in S : the elements of S are tuples, a and b their components
+        ++p;
+        b.tuple = true;
+        do b.names.push_back(ident()); while (is(",") && (++p, true));
+        expect(">>");
+      } else {
+        b.names.push_back(ident());
+        while (is(",")) {
+          const size_t save = p; ++p;
+          if (peek().t == T::Id && (tk[p + 1].s == "," || canon_op(tk[p + 1].s) == "\\in")) b.names.push_back(ident());
+          else { p = save; break; }
+        }
       }
       if (!is("\\in")) fail("unbounded quantifiers are outside the subset");
       ++p;
@@ -243,7 +250,11 @@ struct Parser {
     const std::string s = canon_op(t.s);
     if (t.t == T::Op) {
       if (s == "/\\" || s == "\\/") return junction(s == "/\\");
-      if (s == "(") { ++p; fence.push_back(-1); NP e = expr(0); expect(")"); fence.pop_back(); return e; }
+      if (s == "(") {
+        ++p; fence.push_back(-1); NP e = expr(0); expect(")"); fence.pop_back();
+        if (e->k == K::Binary && e->s == "\\X") e->n = 0;   // (A \X B) \X C: a pair whose first component is a pair
+        return e;
+      }
       if (s == "~") { ++p; NP n = mk(K::Unary, t, "~"); n->a.push_back(expr(4)); return n; }
       if (s == "-") { ++p; NP n = mk(K::Unary, t, "-"); n->a.push_back(expr(12)); return n; }
       if (s == "[]" || s == "<>") { ++p; NP n = mk(K::Temporal, t, s); n->a.push_back(expr(4)); return n; }
@@ -305,7 +316,7 @@ struct Parser {
     if (s == "CHOOSE") {
       ++p; NP n = mk(K::Choose, t);
       n->binds = binds();
-      if (n->binds.size() != 1 || n->binds[0].names.size() != 1) fail("CHOOSE binds one identifier");
+      if (n->binds.size() != 1 || n->binds[0].names.size() != 1 || n->binds[0].tuple) fail("CHOOSE binds one identifier");
       expect(":");
       n->a.push_back(expr(0));
       return n;
@@ -457,6 +468,10 @@ struct Parser {
         const K k = s == "/\\" ? K::And : K::Or;
         if (lhs->k == k && lhs->s == "infix") { lhs->a.push_back(rhs); continue; }
         NP n = mk(k, t, "infix"); n->a.push_back(lhs); n->a.push_back(rhs); lhs = n; continue;
+      }
+      if (s == "\\X") {   // A \X B \X C is the set of triples (\X is not associative)
+        if (lhs->k == K::Binary && lhs->s == s && lhs->n == 1) { lhs->a.push_back(rhs); continue; }
+        NP n = mk(K::Binary, t, s); n->n = 1; n->a.push_back(lhs); n->a.push_back(rhs); lhs = n; continue;
       }
       NP n = mk(K::Binary, t, s); n->a.push_back(lhs); n->a.push_back(rhs); lhs = n;
     }

@@ -133,6 +133,19 @@ def test_recursive_operators_on_gpu(raftmc):
     assert (r.verdict, r.violated, r.depth) == ("EVAL_ERROR", "Runaway", 1)
 
 
+def test_cartesian_products_on_gpu(raftmc):
+    """S \\X T and tuple-bound quantifiers (configs/tlagen/Product.tla) on the GPU, both pipelines: the
+    Python restatement's counts for the whole space."""
+    from test_tlagen import product_model
+    want = product_model()
+    for workers in (1, 0):
+        with raftmc.ModelChecker(os.path.join(CONFIGS, "tlagen", "Product.tla"), os.path.join(CONFIGS, "tlagen", "Product.cfg"),
+                                 workers=workers, **SMALL) as mc:
+            r = mc.run()
+        assert r.verdict == "OK", r.error
+        assert (r.generated, r.distinct, r.depth, [lv[0] for lv in r.levels]) == (want["generated"], want["distinct"], want["depth"], want["levels"])
+
+
 def test_function_and_record_sets_on_gpu(raftmc):
     """[S -> T] / [f : S, ...] as values and as lazily tested sets (configs/tlagen/FunSets.tla) on the GPU:
     the Python restatement's counts for the whole space (TypeOK holding), a negative control's depth;

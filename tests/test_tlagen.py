@@ -107,8 +107,8 @@ def test_unsupported_construct_fails_loudly(tmp_path):
     fallback); an unreached one is not."""
     (tmp_path / "Prod.tla").write_text(
         "---- MODULE Prod ----\nEXTENDS Naturals\nVARIABLE x\n"
-        "Keep(s) == s \\X s\nInit == x = {1, 2}\nNext == x' = Keep(x)\n"
-        "Unused == x \\X x\n====\n")
+        "Keep(s) == {<<a, b>> \\in s \\X s : a > b}\nInit == x = {1, 2}\nNext == x' = Keep(x)\n"
+        "Unused == {<<a, b>> \\in x \\X x : a > b}\n====\n")
     (tmp_path / "Prod.cfg").write_text("INIT Init\nNEXT Next\n")
     r = subprocess.run([TOOL, str(tmp_path / "Prod.tla"), str(tmp_path / "Prod.cfg")], capture_output=True, text=True)
     assert r.returncode == 1 and "Keep" in r.stderr and "does not parse" in r.stderr
@@ -559,3 +559,48 @@ def test_recursive_operators():
     assert (r["verdict"], r["violated"], r["depth"]) == ("INVARIANT_VIOLATION", "SumBelow4", want["sum_below4"])
     r = host_bfs(generate(RECURSIVE_OPS, os.path.join(CONFIGS, "tlagen", "Recursive_Runaway.cfg")))
     assert (r["verdict"], r["violated"], r["depth"]) == ("EVAL_ERROR", "Runaway", 1)
+
+
+PRODUCT = os.path.join(CONFIGS, "tlagen", "Product.tla")
+
+
+def product_model():
+    """configs/tlagen/Product.tla restated in Python: p a pair of {0, 1} x {0, 1, 2} whose first component
+    flips, q a triple over {0, 1} whose sum grows by one; counts, level sizes and QSumBelow2's depth."""
+    import itertools
+
+    def succ(st):
+        p, q = st
+        out = [((a, b), q) for a in (0, 1) for b in (0, 1, 2) if a != p[0]]
+        return out + [(p, t) for t in itertools.product((0, 1), repeat=3) if sum(t) == sum(q) + 1]
+    level = [((a, b), (0, 0, 0)) for a in (0, 1) for b in (0, 1, 2)]
+    seen, gen, levels, first, depth = set(level), len(level), [len(level)], None, 1
+    while level:
+        nxt = []
+        for st in level:
+            for t in succ(st):
+                gen += 1
+                if t not in seen:
+                    seen.add(t)
+                    nxt.append(t)
+        depth += 1
+        if first is None and any(sum(t[1]) >= 2 for t in nxt):
+            first = depth
+        if nxt:
+            levels.append(len(nxt))
+        level = nxt
+    return {"generated": gen, "distinct": len(seen), "depth": len(levels), "levels": levels, "qsum_below2": first}
+
+
+@needs_tool
+def test_cartesian_products_and_tuple_binds():
+    """S \\X T (n-ary: A \\X B \\X C is a set of triples, (A \\X B) \\X C of pairs) and tuple-bound
+    quantifiers (\\E <<a, b>> \\in S in an action, \\A <<x, y, z>> in an invariant, a map over a tuple
+    binding): Inv holds in every state, the whole space equals the Python restatement's, and the
+    negative control fails at its depth."""
+    want = product_model()
+    r = host_bfs(generate(PRODUCT, os.path.join(CONFIGS, "tlagen", "Product.cfg")))
+    assert (r["verdict"], r["err"]) == ("OK", 0)
+    assert {k: r[k] for k in ("generated", "distinct", "depth", "levels")} == {k: want[k] for k in ("generated", "distinct", "depth", "levels")}
+    r = host_bfs(generate(PRODUCT, os.path.join(CONFIGS, "tlagen", "Product_QSumBelow2.cfg")))
+    assert (r["verdict"], r["violated"], r["depth"]) == ("INVARIANT_VIOLATION", "QSumBelow2", want["qsum_below2"])
